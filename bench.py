@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on MI355X through the drop-in MPI API.
+
+  N = 1 : configs[1] — MPI_Reduce_local SUM fp32 on 256 MiB device buffers
+          (the op kernel against the HBM roofline); value = 3*S / t in GB/s.
+  N > 1 : configs[2] — osu_allreduce -d rocm fp32 SUM 256 MiB, one rank per GPU;
+          value = busbw = 2(n-1)/n * S / t (max over ranks), plus the 8-byte latency.
+
+Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+A step is one MPI call on resident device buffers (OSU loop: barrier, t0,
+call, t1).  Kernel time comes from HIP events recorded on the library's own
+stream around the kernel launch (mv2h_timing_enable / mv2h_last_kernel_ms).
+The CPU baseline (rank 0, N = 1 only) times the oracle's restatement of the
+reference op loop on a bounded host sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import mvapich2_amd as m  # noqa: E402
+from mvapich2_amd.consts import OPS, TYPES  # noqa: E402
+
+METRIC = "osu_allreduce busbw GB/s fp32 SUM 256MB at 1/2/4/8 MI355X; 8B latency us"
+HBM_PEAK = 8000.0        # GB/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK = 153.0        # GB/s per link per direction (task statement)
+S_BYTES = 256 * 1024 * 1024
+
+
+def cpu_info():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_reduce_local(seconds=10.0):
+    """Oracle restatement of the reference host op loop (opsum.c via
+    MPIR_OP_TYPE_REDUCE_CASE), single core, on a 64 MiB fp32 sample repeated
+    for ~`seconds`.  Rate in the metric's unit: 3*S algorithmic bytes / t."""
+    from oracle import oracle
+    n = 16 * 1024 * 1024
+    a = np.random.default_rng(1).standard_normal(n).astype(np.float32)
+    b = np.random.default_rng(2).standard_normal(n).astype(np.float32)
+    L = oracle.lib()
+    t1 = L.oracle_time_reduce_local(a.ctypes.data, b.ctypes.data, n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], 1)
+    reps = max(1, int(seconds / max(t1, 1e-6)))
+    t = L.oracle_time_reduce_local(a.ctypes.data, b.ctypes.data, n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], reps)
+    gbs = 3.0 * n * 4 * reps / t / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle reduce_local fp32 SUM, 64 MiB host buffers x {reps} reps ({t:.1f} s), "
+                      f"1 core of '{cpu_info()}'; reference device path adds D2H 2S + H2D S over PCIe"}
+
+
+def reduce_local_run(L, type_name, op_name, nbytes, steps, warmup):
+    h, desc, size, ext = TYPES[type_name]
+    count = nbytes // ext
+    a = m.DeviceBuffer(count * ext)
+    b = m.DeviceBuffer(count * ext)
+    rng = np.random.default_rng(0x5EED)
+    dt = m.np_dtype(type_name)
+    if dt.kind == "f":
+        x = rng.uniform(-1, 1, count).astype(dt)
+        y = rng.uniform(-1, 1, count).astype(dt)
+    else:
+        x = rng.integers(-(2**31), 2**31 - 1, count, dtype=np.int64).astype(dt)
+        y = rng.integers(-(2**31), 2**31 - 1, count, dtype=np.int64).astype(dt)
+    a.upload(x)
+    b.upload(y)
+    for _ in range(warmup):
+        m.check(L.MPI_Reduce_local(a.ptr, b.ptr, count, h, OPS[op_name]), "MPI_Reduce_local")
+    L.mv2h_timing_enable(1)
+    kms = []
+    L.mv2h_device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.check(L.MPI_Reduce_local(a.ptr, b.ptr, count, h, OPS[op_name]), "MPI_Reduce_local")
+        kms.append(L.mv2h_last_kernel_ms())
+    L.mv2h_device_synchronize()
+    t = time.perf_counter() - t0
+    L.mv2h_timing_enable(0)
+    # spot-check correctness of the last call on a slice (exact single-op fp/int)
+    got = b.download(dt, count=4096)
+    del a, b
+    return t / steps, float(np.mean(kms)) / 1e3, count, got
+
+
+def bench_n1(args, L):
+    step_s, kern_s, count, _ = reduce_local_run(L, "MPI_FLOAT", "MPI_SUM", S_BYTES, args.steps, args.warmup)
+    alg_bytes = 3 * count * 4
+    value = alg_bytes / step_s / 1e9
+    achieved = alg_bytes / kern_s / 1e9
+    extra = {}
+    for t, op in (("MPI_FLOAT", "MPI_MAX"), ("MPI_INT", "MPI_SUM"), ("MPI_DOUBLE", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX")):
+        s, k, c, _ = reduce_local_run(L, t, op, S_BYTES, max(3, args.steps // 2), 2)
+        extra[f"{t}:{op}"] = {"GB/s_call": round(3 * S_BYTES / s / 1e9, 1), "GB/s_kernel": round(3 * S_BYTES / k / 1e9, 1)}
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_reduce_local_r01.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "configs[1]: MPI_Reduce_local SUM fp32 on 256 MiB device buffers, 1 MI355X",
+                   "count": count, "bytes_per_operand": S_BYTES, "algorithmic_bytes_per_call": alg_bytes,
+                   "api": "MPI_Reduce_local via libmpi.so (MPICH ABI)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+                     "kernel": "k_reduce_local<R<SUM,F32>,4>", "kernel_ms": round(kern_s * 1e3, 4)},
+        "cpu_baseline": cpu_baseline_reduce_local(args.cpu_seconds) if args.cpu_seconds > 0 else None,
+        "extra": extra,
+    }
+    return line
+
+
+def bench_nranks(args, L, rank, size):
+    h = TYPES["MPI_FLOAT"][0]
+    op = OPS["MPI_SUM"]
+    world = 0x44000000
+    count = S_BYTES // 4
+    sb = m.DeviceBuffer(S_BYTES)
+    rb = m.DeviceBuffer(S_BYTES)
+    x = np.full(count, float(rank + 1), dtype=np.float32)
+    sb.upload(x)
+    for _ in range(args.warmup):
+        m.check(L.MPI_Allreduce(sb.ptr, rb.ptr, count, h, op, world), "MPI_Allreduce")
+    L.mv2h_timing_enable(1)
+    kms = []
+    # contract: barrier + device sync, K timed steps, barrier + device sync
+    L.MPI_Barrier(world)
+    L.mv2h_device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.check(L.MPI_Allreduce(sb.ptr, rb.ptr, count, h, op, world), "MPI_Allreduce")
+        kms.append(L.mv2h_last_kernel_ms())
+    L.mv2h_device_synchronize()
+    L.MPI_Barrier(world)
+    tot = time.perf_counter() - t0
+    L.mv2h_timing_enable(0)
+    got = rb.download(np.float32, count=1024)
+    ok = bool(np.all(got == size * (size + 1) / 2))
+    # 8-byte latency (OSU: 1000 iterations, 100 skip for small messages)
+    s8 = m.DeviceBuffer(8)
+    r8 = m.DeviceBuffer(8)
+    s8.upload(np.ones(2, dtype=np.float32))
+    for _ in range(100):
+        L.MPI_Allreduce(s8.ptr, r8.ptr, 2, h, op, world)
+    lat = 0.0
+    for _ in range(args.lat_iters):
+        L.MPI_Barrier(world)
+        t0 = time.perf_counter()
+        L.MPI_Allreduce(s8.ptr, r8.ptr, 2, h, op, world)
+        lat += time.perf_counter() - t0
+    # max over ranks via a tiny device allreduce (MAX)
+    mx = np.array([tot, lat, float(np.mean(kms)), 0.0 if ok else 1.0], dtype=np.float64)
+    dm = m.DeviceBuffer(mx.nbytes)
+    dm.upload(mx)
+    dr = m.DeviceBuffer(mx.nbytes)
+    m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, 4, TYPES["MPI_DOUBLE"][0], OPS["MPI_MAX"], world), "max")
+    tot, lat, kms_max, bad = dr.download(np.float64, count=4)
+    step_s = tot / args.steps
+    busbw = 2.0 * (size - 1) / size * S_BYTES / step_s / 1e9
+    kbus = 2.0 * (size - 1) / size * S_BYTES / (kms_max / 1e3) / 1e9
+    peak_all = (size - 1) * XGMI_LINK
+    line = {
+        "metric": METRIC, "value": round(busbw, 2), "unit": "GB/s", "n_gpus": size, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "configs[2]: osu_allreduce -d rocm fp32 SUM 256 MiB, 1 rank per GPU over xGMI",
+                   "count": count, "bytes": S_BYTES, "algorithm": "two-shot direct RS+AG (peer reads)",
+                   "latency_8B_us": round(lat / args.lat_iters * 1e6, 2), "correct": not bool(bad)},
+        "roofline": {"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
+                     "frac": round(kbus / peak_all, 4), "traffic": None,
+                     "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_twoshot<R<SUM,F32>,2>",
+                     "kernel_ms": round(kms_max, 4)},
+        "cpu_baseline": None,
+    }
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--lat-iters", type=int, default=1000)
+    args = ap.parse_args()
+    L = m.lib()
+    size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if size != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={size}", file=sys.stderr)
+    m.check(L.MPI_Init(None, None), "MPI_Init")
+    if size == 1:
+        line = bench_n1(args, L)
+    else:
+        line = bench_nranks(args, L, rank, size)
+    L.MPI_Finalize()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,100 @@
+/*
+ * mv2h.h — C-ABI between the MPI entry points (C glue) and the MI355X HIP
+ * layer of mvapich2_amd.  Plain pointers and sizes only; no HIP or torch
+ * types appear in these signatures (`stream` is a hipStream_t passed as
+ * void*, NULL = the library's internal stream).
+ *
+ * Every entry point is synchronous with respect to the caller (MPI blocking
+ * semantics): on return the result is complete in device memory.  Return
+ * value is MPI_SUCCESS (0) or an MPI error class.
+ *
+ * Reference interfaces each entry point replaces (MVAPICH2 2.3.7):
+ *   mv2h_reduce_local   MPIR_Reduce_local_impl        src/mpi/coll/reduce_local.c:36-173
+ *                       (host op kernels              src/mpi/coll/op*.c, oputil.h:50-57)
+ *   mv2h_op_check       MPIR_Op_check_dtype_table     src/mpi/coll/allreduce.c:102-109
+ *   mv2h_allreduce      MPIR_Allreduce_MV2            src/mpi/coll/allreduce_osu.c:3720
+ *                       -> index_tuned_intra_MV2      allreduce_osu.c:3015-3420
+ *   mv2h_reduce         MPIR_Reduce_MV2               src/mpi/coll/reduce_osu.c:2709
+ *   mv2h_reduce_scatter MPIR_Reduce_scatter_MV2       src/mpi/coll/red_scat_osu.c:1771
+ *   mv2h_allgather      MPIR_Allgather_MV2            src/mpi/coll/allgather_osu.c:2593
+ *   mv2h_bcast          MPIR_Bcast_MV2                src/mpi/coll/bcast_osu.c:3347
+ *   mv2h_pack_strided   MPID_Segment_pack_device      src/mpid/ch3/channels/mrail/src/gen2/ibv_cuda_util.c:623
+ *                       pack_unpack_vector_kernel     src/mpid/ch3/channels/mrail/src/cuda/pack_unpack.cu:419
+ *   mv2h_is_device_ptr  is_device_buffer              ibv_cuda_util.c:819
+ */
+#ifndef MV2H_H_INCLUDED
+#define MV2H_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Reduction order used by the n-input device reduction.
+ * Each reproduces the operand order of one MV2 host algorithm bit-for-bit. */
+enum mv2h_order {
+    MV2H_ORDER_LINEAR = 0,    /* ((x0 op x1) op x2) ... : two-level reduce_shmem, allreduce_osu.c:1569-1583 */
+    MV2H_ORDER_BUTTERFLY = 1, /* recursive halving / doubling with non-pof2 fold, allreduce_osu.c:455-947 */
+};
+
+/* ---- library / device bookkeeping ---- */
+const char *mv2h_version(void);
+int mv2h_device_count(void);
+int mv2h_is_device_ptr(const void *ptr);
+int mv2h_malloc(void **ptr, size_t bytes);
+int mv2h_free(void *ptr);
+int mv2h_memcpy_htod(void *dst, const void *src, size_t bytes);
+int mv2h_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+int mv2h_memcpy_dtod(void *dst, const void *src, size_t bytes);
+int mv2h_memset(void *dst, int value, size_t bytes);
+int mv2h_device_synchronize(void);
+
+/* ---- datatypes / op table ---- */
+int mv2h_dtype_info(int dtype, size_t *size, size_t *extent);
+int mv2h_op_check(int op, int dtype);
+
+/* ---- part (1): the MPI_Op reduction layer ---- */
+int mv2h_reduce_local(const void *in, void *inout, size_t count, int dtype, int op, void *stream);
+/* dst = reduce(srcs[0..nsrc-1]) in `order`; owner = newrank whose subtree is the left
+ * operand (butterfly only).  srcs may be peer (IPC-mapped) pointers. */
+int mv2h_reduce_n(const void *const *srcs, int nsrc, void *dst, size_t count, int dtype, int op,
+                  int order, int owner, void *stream);
+
+/* ---- part (2): device collectives over COMM_WORLD (one process per GPU) ---- */
+int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op,
+                   void *stream);
+int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root,
+                void *stream);
+int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype,
+                        int op, void *stream);
+int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes_per_rank, void *stream);
+int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream);
+int mv2h_barrier(void);
+
+/* ---- part (3): strided pack / unpack (MPI_Type_vector family) ----
+ * pack:   dst[i*blk + j] = src[i*stride + j],  i < nblocks, j < blk  (bytes)
+ * unpack: dst[i*stride + j] = src[i*blk + j] */
+int mv2h_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk_bytes,
+                      size_t stride_bytes, void *stream);
+int mv2h_unpack_strided(const void *src, void *dst, size_t nblocks, size_t blk_bytes,
+                        size_t stride_bytes, void *stream);
+
+/* ---- runtime (bootstrap for COMM_WORLD) ---- */
+int mv2h_init(void);
+int mv2h_finalize(void);
+int mv2h_rank(void);
+int mv2h_size(void);
+int mv2h_local_rank(void);
+
+/* ---- measurement hooks (bench.py): HIP-event timing of the last kernel ---- */
+int mv2h_timing_enable(int on);
+double mv2h_last_kernel_ms(void);
+int mv2h_set_tuning(const char *key, long value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MV2H_H_INCLUDED */

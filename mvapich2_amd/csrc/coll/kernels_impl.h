@@ -1,0 +1,430 @@
+// kernels_impl.h — templated gfx950 kernels for the MPI_Op layer and the
+// device collectives.  Instantiated per (op, kind) in kernels_*.hip.
+//
+// Data layout: every buffer is addressed as 16-byte vectors (v4u) holding
+// 16/sizeof(T) elements (pair records with padding keep the accumulator's
+// padding bytes); elements past the last whole vector are a scalar tail.
+// All kernels are HBM- or xGMI-bound: 256-thread workgroups, U vectors per
+// thread in flight per source, grid-stride over tiles, non-temporal stores
+// for results that are not re-read by the kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../ops/functors.h"
+#include "kernels.h"
+
+namespace mv2 {
+
+// ============================================================================
+// MPI_Reduce_local: inout[i] = op(inout[i], in[i])   (reduce_local.c:139)
+// ============================================================================
+template <class Rd, int U>
+__global__ __launch_bounds__(kThreads) void k_reduce_local(const v4u *__restrict__ in,
+                                                           v4u *__restrict__ io, size_t nvec,
+                                                           const typename Rd::T *__restrict__ tin,
+                                                           typename Rd::T *__restrict__ tio,
+                                                           size_t tail_beg, size_t tail_end) {
+    const size_t stride = (size_t)gridDim.x * kThreads * U;
+    for (size_t base = (size_t)blockIdx.x * kThreads * U + threadIdx.x; base < nvec; base += stride) {
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * kThreads;
+            if (i < nvec) {
+                a[u] = io[i];
+                b[u] = in[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * kThreads;
+            if (i < nvec) st_nt(&io[i], vapply<Rd>(a[u], b[u]));
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t e = tail_beg + threadIdx.x; e < tail_end; e += kThreads) tio[e] = Rd::apply(tio[e], tin[e]);
+}
+
+// element-granular variant for buffers that are not 16-byte aligned
+template <class Rd>
+__global__ __launch_bounds__(kThreads) void k_reduce_local_elem(const typename Rd::T *__restrict__ in,
+                                                                typename Rd::T *__restrict__ io,
+                                                                size_t count) {
+    const size_t stride = (size_t)gridDim.x * kThreads;
+    for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < count; e += stride)
+        io[e] = Rd::apply(io[e], in[e]);
+}
+
+template <int OP, int K>
+struct LReduceLocal {
+    static int run(const void *in, void *inout, size_t count, const LaunchCfg &cfg) {
+        using Rd = R<OP, K>;
+        using T = typename Rd::T;
+        constexpr size_t VPT = 16 / sizeof(T);
+        const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)inout % 16 == 0);
+        if (!aligned) {
+            size_t g = (count + kThreads - 1) / kThreads;
+            if (g > (size_t)cfg.grid) g = cfg.grid;
+            if (g == 0) g = 1;
+            hipLaunchKernelGGL((k_reduce_local_elem<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream,
+                               (const T *)in, (T *)inout, count);
+            return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+        }
+        const size_t nvec = count / VPT;
+        const size_t tile = (size_t)kThreads * 4;
+        size_t g = (nvec + tile - 1) / tile;
+        if (g > (size_t)cfg.grid) g = cfg.grid;
+        if (g == 0) g = 1;
+        hipLaunchKernelGGL((k_reduce_local<Rd, 4>), dim3(g), dim3(kThreads), 0, cfg.stream,
+                           (const v4u *)in, (v4u *)inout, nvec, (const T *)in, (T *)inout,
+                           nvec * VPT, count);
+        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+    }
+};
+
+// ============================================================================
+// n-input reduction helpers (sources may be peer-mapped pointers)
+// ============================================================================
+template <class Rd>
+__device__ __forceinline__ int elem_owner(const TreeParams &tp, size_t e) {
+    if (tp.owner_fixed >= 0) return tp.owner_fixed;
+    size_t b = tp.rs_blk ? e / tp.rs_blk : 0;
+    if (b > (size_t)(tp.pof2 - 1)) b = tp.pof2 - 1;
+    return brev_bits((int)b, tp.lg);
+}
+
+// reduce n 16-byte vectors (v[j] from rank j) whose first element index is e0
+template <class Rd>
+__device__ __forceinline__ v4u vreduce_n(const v4u (&v)[kMaxRanks], int n, const TreeParams &tp,
+                                         size_t e0) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    T t[kMaxRanks][N];
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) __builtin_memcpy(t[j], &v[j], 16);
+    T out[N];
+    const int own0 = tp.linear ? 0 : elem_owner<Rd>(tp, e0);
+    const int ownN = tp.linear ? 0 : elem_owner<Rd>(tp, e0 + N - 1);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        T col[kMaxRanks];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) col[j] = t[j][i];
+        const int own = (own0 == ownN) ? own0 : elem_owner<Rd>(tp, e0 + i);
+        out[i] = tree_reduce<Rd>(col, n, tp.linear, tp.pof2, tp.rem, own);
+    }
+    v4u r;
+    __builtin_memcpy(&r, out, 16);
+    return r;
+}
+
+template <class Rd>
+__device__ __forceinline__ typename Rd::T sreduce_n(const typename Rd::T *const *src, int n,
+                                                    const TreeParams &tp, size_t e) {
+    using T = typename Rd::T;
+    T col[kMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) col[j] = (j < n) ? src[j][e] : src[0][e];
+    return tree_reduce<Rd>(col, n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, e));
+}
+
+// plain n-source reduction into dst (single process; used by mv2h_reduce_n and tests)
+template <class Rd, int U>
+__global__ __launch_bounds__(kThreads) void k_reduce_n(PeerTable src, int n, char *dst, size_t count,
+                                                       size_t nvec, TreeParams tp) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    const size_t stride = (size_t)gridDim.x * kThreads * U;
+    for (size_t base = (size_t)blockIdx.x * kThreads * U + threadIdx.x; base < nvec; base += stride) {
+        v4u v[U][kMaxRanks];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * kThreads;
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                v[u][j] = (j < n && i < nvec) ? ((const v4u *)src.p[j])[i] : v4u{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * kThreads;
+            if (i < nvec) st_nt((v4u *)dst + i, vreduce_n<Rd>(v[u], n, tp, i * N));
+        }
+    }
+    if (blockIdx.x == 0) {
+        const T *s[kMaxRanks];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) s[j] = (const T *)src.p[j];
+        for (size_t e = nvec * N + threadIdx.x; e < count; e += kThreads) ((T *)dst)[e] = sreduce_n<Rd>(s, n, tp, e);
+    }
+}
+
+template <class Rd>
+__global__ __launch_bounds__(kThreads) void k_reduce_n_elem(PeerTable src, int n, char *dst, size_t count,
+                                                            TreeParams tp) {
+    using T = typename Rd::T;
+    const T *s[kMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) s[j] = (const T *)src.p[j];
+    const size_t stride = (size_t)gridDim.x * kThreads;
+    for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < count; e += stride)
+        ((T *)dst)[e] = sreduce_n<Rd>(s, n, tp, e);
+}
+
+template <int OP, int K>
+struct LReduceN {
+    static int run(const void *const *srcs, int n, void *dst, size_t count, const TreeParams &tp,
+                   const LaunchCfg &cfg) {
+        using Rd = R<OP, K>;
+        using T = typename Rd::T;
+        constexpr size_t VPT = 16 / sizeof(T);
+        PeerTable pt{};
+        bool aligned = (uintptr_t)dst % 16 == 0;
+        for (int j = 0; j < n; ++j) {
+            pt.p[j] = (const char *)srcs[j];
+            aligned = aligned && ((uintptr_t)srcs[j] % 16 == 0);
+        }
+        for (int j = n; j < kMaxRanks; ++j) pt.p[j] = pt.p[0];
+        if (!aligned) {
+            size_t g = (count + kThreads - 1) / kThreads;
+            if (g > (size_t)cfg.grid) g = cfg.grid;
+            if (g == 0) g = 1;
+            hipLaunchKernelGGL((k_reduce_n_elem<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream, pt, n,
+                               (char *)dst, count, tp);
+        } else {
+            const size_t nvec = count / VPT;
+            size_t g = (nvec + 2 * kThreads - 1) / (2 * kThreads);
+            if (g > (size_t)cfg.grid) g = cfg.grid;
+            if (g == 0) g = 1;
+            hipLaunchKernelGGL((k_reduce_n<Rd, 2>), dim3(g), dim3(kThreads), 0, cfg.stream, pt, n,
+                               (char *)dst, count, nvec, tp);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+    }
+};
+
+// ============================================================================
+// One-shot allreduce (small messages): push my sendbuf into every peer's
+// arena slot, flag, then reduce all n slots locally in reference order.
+// No exit barrier: the arena half used alternates per call (parity), and a
+// peer can only reach call i+2 after every rank finished call i.
+// ============================================================================
+template <class Rd>
+__global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    const int blk = blockIdx.x, G = gridDim.x;
+    const size_t per = (a.nvec + G - 1) / G;
+    const size_t vb = (size_t)blk * per;
+    const size_t ve = vb + per < a.nvec ? vb + per : a.nvec;
+    const v4u *send = (const v4u *)a.send;
+    // phase A: push my data to every peer's slot (me)
+    for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
+        const v4u x = send[i];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j)
+            if (j < a.n && j != a.me) ((v4u *)(a.arena_peer.p[j] + (size_t)a.me * a.slot_bytes))[i] = x;
+    }
+    const size_t tail0 = a.nvec * N;
+    if (blk == 0) {
+        for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {
+            const T x = ((const T *)a.send)[e];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                if (j < a.n && j != a.me) ((T *)(a.arena_peer.p[j] + (size_t)a.me * a.slot_bytes))[e] = x;
+        }
+    }
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch);
+    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
+    // phase B: reduce the n slots (own data straight from sendbuf)
+    for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
+        v4u v[kMaxRanks];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) {
+            v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ((const v4u *)(a.arena_own + (size_t)j * a.slot_bytes))[i];
+        }
+        ((v4u *)a.recv)[i] = vreduce_n<Rd>(v, a.n, a.tp, i * N);
+    }
+    if (blk == 0) {
+        for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {
+            T col[kMaxRanks];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e] : ((const T *)(a.arena_own + (size_t)j * a.slot_bytes))[e];
+            ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
+        }
+    }
+}
+
+// ============================================================================
+// Two-shot allreduce (large messages): direct reduce-scatter + all-gather
+// over xGMI, every rank reading its n-1 peers concurrently (n-1 links).
+// Tiles of TV vectors are owned round-robin (tile t -> rank t % n).
+//   E0: all ranks entered (sendbufs ready)      RS: reduce own tiles -> recv
+//   E1: all reduce-scatters done               AG: copy peers' tiles -> recv
+//   E2: all gathers done (peers stopped reading my buffers)
+// ============================================================================
+template <class Rd, int U>
+__global__ __launch_bounds__(kThreads) void k_twoshot(TwoShotArgs a) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    constexpr size_t TV = (size_t)kThreads * U;
+    const int blk = blockIdx.x, G = gridDim.x;
+    const size_t ntiles = (a.nvec + TV - 1) / TV;
+
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch);
+    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
+
+    // ---- reduce-scatter: my tiles ----
+    for (size_t it = blk;; it += G) {
+        const size_t t = (size_t)a.me + (size_t)a.n * it;
+        if (t >= ntiles) break;
+        v4u v[U][kMaxRanks];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = t * TV + (size_t)u * kThreads + threadIdx.x;
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                v[u][j] = (j < a.n && i < a.nvec) ? ((const v4u *)a.src.p[j])[i] : v4u{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = t * TV + (size_t)u * kThreads + threadIdx.x;
+            if (i < a.nvec) ((v4u *)a.recv)[i] = vreduce_n<Rd>(v[u], a.n, a.tp, i * N);
+        }
+    }
+    // scalar tail: reduced by block 0 of every rank, written after E1
+    const size_t tail0 = a.nvec * N;
+    T tail_val{};
+    const bool has_tail = blk == 0 && tail0 + threadIdx.x < a.count;
+    if (has_tail) {
+        const T *s[kMaxRanks];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) s[j] = (const T *)a.src.p[j];
+        tail_val = sreduce_n<Rd>(s, a.n, a.tp, tail0 + threadIdx.x);
+    }
+
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch + 1);
+    if (!wait_peers(a.sig_own, a.n, blk, a.epoch + 1, a.err, a.timeout)) return;
+
+    // ---- all-gather: peers' tiles ----
+    for (size_t it = blk;; it += G) {
+        const size_t tbase = (size_t)a.n * it;
+        if (tbase >= ntiles) break;
+        v4u v[U][kMaxRanks];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int k = 0; k < kMaxRanks; ++k) {
+                const size_t i = (tbase + k) * TV + (size_t)u * kThreads + threadIdx.x;
+                v[u][k] = (k < a.n && k != a.me && i < a.nvec) ? ((const v4u *)a.agsrc.p[k])[i] : v4u{0, 0, 0, 0};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int k = 0; k < kMaxRanks; ++k) {
+                const size_t i = (tbase + k) * TV + (size_t)u * kThreads + threadIdx.x;
+                if (k < a.n && k != a.me && i < a.nvec) st_nt((v4u *)a.recv + i, v[u][k]);
+            }
+        }
+    }
+    if (has_tail) ((T *)a.recv)[tail0 + threadIdx.x] = tail_val;
+
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch + 2);
+    wait_peers(a.sig_own, a.n, blk, a.epoch + 2, a.err, a.timeout);
+}
+
+// ============================================================================
+// Direct reduce-scatter: rank me reduces elements [off, off+cnt) of every
+// rank's sendbuf into dst (same alignment as src + off).  E0 entry, E1 exit.
+// ============================================================================
+template <class Rd, int U>
+__global__ __launch_bounds__(kThreads) void k_rs(RsArgs a) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    const int blk = blockIdx.x, G = gridDim.x;
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch);
+    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
+    // element range -> vector-aligned body [vb, ve) plus scalar head/tail
+    const size_t eb = a.off, ee = a.off + a.cnt;
+    const size_t vb = (eb + N - 1) / N, ve = ee / N;
+    if (vb < ve) {
+        const size_t stride = (size_t)G * kThreads * U;
+        for (size_t base = vb + (size_t)blk * kThreads * U + threadIdx.x; base < ve; base += stride) {
+            v4u v[U][kMaxRanks];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * kThreads;
+#pragma unroll
+                for (int j = 0; j < kMaxRanks; ++j)
+                    v[u][j] = (j < a.n && i < ve) ? ((const v4u *)a.src.p[j])[i] : v4u{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * kThreads;
+                if (i < ve) st_nt((v4u *)a.dst + i, vreduce_n<Rd>(v[u], a.n, a.tp, i * N));
+            }
+        }
+    }
+    if (blk == 0) {
+        const T *s[kMaxRanks];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) s[j] = (const T *)a.src.p[j];
+        const size_t hb_end = vb < ve ? vb * N : ee;
+        for (size_t e = eb + threadIdx.x; e < hb_end; e += kThreads) ((T *)a.dst)[e] = sreduce_n<Rd>(s, a.n, a.tp, e);
+        if (vb < ve)
+            for (size_t e = ve * N + threadIdx.x; e < ee; e += kThreads) ((T *)a.dst)[e] = sreduce_n<Rd>(s, a.n, a.tp, e);
+    }
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch + 1);
+    wait_peers(a.sig_own, a.n, blk, a.epoch + 1, a.err, a.timeout);
+}
+
+template <int OP, int K>
+struct LOneShot {
+    static int run(const OneShotArgs &a, const LaunchCfg &cfg) {
+        hipLaunchKernelGGL((k_oneshot<R<OP, K>>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+    }
+};
+template <int OP, int K>
+struct LTwoShot {
+    static int run(const TwoShotArgs &a, const LaunchCfg &cfg) {
+        hipLaunchKernelGGL((k_twoshot<R<OP, K>, 2>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+    }
+};
+template <int OP, int K>
+struct LRs {
+    static int run(const RsArgs &a, const LaunchCfg &cfg) {
+        hipLaunchKernelGGL((k_rs<R<OP, K>, 2>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+    }
+};
+
+// ---------------- runtime (op, kind) -> template dispatch ----------------
+template <template <int, int> class L, int OP, int K, class... A>
+inline int call_if(A &&...args) {
+    if constexpr (legal<OP, K>()) return L<OP, K>::run(static_cast<A &&>(args)...);
+    else return E_OP;
+}
+
+template <template <int, int> class L, int K, class... A>
+inline int dispatch_op(int op, A &&...args) {
+    switch (op) {
+    case OP_MAX: return call_if<L, OP_MAX, K>(static_cast<A &&>(args)...);
+    case OP_MIN: return call_if<L, OP_MIN, K>(static_cast<A &&>(args)...);
+    case OP_SUM: return call_if<L, OP_SUM, K>(static_cast<A &&>(args)...);
+    case OP_PROD: return call_if<L, OP_PROD, K>(static_cast<A &&>(args)...);
+    case OP_LAND: return call_if<L, OP_LAND, K>(static_cast<A &&>(args)...);
+    case OP_BAND: return call_if<L, OP_BAND, K>(static_cast<A &&>(args)...);
+    case OP_LOR: return call_if<L, OP_LOR, K>(static_cast<A &&>(args)...);
+    case OP_BOR: return call_if<L, OP_BOR, K>(static_cast<A &&>(args)...);
+    case OP_LXOR: return call_if<L, OP_LXOR, K>(static_cast<A &&>(args)...);
+    case OP_BXOR: return call_if<L, OP_BXOR, K>(static_cast<A &&>(args)...);
+    case OP_MINLOC: return call_if<L, OP_MINLOC, K>(static_cast<A &&>(args)...);
+    case OP_MAXLOC: return call_if<L, OP_MAXLOC, K>(static_cast<A &&>(args)...);
+    default: return E_OP;
+    }
+}
+
+}  // namespace mv2

@@ -1,0 +1,162 @@
+// device_util.h — gfx950 device helpers shared by the op and collective kernels.
+//
+// Cross-GPU hand-off protocol (one process per GPU, peers' memory mapped with
+// hipIpcOpenMemHandle, flags in hipDeviceMallocUncached signal pages):
+//   producer: stores -> every wave s_waitcnt vmcnt(0) -> __syncthreads ->
+//             lane 0 system-scope release fence (buffer_wbl2) -> asm vmcnt(0)
+//             -> relaxed system-scope flag stores (one lane per peer)
+//   consumer: one wave polls its own (uncached, local) flag words relaxed,
+//             with s_sleep, bounded by a wall-clock timeout -> lane 0
+//             system-scope acquire fence (buffer_inv sc0 sc1: drops stale
+//             L1/L2 lines of peer memory) -> __syncthreads -> plain loads.
+// Flags carry monotonically increasing 64-bit epochs (never reset), so no
+// per-call memset is needed and a stale flag can only read as "not yet".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mv2 {
+
+constexpr int kMaxRanks = 8;        // device collectives: ranks per node
+constexpr int kMaxBlocks = 1024;    // flag slots per (source rank)
+constexpr int kThreads = 256;
+
+struct PeerTable {
+    const char *p[kMaxRanks];
+};
+struct PeerTableW {
+    char *p[kMaxRanks];
+};
+struct SigTable {
+    uint64_t *p[kMaxRanks];
+};
+
+#ifdef __HIPCC__  // device code below: only in hipcc-compiled translation units
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void st_nt(v4u *p, v4u v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ v4u ld_v(const v4u *p) { return *p; }
+
+__device__ __forceinline__ void flag_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t flag_load(uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Release this workgroup's prior global stores at system scope and raise
+// flag[me][blk] = epoch on every rank in [0, n).  Call from all threads.
+__device__ __forceinline__ void signal_peers(const SigTable &sig, int n, int me, int blk,
+                                             uint64_t epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        // same wave as the fence: lanes 0..n-1 store after it in program order
+        __builtin_amdgcn_wave_barrier();
+        if ((int)threadIdx.x < n) flag_store(sig.p[threadIdx.x] + (size_t)me * kMaxBlocks + blk, epoch);
+    }
+}
+
+// Wait until flag[j][blk] >= epoch for every j in [0, n) (own slot included),
+// then acquire at system scope.  Returns false (and records *err) on timeout.
+// Call from all threads; the result is block-uniform.
+__device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, uint64_t epoch,
+                                           int *err, uint64_t timeout_ticks) {
+    __shared__ int s_ok;
+    if (threadIdx.x < 64) {
+        const int j = threadIdx.x;
+        bool ok = j >= n;
+        const uint64_t t0 = wall_clock64();
+        bool timed_out = false;
+        while (!__all(ok)) {
+            if (!ok) ok = flag_load(own_sig + (size_t)j * kMaxBlocks + blk) >= epoch;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > timeout_ticks) { timed_out = true; break; }
+        }
+        if (threadIdx.x == 0) {
+            if (timed_out) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s_ok = 0;
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                s_ok = 1;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+// a x b elementwise on one 16-byte vector holding 16/sizeof(T) elements
+template <class Rd>
+__device__ __forceinline__ v4u vapply(v4u a, v4u b) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    T ta[N], tb[N];
+    __builtin_memcpy(ta, &a, 16);
+    __builtin_memcpy(tb, &b, 16);
+#pragma unroll
+    for (int i = 0; i < N; ++i) ta[i] = Rd::apply(ta[i], tb[i]);
+    __builtin_memcpy(&a, ta, 16);
+    return a;
+}
+
+// ---- n-input reduction tree on one element (n <= 8, all indices constant) ----
+// LINEAR   : ((v0 . v1) . v2) ...                (two-level reduce_shmem order)
+// BUTTERFLY: non-pof2 fold w[i] = v[2i+1] . v[2i] for i < rem, then levels
+//            m = 1, 2, 4 pairing (j, j+m); the left operand is the subtree
+//            containing `owner` (recursive halving / doubling order).
+template <class Rd>
+__device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[kMaxRanks], int n,
+                                                      int linear, int pof2, int rem, int owner) {
+    using T = typename Rd::T;
+    if (linear) {
+        T acc = v[0];
+#pragma unroll
+        for (int i = 1; i < kMaxRanks; ++i)
+            if (i < n) acc = Rd::apply(acc, v[i]);
+        return acc;
+    }
+    T w[kMaxRanks];
+#pragma unroll
+    for (int i = 0; i < kMaxRanks; ++i) {
+        const int k0 = i < kMaxRanks ? i : kMaxRanks - 1;
+        const int k1 = i + 1 < kMaxRanks ? i + 1 : kMaxRanks - 1;
+        const int k2 = i + 2 < kMaxRanks ? i + 2 : kMaxRanks - 1;
+        const int k3 = i + 3 < kMaxRanks ? i + 3 : kMaxRanks - 1;
+        w[i] = rem == 0 ? v[k0] : rem == 1 ? v[k1] : rem == 2 ? v[k2] : v[k3];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < rem) w[i] = Rd::apply(v[2 * i + 1], v[2 * i]);
+#pragma unroll
+    for (int m = 1; m < kMaxRanks; m <<= 1) {
+        if (m < pof2) {
+#pragma unroll
+            for (int j = 0; j + m < kMaxRanks; j += 2 * m) {
+                if (j + m < pof2) {
+                    const bool up = (owner & m) != 0;
+                    const T x = up ? w[j + m] : w[j];
+                    const T y = up ? w[j] : w[j + m];
+                    w[j] = Rd::apply(x, y);
+                }
+            }
+        }
+    }
+    return w[0];
+}
+
+// bit-reverse of b over lg bits (owner newrank of reduce-scatter block b)
+__device__ __forceinline__ int brev_bits(int b, int lg) {
+    return lg == 0 ? 0 : (int)(__builtin_bitreverse32((uint32_t)b) >> (32 - lg));
+}
+
+#endif  // __HIPCC__
+
+}  // namespace mv2

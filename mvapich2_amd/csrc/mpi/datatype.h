@@ -1,0 +1,11 @@
+// datatype.h — builtin + derived datatype queries used by the MPI glue.
+#pragma once
+#include "../../../include/mpi.h"
+
+bool dtype_valid(MPI_Datatype dt);
+bool dtype_is_builtin(MPI_Datatype dt);
+bool dtype_is_contiguous(MPI_Datatype dt);
+long dtype_size(MPI_Datatype dt);
+long dtype_extent(MPI_Datatype dt);
+// bytes from the first to one past the last byte touched by `count` elements (lb = 0)
+long dtype_span(MPI_Datatype dt, int count);

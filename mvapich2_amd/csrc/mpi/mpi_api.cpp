@@ -1,0 +1,505 @@
+// mpi_api.cpp — the MPI-3.1 C entry points (include/mpi.h) over the mv2h
+// C-ABI.  Argument checking and error-handler behaviour follow the
+// reference's MPI layer (e.g. allreduce.c:827-960, reduce_local.c:206-268):
+// count == 0 returns immediately, a predefined op on a type outside its
+// groups is MPI_ERR_OP, errors go through the communicator's error handler
+// (default MPI_ERRORS_ARE_FATAL).  Every MPI_X is a weak alias of PMPI_X
+// (allreduce.c:80-84).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../../include/mpi.h"
+#include "../../../include/mv2h.h"
+#include "../common.h"
+#include "../runtime/log.h"
+#include "../runtime/world.h"
+#include "datatype.h"
+
+using namespace mv2;
+
+namespace {
+
+std::recursive_mutex g_cs;  // global critical section (allreduce.c:838)
+MPI_Errhandler g_eh[2] = {MPI_ERRORS_ARE_FATAL, MPI_ERRORS_ARE_FATAL};
+bool g_initialized = false, g_finalized = false;
+
+struct UserOp {
+    MPI_User_function *fn;
+    int commute;
+    bool live;
+};
+std::vector<UserOp> g_uops;
+constexpr int kUserOpBase = (int)0x98000000;  // direct-kind op handles (MPICH kind bits 10, object 0x18)
+
+const char *err_name(int c) {
+    switch (c) {
+    case MPI_SUCCESS: return "MPI_SUCCESS: no error";
+    case MPI_ERR_BUFFER: return "MPI_ERR_BUFFER: invalid buffer pointer";
+    case MPI_ERR_COUNT: return "MPI_ERR_COUNT: invalid count argument";
+    case MPI_ERR_TYPE: return "MPI_ERR_TYPE: invalid datatype";
+    case MPI_ERR_COMM: return "MPI_ERR_COMM: invalid communicator";
+    case MPI_ERR_ROOT: return "MPI_ERR_ROOT: invalid root";
+    case MPI_ERR_OP: return "MPI_ERR_OP: invalid reduce operation";
+    case MPI_ERR_ARG: return "MPI_ERR_ARG: invalid argument";
+    case MPI_ERR_TRUNCATE: return "MPI_ERR_TRUNCATE: message truncated";
+    case MPI_ERR_OTHER: return "MPI_ERR_OTHER: other error";
+    case MPI_ERR_INTERN: return "MPI_ERR_INTERN: internal error";
+    case MPI_ERR_NO_MEM: return "MPI_ERR_NO_MEM: out of memory";
+    case MPI_ERR_UNSUPPORTED_OPERATION: return "MPI_ERR_UNSUPPORTED_OPERATION: unsupported operation";
+    default: return "unknown error";
+    }
+}
+
+int comm_index(MPI_Comm c) {
+    if (c == MPI_COMM_WORLD) return 0;
+    if (c == MPI_COMM_SELF) return 1;
+    return -1;
+}
+
+// MPIR_Err_return_comm (allreduce.c:956): fatal handler aborts, return handler passes the code
+int err_return(MPI_Comm comm, int code, const char *fn) {
+    if (code == MPI_SUCCESS) return code;
+    const int ci = comm_index(comm);
+    const MPI_Errhandler eh = ci >= 0 ? g_eh[ci] : MPI_ERRORS_ARE_FATAL;
+    if (eh == MPI_ERRORS_ARE_FATAL) {
+        fprintf(stderr, "[mv2amd rank %d] Fatal error in %s: %s\n", world().rank, fn, err_name(code));
+        fflush(stderr);
+        abort();
+    }
+    return code;
+}
+
+UserOp *user_op(MPI_Op op) {
+    const unsigned idx = (unsigned)(op - kUserOpBase);
+    if ((op & 0xff000000) != (kUserOpBase & 0xff000000) || idx >= g_uops.size() || !g_uops[idx].live) return nullptr;
+    return &g_uops[idx];
+}
+
+bool op_valid(MPI_Op op) { return is_builtin_op(op) || user_op(op) != nullptr; }
+
+bool is_dev(const void *p) { return p && p != MPI_IN_PLACE && mv2h_is_device_ptr(p); }
+
+// ---- user-op path: user functions are host callbacks (the reference also
+// calls them on host copies of device buffers, reduce_local.c:54-164) ----
+int copy_to_host(std::vector<char> &h, const void *p, size_t bytes) {
+    h.resize(bytes ? bytes : 1);
+    if (is_dev(p)) return mv2h_memcpy_dtoh(h.data(), p, bytes);
+    memcpy(h.data(), p, bytes);
+    return 0;
+}
+int copy_from_host(void *p, const std::vector<char> &h, size_t bytes) {
+    if (is_dev(p)) return mv2h_memcpy_htod(p, h.data(), bytes);
+    memcpy(p, h.data(), bytes);
+    return 0;
+}
+
+int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, UserOp *u) {
+    long span = dtype_span(dt, count);
+    if (span < 0) return MPI_ERR_TYPE;
+    std::vector<char> hin, hio;
+    int rc = copy_to_host(hin, in, span);
+    if (!rc) rc = copy_to_host(hio, inout, span);
+    if (rc) return MPI_ERR_OTHER;
+    int c = count;
+    MPI_Datatype d = dt;
+    u->fn(hin.data(), hio.data(), &c, &d);
+    return copy_from_host(inout, hio, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+// Allreduce with a user op: gather every rank's operand, then apply the
+// reference's order on host: two-level linear chain for commutative ops
+// below 1 KB (allreduce_osu.c:1569-1583), recursive doubling otherwise
+// (pt2pt_rs falls back to RD for user ops, allreduce_osu.c:802;
+// operand order :824-845, non-pof2 fold :734-777).
+int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u) {
+    World &w = world();
+    const long span = dtype_span(dt, count);
+    if (span < 0) return MPI_ERR_TYPE;
+    const int n = w.size, me = w.rank;
+    const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+    std::vector<char> all((size_t)span * n + 1);
+    std::vector<char> mine;
+    if (copy_to_host(mine, src, span)) return MPI_ERR_OTHER;
+    if (n > 1) {
+        int rc = mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
+        if (rc) return rc;
+    } else {
+        memcpy(all.data(), mine.data(), span);
+    }
+    auto X = [&](int r) { return all.data() + (size_t)r * span; };
+    int c = count;
+    MPI_Datatype d = dt;
+    long tsize = dtype_size(dt);
+    std::vector<char> result((size_t)span + 1);
+    if (n == 1) {
+        memcpy(result.data(), X(0), span);
+    } else if (u->commute && (long)count * tsize < 1024) {
+        memcpy(result.data(), X(0), span);
+        for (int i = 1; i < n; ++i) u->fn(X(i), result.data(), &c, &d);
+    } else {
+        int pof2 = 1;
+        while (pof2 * 2 <= n) pof2 *= 2;
+        const int rem = n - pof2;
+        std::vector<std::vector<char>> rb(n, std::vector<char>((size_t)span + 1));
+        for (int r = 0; r < n; ++r) memcpy(rb[r].data(), X(r), span);
+        std::vector<int> newrank(n), real(pof2);
+        for (int r = 0; r < n; ++r) {
+            if (r < 2 * rem) {
+                if (r % 2 == 0) newrank[r] = -1;
+                else {
+                    u->fn(X(r - 1), rb[r].data(), &c, &d);
+                    newrank[r] = r / 2;
+                }
+            } else newrank[r] = r - rem;
+            if (newrank[r] >= 0) real[newrank[r]] = r;
+        }
+        for (int mask = 1; mask < pof2; mask <<= 1) {
+            std::vector<std::vector<char>> prev(pof2);
+            for (int nr = 0; nr < pof2; ++nr) prev[nr] = rb[real[nr]];
+            for (int nr = 0; nr < pof2; ++nr) {
+                const int r = real[nr], dst = real[nr ^ mask];
+                std::vector<char> tmp = prev[nr ^ mask];
+                if (u->commute || dst < r) {
+                    u->fn(tmp.data(), rb[r].data(), &c, &d);
+                } else {
+                    u->fn(rb[r].data(), tmp.data(), &c, &d);
+                    rb[r] = tmp;
+                }
+            }
+        }
+        for (int r = 0; r < 2 * rem; r += 2) rb[r] = rb[r + 1];
+        memcpy(result.data(), rb[me].data(), span);
+    }
+    return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+}  // namespace
+
+#define WEAK(name) __attribute__((weak, alias("P" #name)))
+
+extern "C" {
+
+// ---------------------------------------------------------------- environment
+int PMPI_Init(int *, char ***) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (g_initialized) return err_return(MPI_COMM_WORLD, MPI_ERR_OTHER, "MPI_Init");
+    int rc = world_init();
+    if (rc) return err_return(MPI_COMM_WORLD, rc, "MPI_Init");
+    g_initialized = true;
+    return MPI_SUCCESS;
+}
+int MPI_Init(int *argc, char ***argv) WEAK(MPI_Init);
+
+int PMPI_Init_thread(int *argc, char ***argv, int required, int *provided) {
+    int rc = PMPI_Init(argc, argv);
+    if (provided) *provided = required > MPI_THREAD_SERIALIZED ? MPI_THREAD_SERIALIZED : required;
+    return rc;
+}
+int MPI_Init_thread(int *argc, char ***argv, int required, int *provided) WEAK(MPI_Init_thread);
+
+int PMPI_Finalize(void) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    world_finalize();
+    g_finalized = true;
+    return MPI_SUCCESS;
+}
+int MPI_Finalize(void) WEAK(MPI_Finalize);
+
+int PMPI_Initialized(int *flag) {
+    *flag = g_initialized ? 1 : 0;
+    return MPI_SUCCESS;
+}
+int MPI_Initialized(int *flag) WEAK(MPI_Initialized);
+
+int PMPI_Finalized(int *flag) {
+    *flag = g_finalized ? 1 : 0;
+    return MPI_SUCCESS;
+}
+int MPI_Finalized(int *flag) WEAK(MPI_Finalized);
+
+int PMPI_Abort(MPI_Comm, int errorcode) {
+    fprintf(stderr, "[mv2amd rank %d] MPI_Abort(%d)\n", world().rank, errorcode);
+    fflush(stderr);
+    _exit(errorcode ? errorcode : 1);
+}
+int MPI_Abort(MPI_Comm comm, int errorcode) WEAK(MPI_Abort);
+
+double PMPI_Wtime(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+double MPI_Wtime(void) WEAK(MPI_Wtime);
+
+double PMPI_Wtick(void) { return 1e-9; }
+double MPI_Wtick(void) WEAK(MPI_Wtick);
+
+int PMPI_Get_processor_name(char *name, int *len) {
+    gethostname(name, MPI_MAX_PROCESSOR_NAME);
+    name[MPI_MAX_PROCESSOR_NAME - 1] = 0;
+    *len = (int)strlen(name);
+    return MPI_SUCCESS;
+}
+int MPI_Get_processor_name(char *name, int *len) WEAK(MPI_Get_processor_name);
+
+int PMPI_Error_string(int code, char *s, int *len) {
+    snprintf(s, MPI_MAX_ERROR_STRING, "%s", err_name(code));
+    *len = (int)strlen(s);
+    return MPI_SUCCESS;
+}
+int MPI_Error_string(int code, char *s, int *len) WEAK(MPI_Error_string);
+
+int PMPI_Error_class(int code, int *cls) {
+    *cls = code & 0x7f;
+    return MPI_SUCCESS;
+}
+int MPI_Error_class(int code, int *cls) WEAK(MPI_Error_class);
+
+int PMPI_Comm_set_errhandler(MPI_Comm comm, MPI_Errhandler eh) {
+    const int ci = comm_index(comm);
+    if (ci < 0) return MPI_ERR_COMM;
+    if (eh != MPI_ERRORS_ARE_FATAL && eh != MPI_ERRORS_RETURN) return MPI_ERR_ARG;
+    g_eh[ci] = eh;
+    return MPI_SUCCESS;
+}
+int MPI_Comm_set_errhandler(MPI_Comm comm, MPI_Errhandler eh) WEAK(MPI_Comm_set_errhandler);
+
+int PMPI_Errhandler_set(MPI_Comm comm, MPI_Errhandler eh) { return PMPI_Comm_set_errhandler(comm, eh); }
+int MPI_Errhandler_set(MPI_Comm comm, MPI_Errhandler eh) WEAK(MPI_Errhandler_set);
+
+int PMPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler *eh) {
+    const int ci = comm_index(comm);
+    if (ci < 0) return MPI_ERR_COMM;
+    *eh = g_eh[ci];
+    return MPI_SUCCESS;
+}
+int MPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler *eh) WEAK(MPI_Comm_get_errhandler);
+
+// ---------------------------------------------------------------- communicators
+int PMPI_Comm_rank(MPI_Comm comm, int *rank) {
+    const int ci = comm_index(comm);
+    if (ci < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPI_Comm_rank");
+    *rank = ci == 0 ? world().rank : 0;
+    return MPI_SUCCESS;
+}
+int MPI_Comm_rank(MPI_Comm comm, int *rank) WEAK(MPI_Comm_rank);
+
+int PMPI_Comm_size(MPI_Comm comm, int *size) {
+    const int ci = comm_index(comm);
+    if (ci < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPI_Comm_size");
+    *size = ci == 0 ? world().size : 1;
+    return MPI_SUCCESS;
+}
+int MPI_Comm_size(MPI_Comm comm, int *size) WEAK(MPI_Comm_size);
+
+int PMPI_Barrier(MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const int ci = comm_index(comm);
+    if (ci < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPI_Barrier");
+    if (ci == 0) host_barrier();
+    return MPI_SUCCESS;
+}
+int MPI_Barrier(MPI_Comm comm) WEAK(MPI_Barrier);
+
+// ---------------------------------------------------------------- user ops
+int PMPI_Op_create(MPI_User_function *fn, int commute, MPI_Op *op) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (!fn || !op) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Op_create");
+    g_uops.push_back(UserOp{fn, commute ? 1 : 0, true});
+    *op = kUserOpBase + (int)(g_uops.size() - 1);
+    return MPI_SUCCESS;
+}
+int MPI_Op_create(MPI_User_function *fn, int commute, MPI_Op *op) WEAK(MPI_Op_create);
+
+int PMPI_Op_free(MPI_Op *op) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    UserOp *u = op ? user_op(*op) : nullptr;
+    if (!u) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, "MPI_Op_free");
+    u->live = false;
+    *op = MPI_OP_NULL;
+    return MPI_SUCCESS;
+}
+int MPI_Op_free(MPI_Op *op) WEAK(MPI_Op_free);
+
+int PMPI_Op_commutative(MPI_Op op, int *commute) {
+    if (is_builtin_op(op)) {
+        *commute = 1;
+        return MPI_SUCCESS;
+    }
+    UserOp *u = user_op(op);
+    if (!u) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, "MPI_Op_commutative");
+    *commute = u->commute;
+    return MPI_SUCCESS;
+}
+int MPI_Op_commutative(MPI_Op op, int *commute) WEAK(MPI_Op_commutative);
+
+// ---------------------------------------------------------------- reductions
+int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype dt, MPI_Op op) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPI_Reduce_local";
+    if (count < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COUNT, fn);
+    if (!op_valid(op)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
+    if (!dtype_valid(dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_TYPE, fn);
+    if (count == 0) return MPI_SUCCESS;
+    if (inbuf == MPI_IN_PLACE || inoutbuf == MPI_IN_PLACE) return err_return(MPI_COMM_WORLD, MPI_ERR_BUFFER, fn);
+    if (UserOp *u = user_op(op)) return err_return(MPI_COMM_WORLD, user_reduce_local(inbuf, inoutbuf, count, dt, u), fn);
+    if (!dtype_is_builtin(dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
+    return err_return(MPI_COMM_WORLD, mv2h_reduce_local(inbuf, inoutbuf, (size_t)count, dt, op, nullptr), fn);
+}
+int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype dt, MPI_Op op) WEAK(MPI_Reduce_local);
+
+static int coll_checks(MPI_Comm comm, int count, MPI_Datatype dt, MPI_Op op) {
+    if (!g_initialized || g_finalized) return MPI_ERR_OTHER;
+    if (comm_index(comm) < 0) return MPI_ERR_COMM;
+    if (count < 0) return MPI_ERR_COUNT;
+    if (!dtype_valid(dt)) return MPI_ERR_TYPE;
+    if (!op_valid(op)) return MPI_ERR_OP;
+    if (is_builtin_op(op) && !dtype_is_builtin(dt)) return MPI_ERR_OP;  // e.g. opsum.c:119-121
+    if (is_builtin_op(op) && mv2h_op_check(op, dt)) return MPI_ERR_OP;
+    return MPI_SUCCESS;
+}
+
+int PMPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPI_Allreduce";
+    int rc = coll_checks(comm, count, dt, op);
+    if (rc) return err_return(comm, rc, fn);
+    if (count == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) {
+        if (sendbuf != MPI_IN_PLACE && sendbuf != recvbuf) {
+            const long span = dtype_span(dt, count);
+            rc = is_dev(recvbuf) || is_dev(sendbuf) ? mv2h_memcpy_dtod(recvbuf, sendbuf, span) : (memcpy(recvbuf, sendbuf, span), 0);
+        }
+        return err_return(comm, rc, fn);
+    }
+    if (UserOp *u = user_op(op)) return err_return(comm, user_allreduce(sendbuf, recvbuf, count, dt, u), fn);
+    rc = mv2h_allreduce(sendbuf, recvbuf, (size_t)count, dt, op, nullptr);
+    return err_return(comm, rc, fn);
+}
+int MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm) WEAK(MPI_Allreduce);
+
+int PMPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPI_Reduce";
+    int rc = coll_checks(comm, count, dt, op);
+    if (rc) return err_return(comm, rc, fn);
+    int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (count == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) {
+        if (sendbuf != MPI_IN_PLACE && sendbuf != recvbuf) {
+            const long span = dtype_span(dt, count);
+            rc = is_dev(recvbuf) || is_dev(sendbuf) ? mv2h_memcpy_dtod(recvbuf, sendbuf, span) : (memcpy(recvbuf, sendbuf, span), 0);
+        }
+        return err_return(comm, rc, fn);
+    }
+    if (UserOp *u = user_op(op)) {
+        // result needed only at root; every rank computes it (same order as allreduce)
+        std::vector<char> scratch;
+        void *dst = recvbuf;
+        if (world().rank != root) {
+            scratch.resize(dtype_span(dt, count) + 1);
+            dst = scratch.data();
+        }
+        return err_return(comm, user_allreduce(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, dst, count, dt, u), fn);
+    }
+    rc = mv2h_reduce(sendbuf, recvbuf, (size_t)count, dt, op, root, nullptr);
+    return err_return(comm, rc, fn);
+}
+int MPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm) WEAK(MPI_Reduce);
+
+int PMPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
+                        MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPI_Reduce_scatter";
+    int rc = coll_checks(comm, 0, dt, op);
+    if (rc) return err_return(comm, rc, fn);
+    const int n = comm == MPI_COMM_SELF ? 1 : world().size;
+    std::vector<size_t> rc_sz(n);
+    size_t total = 0;
+    for (int j = 0; j < n; ++j) {
+        if (recvcounts[j] < 0) return err_return(comm, MPI_ERR_COUNT, fn);
+        rc_sz[j] = (size_t)recvcounts[j];
+        total += rc_sz[j];
+    }
+    if (total == 0) return MPI_SUCCESS;
+    if (user_op(op)) return err_return(comm, MPI_ERR_UNSUPPORTED_OPERATION, fn);
+    if (comm == MPI_COMM_SELF) {
+        if (sendbuf != MPI_IN_PLACE)
+            rc = mv2h_memcpy_dtod(recvbuf, sendbuf, dtype_span(dt, recvcounts[0]));
+        return err_return(comm, rc, fn);
+    }
+    rc = mv2h_reduce_scatter(sendbuf, recvbuf, rc_sz.data(), dt, op, nullptr);
+    return err_return(comm, rc, fn);
+}
+int MPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
+                       MPI_Comm comm) WEAK(MPI_Reduce_scatter);
+
+int PMPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
+                              MPI_Comm comm) {
+    const int n = comm == MPI_COMM_SELF ? 1 : world().size;
+    std::vector<int> counts(n, recvcount);
+    return PMPI_Reduce_scatter(sendbuf, recvbuf, counts.data(), dt, op, comm);
+}
+int MPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
+                             MPI_Comm comm) WEAK(MPI_Reduce_scatter_block);
+
+int PMPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                   MPI_Datatype recvtype, MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPI_Allgather";
+    if (!g_initialized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
+    if (recvcount < 0 || (sendbuf != MPI_IN_PLACE && sendcount < 0)) return err_return(comm, MPI_ERR_COUNT, fn);
+    if (!dtype_valid(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_valid(sendtype)))
+        return err_return(comm, MPI_ERR_TYPE, fn);
+    if (!dtype_is_contiguous(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_is_contiguous(sendtype)))
+        return err_return(comm, MPI_ERR_UNSUPPORTED_OPERATION, fn);
+    const size_t rbytes = (size_t)dtype_span(recvtype, recvcount);
+    if (sendbuf != MPI_IN_PLACE && (size_t)dtype_span(sendtype, sendcount) != rbytes)
+        return err_return(comm, MPI_ERR_TRUNCATE, fn);
+    if (rbytes == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) {
+        int rc = sendbuf == MPI_IN_PLACE ? 0 : mv2h_memcpy_dtod(recvbuf, sendbuf, rbytes);
+        return err_return(comm, rc, fn);
+    }
+    return err_return(comm, mv2h_allgather(sendbuf, recvbuf, rbytes, nullptr), fn);
+}
+int MPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                  MPI_Datatype recvtype, MPI_Comm comm) WEAK(MPI_Allgather);
+
+int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPI_Bcast";
+    if (!g_initialized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
+    if (count < 0) return err_return(comm, MPI_ERR_COUNT, fn);
+    if (!dtype_valid(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
+    const int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (count == 0 || size == 1) return MPI_SUCCESS;
+    if (dtype_is_contiguous(dt)) return err_return(comm, mv2h_bcast(buffer, (size_t)dtype_span(dt, count), root, nullptr), fn);
+    // derived (non-contiguous) type: pack on device at the root, broadcast the
+    // packed bytes, unpack on device everywhere else
+    int psize = 0;
+    PMPI_Pack_size(count, dt, comm, &psize);
+    void *packed = nullptr;
+    if (mv2h_malloc(&packed, (size_t)psize)) return err_return(comm, MPI_ERR_NO_MEM, fn);
+    int pos = 0, rc = MPI_SUCCESS;
+    if (world().rank == root) rc = PMPI_Pack(buffer, count, dt, packed, psize, &pos, comm);
+    if (!rc) rc = mv2h_bcast(packed, (size_t)psize, root, nullptr);
+    pos = 0;
+    if (!rc && world().rank != root) rc = PMPI_Unpack(packed, psize, &pos, buffer, count, dt, comm);
+    mv2h_free(packed);
+    return err_return(comm, rc, fn);
+}
+int MPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm) WEAK(MPI_Bcast);
+
+}  // extern "C"

@@ -1,0 +1,291 @@
+// world.cpp — bootstrap of COMM_WORLD: rank discovery, /dev/shm control
+// segment, host barrier, device selection and the IPC-shared signal pages /
+// one-shot arenas.  (Replaces MPI_Init's MV2_Read_env_vars + shmem-coll
+// init + CUDA IPC region setup: reference init.c:186-300,
+// ch3_shmem_coll.c:1365-1455, ibv_cuda_ipc.c:400.)
+#include "world.h"
+
+#include <fcntl.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <thread>
+
+#include "log.h"
+
+namespace mv2 {
+
+static World g_world;
+World &world() { return g_world; }
+
+static int env_int(const char *const *names, int dflt) {
+    for (int i = 0; names[i]; ++i) {
+        const char *v = getenv(names[i]);
+        if (v && *v) return atoi(v);
+    }
+    return dflt;
+}
+
+static long env_long(const char *name, long dflt) {
+    const char *v = getenv(name);
+    return (v && *v) ? atol(v) : dflt;
+}
+
+// start time of the parent process (jiffies since boot): with the parent pid
+// it names one launch of one launcher (torchrun agent, mv2run, pytest)
+static unsigned long long parent_start_time(pid_t ppid) {
+    char path[64];
+    snprintf(path, sizeof(path), "/proc/%d/stat", (int)ppid);
+    FILE *f = fopen(path, "r");
+    if (!f) return 0;
+    char buf[1024];
+    size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')');
+    if (!p) return 0;
+    // fields after ')' start at field 3; starttime is field 22
+    int field = 2;
+    unsigned long long st = 0;
+    for (const char *q = p + 1; *q; ++q) {
+        if (*q == ' ') {
+            ++field;
+            if (field == 22) {
+                st = strtoull(q + 1, nullptr, 10);
+                break;
+            }
+        }
+    }
+    return st;
+}
+
+static std::string job_key() {
+    const char *j = getenv("MV2AMD_JOBID");
+    if (j && *j) return std::string(j);
+    pid_t pp = getppid();
+    char buf[128];
+    const char *port = getenv("MASTER_PORT");
+    snprintf(buf, sizeof(buf), "%d_%llu_%s", (int)pp, parent_start_time(pp), port ? port : "0");
+    return std::string(buf);
+}
+
+void host_barrier() {
+    World &w = g_world;
+    if (w.size == 1 || !w.shm) return;
+    const uint64_t g = ++w.bar_gen;
+    w.shm->r[w.rank].arrive.store(g, std::memory_order_release);
+    const auto t0 = std::chrono::steady_clock::now();
+    const double limit = (double)env_long("MV2AMD_TIMEOUT_S", 120);
+    for (int j = 0; j < w.size; ++j) {
+        unsigned spins = 0;
+        while (w.shm->r[j].arrive.load(std::memory_order_acquire) < g) {
+            if (++spins > 2000) {
+                sched_yield();
+                if ((spins & 0xfff) == 0) {
+                    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                    if (el > limit) MV2_FATAL("host barrier timed out after %.0f s waiting for rank %d", el, j);
+                }
+            }
+        }
+    }
+}
+
+void *get_scratch(int idx, size_t bytes) {
+    World &w = g_world;
+    if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];
+    if (w.scratch[idx]) {
+        hipStreamSynchronize(w.stream);
+        // evict this allocation from our own IPC handle cache before freeing
+        uint64_t bid = 0;
+        if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)w.scratch[idx]) == hipSuccess)
+            w.own_handles.erase(bid);
+        hipFree(w.scratch[idx]);
+        w.scratch[idx] = nullptr;
+        w.scratch_bytes[idx] = 0;
+    }
+    size_t sz = bytes < 4096 ? 4096 : bytes;
+    if (hipMalloc(&w.scratch[idx], sz) != hipSuccess) return nullptr;
+    w.scratch_bytes[idx] = sz;
+    return w.scratch[idx];
+}
+
+static int setup_device_common() {
+    World &w = g_world;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        MV2_ERR("no HIP device visible: this library runs its reduction path on MI355X only");
+        return E_OTHER;
+    }
+    const char *dn[] = {"MV2AMD_DEVICE", nullptr};
+    w.device = env_int(dn, w.local_rank % ndev);
+    if (hipSetDevice(w.device) != hipSuccess) return E_OTHER;
+    // blocking stream: orders after legacy null-stream work (buffer readiness)
+    if (hipStreamCreate(&w.stream) != hipSuccess) return E_OTHER;
+    if (hipHostMalloc((void **)&w.h_err, 64, hipHostMallocDefault) != hipSuccess) return E_OTHER;
+    memset(w.h_err, 0, 64);
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, w.device) == hipSuccess && khz > 0)
+        w.wall_clock_khz = khz;
+    w.timeout_ticks = (uint64_t)(env_long("MV2AMD_TIMEOUT_S", 120) * w.wall_clock_khz * 1000.0);
+    w.oneshot_max = (size_t)env_long("MV2AMD_ONESHOT_MAX", (long)w.oneshot_max);
+    w.max_grid = (int)env_long("MV2AMD_MAX_GRID", w.max_grid);
+    w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
+    hipEventCreate(&w.ev0);
+    hipEventCreate(&w.ev1);
+    return 0;
+}
+
+int ensure_init_for_device() {
+    World &w = g_world;
+    if (w.stream) return 0;
+    return setup_device_common();
+}
+
+int world_init() {
+    World &w = g_world;
+    if (w.inited) return 0;
+    const char *rn[] = {"MV2_COMM_WORLD_RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "RANK", nullptr};
+    const char *sn[] = {"MV2_COMM_WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "WORLD_SIZE", nullptr};
+    const char *ln[] = {"MV2_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", nullptr};
+    const char *lsn[] = {"MV2_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "OMPI_COMM_WORLD_LOCAL_SIZE", "LOCAL_WORLD_SIZE", nullptr};
+    w.rank = env_int(rn, 0);
+    w.size = env_int(sn, 1);
+    w.local_rank = env_int(ln, w.rank);
+    const int lsize = env_int(lsn, w.size);
+    if (w.size < 1 || w.rank < 0 || w.rank >= w.size) {
+        MV2_ERR("invalid rank/size from environment: rank=%d size=%d", w.rank, w.size);
+        return E_OTHER;
+    }
+    if (lsize != w.size) {
+        MV2_ERR("multi-node launch (local size %d != world size %d) is not supported yet", lsize, w.size);
+        return E_UNSUPPORTED;
+    }
+    if (w.size > kShmMaxRanks) {
+        MV2_ERR("world size %d exceeds %d", w.size, kShmMaxRanks);
+        return E_UNSUPPORTED;
+    }
+    // MV2AMD_CONTROL_PLANE_ONLY=1: bootstrap the shm control plane without a
+    // GPU (CPU tests of rank discovery / barriers).  Every data-path entry
+    // point still requires the device and fails loudly without it.
+    const char *cpo = getenv("MV2AMD_CONTROL_PLANE_ONLY");
+    const bool control_only = cpo && *cpo == '1';
+    if (!w.stream && !control_only) {
+        int rc = setup_device_common();
+        if (rc) return rc;
+    }
+
+    if (w.size > 1) {
+        w.shm_name = "/mv2amd." + job_key();
+        int fd = shm_open(w.shm_name.c_str(), O_CREAT | O_RDWR, 0600);
+        if (fd < 0) {
+            MV2_ERR("shm_open(%s) failed", w.shm_name.c_str());
+            return E_OTHER;
+        }
+        if (ftruncate(fd, sizeof(ShmSeg)) != 0) {
+            close(fd);
+            return E_OTHER;
+        }
+        void *p = mmap(nullptr, sizeof(ShmSeg), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) return E_OTHER;
+        w.shm = (ShmSeg *)p;
+        ShmRank &me = w.shm->r[w.rank];
+        me.pid = getpid();
+        me.device = w.device;
+        if (!control_only) {
+            hipDeviceGetAttribute(&me.pci_bus, hipDeviceAttributePciBusId, w.device);
+            hipDeviceGetAttribute(&me.pci_device, hipDeviceAttributePciDeviceId, w.device);
+        }
+        w.shm->attached.fetch_add(1);
+        host_barrier();  // everyone attached and published pid/device
+
+        // ranks sharing this GPU (tests run several ranks on one device)
+        w.nshare = 0;
+        for (int j = 0; j < w.size; ++j)
+            if (w.shm->r[j].pci_bus == me.pci_bus && w.shm->r[j].pci_device == me.pci_device) ++w.nshare;
+
+        if (w.size <= kMaxRanks && !control_only) {
+            // signal page + one-shot arena, IPC-exported
+            const size_t sig_bytes = (size_t)kMaxRanks * kMaxBlocks * sizeof(uint64_t);
+            if (hipExtMallocWithFlags((void **)&w.sig, sig_bytes, hipDeviceMallocUncached) != hipSuccess) {
+                MV2_ERR("hipExtMallocWithFlags(uncached) for the signal page failed");
+                return E_NO_MEM;
+            }
+            hipMemset(w.sig, 0, sig_bytes);
+            w.slot_bytes = (w.oneshot_max + 4095) & ~(size_t)4095;
+            const size_t arena_bytes = 2 * (size_t)kMaxRanks * w.slot_bytes;
+            if (hipExtMallocWithFlags((void **)&w.arena, arena_bytes, hipDeviceMallocUncached) != hipSuccess) {
+                MV2_ERR("hipExtMallocWithFlags(uncached) for the one-shot arena failed");
+                return E_NO_MEM;
+            }
+            hipDeviceSynchronize();
+            if (hipIpcGetMemHandle(&me.sig_handle, w.sig) != hipSuccess ||
+                hipIpcGetMemHandle(&me.arena_handle, w.arena) != hipSuccess) {
+                MV2_ERR("hipIpcGetMemHandle failed for the signal page / arena");
+                return E_OTHER;
+            }
+            me.arena_bytes = arena_bytes;
+            me.slot_bytes = w.slot_bytes;
+            host_barrier();
+            for (int j = 0; j < w.size; ++j) {
+                if (j == w.rank) {
+                    w.peer_sig.p[j] = w.sig;
+                    w.peer_arena[j] = w.arena;
+                    continue;
+                }
+                if (w.shm->r[j].slot_bytes != w.slot_bytes) {
+                    MV2_ERR("MV2AMD_ONESHOT_MAX differs between ranks");
+                    return E_OTHER;
+                }
+                void *ps = nullptr, *pa = nullptr;
+                if (hipIpcOpenMemHandle(&ps, w.shm->r[j].sig_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                    hipIpcOpenMemHandle(&pa, w.shm->r[j].arena_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    MV2_ERR("hipIpcOpenMemHandle failed for rank %d (peer access over xGMI?)", j);
+                    return E_OTHER;
+                }
+                w.peer_sig.p[j] = (uint64_t *)ps;
+                w.peer_arena[j] = (char *)pa;
+            }
+            host_barrier();
+        }
+    }
+    w.inited = true;
+    MV2_DEBUG("init rank %d/%d local %d device %d nshare %d", w.rank, w.size, w.local_rank, w.device, w.nshare);
+    return 0;
+}
+
+int world_finalize() {
+    World &w = g_world;
+    if (!w.inited || w.finalized) return 0;
+    if (w.stream) hipStreamSynchronize(w.stream);
+    if (w.size > 1 && w.shm) {
+        host_barrier();
+        for (int j = 0; j < kMaxRanks; ++j) {
+            for (auto &kv : w.peer_maps[j]) hipIpcCloseMemHandle(kv.second.ptr);
+            w.peer_maps[j].clear();
+            if (j != w.rank && j < w.size && w.size <= kMaxRanks) {
+                if (w.peer_sig.p[j]) hipIpcCloseMemHandle(w.peer_sig.p[j]);
+                if (w.peer_arena[j]) hipIpcCloseMemHandle(w.peer_arena[j]);
+            }
+        }
+        host_barrier();  // nobody maps our pages any more
+        if (w.rank == 0) shm_unlink(w.shm_name.c_str());
+        munmap(w.shm, sizeof(ShmSeg));
+        w.shm = nullptr;
+    }
+    for (int i = 0; i < 3; ++i)
+        if (w.scratch[i]) hipFree(w.scratch[i]);
+    if (w.sig) hipFree(w.sig);
+    if (w.arena) hipFree(w.arena);
+    w.finalized = true;
+    return 0;
+}
+
+}  // namespace mv2

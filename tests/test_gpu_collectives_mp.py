@@ -1,0 +1,196 @@
+"""Part (2) parity: the device collectives, one process per rank, several
+ranks sharing the test box's single GPU (peer buffers mapped through hipIpc
+exactly as across GPUs).  Results are compared bit-exactly with the oracle's
+simulation of the reference's algorithm for the same selection."""
+import json
+import os
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+from mvapich2_amd.consts import DEVICE_UNSUPPORTED, OPS, TYPES
+from oracle import oracle
+from tests.helpers import as_bytes, assert_bytes_equal, rand_typed
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def inputs(case, rank):
+    rng = np.random.default_rng(case["seed"] * 1000 + rank)
+    return rand_typed(case["type"], case["count"], rng, small=case.get("small", False))
+
+
+def run_workers(n, cases, tmp_path, timeout=400):
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"cases": cases}))
+    out = tmp_path / "out"
+    out.mkdir()
+    jobid = "g" + uuid.uuid4().hex[:12]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="60", MV2AMD_DEVICE="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), str(spec),
+                                       str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            logs.append(o.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
+    return lambda cid, r: np.load(out / f"{cid}_r{r}.npy")
+
+
+def expected_allreduce(case, n):
+    sends = [inputs(case, r) for r in range(n)]
+    return oracle.allreduce([s.copy() for s in sends], case["count"], TYPES[case["type"]][0], OPS[case["op"]])
+
+
+BASIC = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_FLOAT"), ("MPI_MIN", "MPI_DOUBLE"),
+         ("MPI_SUM", "MPI_INT"), ("MPI_PROD", "MPI_INT"), ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_LAND", "MPI_C_BOOL"),
+         ("MPI_MAXLOC", "MPI_DOUBLE_INT"), ("MPI_MINLOC", "MPI_2INT"), ("MPI_SUM", "MPI_C_FLOAT_COMPLEX"),
+         ("MPI_MAXLOC", "MPI_SHORT_INT")]
+COUNTS = [1, 3, 100, 4099, 70001, 300007]  # one-shot (<=256 KiB) and two-shot sizes, ragged tails
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_collectives_multiprocess(n, tmp_path, golden):
+    cases = []
+    seed = 1
+    for op, t in BASIC:
+        for count in COUNTS:
+            if t in ("MPI_SHORT_INT", "MPI_C_FLOAT_COMPLEX") and count > 5000:
+                continue
+            cases.append({"id": f"ar{seed}", "kind": "allreduce", "type": t, "op": op, "count": count,
+                          "seed": seed, "small": op == "MPI_PROD"})
+            seed += 1
+    for count in (10, 70001, 300007):
+        cases.append({"id": f"ip{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
+                      "count": count, "seed": seed})
+        seed += 1
+    cases.append({"id": f"rd{seed}", "kind": "reduce", "type": "MPI_DOUBLE", "op": "MPI_SUM", "count": 5000,
+                  "seed": seed, "root": n - 1})
+    seed += 1
+    for counts in ([1] * n, [1000 + r for r in range(n)], [70001] * n, [0] + [33] * (n - 1)):
+        cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
+                      "recvcounts": counts, "count": sum(counts), "seed": seed})
+        seed += 1
+    for count in (1, 13, 4096, 1 << 20):
+        cases.append({"id": f"ag{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": count,
+                      "seed": seed})
+        seed += 1
+    for count in (1, 1000, 1 << 20):
+        cases.append({"id": f"bc{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": 1 % n})
+        seed += 1
+    for commute in (0, 1):
+        for count in (10, 1000):
+            cases.append({"id": f"uo{seed}", "kind": "user_allreduce", "count": count, "commute": commute,
+                          "seed": seed, "type": "MPI_INT", "op": "MPI_SUM"})
+            seed += 1
+    cases.append({"id": f"vb{seed}", "kind": "vector_bcast", "nblocks": 1000, "root": 0, "count": 8000,
+                  "seed": seed, "type": "MPI_FLOAT", "op": "MPI_SUM"})
+    seed += 1
+    gcases, arrs = golden
+    for c in gcases:
+        if c["family"] == "allred" and c["n"] == n and c["type"] not in DEVICE_UNSUPPORTED:
+            cases.append({"id": f"gd{seed}", "kind": "allreduce", "type": c["type"], "op": c["op"],
+                          "count": c["count"], "seed": seed, "golden": c["id"]})
+            seed += 1
+
+    res = run_workers(n, cases, tmp_path)
+
+    for case in cases:
+        k, cid, t = case["kind"], case["id"], case.get("type")
+        if k in ("allreduce", "allreduce_inplace") and "golden" in case:
+            sol = arrs[case["golden"] + "__sol"]
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), sol, t, case["count"], f"{cid} {case['golden']} rank {r}")
+        elif k in ("allreduce", "allreduce_inplace"):
+            want = expected_allreduce(case, n)
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {case['op']} n={n} rank {r}")
+        elif k == "reduce":
+            want = expected_allreduce(case, n)
+            root = case["root"]
+            assert_bytes_equal(res(cid, root), want[root], t, case["count"], f"{cid} reduce")
+        elif k == "reduce_scatter":
+            counts = case["recvcounts"]
+            sends = [inputs(dict(case, count=sum(counts)), r) for r in range(n)]
+            full = oracle.reduce_linear(sends, sum(counts), TYPES[t][0], OPS[case["op"]]).view(np.int32)
+            off = 0
+            for r in range(n):
+                got = res(cid, r).view(np.int32)
+                assert np.array_equal(got, full[off:off + counts[r]]), (cid, r)
+                off += counts[r]
+        elif k == "allgather":
+            want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        elif k == "bcast":
+            want = as_bytes(inputs(case, case["root"]))
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        elif k == "user_allreduce":
+            want = user_allreduce_expected(n, case["count"], case["commute"])
+            for r in range(n):
+                assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
+        elif k == "vector_bcast":
+            nb = case["nblocks"]
+            src = np.arange(nb * 8, dtype=np.float32).reshape(nb, 8)
+            for r in range(n):
+                got = res(cid, r).view(np.float32).reshape(nb, 8)
+                assert np.array_equal(got[:, :4], src[:, :4]), (cid, r)
+                if r != case["root"]:
+                    assert np.all(got[:, 4:] == -1.0), "gap bytes of a vector type must not be written"
+
+
+def user_allreduce_expected(n, count, commute):
+    """Reference order for user ops (allreduce_osu.c): commutative & < 1 KB ->
+    two-level chain fn(x_i, acc); else recursive doubling with the
+    dst < rank operand swap (:824-845) and the non-pof2 fold (:734-777)."""
+    def fn(inp, io):
+        return (inp * 2 + io * 3).astype(np.int32)
+    xs = [((np.arange(count) + r) % 7).astype(np.int32) for r in range(n)]
+    if commute and count * 4 < 1024:
+        acc = xs[0].copy()
+        for i in range(1, n):
+            acc = fn(xs[i], acc)
+        return [acc] * n
+    pof2 = 1
+    while pof2 * 2 <= n:
+        pof2 *= 2
+    rem = n - pof2
+    rb = [x.copy() for x in xs]
+    newrank, real = [0] * n, [0] * pof2
+    for r in range(n):
+        if r < 2 * rem:
+            if r % 2 == 0:
+                newrank[r] = -1
+            else:
+                rb[r] = fn(xs[r - 1], rb[r])
+                newrank[r] = r // 2
+        else:
+            newrank[r] = r - rem
+        if newrank[r] >= 0:
+            real[newrank[r]] = r
+    mask = 1
+    while mask < pof2:
+        prev = [rb[real[nr]].copy() for nr in range(pof2)]
+        for nr in range(pof2):
+            r, dst = real[nr], real[nr ^ mask]
+            tmp = prev[nr ^ mask]
+            rb[r] = fn(tmp, rb[r]) if (commute or dst < r) else fn(rb[r], tmp)
+        mask <<= 1
+    for r in range(0, 2 * rem, 2):
+        rb[r] = rb[r + 1]
+    return rb

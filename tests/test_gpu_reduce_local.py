@@ -1,0 +1,128 @@
+"""Part (1) parity: MPI_Reduce_local / mv2h_reduce_local on device buffers vs
+the oracle, bit-exact for every (op, type) pair the reference accepts."""
+import numpy as np
+import pytest
+
+import mvapich2_amd as m
+from mvapich2_amd.consts import DEVICE_UNSUPPORTED, OPS, TYPES, legal_pairs
+from oracle import oracle
+from tests.helpers import as_bytes, assert_bytes_equal, rand_typed
+
+pytestmark = pytest.mark.gpu
+PAIRS = [(op, t) for op, t in legal_pairs() if t not in DEVICE_UNSUPPORTED]
+
+
+def run_rl(tname, op, x, y, count, off=0):
+    """device: y <- op(y, x) with both operands shifted by `off` elements."""
+    ext = TYPES[tname][3]
+    a = m.DeviceBuffer((count + off) * ext)
+    b = m.DeviceBuffer((count + off) * ext)
+    a.upload(x, off * ext)
+    b.upload(y, off * ext)
+    rc = m.lib().MPI_Reduce_local(a.ptr + off * ext, b.ptr + off * ext, count, TYPES[tname][0], OPS[op])
+    assert rc == 0, (tname, op, rc)
+    return b.download(np.uint8, count=count * ext, offset=off * ext)
+
+
+@pytest.mark.parametrize("count", [1, 7, 1000, 4099])
+def test_all_pairs_bit_exact(count):
+    rng = np.random.default_rng(count)
+    for op, t in PAIRS:
+        small = op == "MPI_PROD"
+        x = rand_typed(t, count, rng, small=small)
+        y = rand_typed(t, count, rng, small=small)
+        want = y.copy()
+        assert oracle.reduce_local(x, want, count, TYPES[t][0], OPS[op]) == 0
+        for off in (0, 1):
+            got = run_rl(t, op, x, y, count, off)
+            assert_bytes_equal(got, want, t, count, f"{op} off={off}")
+
+
+def test_reduce_local_c_known_answers(golden):
+    cases, arrs = golden
+    for c in cases:
+        if c["family"] != "reduce_local":
+            continue
+        ins = arrs[c["id"] + "__in"]
+        sol = arrs[c["id"] + "__sol"]
+        if c["count"] == 0:
+            continue
+        got = run_rl("MPI_INT", "MPI_SUM", ins[0].view(np.int32), ins[1].view(np.int32), c["count"])
+        assert np.array_equal(got, sol), c["id"]
+
+
+def test_count_zero_and_replace_no_op():
+    L = m.lib()
+    a = m.DeviceBuffer.from_array(np.arange(16, dtype=np.int32))
+    b = m.DeviceBuffer.from_array(np.full(16, 7, dtype=np.int32))
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 0, TYPES["MPI_INT"][0], OPS["MPI_SUM"]) == 0
+    assert np.all(b.download(np.int32) == 7)
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 16, TYPES["MPI_INT"][0], OPS["MPI_NO_OP"]) == 0
+    assert np.all(b.download(np.int32) == 7)
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 16, TYPES["MPI_INT"][0], OPS["MPI_REPLACE"]) == 0
+    assert np.array_equal(b.download(np.int32), np.arange(16))
+
+
+def test_errors_are_mpi_classes():
+    L = m.lib()
+    L.MPI_Comm_set_errhandler(0x44000000, 0x54000001)  # MPI_ERRORS_RETURN
+    a = m.DeviceBuffer(64)
+    b = m.DeviceBuffer(64)
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, TYPES["MPI_FLOAT"][0], OPS["MPI_BAND"]) == 9  # MPI_ERR_OP
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, TYPES["MPI_INT"][0], OPS["MPI_MAXLOC"]) == 9
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, 0x1234, OPS["MPI_SUM"]) == 3    # MPI_ERR_TYPE
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, -1, TYPES["MPI_INT"][0], OPS["MPI_SUM"]) == 2
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 1, TYPES["MPI_LONG_DOUBLE"][0], OPS["MPI_SUM"]) == 3
+
+
+def test_host_buffers_are_reduced_on_the_gpu():
+    x = np.arange(1000, dtype=np.float64)
+    y = np.ones(1000, dtype=np.float64)
+    assert m.lib().MPI_Reduce_local(x.ctypes.data, y.ctypes.data, 1000, TYPES["MPI_DOUBLE"][0], OPS["MPI_SUM"]) == 0
+    assert np.array_equal(y, np.arange(1000) + 1.0)
+
+
+def test_user_op_non_commutative():
+    """reduce_local.c user_op: inout = 2*in + inout (non-commutative), device buffers."""
+    import ctypes
+    L = m.lib()
+    FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+
+    def uop(inp, io, ln, dt):
+        n = ln[0]
+        a = np.ctypeslib.as_array((ctypes.c_int * n).from_address(inp))
+        b = np.ctypeslib.as_array((ctypes.c_int * n).from_address(io))
+        b[:] = a * 2 + b
+    cb = FN(uop)
+    op = ctypes.c_int()
+    assert L.MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), 0, ctypes.byref(op)) == 0
+    count = 1
+    while count < 65000:
+        i = np.arange(count, dtype=np.int32)
+        a, b = m.DeviceBuffer.from_array(i), m.DeviceBuffer.from_array(i)
+        assert L.MPI_Reduce_local(a.ptr, b.ptr, count, TYPES["MPI_INT"][0], op.value) == 0
+        assert np.array_equal(b.download(np.int32), 3 * i)
+        count *= 2
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0
+
+
+@pytest.mark.parametrize("tname,op", [("MPI_FLOAT", "MPI_SUM"), ("MPI_FLOAT", "MPI_MAX"), ("MPI_INT", "MPI_SUM"),
+                                      ("MPI_DOUBLE", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX")])
+def test_full_size_256MiB(tname, op):
+    """BASELINE config 2 sizes: each output element is one IEEE op / one integer
+    op, so numpy's elementwise result is the exact expected value."""
+    dt = m.np_dtype(tname)
+    count = 256 * 1024 * 1024 // dt.itemsize
+    rng = np.random.default_rng(0x5EED)
+    if dt.kind == "f":
+        x = rng.uniform(-1, 1, count).astype(dt)
+        y = rng.uniform(-1, 1, count).astype(dt)
+    else:
+        x = rng.integers(-(2**31), 2**31 - 1, count, dtype=np.int64).astype(dt)
+        y = rng.integers(-(2**31), 2**31 - 1, count, dtype=np.int64).astype(dt)
+    a, b = m.DeviceBuffer.from_array(x), m.DeviceBuffer.from_array(y)
+    assert m.lib().MPI_Reduce_local(a.ptr, b.ptr, count, TYPES[tname][0], OPS[op]) == 0
+    got = b.download(dt)
+    with np.errstate(over="ignore"):
+        want = (x + y) if op == "MPI_SUM" else np.maximum(x, y)
+    assert np.array_equal(got, want)
