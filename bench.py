@@ -49,10 +49,11 @@ def cpu_info():
 
 def cpu_baseline_reduce_local(seconds=10.0):
     """Oracle restatement of the reference host op loop (opsum.c via
-    MPIR_OP_TYPE_REDUCE_CASE), single core, on a 64 MiB fp32 sample repeated
-    for ~`seconds`.  Rate in the metric's unit: 3*S algorithmic bytes / t."""
+    MPIR_OP_TYPE_REDUCE_CASE), single core, on the full 256 MiB fp32 operands
+    (larger than the host L3) repeated for ~`seconds`.  Rate in the metric's
+    unit: 3*S algorithmic bytes / t."""
     from oracle import oracle
-    n = 16 * 1024 * 1024
+    n = 64 * 1024 * 1024
     a = np.random.default_rng(1).standard_normal(n).astype(np.float32)
     b = np.random.default_rng(2).standard_normal(n).astype(np.float32)
     L = oracle.lib()
@@ -61,7 +62,7 @@ def cpu_baseline_reduce_local(seconds=10.0):
     t = L.oracle_time_reduce_local(a.ctypes.data, b.ctypes.data, n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], reps)
     gbs = 3.0 * n * 4 * reps / t / 1e9
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"oracle reduce_local fp32 SUM, 64 MiB host buffers x {reps} reps ({t:.1f} s), "
+            "sample": f"oracle reduce_local fp32 SUM, 256 MiB host operands x {reps} reps ({t:.1f} s), "
                       f"1 core of '{cpu_info()}'; reference device path adds D2H 2S + H2D S over PCIe"}
 
 

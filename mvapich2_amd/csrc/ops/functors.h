@@ -77,11 +77,33 @@ template <typename T> __device__ __forceinline__ T wmul(T a, T b) {
     return (T)(U)((W)(U)a * (W)(U)b);
 }
 
+// ---- x86-64 SSE NaN semantics for the reference's fp arithmetic ----
+// A NaN result of `a op b` on x86 SSE (the reference's host loops, gcc -O2)
+// is the first operand's NaN quieted if a is NaN, else b's NaN quieted,
+// else the x86 default NaN (sign bit set).  gfx950 returns its own
+// canonical NaN, so the result is rewritten bit-exactly.
+template <typename F> struct FBits;
+template <> struct FBits<float> { using U = uint32_t; static constexpr U quiet = 0x00400000u, dflt = 0xFFC00000u; };
+template <> struct FBits<double> { using U = uint64_t; static constexpr U quiet = 0x0008000000000000ull, dflt = 0xFFF8000000000000ull; };
+
+template <typename F> __device__ __forceinline__ F x86_nan(F r, F a, F b) {
+    using B = FBits<F>;
+    if (!__builtin_isnan(r)) return r;
+    typename B::U u;
+    if (__builtin_isnan(a)) u = __builtin_bit_cast(typename B::U, a) | B::quiet;
+    else if (__builtin_isnan(b)) u = __builtin_bit_cast(typename B::U, b) | B::quiet;
+    else u = B::dflt;
+    return __builtin_bit_cast(F, u);
+}
+template <typename F> __device__ __forceinline__ F fadd(F a, F b) { return x86_nan<F>(a + b, a, b); }
+template <typename F> __device__ __forceinline__ F fsub(F a, F b) { return x86_nan<F>(a - b, a, b); }
+template <typename F> __device__ __forceinline__ F fmul(F a, F b) { return x86_nan<F>(a * b, a, b); }
+
 // C99 Annex G complex multiply (the libgcc __mulsc3 / __muldc3 algorithm)
 template <typename F> __device__ __forceinline__ void annexg_mul(F a, F b, F c, F d, F &x, F &y) {
-    F ac = a * c, bd = b * d, ad = a * d, bc = b * c;
-    x = ac - bd;
-    y = ad + bc;
+    F ac = fmul(a, c), bd = fmul(b, d), ad = fmul(a, d), bc = fmul(b, c);
+    x = fsub(ac, bd);
+    y = fadd(ad, bc);
     if (__builtin_isnan(x) && __builtin_isnan(y)) {
         bool recalc = false;
         if (__builtin_isinf(a) || __builtin_isinf(b)) {
@@ -107,8 +129,8 @@ template <typename F> __device__ __forceinline__ void annexg_mul(F a, F b, F c, 
         }
         if (recalc) {
             const F inf = (F)__builtin_inf();
-            x = inf * (a * c - b * d);
-            y = inf * (a * d + b * c);
+            x = fmul(inf, fsub(fmul(a, c), fmul(b, d)));
+            y = fmul(inf, fadd(fmul(a, d), fmul(b, c)));
         }
     }
 }
@@ -125,9 +147,9 @@ struct R<OP, K, typename std::enable_if<is_scalar_kind<K>()>::type> {
     using T = typename KT<K>::T;
     static __device__ __forceinline__ T apply(T a, T b) {
         if constexpr (OP == OP_SUM) {
-            if constexpr (is_int_kind<K>()) return wadd(a, b); else return a + b;
+            if constexpr (is_int_kind<K>()) return wadd(a, b); else return fadd(a, b);
         } else if constexpr (OP == OP_PROD) {
-            if constexpr (is_int_kind<K>()) return wmul(a, b); else return a * b;
+            if constexpr (is_int_kind<K>()) return wmul(a, b); else return fmul(a, b);
         } else if constexpr (OP == OP_MAX) {
             return mpir_max(a, b);
         } else if constexpr (OP == OP_MIN) {
@@ -157,13 +179,13 @@ struct R<OP, K, typename std::enable_if<(K >= K_CF32_C99 && K <= K_CF64_S)>::typ
     static __device__ __forceinline__ T apply(T a, T b) {
         T r;
         if constexpr (OP == OP_SUM) {
-            r.re = a.re + b.re;
-            r.im = a.im + b.im;
+            r.re = fadd(a.re, b.re);
+            r.im = fadd(a.im, b.im);
         } else if constexpr (OP == OP_PROD) {
             if constexpr (K == K_CF32_S || K == K_CF64_S) {
                 // opprod.c:50-51: c = a; re = c.re*b.re - c.im*b.im; im = c.im*b.re + c.re*b.im
-                r.re = a.re * b.re - a.im * b.im;
-                r.im = a.im * b.re + a.re * b.im;
+                r.re = fsub(fmul(a.re, b.re), fmul(a.im, b.im));
+                r.im = fadd(fmul(a.im, b.re), fmul(a.re, b.im));
             } else {
                 annexg_mul(a.re, a.im, b.re, b.im, r.re, r.im);
             }

@@ -31,6 +31,8 @@ def np_dtype(type_name):
 def rand_typed(type_name, count, rng, edges=True, small=False):
     """Seeded random operand of `count` elements (as a byte-backed numpy array)."""
     dt = np_dtype(type_name)
+    if type_name == "MPI_C_BOOL":  # _Bool objects hold only 0 / 1 (other bytes are UB in C)
+        return rng.integers(0, 2, count).astype(dt)
     if dt.names:
         x = np.zeros(count, dtype=dt)
         vt = dt["value"]
@@ -49,15 +51,20 @@ def rand_typed(type_name, count, rng, edges=True, small=False):
         im = rng.standard_normal(count)
         x = (re + 1j * im).astype(dt)
         if edges and count >= 8:
-            x[:6] = [complex(np.inf, np.nan), complex(np.nan, np.inf), complex(np.nan, np.nan),
-                     complex(0.0, -0.0), complex(np.inf, 0.0), complex(1e38, 1e38)]
+            e = np.array([complex(np.inf, np.nan), complex(np.nan, np.inf), complex(np.nan, np.nan),
+                          complex(0.0, -0.0), complex(np.inf, 0.0), complex(1e38, 1e38)], dtype=dt)
+            x[:6] = e[rng.permutation(6)]
         return x
     if dt.kind == "f":
         x = rng.standard_normal(count).astype(dt)
         if small:
             x = np.floor(rng.uniform(-4, 4, count)).astype(dt)
         if edges and count >= len(EDGE_F):
-            x[: len(EDGE_F)] = np.array(EDGE_F, dtype=dt)
+            e = np.array(EDGE_F, dtype=dt)
+            if dt.itemsize == 4:  # NaNs with distinct payloads / signs
+                e[0] = np.array([0x7FC00011], dtype=np.uint32).view(np.float32)[0]
+                e[1] = np.array([0xFFA00022], dtype=np.uint32).view(np.float32)[0]  # signalling
+            x[: len(EDGE_F)] = e[rng.permutation(len(EDGE_F))]
             if dt.itemsize >= 4 and count > 12:
                 x[8] = np.finfo(dt).tiny / 4  # denormal
                 x[9] = -np.finfo(dt).tiny / 8
