@@ -1,0 +1,116 @@
+// rl_variants.hip — micro-benchmark of Reduce_local (fp32 SUM, 256 MiB)
+// kernel shapes on one MI355X, to pick the product kernel's configuration.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/rl_variants.hip -o tools/rl_variants
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+template <int U, bool LNT, bool SNT, int T>
+__global__ __launch_bounds__(T) void k_rl(const v4f *__restrict__ in, v4f *__restrict__ io, size_t nvec) {
+    const size_t stride = (size_t)gridDim.x * T * U;
+    for (size_t base = (size_t)blockIdx.x * T * U + threadIdx.x; base < nvec; base += stride) {
+        v4f a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * T;
+            if (i < nvec) {
+                if (LNT) {
+                    a[u] = __builtin_nontemporal_load(&io[i]);
+                    b[u] = __builtin_nontemporal_load(&in[i]);
+                } else {
+                    a[u] = io[i];
+                    b[u] = in[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * T;
+            if (i < nvec) {
+                v4f r = a[u] + b[u];
+                if (SNT) __builtin_nontemporal_store(r, &io[i]);
+                else io[i] = r;
+            }
+        }
+    }
+}
+
+// pure copy (1 read + 1 write stream): the bandwidth ceiling reference
+template <int U, int T>
+__global__ __launch_bounds__(T) void k_copy(const v4f *__restrict__ in, v4f *__restrict__ out, size_t nvec) {
+    const size_t stride = (size_t)gridDim.x * T * U;
+    for (size_t base = (size_t)blockIdx.x * T * U + threadIdx.x; base < nvec; base += stride) {
+        v4f a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * T;
+            if (i < nvec) a[u] = in[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * T;
+            if (i < nvec) __builtin_nontemporal_store(a[u], &out[i]);
+        }
+    }
+}
+
+template <class F>
+static float timeit(F f, int iters) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    std::vector<float> v;
+    for (int i = 0; i < 3; ++i) f();
+    for (int i = 0; i < iters; ++i) {
+        hipEventRecord(e0);
+        f();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        v.push_back(ms);
+    }
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+int main() {
+    const size_t S = 256ull << 20, nvec = S / 16;
+    v4f *a, *b, *c;
+    hipMalloc(&a, S);
+    hipMalloc(&b, S);
+    hipMalloc(&c, S);
+    hipMemset(a, 0, S);
+    hipMemset(b, 0, S);
+    hipMemset(c, 0, S);
+    auto report = [&](const char *name, int grid, float ms, double bytes) {
+        printf("%-34s grid=%7d  %.4f ms  %7.1f GB/s\n", name, grid, ms, bytes / ms / 1e6);
+    };
+#define RUN(NAME, U, LNT, SNT, T, GRID)                                                                   \
+    {                                                                                                     \
+        int g = GRID;                                                                                     \
+        if (g <= 0) g = (int)((nvec + (size_t)T * U - 1) / ((size_t)T * U));                             \
+        float ms = timeit([&] { hipLaunchKernelGGL((k_rl<U, LNT, SNT, T>), dim3(g), dim3(T), 0, 0, a, b, nvec); }, 20); \
+        report(NAME, g, ms, 3.0 * S);                                                                     \
+    }
+    for (int grid : {1024, 2048, 4096, 0}) {
+        RUN("U4 ld    st_nt   256", 4, false, true, 256, grid);
+        RUN("U4 ld    st      256", 4, false, false, 256, grid);
+        RUN("U4 ld_nt st_nt   256", 4, true, true, 256, grid);
+        RUN("U8 ld    st_nt   256", 8, false, true, 256, grid);
+        RUN("U2 ld    st_nt   256", 2, false, true, 256, grid);
+        RUN("U4 ld    st_nt   512", 4, false, true, 512, grid);
+        RUN("U2 ld    st_nt  1024", 2, false, true, 1024, grid);
+    }
+    for (int grid : {2048, 0}) {
+        int g = grid ? grid : (int)(nvec / 1024);
+        float ms = timeit([&] { hipLaunchKernelGGL((k_copy<4, 256>), dim3(g), dim3(256), 0, 0, a, c, nvec); }, 20);
+        report("copy U4 (1R+1W ceiling)", g, ms, 2.0 * S);
+    }
+    return 0;
+}
