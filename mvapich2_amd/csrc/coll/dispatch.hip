@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs a, int vec) {
                 const size_t i = base + (size_t)u * kThreads;
 #pragma unroll
                 for (int j = 0; j < kMaxRanks; ++j)
-                    v[u][j] = (j < a.n && a.src.p[j] && i < nv) ? ((const v4u *)a.src.p[j])[i] : v4u{0, 0, 0, 0};
+                    v[u][j] = (j < a.n && a.src.p[j] && i < nv) ? ld_nt((const v4u *)a.src.p[j] + i) : v4u{0, 0, 0, 0};
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {

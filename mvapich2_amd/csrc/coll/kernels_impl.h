@@ -31,8 +31,8 @@ __global__ __launch_bounds__(kThreads) void k_reduce_local(const v4u *__restrict
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * kThreads;
             if (i < nvec) {
-                a[u] = io[i];
-                b[u] = in[i];
+                a[u] = ld_nt(&io[i]);
+                b[u] = ld_nt(&in[i]);
             }
         }
 #pragma unroll
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_n(PeerTable src, int n, cha
             const size_t i = base + (size_t)u * kThreads;
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
-                v[u][j] = (j < n && i < nvec) ? ((const v4u *)src.p[j])[i] : v4u{0, 0, 0, 0};
+                v[u][j] = (j < n && i < nvec) ? ld_nt((const v4u *)src.p[j] + i) : v4u{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kThreads) void k_twoshot(TwoShotArgs a) {
             const size_t i = t * TV + (size_t)u * kThreads + threadIdx.x;
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
-                v[u][j] = (j < a.n && i < a.nvec) ? ((const v4u *)a.src.p[j])[i] : v4u{0, 0, 0, 0};
+                v[u][j] = (j < a.n && i < a.nvec) ? ld_nt((const v4u *)a.src.p[j] + i) : v4u{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kThreads) void k_twoshot(TwoShotArgs a) {
 #pragma unroll
             for (int k = 0; k < kMaxRanks; ++k) {
                 const size_t i = (tbase + k) * TV + (size_t)u * kThreads + threadIdx.x;
-                v[u][k] = (k < a.n && k != a.me && i < a.nvec) ? ((const v4u *)a.agsrc.p[k])[i] : v4u{0, 0, 0, 0};
+                v[u][k] = (k < a.n && k != a.me && i < a.nvec) ? ld_nt((const v4u *)a.agsrc.p[k] + i) : v4u{0, 0, 0, 0};
             }
         }
 #pragma unroll
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void k_rs(RsArgs a) {
                 const size_t i = base + (size_t)u * kThreads;
 #pragma unroll
                 for (int j = 0; j < kMaxRanks; ++j)
-                    v[u][j] = (j < a.n && i < ve) ? ((const v4u *)a.src.p[j])[i] : v4u{0, 0, 0, 0};
+                    v[u][j] = (j < a.n && i < ve) ? ld_nt((const v4u *)a.src.p[j] + i) : v4u{0, 0, 0, 0};
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {

@@ -35,7 +35,9 @@ struct SigTable {
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void st_nt(v4u *p, v4u v) { __builtin_nontemporal_store(v, p); }
-__device__ __forceinline__ v4u ld_v(const v4u *p) { return *p; }
+// streamed (read-once) loads: non-temporal.  Measured on MI355X for the 2-read/1-write
+// Reduce_local stream (tools/rl_variants.hip): 6.2-6.3 TB/s vs 5.2-5.3 TB/s with plain loads.
+__device__ __forceinline__ v4u ld_nt(const v4u *p) { return __builtin_nontemporal_load(p); }
 
 __device__ __forceinline__ void flag_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

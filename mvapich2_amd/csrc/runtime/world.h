@@ -85,7 +85,7 @@ struct World {
     // tuning
     size_t oneshot_max = 256 * 1024;
     int max_grid = 256;
-    int rl_grid = 2048;       // reduce_local grid cap
+    int rl_grid = 4096;       // reduce_local grid cap (tools/rl_variants.hip sweep)
 
     // timing (bench)
     bool timing = false;
