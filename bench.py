@@ -164,11 +164,15 @@ def bench_nranks(args, L, rank, size):
     for _ in range(100):
         L.MPI_Allreduce(s8.ptr, r8.ptr, 2, h, op, world)
     lat = 0.0
+    lat_k = []
+    L.mv2h_timing_enable(1)
     for _ in range(args.lat_iters):
         L.MPI_Barrier(world)
         t0 = time.perf_counter()
         L.MPI_Allreduce(s8.ptr, r8.ptr, 2, h, op, world)
         lat += time.perf_counter() - t0
+        lat_k.append(L.mv2h_last_kernel_ms())
+    L.mv2h_timing_enable(0)
     # max over ranks via a tiny device allreduce (MAX)
     mx = np.array([tot, lat, float(np.mean(kms)), 0.0 if ok else 1.0], dtype=np.float64)
     dm = m.DeviceBuffer(mx.nbytes)
@@ -186,7 +190,8 @@ def bench_nranks(args, L, rank, size):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "configs[2]: osu_allreduce -d rocm fp32 SUM 256 MiB, 1 rank per GPU over xGMI",
                    "count": count, "bytes": S_BYTES, "algorithm": "two-shot direct RS+AG (peer reads)",
-                   "latency_8B_us": round(lat / args.lat_iters * 1e6, 2), "correct": not bool(bad)},
+                   "latency_8B_us": round(lat / args.lat_iters * 1e6, 2),
+                   "latency_8B_kernel_us": round(float(np.median(lat_k)) * 1e3, 2), "correct": not bool(bad)},
         "roofline": {"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
                      "frac": round(kbus / peak_all, 4), "traffic": None,
                      "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_twoshot<R<SUM,F32>,2>",

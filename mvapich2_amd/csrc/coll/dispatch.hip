@@ -112,7 +112,9 @@ int launch_gather(const GatherArgs &a, const LaunchCfg &cfg) {
         if (!a.src.p[j]) continue;
         vec = vec && ((uintptr_t)a.src.p[j] % 16 == 0) && (a.dst_off[j] % 16 == 0);
     }
-    hipLaunchKernelGGL((k_gather<2>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a, vec ? 1 : 0);
+    static const int cap = resident_grid((const void *)k_gather<2>, cfg);
+    const int g = cfg.grid < cap ? cfg.grid : cap;
+    hipLaunchKernelGGL((k_gather<2>), dim3(g), dim3(kThreads), 0, cfg.stream, a, vec ? 1 : 0);
     return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
 }
 

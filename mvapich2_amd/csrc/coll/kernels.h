@@ -74,7 +74,25 @@ struct LaunchCfg {
     int grid;
     int unroll;
     hipStream_t stream;
+    int cus = 256;    // compute units of the device
+    int nshare = 1;   // max ranks sharing one GPU (same on every rank)
 };
+
+// vectors per thread per tile of the two-shot kernel: fewer sources -> more
+// vectors, so every thread keeps >= 8 16-byte loads in flight
+inline int twoshot_unroll(int n) { return n <= 3 ? 4 : 2; }
+
+// Workgroups that are guaranteed co-resident for a kernel (the per-workgroup
+// cross-GPU flags need block b of every rank running together).  The
+// occupancy API can over-report by one block per CU (MI355X_MICROARCH.md,
+// Residency), so one block per CU is held back.
+inline int resident_grid(const void *kernel, const LaunchCfg &cfg) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kThreads, 0) != hipSuccess || nb < 1) nb = 1;
+    nb = nb > 1 ? nb - 1 : 1;
+    int cap = nb * cfg.cus / (cfg.nshare > 0 ? cfg.nshare : 1);
+    return cap < 1 ? 1 : cap;
+}
 
 // all return an MPI error class (0 = launched)
 int launch_reduce_local(int op, int kind, const void *in, void *inout, size_t count, size_t esize,

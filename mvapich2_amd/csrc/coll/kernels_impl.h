@@ -382,21 +382,33 @@ __global__ __launch_bounds__(kThreads) void k_rs(RsArgs a) {
 template <int OP, int K>
 struct LOneShot {
     static int run(const OneShotArgs &a, const LaunchCfg &cfg) {
-        hipLaunchKernelGGL((k_oneshot<R<OP, K>>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        static const int cap = resident_grid((const void *)k_oneshot<R<OP, K>>, cfg);
+        const int g = cfg.grid < cap ? cfg.grid : cap;
+        hipLaunchKernelGGL((k_oneshot<R<OP, K>>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };
 template <int OP, int K>
 struct LTwoShot {
     static int run(const TwoShotArgs &a, const LaunchCfg &cfg) {
-        hipLaunchKernelGGL((k_twoshot<R<OP, K>, 2>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        if (twoshot_unroll(a.n) == 4) {
+            static const int cap = resident_grid((const void *)k_twoshot<R<OP, K>, 4>, cfg);
+            const int g = cfg.grid < cap ? cfg.grid : cap;
+            hipLaunchKernelGGL((k_twoshot<R<OP, K>, 4>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+            return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+        }
+        static const int cap = resident_grid((const void *)k_twoshot<R<OP, K>, 2>, cfg);
+        const int g = cfg.grid < cap ? cfg.grid : cap;
+        hipLaunchKernelGGL((k_twoshot<R<OP, K>, 2>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };
 template <int OP, int K>
 struct LRs {
     static int run(const RsArgs &a, const LaunchCfg &cfg) {
-        hipLaunchKernelGGL((k_rs<R<OP, K>, 2>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        static const int cap = resident_grid((const void *)k_rs<R<OP, K>, 2>, cfg);
+        const int g = cfg.grid < cap ? cfg.grid : cap;
+        hipLaunchKernelGGL((k_rs<R<OP, K>, 2>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };

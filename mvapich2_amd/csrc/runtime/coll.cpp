@@ -122,6 +122,16 @@ static int grid_cap() {
     return g;
 }
 
+// launch config of a collective kernel: identical on every rank (the grid
+// must match across ranks: workgroup b of each rank pairs with workgroup b)
+static LaunchCfg coll_cfg(int grid, hipStream_t st) {
+    World &w = world();
+    LaunchCfg c{grid, 2, st};
+    c.cus = w.cus;
+    c.nshare = w.nshare;
+    return c;
+}
+
 // ---------------------------------------------------------------------------
 // IPC export / import of user buffers
 // ---------------------------------------------------------------------------
@@ -169,9 +179,15 @@ static const char *peer_buffer(int j, int slot, int *rc) {
     auto &m = w.peer_maps[j];
     auto it = m.find(d.buffer_id);
     if (it == m.end()) {
-        // evict a mapping of the same base (freed and re-allocated on the peer)
+        // a cached mapping whose peer range overlaps this new allocation belongs to
+        // a buffer the peer has freed (its address was reused): unmap it
         for (auto e = m.begin(); e != m.end();) {
-            if (e->second.alloc_size == 0) { e = m.erase(e); continue; }
+            const Mapping &mp = e->second;
+            if (mp.peer_base < d.base + d.alloc_size && d.base < mp.peer_base + mp.alloc_size) {
+                hipIpcCloseMemHandle(mp.ptr);
+                e = m.erase(e);
+                continue;
+            }
             ++e;
         }
         if (m.size() >= 64) {
@@ -188,7 +204,7 @@ static const char *peer_buffer(int j, int slot, int *rc) {
             *rc = E_OTHER;
             return nullptr;
         }
-        it = m.emplace(d.buffer_id, Mapping{(char *)p, d.alloc_size, 0}).first;
+        it = m.emplace(d.buffer_id, Mapping{(char *)p, d.base, d.alloc_size, 0}).first;
     }
     it->second.last_use = ++w.use_clock;
     *rc = 0;
@@ -452,7 +468,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.timeout = w.timeout_ticks;
         int g = (int)((nvec + 511) / 512);
         g = std::max(1, std::min(g, std::min(gcap, 32)));
-        LaunchCfg cfg{g, 1, st};
+        LaunchCfg cfg = coll_cfg(g, st);
         tmark0(st);
         rc = launch_oneshot(oi, dt->kind, a, dt->extent, cfg);
         tmark1(st);
@@ -491,11 +507,11 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     a.epoch = epoch;
     a.err = w.h_err;
     a.timeout = w.timeout_ticks;
-    const size_t tv = (size_t)kThreads * 2;
+    const size_t tv = (size_t)kThreads * twoshot_unroll(n);
     const size_t ntiles = (nvec + tv - 1) / tv;
     int g = (int)std::min<size_t>((ntiles + n - 1) / n, (size_t)gcap);
     if (g < 1) g = 1;
-    LaunchCfg cfg{g, 2, st};
+    LaunchCfg cfg = coll_cfg(g, st);
     tmark0(st);
     rc = launch_twoshot(oi, dt->kind, a, dt->extent, cfg);
     tmark1(st);
@@ -602,7 +618,7 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     const size_t nv = mycnt * ext / 16;
     int g = (int)std::min<size_t>((nv + 511) / 512, (size_t)grid_cap());
     if (g < 1) g = 1;
-    LaunchCfg cfg{g, 2, st};
+    LaunchCfg cfg = coll_cfg(g, st);
     tmark0(st);
     rc = launch_rs(oi, dt->kind, a, ext, cfg);
     tmark1(st);
@@ -627,7 +643,7 @@ static int gather_impl(const char *const *srcs, char *dst, const size_t *dst_off
     a.timeout = w.timeout_ticks;
     int g = (int)std::min<size_t>((bytes / 16 + 511) / 512, (size_t)grid_cap());
     if (g < 1) g = 1;
-    LaunchCfg cfg{g, 2, st};
+    LaunchCfg cfg = coll_cfg(g, st);
     tmark0(st);
     int rc = launch_gather(a, cfg);
     tmark1(st);

@@ -130,6 +130,7 @@ static int setup_device_common() {
     if (hipStreamCreate(&w.stream) != hipSuccess) return E_OTHER;
     if (hipHostMalloc((void **)&w.h_err, 64, hipHostMallocDefault) != hipSuccess) return E_OTHER;
     memset(w.h_err, 0, 64);
+    hipDeviceGetAttribute(&w.cus, hipDeviceAttributeMultiprocessorCount, w.device);
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, w.device) == hipSuccess && khz > 0)
         w.wall_clock_khz = khz;
@@ -206,10 +207,15 @@ int world_init() {
         w.shm->attached.fetch_add(1);
         host_barrier();  // everyone attached and published pid/device
 
-        // ranks sharing this GPU (tests run several ranks on one device)
-        w.nshare = 0;
-        for (int j = 0; j < w.size; ++j)
-            if (w.shm->r[j].pci_bus == me.pci_bus && w.shm->r[j].pci_device == me.pci_device) ++w.nshare;
+        // ranks sharing one GPU (tests run several ranks on one device): the
+        // maximum over all GPUs, so every rank derives the same kernel grids
+        w.nshare = 1;
+        for (int i = 0; i < w.size; ++i) {
+            int c = 0;
+            for (int j = 0; j < w.size; ++j)
+                if (w.shm->r[j].pci_bus == w.shm->r[i].pci_bus && w.shm->r[j].pci_device == w.shm->r[i].pci_device) ++c;
+            if (c > w.nshare) w.nshare = c;
+        }
 
         if (w.size <= kMaxRanks && !control_only) {
             // signal page + one-shot arena, IPC-exported

@@ -57,6 +57,7 @@ struct ShmSeg {
 
 struct Mapping {
     char *ptr;        // mapped base in this process
+    uint64_t peer_base;  // allocation base in the peer's address space
     uint64_t alloc_size;
     uint64_t last_use;
 };
@@ -65,7 +66,8 @@ struct World {
     bool inited = false;
     bool finalized = false;
     int rank = 0, size = 1, local_rank = 0, device = 0;
-    int nshare = 1;  // ranks sharing this rank's GPU (test setups)
+    int nshare = 1;  // max over ranks of the ranks sharing one GPU (test setups); same on all ranks
+    int cus = 256;   // compute units of this GPU
     hipStream_t stream = nullptr;
     std::string shm_name;
     ShmSeg *shm = nullptr;
@@ -84,7 +86,7 @@ struct World {
 
     // tuning
     size_t oneshot_max = 256 * 1024;
-    int max_grid = 256;
+    int max_grid = 1024;
     int rl_grid = 4096;       // reduce_local grid cap (tools/rl_variants.hip sweep)
 
     // timing (bench)
