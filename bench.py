@@ -189,12 +189,12 @@ def bench_nranks(args, L, rank, size):
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "configs[2]: osu_allreduce -d rocm fp32 SUM 256 MiB, 1 rank per GPU over xGMI",
-                   "count": count, "bytes": S_BYTES, "algorithm": "two-shot direct RS+AG (peer reads)",
+                   "count": count, "bytes": S_BYTES, "algorithm": "pipelined direct RS+AG (pushes into peer arenas over xGMI)",
                    "latency_8B_us": round(lat / args.lat_iters * 1e6, 2),
                    "latency_8B_kernel_us": round(float(np.median(lat_k)) * 1e3, 2), "correct": not bool(bad)},
         "roofline": {"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
                      "frac": round(kbus / peak_all, 4), "traffic": None,
-                     "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_twoshot<R<SUM,F32>,2>",
+                     "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
                      "kernel_ms": round(kms_max, 4)},
         "cpu_baseline": None,
     }

@@ -30,42 +30,46 @@ struct OneShotArgs {
     uint64_t timeout;
 };
 
-struct TwoShotArgs {
-    PeerTable src;    // every rank's sendbuf (mapped into this process)
-    PeerTable agsrc;  // every rank's recvbuf (mapped)
-    char *recv;
-    SigTable sig_peer;
-    uint64_t *sig_own;
-    size_t count, nvec;
-    int n, me;
-    TreeParams tp;
-    uint64_t epoch;   // uses epoch, epoch+1, epoch+2
-    int *err;
-    uint64_t timeout;
+// ---------------------------------------------------------------------------
+// Pipelined push collectives through IPC-registered arenas (coll/pipe.h).
+// User buffers are never mapped by peers: every cross-GPU byte is a store
+// into a library-owned, uncached arena slot of the destination GPU, so
+// applications may free or reuse their buffers as soon as a call returns.
+// ---------------------------------------------------------------------------
+enum PipeMode : int {
+    PIPE_AR = 0,   // allreduce: scatter -> reduce own segment + push -> gather
+    PIPE_RS = 1,   // reduce-scatter: scatter -> reduce own segment into recv
+    PIPE_RED = 2,  // reduce to root: scatter -> reduce -> push to root -> root gathers
+    PIPE_AG = 3,   // allgather: push own contribution -> gather
+    PIPE_BC = 4,   // broadcast: root scatters segments -> owners push -> gather
 };
 
-struct RsArgs {
-    PeerTable src;    // every rank's sendbuf (mapped)
-    char *dst;        // my result region base (aligned like src + off)
-    SigTable sig_peer;
-    uint64_t *sig_own;
-    size_t off, cnt;  // my block: elements [off, off+cnt)
-    int n, me;
-    TreeParams tp;
-    uint64_t epoch;   // epoch, epoch+1
-    int *err;
-    uint64_t timeout;
-};
+// Arena layout per rank and region (RS region, AG region):
+//   [parity 0..1][source rank 0..kMaxRanks-1][kPipeSlot bytes]
+// Round k of a call uses parity (round0 + k) & 1; block b moves the bytes
+// [k*tseg + b*tsub, +tsub) of every segment, stored at slot offset b*tsub.
+constexpr size_t kPipeSlot = (size_t)8 << 20;   // >= kPipeMaxGrid * kPipeMaxSub
+constexpr int kPipeMaxGrid = 128;
+constexpr size_t kPipeMaxSub = (size_t)64 << 10;
+constexpr size_t kPipeRegion = 2 * (size_t)kMaxRanks * kPipeSlot;
 
-struct GatherArgs {
-    PeerTable src;    // per source rank: base to read (mapped), nullptr = skip
-    char *dst;        // my destination base
-    size_t dst_off[kMaxRanks];  // byte offset in dst for source j
-    size_t bytes;     // bytes per source
+struct PipeArgs {
+    int mode, n, me, root;
+    const char *send;               // AR/RS/RED: full operand; AG: my contribution; BC: the buffer
+    char *recv;                     // destination base
+    size_t seg_off[kMaxRanks];      // byte offset of segment j in `send` (16-byte aligned)
+    size_t seg_len[kMaxRanks];      // bytes of segment j
+    size_t recv_off[kMaxRanks];     // byte offset in `recv` where segment j lands (16-byte aligned)
+    PeerTableW rs_peer;             // rank j's RS region (mapped); entry me = my own
+    PeerTableW ag_peer;             // rank j's AG region (mapped); entry me = my own
+    size_t tseg, tsub;              // bytes per segment per round / per block per segment per round
+    uint64_t round0;                // global round counter at launch (slot parity)
+    int nrounds;
+    int esize;                      // element extent (reducing modes)
     SigTable sig_peer;
     uint64_t *sig_own;
-    int n, me;
-    uint64_t epoch;   // epoch, epoch+1
+    uint64_t epoch0;                // round k uses epochs epoch0 + 2k and epoch0 + 2k + 1
+    TreeParams tp;
     int *err;
     uint64_t timeout;
 };
@@ -77,10 +81,6 @@ struct LaunchCfg {
     int cus = 256;    // compute units of the device
     int nshare = 1;   // max ranks sharing one GPU (same on every rank)
 };
-
-// vectors per thread per tile of the two-shot kernel: fewer sources -> more
-// vectors, so every thread keeps >= 8 16-byte loads in flight
-inline int twoshot_unroll(int n) { return n <= 3 ? 4 : 2; }
 
 // Workgroups that are guaranteed co-resident for a kernel (the per-workgroup
 // cross-GPU flags need block b of every rank running together).  The
@@ -100,9 +100,10 @@ int launch_reduce_local(int op, int kind, const void *in, void *inout, size_t co
 int launch_reduce_n(int op, int kind, const void *const *srcs, int n, void *dst, size_t count,
                     size_t esize, const TreeParams &tp, const LaunchCfg &cfg);
 int launch_oneshot(int op, int kind, const OneShotArgs &a, size_t esize, const LaunchCfg &cfg);
-int launch_twoshot(int op, int kind, const TwoShotArgs &a, size_t esize, const LaunchCfg &cfg);
-int launch_rs(int op, int kind, const RsArgs &a, size_t esize, const LaunchCfg &cfg);
-int launch_gather(const GatherArgs &a, const LaunchCfg &cfg);
+// reducing pipeline modes (AR / RS / RED), dispatched on (op, kind)
+int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg);
+// data-movement pipeline modes (AG / BC)
+int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg);
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride,
                         int unpack, hipStream_t stream);
 

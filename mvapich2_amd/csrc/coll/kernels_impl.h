@@ -255,130 +255,6 @@ __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
     }
 }
 
-// ============================================================================
-// Two-shot allreduce (large messages): direct reduce-scatter + all-gather
-// over xGMI, every rank reading its n-1 peers concurrently (n-1 links).
-// Tiles of TV vectors are owned round-robin (tile t -> rank t % n).
-//   E0: all ranks entered (sendbufs ready)      RS: reduce own tiles -> recv
-//   E1: all reduce-scatters done               AG: copy peers' tiles -> recv
-//   E2: all gathers done (peers stopped reading my buffers)
-// ============================================================================
-template <class Rd, int U>
-__global__ __launch_bounds__(kThreads) void k_twoshot(TwoShotArgs a) {
-    using T = typename Rd::T;
-    constexpr int N = 16 / sizeof(T);
-    constexpr size_t TV = (size_t)kThreads * U;
-    const int blk = blockIdx.x, G = gridDim.x;
-    const size_t ntiles = (a.nvec + TV - 1) / TV;
-
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch);
-    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
-
-    // ---- reduce-scatter: my tiles ----
-    for (size_t it = blk;; it += G) {
-        const size_t t = (size_t)a.me + (size_t)a.n * it;
-        if (t >= ntiles) break;
-        v4u v[U][kMaxRanks];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t i = t * TV + (size_t)u * kThreads + threadIdx.x;
-#pragma unroll
-            for (int j = 0; j < kMaxRanks; ++j)
-                v[u][j] = (j < a.n && i < a.nvec) ? ld_nt((const v4u *)a.src.p[j] + i) : v4u{0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t i = t * TV + (size_t)u * kThreads + threadIdx.x;
-            if (i < a.nvec) ((v4u *)a.recv)[i] = vreduce_n<Rd>(v[u], a.n, a.tp, i * N);
-        }
-    }
-    // scalar tail: reduced by block 0 of every rank, written after E1
-    const size_t tail0 = a.nvec * N;
-    T tail_val{};
-    const bool has_tail = blk == 0 && tail0 + threadIdx.x < a.count;
-    if (has_tail) {
-        const T *s[kMaxRanks];
-#pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) s[j] = (const T *)a.src.p[j];
-        tail_val = sreduce_n<Rd>(s, a.n, a.tp, tail0 + threadIdx.x);
-    }
-
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch + 1);
-    if (!wait_peers(a.sig_own, a.n, blk, a.epoch + 1, a.err, a.timeout)) return;
-
-    // ---- all-gather: peers' tiles ----
-    for (size_t it = blk;; it += G) {
-        const size_t tbase = (size_t)a.n * it;
-        if (tbase >= ntiles) break;
-        v4u v[U][kMaxRanks];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-#pragma unroll
-            for (int k = 0; k < kMaxRanks; ++k) {
-                const size_t i = (tbase + k) * TV + (size_t)u * kThreads + threadIdx.x;
-                v[u][k] = (k < a.n && k != a.me && i < a.nvec) ? ld_nt((const v4u *)a.agsrc.p[k] + i) : v4u{0, 0, 0, 0};
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-#pragma unroll
-            for (int k = 0; k < kMaxRanks; ++k) {
-                const size_t i = (tbase + k) * TV + (size_t)u * kThreads + threadIdx.x;
-                if (k < a.n && k != a.me && i < a.nvec) st_nt((v4u *)a.recv + i, v[u][k]);
-            }
-        }
-    }
-    if (has_tail) ((T *)a.recv)[tail0 + threadIdx.x] = tail_val;
-
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch + 2);
-    wait_peers(a.sig_own, a.n, blk, a.epoch + 2, a.err, a.timeout);
-}
-
-// ============================================================================
-// Direct reduce-scatter: rank me reduces elements [off, off+cnt) of every
-// rank's sendbuf into dst (same alignment as src + off).  E0 entry, E1 exit.
-// ============================================================================
-template <class Rd, int U>
-__global__ __launch_bounds__(kThreads) void k_rs(RsArgs a) {
-    using T = typename Rd::T;
-    constexpr int N = 16 / sizeof(T);
-    const int blk = blockIdx.x, G = gridDim.x;
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch);
-    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
-    // element range -> vector-aligned body [vb, ve) plus scalar head/tail
-    const size_t eb = a.off, ee = a.off + a.cnt;
-    const size_t vb = (eb + N - 1) / N, ve = ee / N;
-    if (vb < ve) {
-        const size_t stride = (size_t)G * kThreads * U;
-        for (size_t base = vb + (size_t)blk * kThreads * U + threadIdx.x; base < ve; base += stride) {
-            v4u v[U][kMaxRanks];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * kThreads;
-#pragma unroll
-                for (int j = 0; j < kMaxRanks; ++j)
-                    v[u][j] = (j < a.n && i < ve) ? ld_nt((const v4u *)a.src.p[j] + i) : v4u{0, 0, 0, 0};
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * kThreads;
-                if (i < ve) st_nt((v4u *)a.dst + i, vreduce_n<Rd>(v[u], a.n, a.tp, i * N));
-            }
-        }
-    }
-    if (blk == 0) {
-        const T *s[kMaxRanks];
-#pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) s[j] = (const T *)a.src.p[j];
-        const size_t hb_end = vb < ve ? vb * N : ee;
-        for (size_t e = eb + threadIdx.x; e < hb_end; e += kThreads) ((T *)a.dst)[e] = sreduce_n<Rd>(s, a.n, a.tp, e);
-        if (vb < ve)
-            for (size_t e = ve * N + threadIdx.x; e < ee; e += kThreads) ((T *)a.dst)[e] = sreduce_n<Rd>(s, a.n, a.tp, e);
-    }
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch + 1);
-    wait_peers(a.sig_own, a.n, blk, a.epoch + 1, a.err, a.timeout);
-}
-
 template <int OP, int K>
 struct LOneShot {
     static int run(const OneShotArgs &a, const LaunchCfg &cfg) {
@@ -388,31 +264,6 @@ struct LOneShot {
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };
-template <int OP, int K>
-struct LTwoShot {
-    static int run(const TwoShotArgs &a, const LaunchCfg &cfg) {
-        if (twoshot_unroll(a.n) == 4) {
-            static const int cap = resident_grid((const void *)k_twoshot<R<OP, K>, 4>, cfg);
-            const int g = cfg.grid < cap ? cfg.grid : cap;
-            hipLaunchKernelGGL((k_twoshot<R<OP, K>, 4>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
-            return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
-        }
-        static const int cap = resident_grid((const void *)k_twoshot<R<OP, K>, 2>, cfg);
-        const int g = cfg.grid < cap ? cfg.grid : cap;
-        hipLaunchKernelGGL((k_twoshot<R<OP, K>, 2>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
-        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
-    }
-};
-template <int OP, int K>
-struct LRs {
-    static int run(const RsArgs &a, const LaunchCfg &cfg) {
-        static const int cap = resident_grid((const void *)k_rs<R<OP, K>, 2>, cfg);
-        const int g = cfg.grid < cap ? cfg.grid : cap;
-        hipLaunchKernelGGL((k_rs<R<OP, K>, 2>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
-        return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
-    }
-};
-
 // ---------------- runtime (op, kind) -> template dispatch ----------------
 template <template <int, int> class L, int OP, int K, class... A>
 inline int call_if(A &&...args) {

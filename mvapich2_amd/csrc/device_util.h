@@ -63,15 +63,16 @@ __device__ __forceinline__ void signal_peers(const SigTable &sig, int n, int me,
     }
 }
 
-// Wait until flag[j][blk] >= epoch for every j in [0, n) (own slot included),
-// then acquire at system scope.  Returns false (and records *err) on timeout.
-// Call from all threads; the result is block-uniform.
-__device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, uint64_t epoch,
-                                           int *err, uint64_t timeout_ticks) {
+// Wait until flag[j][blk] >= epoch for every rank j whose bit is set in
+// `mask` (own slot may be included), then acquire at system scope.  Returns
+// false (and records *err) on timeout.  Call from all threads; the result is
+// block-uniform.
+__device__ __forceinline__ bool wait_mask(uint64_t *own_sig, unsigned mask, int blk, uint64_t epoch,
+                                          int *err, uint64_t timeout_ticks) {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int j = threadIdx.x;
-        bool ok = j >= n;
+        bool ok = j >= kMaxRanks || !((mask >> j) & 1u);
         const uint64_t t0 = wall_clock64();
         bool timed_out = false;
         while (!__all(ok)) {
@@ -93,6 +94,12 @@ __device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, ui
     }
     __syncthreads();
     return s_ok != 0;
+}
+
+// wait on every rank in [0, n)
+__device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, uint64_t epoch,
+                                           int *err, uint64_t timeout_ticks) {
+    return wait_mask(own_sig, (1u << n) - 1u, blk, epoch, err, timeout_ticks);
 }
 
 // a x b elementwise on one 16-byte vector holding 16/sizeof(T) elements
@@ -125,15 +132,14 @@ __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[
             if (i < n) acc = Rd::apply(acc, v[i]);
         return acc;
     }
+    // w[i] = v[i + rem] as a two-stage shifter (selects between constant
+    // indices only: a 4-way select chain is turned into a private-memory
+    // table lookup by the compiler)
     T w[kMaxRanks];
 #pragma unroll
-    for (int i = 0; i < kMaxRanks; ++i) {
-        const int k0 = i < kMaxRanks ? i : kMaxRanks - 1;
-        const int k1 = i + 1 < kMaxRanks ? i + 1 : kMaxRanks - 1;
-        const int k2 = i + 2 < kMaxRanks ? i + 2 : kMaxRanks - 1;
-        const int k3 = i + 3 < kMaxRanks ? i + 3 : kMaxRanks - 1;
-        w[i] = rem == 0 ? v[k0] : rem == 1 ? v[k1] : rem == 2 ? v[k2] : v[k3];
-    }
+    for (int i = 0; i < kMaxRanks; ++i) w[i] = (rem & 1) ? v[i + 1 < kMaxRanks ? i + 1 : kMaxRanks - 1] : v[i];
+#pragma unroll
+    for (int i = 0; i < kMaxRanks; ++i) w[i] = (rem & 2) ? w[i + 2 < kMaxRanks ? i + 2 : kMaxRanks - 1] : w[i];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
         if (i < rem) w[i] = Rd::apply(v[2 * i + 1], v[2 * i]);

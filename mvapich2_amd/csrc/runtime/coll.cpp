@@ -133,82 +133,71 @@ static LaunchCfg coll_cfg(int grid, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
-// IPC export / import of user buffers
+// pipelined collectives (coll/pipe.h)
 // ---------------------------------------------------------------------------
-static int publish(int slot, const void *ptr) {
+struct PipeGeom {
+    int grid;
+    size_t tsub, tseg;
+    int nrounds;
+};
+
+// Grid and per-block range of a pipelined call.  A pure function of the
+// message geometry and of values every rank shares (CU count, ranks per GPU,
+// tuning knobs), so block b of every rank handles the same bytes.
+static PipeGeom pipe_geom(size_t maxlen) {
     World &w = world();
-    BufDesc &d = w.shm->r[w.rank].desc[slot];
-    uint64_t bid = 0;
-    hipDeviceptr_t base = nullptr;
-    size_t asz = 0;
-    if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)ptr) != hipSuccess ||
-        hipMemGetAddressRange(&base, &asz, (hipDeviceptr_t)ptr) != hipSuccess) {
-        hipGetLastError();
-        MV2_ERR("buffer %p is not a device allocation that can be shared over IPC", ptr);
-        return E_BUFFER;
-    }
-    auto it = w.own_handles.find(bid);
-    if (it == w.own_handles.end()) {
-        hipIpcMemHandle_t h;
-        if (hipIpcGetMemHandle(&h, (void *)base) != hipSuccess) {
-            hipGetLastError();
-            MV2_ERR("hipIpcGetMemHandle failed for %p", ptr);
-            return E_BUFFER;
-        }
-        it = w.own_handles.emplace(bid, h).first;
-    }
-    d.handle = it->second;
-    d.buffer_id = bid;
-    d.base = (uint64_t)(uintptr_t)base;
-    d.alloc_size = asz;
-    d.offset = (uint64_t)((const char *)ptr - (const char *)base);
-    d.seq = w.seq;
-    return 0;
+    int cap = std::min(kPipeMaxGrid, std::max(1, w.cus / std::max(1, w.nshare)));
+    cap = std::min(cap, std::max(1, w.pipe_grid));
+    const size_t kMinSub = (size_t)16 << 10;
+    PipeGeom g{};
+    g.grid = (int)std::min<size_t>((size_t)cap, std::max<size_t>(1, (maxlen + kMinSub - 1) / kMinSub));
+    size_t tsub = (maxlen + g.grid - 1) / g.grid;
+    tsub = (tsub + 4095) & ~(size_t)4095;
+    g.tsub = std::min(tsub, std::min(kPipeMaxSub, std::max<size_t>(4096, w.pipe_sub)));
+    g.tseg = (size_t)g.grid * g.tsub;
+    g.nrounds = (int)((maxlen + g.tseg - 1) / g.tseg);
+    return g;
 }
 
-// pointer of peer j's published buffer `slot` in this process
-static const char *peer_buffer(int j, int slot, int *rc) {
+// n contiguous 16-byte-aligned segments of a `bytes` buffer (the last may be short or empty)
+static void even_segments(PipeArgs &a, size_t bytes, int n) {
+    const size_t seg = (((bytes + n - 1) / n) + 15) & ~(size_t)15;
+    for (int j = 0; j < n; ++j) {
+        const size_t off = std::min((size_t)j * seg, bytes);
+        a.seg_off[j] = a.recv_off[j] = off;
+        a.seg_len[j] = std::min(seg, bytes - off);
+    }
+}
+
+// Fill the runtime part of `a`, reserve rounds/epochs and launch (no sync).
+// dt == nullptr: data-movement modes (AG / BC).
+static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
     World &w = world();
-    const BufDesc &d = w.shm->r[j].desc[slot];
-    if (d.seq != w.seq) {
-        MV2_ERR("rank %d published a stale buffer descriptor (seq %llu vs %llu)", j,
-                (unsigned long long)d.seq, (unsigned long long)w.seq);
-        *rc = E_INTERN;
-        return nullptr;
-    }
-    auto &m = w.peer_maps[j];
-    auto it = m.find(d.buffer_id);
-    if (it == m.end()) {
-        // a cached mapping whose peer range overlaps this new allocation belongs to
-        // a buffer the peer has freed (its address was reused): unmap it
-        for (auto e = m.begin(); e != m.end();) {
-            const Mapping &mp = e->second;
-            if (mp.peer_base < d.base + d.alloc_size && d.base < mp.peer_base + mp.alloc_size) {
-                hipIpcCloseMemHandle(mp.ptr);
-                e = m.erase(e);
-                continue;
-            }
-            ++e;
-        }
-        if (m.size() >= 64) {
-            auto victim = std::min_element(m.begin(), m.end(), [](const auto &a, const auto &b) {
-                return a.second.last_use < b.second.last_use;
-            });
-            hipIpcCloseMemHandle(victim->second.ptr);
-            m.erase(victim);
-        }
-        void *p = nullptr;
-        if (hipIpcOpenMemHandle(&p, d.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-            hipGetLastError();
-            MV2_ERR("hipIpcOpenMemHandle failed for rank %d buffer", j);
-            *rc = E_OTHER;
-            return nullptr;
-        }
-        it = m.emplace(d.buffer_id, Mapping{(char *)p, d.base, d.alloc_size, 0}).first;
-    }
-    it->second.last_use = ++w.use_clock;
-    *rc = 0;
-    return it->second.ptr + d.offset;
+    a.n = w.size;
+    a.me = w.rank;
+    size_t maxlen = 0;
+    for (int j = 0; j < a.n; ++j) maxlen = std::max(maxlen, a.seg_len[j]);
+    if (maxlen == 0) return 0;  // every rank sees the same geometry
+    const PipeGeom g = pipe_geom(maxlen);
+    a.rs_peer = w.peer_rs;
+    a.ag_peer = w.peer_ag;
+    a.sig_peer = w.peer_sig;
+    a.sig_own = w.sig;
+    a.tsub = g.tsub;
+    a.tseg = g.tseg;
+    a.nrounds = g.nrounds;
+    a.round0 = w.round;
+    w.round += (uint64_t)g.nrounds;
+    a.epoch0 = w.epoch + 1;
+    w.epoch += 2 * (uint64_t)g.nrounds;
+    a.err = w.h_err;
+    a.timeout = w.timeout_ticks;
+    MV2_DEBUG("pipe mode %d grid %d tsub %zu rounds %d maxlen %zu", a.mode, g.grid, g.tsub, g.nrounds, maxlen);
+    LaunchCfg cfg = coll_cfg(g.grid, st);
+    tmark0(st);
+    const int rc = dt ? launch_pipe_reduce(oi, dt->kind, a, cfg) : launch_pipe_copy(a, cfg);
+    tmark1(st);
+    return rc;
 }
 
 }  // namespace mv2
@@ -264,6 +253,8 @@ int mv2h_set_tuning(const char *key, long value) {
     World &w = world();
     if (!strcmp(key, "max_grid")) w.max_grid = (int)value;
     else if (!strcmp(key, "rl_grid")) w.rl_grid = (int)value;
+    else if (!strcmp(key, "pipe_grid")) w.pipe_grid = (int)value;
+    else if (!strcmp(key, "pipe_sub")) w.pipe_sub = (size_t)value;
     else if (!strcmp(key, "oneshot_max")) {
         if ((size_t)value > w.slot_bytes && w.size > 1) return E_ARG;
         w.oneshot_max = (size_t)value;
@@ -443,8 +434,6 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         return mv2h_bcast(recvbuf, bytes, n - 1, nullptr);
     }
     const TreeParams tp = make_tree(n, count, dt, w.rank);
-    const uint64_t seq = ++w.seq;
-    const uint64_t epoch = seq * 4 + 1;
     const size_t nvec = bytes / 16;
     const int gcap = grid_cap();
     if (bytes <= w.oneshot_max && bytes <= w.slot_bytes) {
@@ -452,7 +441,8 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.send = s.send;
         a.recv = s.recv;
         const size_t half = (size_t)kMaxRanks * w.slot_bytes;
-        const size_t par = (seq & 1) * half;
+        const size_t par = (w.os_calls++ & 1) * half;
+        const uint64_t epoch = ++w.epoch;
         for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j] + par;
         a.arena_own = w.arena + par;
         a.sig_peer = w.peer_sig;
@@ -476,46 +466,15 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         stage_out(s, st);
         return finish(st, w.timing);
     }
-    // two-shot: exchange buffer descriptors (host), then one kernel
-    if ((rc = publish(0, s.send))) return rc;
-    if ((rc = publish(1, s.recv))) return rc;
-    host_barrier();
-    TwoShotArgs a{};
-    for (int j = 0; j < n; ++j) {
-        if (j == w.rank) {
-            a.src.p[j] = s.send;
-            a.agsrc.p[j] = s.recv;
-            continue;
-        }
-        a.src.p[j] = peer_buffer(j, 0, &rc);
-        if (rc) return rc;
-        a.agsrc.p[j] = peer_buffer(j, 1, &rc);
-        if (rc) return rc;
-    }
-    for (int j = n; j < kMaxRanks; ++j) {
-        a.src.p[j] = a.src.p[0];
-        a.agsrc.p[j] = a.agsrc.p[0];
-    }
+    // pipelined direct reduce-scatter + all-gather, pushed through the arenas
+    PipeArgs a{};
+    a.mode = PIPE_AR;
+    a.send = s.send;
     a.recv = s.recv;
-    a.sig_peer = w.peer_sig;
-    a.sig_own = w.sig;
-    a.count = count;
-    a.nvec = nvec;
-    a.n = n;
-    a.me = w.rank;
+    a.esize = dt->extent;
     a.tp = tp;
-    a.epoch = epoch;
-    a.err = w.h_err;
-    a.timeout = w.timeout_ticks;
-    const size_t tv = (size_t)kThreads * twoshot_unroll(n);
-    const size_t ntiles = (nvec + tv - 1) / tv;
-    int g = (int)std::min<size_t>((ntiles + n - 1) / n, (size_t)gcap);
-    if (g < 1) g = 1;
-    LaunchCfg cfg = coll_cfg(g, st);
-    tmark0(st);
-    rc = launch_twoshot(oi, dt->kind, a, dt->extent, cfg);
-    tmark1(st);
-    if (rc) return rc;
+    even_segments(a, bytes, n);
+    if ((rc = run_pipe(a, oi, dt, st))) return rc;
     stage_out(s, st);
     return finish(st, w.timing);
 }
@@ -541,12 +500,45 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
     if (root < 0 || root >= w.size) return E_ROOT;
     hipStream_t st = pick_stream(stream);
     const size_t bytes = count * (size_t)dt->extent;
-    if (w.rank == root) return allreduce_impl(sendbuf, recvbuf, count, dt, op_index(op), st);
-    // non-roots: recvbuf is insignificant; reduce into scratch
-    void *tmp = get_scratch(2, bytes);
-    if (!tmp) return E_NO_MEM;
-    const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;
-    return allreduce_impl(src, tmp, count, dt, op_index(op), st);
+    const int oi = op_index(op);
+    const bool is_root = w.rank == root;
+    const bool in_place = sendbuf == (const void *)-1 || (is_root && sendbuf == recvbuf);
+    // small messages, REPLACE / NO_OP, one rank: every rank computes the result
+    // (one-shot); non-roots discard theirs
+    if (w.size == 1 || oi >= OP_REPLACE || (bytes <= w.oneshot_max && bytes <= w.slot_bytes)) {
+        if (is_root) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st);
+        void *tmp = get_scratch(2, bytes);
+        if (!tmp) return E_NO_MEM;
+        return allreduce_impl(in_place ? recvbuf : sendbuf, tmp, count, dt, oi, st);
+    }
+    // pipelined: scatter -> reduce -> push to the root -> root gathers
+    Staged s{};
+    if (is_root) {
+        if ((rc = stage_in(sendbuf, recvbuf, bytes, bytes, in_place, st, s))) return rc;
+    } else {
+        s.recv = nullptr;
+        s.copy_back = false;
+        const void *src = in_place ? recvbuf : sendbuf;
+        if (is_device(src) && (uintptr_t)src % 16 == 0) {
+            s.send = (const char *)src;
+        } else {
+            char *t = (char *)get_scratch(0, bytes);
+            if (!t) return E_NO_MEM;
+            hipMemcpyAsync(t, src, bytes, hipMemcpyDefault, st);
+            s.send = t;
+        }
+    }
+    PipeArgs a{};
+    a.mode = PIPE_RED;
+    a.root = root;
+    a.send = s.send;
+    a.recv = s.recv;
+    a.esize = dt->extent;
+    a.tp = make_tree(w.size, count, dt, root);
+    even_segments(a, bytes, w.size);
+    if ((rc = run_pipe(a, oi, dt, st))) return rc;
+    if (is_root) stage_out(s, st);
+    return finish(st, w.timing);
 }
 
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
@@ -558,52 +550,62 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     if ((rc = require_world())) return rc;
     World &w = world();
     const int n = w.size;
-    size_t total = 0, off = 0;
+    const size_t ext = dt->extent;
+    size_t total = 0, off = 0, padded = 0;
+    bool natural = true;  // every segment starts 16-byte aligned in the caller's layout
     for (int j = 0; j < n; ++j) {
         if (j == w.rank) off = total;
+        if ((total * ext) % 16) natural = false;
         total += recvcounts[j];
+        padded += (recvcounts[j] * ext + 15) & ~(size_t)15;
     }
     if (total == 0) return 0;
     const int oi = op_index(op);
     hipStream_t st = pick_stream(stream);
-    const size_t ext = dt->extent;
     const size_t mycnt = recvcounts[w.rank];
     const bool in_place = sendbuf == (const void *)-1;
     const void *send = in_place ? recvbuf : sendbuf;
-    // sendbuf must be shareable device memory, 16-byte aligned: stage otherwise
-    const char *s_dev = (const char *)send;
-    if (!is_device(send) || (uintptr_t)send % 16) {
-        char *t = (char *)get_scratch(0, total * ext);
-        if (!t) return E_NO_MEM;
-        hipMemcpyAsync(t, send, total * ext, hipMemcpyDefault, st);
-        s_dev = t;
-    }
     if (n == 1 || oi == OP_NO_OP || oi == OP_REPLACE) {
-        if (!in_place && oi != OP_NO_OP) hipMemcpyAsync(recvbuf, s_dev, mycnt * ext, hipMemcpyDefault, st);
+        if (!in_place && oi != OP_NO_OP && mycnt)
+            hipMemcpyAsync(recvbuf, (const char *)send + off * ext, mycnt * ext, hipMemcpyDefault, st);
         return finish(st, false);
     }
-    char *dst = (char *)get_scratch(1, total * ext);
-    if (!dst) return E_NO_MEM;
-    w.seq++;
-    if ((rc = publish(0, s_dev))) return rc;
-    host_barrier();
-    RsArgs a{};
-    for (int j = 0; j < n; ++j) {
-        if (j == w.rank) {
-            a.src.p[j] = s_dev;
-            continue;
+    PipeArgs a{};
+    a.mode = PIPE_RS;
+    a.esize = (int)ext;
+    // operand: the caller's buffer when it is aligned device memory with aligned
+    // segments (and not IN_PLACE: the result overwrites the operand's head);
+    // otherwise a staged copy with every segment padded to 16 bytes
+    if (!in_place && natural && is_device(send) && (uintptr_t)send % 16 == 0) {
+        a.send = (const char *)send;
+        size_t o = 0;
+        for (int j = 0; j < n; ++j) {
+            a.seg_off[j] = o * ext;
+            a.seg_len[j] = recvcounts[j] * ext;
+            o += recvcounts[j];
         }
-        a.src.p[j] = peer_buffer(j, 0, &rc);
-        if (rc) return rc;
+    } else {
+        char *t = (char *)get_scratch(0, padded);
+        if (!t) return E_NO_MEM;
+        size_t o = 0, po = 0;
+        for (int j = 0; j < n; ++j) {
+            const size_t len = recvcounts[j] * ext;
+            if (len) hipMemcpyAsync(t + po, (const char *)send + o * ext, len, hipMemcpyDefault, st);
+            a.seg_off[j] = po;
+            a.seg_len[j] = len;
+            o += recvcounts[j];
+            po += (len + 15) & ~(size_t)15;
+        }
+        a.send = t;
     }
-    for (int j = n; j < kMaxRanks; ++j) a.src.p[j] = a.src.p[0];
-    a.dst = dst;
-    a.sig_peer = w.peer_sig;
-    a.sig_own = w.sig;
-    a.off = off;
-    a.cnt = mycnt;
-    a.n = n;
-    a.me = w.rank;
+    const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0;
+    char *dst = (char *)recvbuf;
+    if (!direct && mycnt) {
+        dst = (char *)get_scratch(1, mycnt * ext);
+        if (!dst) return E_NO_MEM;
+    }
+    a.recv = dst;
+    a.recv_off[w.rank] = 0;
     TreeParams tp{};
     int pof2 = 1, lg = 0;
     while (pof2 * 2 <= n) { pof2 *= 2; ++lg; }
@@ -612,42 +614,8 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     tp.rem = n - pof2;
     tp.linear = 1;
     a.tp = tp;
-    a.epoch = w.seq * 4 + 1;
-    a.err = w.h_err;
-    a.timeout = w.timeout_ticks;
-    const size_t nv = mycnt * ext / 16;
-    int g = (int)std::min<size_t>((nv + 511) / 512, (size_t)grid_cap());
-    if (g < 1) g = 1;
-    LaunchCfg cfg = coll_cfg(g, st);
-    tmark0(st);
-    rc = launch_rs(oi, dt->kind, a, ext, cfg);
-    tmark1(st);
-    if (rc) return rc;
-    if (mycnt) hipMemcpyAsync(recvbuf, dst + off * ext, mycnt * ext, hipMemcpyDefault, st);
-    return finish(st, w.timing);
-}
-
-static int gather_impl(const char *const *srcs, char *dst, const size_t *dst_off, size_t bytes, hipStream_t st) {
-    World &w = world();
-    GatherArgs a{};
-    for (int j = 0; j < kMaxRanks; ++j) a.src.p[j] = j < w.size ? srcs[j] : nullptr;
-    for (int j = 0; j < kMaxRanks; ++j) a.dst_off[j] = j < w.size ? dst_off[j] : 0;
-    a.dst = dst;
-    a.bytes = bytes;
-    a.sig_peer = w.peer_sig;
-    a.sig_own = w.sig;
-    a.n = w.size;
-    a.me = w.rank;
-    a.epoch = w.seq * 4 + 1;
-    a.err = w.h_err;
-    a.timeout = w.timeout_ticks;
-    int g = (int)std::min<size_t>((bytes / 16 + 511) / 512, (size_t)grid_cap());
-    if (g < 1) g = 1;
-    LaunchCfg cfg = coll_cfg(g, st);
-    tmark0(st);
-    int rc = launch_gather(a, cfg);
-    tmark1(st);
-    if (rc) return rc;
+    if ((rc = run_pipe(a, oi, dt, st))) return rc;
+    if (!direct && mycnt) hipMemcpyAsync(recvbuf, dst, mycnt * ext, hipMemcpyDefault, st);
     return finish(st, w.timing);
 }
 
@@ -658,43 +626,35 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
     World &w = world();
     hipStream_t st = pick_stream(stream);
     const int n = w.size;
+    const int me = w.rank;
     const bool in_place = sendbuf == (const void *)-1;
-    char *rdst = (char *)recvbuf;
-    bool copy_back = false;
-    if (!is_device(recvbuf)) {
-        rdst = (char *)get_scratch(1, bytes * n);
-        if (!rdst) return E_NO_MEM;
-        copy_back = true;
-        if (in_place) hipMemcpyAsync(rdst, recvbuf, bytes * n, hipMemcpyDefault, st);
+    const size_t pitch = (bytes + 15) & ~(size_t)15;
+    const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0 && pitch == bytes;
+    char *dst = direct ? (char *)recvbuf : (char *)get_scratch(1, pitch * n);
+    if (!dst) return E_NO_MEM;
+    const char *src = in_place ? (const char *)recvbuf + (size_t)me * bytes : (const char *)sendbuf;
+    if (n == 1) {
+        if (!in_place) hipMemcpyAsync(recvbuf, src, bytes, hipMemcpyDefault, st);
+        return finish(st, false);
     }
-    const char *src = in_place ? rdst + (size_t)w.rank * bytes : (const char *)sendbuf;
-    if (!in_place && !is_device(sendbuf)) {
+    if (!(direct && in_place) && !(is_device(src) && (uintptr_t)src % 16 == 0)) {
         char *t = (char *)get_scratch(0, bytes);
         if (!t) return E_NO_MEM;
-        hipMemcpyAsync(t, sendbuf, bytes, hipMemcpyDefault, st);
+        hipMemcpyAsync(t, src, bytes, hipMemcpyDefault, st);
         src = t;
     }
-    if (n == 1) {
-        if (!in_place) hipMemcpyAsync(rdst, src, bytes, hipMemcpyDeviceToDevice, st);
-    } else {
-        w.seq++;
-        if ((rc = publish(0, src))) return rc;
-        host_barrier();
-        const char *srcs[kMaxRanks];
-        size_t offs[kMaxRanks];
-        for (int j = 0; j < n; ++j) {
-            offs[j] = (size_t)j * bytes;
-            if (j == w.rank) {
-                srcs[j] = in_place ? nullptr : src;
-                continue;
-            }
-            srcs[j] = peer_buffer(j, 0, &rc);
-            if (rc) return rc;
-        }
-        if ((rc = gather_impl(srcs, rdst, offs, bytes, st))) return rc;
+    PipeArgs a{};
+    a.mode = PIPE_AG;
+    a.send = src;
+    a.recv = dst;
+    a.esize = 1;
+    for (int j = 0; j < n; ++j) {
+        a.seg_len[j] = bytes;
+        a.recv_off[j] = (size_t)j * pitch;
     }
-    if (copy_back) hipMemcpyAsync(recvbuf, rdst, bytes * n, hipMemcpyDefault, st);
-    return finish(st, false);
+    if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
+    if (!direct) hipMemcpy2DAsync(recvbuf, bytes, dst, pitch, bytes, n, hipMemcpyDefault, st);
+    return finish(st, w.timing);
 }
 
 int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
@@ -706,28 +666,22 @@ int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
     if (w.size == 1) return 0;
     hipStream_t st = pick_stream(stream);
     char *buf = (char *)buffer;
-    bool copy_back = false;
-    if (!is_device(buffer)) {
+    const bool direct = is_device(buffer) && (uintptr_t)buffer % 16 == 0;
+    if (!direct) {
         buf = (char *)get_scratch(1, bytes);
         if (!buf) return E_NO_MEM;
-        copy_back = w.rank != root;
-        if (w.rank == root) hipMemcpyAsync(buf, buffer, bytes, hipMemcpyHostToDevice, st);
+        if (w.rank == root) hipMemcpyAsync(buf, buffer, bytes, hipMemcpyDefault, st);
     }
-    w.seq++;
-    if (w.rank == root && (rc = publish(0, buf))) return rc;
-    host_barrier();
-    const char *srcs[kMaxRanks] = {};
-    size_t offs[kMaxRanks] = {};
-    if (w.rank != root) {
-        srcs[root] = peer_buffer(root, 0, &rc);
-        if (rc) return rc;
-    }
-    if ((rc = gather_impl(srcs, buf, offs, bytes, st))) return rc;
-    if (copy_back) {
-        hipMemcpyAsync(buffer, buf, bytes, hipMemcpyDeviceToHost, st);
-        return finish(st, false);
-    }
-    return 0;
+    PipeArgs a{};
+    a.mode = PIPE_BC;
+    a.root = root;
+    a.send = buf;
+    a.recv = buf;
+    a.esize = 1;
+    even_segments(a, bytes, w.size);
+    if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
+    if (!direct && w.rank != root) hipMemcpyAsync(buffer, buf, bytes, hipMemcpyDefault, st);
+    return finish(st, w.timing);
 }
 
 // ---------------------------------------------------------------------------

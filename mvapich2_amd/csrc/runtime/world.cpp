@@ -102,10 +102,6 @@ void *get_scratch(int idx, size_t bytes) {
     if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];
     if (w.scratch[idx]) {
         hipStreamSynchronize(w.stream);
-        // evict this allocation from our own IPC handle cache before freeing
-        uint64_t bid = 0;
-        if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)w.scratch[idx]) == hipSuccess)
-            w.own_handles.erase(bid);
         hipFree(w.scratch[idx]);
         w.scratch[idx] = nullptr;
         w.scratch_bytes[idx] = 0;
@@ -137,6 +133,8 @@ static int setup_device_common() {
     w.timeout_ticks = (uint64_t)(env_long("MV2AMD_TIMEOUT_S", 120) * w.wall_clock_khz * 1000.0);
     w.oneshot_max = (size_t)env_long("MV2AMD_ONESHOT_MAX", (long)w.oneshot_max);
     w.max_grid = (int)env_long("MV2AMD_MAX_GRID", w.max_grid);
+    w.pipe_grid = (int)env_long("MV2AMD_PIPE_GRID", w.pipe_grid);
+    w.pipe_sub = (size_t)env_long("MV2AMD_PIPE_SUB", (long)w.pipe_sub);
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
     hipEventCreate(&w.ev0);
     hipEventCreate(&w.ev1);
@@ -231,10 +229,18 @@ int world_init() {
                 MV2_ERR("hipExtMallocWithFlags(uncached) for the one-shot arena failed");
                 return E_NO_MEM;
             }
+            if (hipExtMallocWithFlags((void **)&w.pipe_rs, kPipeRegion, hipDeviceMallocUncached) != hipSuccess ||
+                hipExtMallocWithFlags((void **)&w.pipe_ag, kPipeRegion, hipDeviceMallocUncached) != hipSuccess) {
+                MV2_ERR("hipExtMallocWithFlags(uncached) for the pipeline arenas (2 x %zu MiB) failed",
+                        kPipeRegion >> 20);
+                return E_NO_MEM;
+            }
             hipDeviceSynchronize();
             if (hipIpcGetMemHandle(&me.sig_handle, w.sig) != hipSuccess ||
-                hipIpcGetMemHandle(&me.arena_handle, w.arena) != hipSuccess) {
-                MV2_ERR("hipIpcGetMemHandle failed for the signal page / arena");
+                hipIpcGetMemHandle(&me.arena_handle, w.arena) != hipSuccess ||
+                hipIpcGetMemHandle(&me.pipe_rs_handle, w.pipe_rs) != hipSuccess ||
+                hipIpcGetMemHandle(&me.pipe_ag_handle, w.pipe_ag) != hipSuccess) {
+                MV2_ERR("hipIpcGetMemHandle failed for the signal page / arenas");
                 return E_OTHER;
             }
             me.arena_bytes = arena_bytes;
@@ -244,20 +250,26 @@ int world_init() {
                 if (j == w.rank) {
                     w.peer_sig.p[j] = w.sig;
                     w.peer_arena[j] = w.arena;
+                    w.peer_rs.p[j] = w.pipe_rs;
+                    w.peer_ag.p[j] = w.pipe_ag;
                     continue;
                 }
                 if (w.shm->r[j].slot_bytes != w.slot_bytes) {
                     MV2_ERR("MV2AMD_ONESHOT_MAX differs between ranks");
                     return E_OTHER;
                 }
-                void *ps = nullptr, *pa = nullptr;
+                void *ps = nullptr, *pa = nullptr, *pr = nullptr, *pg = nullptr;
                 if (hipIpcOpenMemHandle(&ps, w.shm->r[j].sig_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
-                    hipIpcOpenMemHandle(&pa, w.shm->r[j].arena_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    hipIpcOpenMemHandle(&pa, w.shm->r[j].arena_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                    hipIpcOpenMemHandle(&pr, w.shm->r[j].pipe_rs_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                    hipIpcOpenMemHandle(&pg, w.shm->r[j].pipe_ag_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                     MV2_ERR("hipIpcOpenMemHandle failed for rank %d (peer access over xGMI?)", j);
                     return E_OTHER;
                 }
                 w.peer_sig.p[j] = (uint64_t *)ps;
                 w.peer_arena[j] = (char *)pa;
+                w.peer_rs.p[j] = (char *)pr;
+                w.peer_ag.p[j] = (char *)pg;
             }
             host_barrier();
         }
@@ -274,11 +286,11 @@ int world_finalize() {
     if (w.size > 1 && w.shm) {
         host_barrier();
         for (int j = 0; j < kMaxRanks; ++j) {
-            for (auto &kv : w.peer_maps[j]) hipIpcCloseMemHandle(kv.second.ptr);
-            w.peer_maps[j].clear();
             if (j != w.rank && j < w.size && w.size <= kMaxRanks) {
                 if (w.peer_sig.p[j]) hipIpcCloseMemHandle(w.peer_sig.p[j]);
                 if (w.peer_arena[j]) hipIpcCloseMemHandle(w.peer_arena[j]);
+                if (w.peer_rs.p[j]) hipIpcCloseMemHandle(w.peer_rs.p[j]);
+                if (w.peer_ag.p[j]) hipIpcCloseMemHandle(w.peer_ag.p[j]);
             }
         }
         host_barrier();  // nobody maps our pages any more
@@ -290,6 +302,8 @@ int world_finalize() {
         if (w.scratch[i]) hipFree(w.scratch[i]);
     if (w.sig) hipFree(w.sig);
     if (w.arena) hipFree(w.arena);
+    if (w.pipe_rs) hipFree(w.pipe_rs);
+    if (w.pipe_ag) hipFree(w.pipe_ag);
     w.finalized = true;
     return 0;
 }

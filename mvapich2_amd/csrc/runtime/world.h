@@ -6,15 +6,18 @@
 //   * signal page per rank (hipDeviceMallocUncached, IPC-shared): 64-bit
 //     epoch flags [source rank][workgroup]
 //   * one-shot arena per rank (uncached, IPC-shared): [parity][source][slot]
-//   * user buffers exported on demand through a hipIpc handle cache keyed by
-//     allocation id (the reference's cudaipc regcache, ibv_cuda_ipc.c:71-187)
+//   * pipeline arenas per rank (uncached, IPC-shared): RS and AG regions of
+//     [parity][source][kPipeSlot] (coll/pipe.h)
+// User buffers are never exported: peers only ever store into these
+// library-owned arenas, so an application may hipFree a buffer right after
+// a call (the reference's cudaipc regcache, ibv_cuda_ipc.c:71-187, is not
+// needed and its stale-mapping hazard does not exist).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <atomic>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "../common.h"
@@ -23,15 +26,6 @@
 namespace mv2 {
 
 constexpr int kShmMaxRanks = 64;
-
-struct BufDesc {
-    hipIpcMemHandle_t handle;
-    uint64_t buffer_id;
-    uint64_t base;
-    uint64_t alloc_size;
-    uint64_t offset;
-    uint64_t seq;
-};
 
 struct alignas(64) ShmRank {
     std::atomic<uint64_t> arrive;  // host barrier generation
@@ -44,7 +38,8 @@ struct alignas(64) ShmRank {
     hipIpcMemHandle_t arena_handle;
     uint64_t arena_bytes;
     uint64_t slot_bytes;
-    BufDesc desc[2];  // per-call published buffers (send, recv)
+    hipIpcMemHandle_t pipe_rs_handle;
+    hipIpcMemHandle_t pipe_ag_handle;
 };
 
 struct ShmSeg {
@@ -53,13 +48,6 @@ struct ShmSeg {
     int size;
     int pad;
     ShmRank r[kShmMaxRanks];
-};
-
-struct Mapping {
-    char *ptr;        // mapped base in this process
-    uint64_t peer_base;  // allocation base in the peer's address space
-    uint64_t alloc_size;
-    uint64_t last_use;
 };
 
 struct World {
@@ -79,6 +67,12 @@ struct World {
     char *arena = nullptr;
     char *peer_arena[kMaxRanks] = {};
     size_t slot_bytes = 0;
+    // pipelined-collective arenas (coll/pipe.h): RS and AG regions, kPipeRegion bytes each
+    char *pipe_rs = nullptr, *pipe_ag = nullptr;
+    PeerTableW peer_rs{}, peer_ag{};
+    uint64_t epoch = 0;       // last flag epoch used (identical on every rank)
+    uint64_t round = 0;       // pipeline rounds issued (slot parity)
+    uint64_t os_calls = 0;    // one-shot calls issued (arena parity)
 
     int *h_err = nullptr;     // pinned host error word written by kernels on timeout
     uint64_t timeout_ticks = 0;
@@ -87,17 +81,14 @@ struct World {
     // tuning
     size_t oneshot_max = 256 * 1024;
     int max_grid = 1024;
+    int pipe_grid = kPipeMaxGrid;                 // pipelined collectives: workgroups (<= kPipeMaxGrid)
+    size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int rl_grid = 4096;       // reduce_local grid cap (tools/rl_variants.hip sweep)
 
     // timing (bench)
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
-
-    // ipc caches
-    std::unordered_map<uint64_t, hipIpcMemHandle_t> own_handles;  // buffer_id -> handle
-    std::unordered_map<uint64_t, Mapping> peer_maps[kMaxRanks];    // (peer) buffer_id -> mapping
-    uint64_t use_clock = 0;
 
     // scratch device buffers (host-buffer staging, misalignment, Reduce non-roots)
     void *scratch[3] = {};

@@ -1,7 +1,9 @@
 """Part (2) parity: the device collectives, one process per rank, several
-ranks sharing the test box's single GPU (peer buffers mapped through hipIpc
+ranks sharing the test box's single GPU (peers' arenas mapped through hipIpc
 exactly as across GPUs).  Results are compared bit-exactly with the oracle's
-simulation of the reference's algorithm for the same selection."""
+simulation of the reference's algorithm for the same selection.  The "small"
+geometry forces 3 workgroups x 4 KiB per round, so large cases run dozens of
+rounds and reuse both arena parities within and across calls."""
 import json
 import os
 import subprocess
@@ -24,7 +26,10 @@ def inputs(case, rank):
     return rand_typed(case["type"], case["count"], rng, small=case.get("small", False))
 
 
-def run_workers(n, cases, tmp_path, timeout=400):
+GEOMS = {"default": {}, "small": {"MV2AMD_PIPE_GRID": "3", "MV2AMD_PIPE_SUB": "4096"}}
+
+
+def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"cases": cases}))
     out = tmp_path / "out"
@@ -33,7 +38,7 @@ def run_workers(n, cases, tmp_path, timeout=400):
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
-                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="60", MV2AMD_DEVICE="0")
+                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="30", MV2AMD_DEVICE="0", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), str(spec),
                                        str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
@@ -59,11 +64,11 @@ BASIC = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_F
          ("MPI_SUM", "MPI_INT"), ("MPI_PROD", "MPI_INT"), ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_LAND", "MPI_C_BOOL"),
          ("MPI_MAXLOC", "MPI_DOUBLE_INT"), ("MPI_MINLOC", "MPI_2INT"), ("MPI_SUM", "MPI_C_FLOAT_COMPLEX"),
          ("MPI_MAXLOC", "MPI_SHORT_INT")]
-COUNTS = [1, 3, 100, 4099, 70001, 300007]  # one-shot (<=256 KiB) and two-shot sizes, ragged tails
+COUNTS = [1, 3, 100, 4099, 70001, 300007]  # one-shot (<=256 KiB) and pipelined sizes, ragged tails
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
-def test_collectives_multiprocess(n, tmp_path, golden):
+@pytest.mark.parametrize("n,geom", [(2, "default"), (3, "default"), (4, "default"), (3, "small"), (4, "small")])
+def test_collectives_multiprocess(n, geom, tmp_path, golden):
     cases = []
     seed = 1
     for op, t in BASIC:
@@ -77,18 +82,22 @@ def test_collectives_multiprocess(n, tmp_path, golden):
         cases.append({"id": f"ip{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
                       "count": count, "seed": seed})
         seed += 1
-    cases.append({"id": f"rd{seed}", "kind": "reduce", "type": "MPI_DOUBLE", "op": "MPI_SUM", "count": 5000,
-                  "seed": seed, "root": n - 1})
+    for count, root in ((5000, n - 1), (70001, 1), (300007, 0)):
+        cases.append({"id": f"rd{seed}", "kind": "reduce", "type": "MPI_DOUBLE", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
+    cases.append({"id": f"ar{seed}", "kind": "allreduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": 1 << 21,
+                  "seed": seed})
     seed += 1
-    for counts in ([1] * n, [1000 + r for r in range(n)], [70001] * n, [0] + [33] * (n - 1)):
+    for counts in ([1] * n, [1000 + r for r in range(n)], [70001] * n, [65536] * n, [0] + [33] * (n - 1)):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
                       "recvcounts": counts, "count": sum(counts), "seed": seed})
         seed += 1
-    for count in (1, 13, 4096, 1 << 20):
+    for count in (1, 13, 4096, 100003, 1 << 20):
         cases.append({"id": f"ag{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": count,
                       "seed": seed})
         seed += 1
-    for count in (1, 1000, 1 << 20):
+    for count in (1, 1000, 70001, 1 << 20):
         cases.append({"id": f"bc{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
                       "seed": seed, "root": 1 % n})
         seed += 1
@@ -107,7 +116,7 @@ def test_collectives_multiprocess(n, tmp_path, golden):
                           "count": c["count"], "seed": seed, "golden": c["id"]})
             seed += 1
 
-    res = run_workers(n, cases, tmp_path)
+    res = run_workers(n, cases, tmp_path, extra_env=GEOMS[geom])
 
     for case in cases:
         k, cid, t = case["kind"], case["id"], case.get("type")

@@ -1,0 +1,120 @@
+"""The N>1 decomposition of the device allreduce (k_pipe PIPE_AR), on CPU.
+
+Each rank reduces its 16-byte-aligned segment in the reference's order from
+the other ranks' arena slots and pushes the result to every peer's AG slot.
+A host model of the segments, rounds, workgroup ranges and slots
+(tests/pipe_model.py) must reproduce the oracle's rank-by-rank simulation of
+MV2's MPI_Allreduce bit for bit, for n = 2..8 and geometries with several
+rounds and workgroups.  A two-process gloo run exchanges the slot contents
+over torch.distributed where the kernel stores into peers' arenas."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from mvapich2_amd.consts import OPS, TYPES
+from oracle import oracle
+from tests import pipe_model as pm
+from tests.helpers import assert_bytes_equal, rand_typed
+
+CASES = [("MPI_FLOAT", "MPI_SUM", 70001), ("MPI_DOUBLE", "MPI_MAX", 20011), ("MPI_INT", "MPI_PROD", 9000),
+         ("MPI_DOUBLE_INT", "MPI_MAXLOC", 5003), ("MPI_FLOAT", "MPI_SUM", 100), ("MPI_SHORT_INT", "MPI_MINLOC", 3001),
+         ("MPI_UNSIGNED_CHAR", "MPI_BXOR", 40003)]
+
+
+def inputs(t, count, rank, seed):
+    return rand_typed(t, count, np.random.default_rng(seed * 100 + rank), small=True).view(np.uint8).ravel().copy()
+
+
+def test_geometry_matches_runtime_rules():
+    # 256 MiB fp32 on 8 ranks: 32 MiB segments, 128 workgroups x 64 KiB, 4 rounds
+    assert pm.pipe_geom(32 << 20) == (128, 64 << 10, 8 << 20, 4)
+    # 1 MiB segment: 64 workgroups x 16 KiB, one round
+    assert pm.pipe_geom(1 << 20) == (64, 16 << 10, 1 << 20, 1)
+    # tests sharing one GPU between 4 ranks: grid capped at cus / 4
+    assert pm.pipe_geom(32 << 20, nshare=4)[0] == 64
+    segs = pm.even_segments(1000003, 8)
+    assert all(o % 16 == 0 for o, _ in segs) and sum(l for _, l in segs) == 1000003
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8])
+def test_pipe_allreduce_model_matches_oracle(n):
+    for seed, (t, op, count) in enumerate(CASES):
+        h, _, size, ext = TYPES[t]
+        xs = [inputs(t, count, r, seed) for r in range(n)]
+        tp = pm.tree_params(n, count, size)
+        # small pipe_sub / grid: several rounds and workgroups per segment, ragged last ranges
+        got = pm.allreduce(xs, count, ext, h, OPS[op], tp, geom_kw={"pipe_grid": 3, "pipe_sub": 4096})
+        want = oracle.allreduce([x.copy() for x in xs], count, h, OPS[op])
+        for r in range(n):
+            assert_bytes_equal(got[r], want[r], t, count, f"n={n} rank {r} {t} {op}")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, n, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    try:
+        for seed, (t, op, count) in enumerate(CASES[:4]):
+            h, _, size, ext = TYPES[t]
+            mine = inputs(t, count, rank, seed)
+            nbytes = count * ext
+            segs = pm.even_segments(nbytes, n)
+            tp = pm.tree_params(n, count, size)
+            # P1: my part of segment j goes to rank j (all_to_all of the segment slices)
+            send = [torch.from_numpy(mine[o:o + ln].copy()) for o, ln in segs]
+            myo, myl = segs[rank]
+            recv = [torch.zeros(myl, dtype=torch.uint8) for _ in range(n)]
+            reqs = []
+            for j in range(n):
+                if j == rank:
+                    recv[j] = send[j]
+                else:
+                    reqs.append(dist.isend(send[j], j))
+                    reqs.append(dist.irecv(recv[j], j))
+            for r in reqs:
+                r.wait()
+            res = pm.reduce_range([r.numpy() for r in recv], myo // ext, ext, h, OPS[op], tp)
+            # P2 push + P3 gather: every rank receives every reduced segment
+            maxl = max(ln for _, ln in segs)
+            pad = np.zeros(maxl, dtype=np.uint8)
+            pad[:len(res)] = res
+            allr = [torch.zeros(maxl, dtype=torch.uint8) for _ in range(n)]
+            dist.all_gather(allr, torch.from_numpy(pad))
+            out = np.zeros(nbytes, dtype=np.uint8)
+            for j, (o, ln) in enumerate(segs):
+                out[o:o + ln] = allr[j].numpy()[:ln]
+            allx = [torch.zeros(len(mine), dtype=torch.uint8) for _ in range(n)]
+            dist.all_gather(allx, torch.from_numpy(mine))
+            xs = [a.numpy() for a in allx]
+            want = oracle.allreduce([x.copy() for x in xs], count, h, OPS[op])[rank]
+            assert_bytes_equal(out, want, t, count, f"gloo rank {rank} {t} {op}")
+        q.put((rank, "ok"))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipe_decomposition_gloo_world2():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
