@@ -57,7 +57,7 @@ int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg
 }
 
 int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg) {
-    hipLaunchKernelGGL((k_pipe<NoReduce>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+    hipLaunchKernelGGL((k_pipe<NoReduce>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
     return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
 }
 

@@ -48,9 +48,10 @@ enum PipeMode : int {
 //   [parity 0..1][source rank 0..kMaxRanks-1][kPipeSlot bytes]
 // Round k of a call uses parity (round0 + k) & 1; block b moves the bytes
 // [k*tseg + b*tsub, +tsub) of every segment, stored at slot offset b*tsub.
-constexpr size_t kPipeSlot = (size_t)8 << 20;   // >= kPipeMaxGrid * kPipeMaxSub
-constexpr int kPipeMaxGrid = 128;
+constexpr int kPipeThreads = 512;                // 8 waves per workgroup
+constexpr int kPipeMaxGrid = 256;                // one workgroup per CU
 constexpr size_t kPipeMaxSub = (size_t)64 << 10;
+constexpr size_t kPipeSlot = (size_t)kPipeMaxGrid * kPipeMaxSub;  // 16 MiB
 constexpr size_t kPipeRegion = 2 * (size_t)kMaxRanks * kPipeSlot;
 
 struct PipeArgs {
@@ -69,6 +70,7 @@ struct PipeArgs {
     SigTable sig_peer;
     uint64_t *sig_own;
     uint64_t epoch0;                // round k uses epochs epoch0 + 2k and epoch0 + 2k + 1
+    int light;                      // 1: signal without the system-scope L2 writeback (uncached data)
     TreeParams tp;
     int *err;
     uint64_t timeout;

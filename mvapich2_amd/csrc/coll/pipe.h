@@ -23,9 +23,15 @@
 //       P3 gather (scatter + allgather broadcast, bcast_osu.c:1905 family)
 //
 // Slot reuse: round k writes parity (round0+k)&1.  A rank writes a slot of
-// parity p in round k+2 only after waiting (in round k+1) on a flag the
-// owner raised after it finished reading round k, and successive calls are
-// stream-ordered on every GPU, so two rounds of slots are enough.
+// parity p in round k+2 only after waiting on a flag the owner raised after
+// it finished reading round k (AR/RS/RED: E(k+2) follows the owner's P2(k+1),
+// which follows its P3(k) and P2(k)), and successive calls are stream-ordered
+// on every GPU, so two rounds of slots are enough.
+//
+// Release: every byte a peer reads lives in uncached arena memory, so a
+// signal only needs the workgroup's stores acknowledged (s_waitcnt vmcnt(0))
+// before the flag store; the system-scope release fence (an L2 writeback of
+// unrelated dirty lines on every signal) is kept as an option (light = 0).
 #pragma once
 #include <type_traits>
 
@@ -39,34 +45,139 @@ struct Dsts {
     char *p[kMaxRanks + 1];  // nullptr = skip
 };
 
+// up to kMaxRanks independent copies (len 0 = unused); all pointers 16-byte aligned
+struct Jobs {
+    const char *src[kMaxRanks];
+    char *dst[kMaxRanks];
+    size_t len[kMaxRanks];
+};
+
 __device__ __forceinline__ char *pslot(char *region, uint64_t par, int src) {
     return region + ((size_t)par * kMaxRanks + (size_t)src) * kPipeSlot;
 }
 
-// Block-wide copy of nbytes from src to every non-null destination.
-// src and destinations 16-byte aligned; the last partial vector goes bytewise.
-template <int U>
-__device__ __forceinline__ void blk_copy(const Dsts &d, const char *src, size_t nbytes) {
-    const size_t nv = nbytes >> 4;
-    const v4u *s = (const v4u *)src;
-    size_t i = threadIdx.x;
-    for (; i + (size_t)(U - 1) * kThreads < nv; i += (size_t)U * kThreads) {
-        v4u v[U];
+// The copy / reduce loops below are software-pipelined: the loads of the next
+// 16-byte column are issued before the stores of the current one.  Stores and
+// loads share the in-order vmcnt counter on CDNA, so without the prefetch
+// every column would wait for the previous column's (remote, xGMI) stores to
+// be acknowledged before its own loads could return.
+
+// Block-wide: every job j copies len[j] bytes.  The jobs' 16-byte columns
+// form one flat, job-major index space, so each thread keeps U columns (plus
+// the next U) in flight whatever the number of jobs (1 peer at n = 2, 7 at 8).
+// The job table lives in LDS: a column's job is found by a scan over the
+// prefix sums there (dynamically indexed private arrays would go to scratch).
+struct JobTable {
+    size_t pre[kMaxRanks + 1];
+    const char *src[kMaxRanks];
+    char *dst[kMaxRanks];
+};
+
+__device__ __forceinline__ void job_addr(const JobTable &t, size_t f, const v4u *&s, v4u *&d) {
+    int j = 0;
+    for (int k = 1; k < kMaxRanks; ++k) j = f >= t.pre[k] ? k : j;
+    s = (const v4u *)t.src[j] + (f - t.pre[j]);
+    d = (v4u *)t.dst[j] + (f - t.pre[j]);
+}
+
+__device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
+    constexpr int U = 4;
+    __shared__ JobTable t;
+    __syncthreads();  // previous users of the table are done
+    if (threadIdx.x == 0) {
+        size_t acc = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = ld_nt(s + i + (size_t)u * kThreads);
+        for (int j = 0; j < kMaxRanks; ++j) {
+            t.pre[j] = acc;
+            t.src[j] = jb.src[j];
+            t.dst[j] = jb.dst[j];
+            acc += jb.len[j] >> 4;
+        }
+        t.pre[kMaxRanks] = acc;
+    }
+    __syncthreads();
+    const size_t NV = t.pre[kMaxRanks];
+    size_t f = threadIdx.x;
+    if (f < NV) {
+        v4u cur[U], nxt[U];
+        const v4u *s;
+        v4u *d;
 #pragma unroll
-        for (int k = 0; k < kMaxRanks + 1; ++k) {
-            if (d.p[k]) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) st_nt((v4u *)d.p[k] + i + (size_t)u * kThreads, v[u]);
+        for (int u = 0; u < U; ++u) {
+            const size_t fu = f + (size_t)u * kPipeThreads;
+            if (fu < NV) {
+                job_addr(t, fu, s, d);
+                cur[u] = ld_nt(s);
             }
         }
-    }
-    for (; i < nv; i += kThreads) {
-        const v4u v = ld_nt(s + i);
+        for (;;) {
+            const size_t fn = f + (size_t)U * kPipeThreads;
+            const bool more = fn < NV;
+            if (more) {
 #pragma unroll
-        for (int k = 0; k < kMaxRanks + 1; ++k)
-            if (d.p[k]) st_nt((v4u *)d.p[k] + i, v);
+                for (int u = 0; u < U; ++u) {
+                    const size_t fu = fn + (size_t)u * kPipeThreads;
+                    if (fu < NV) {
+                        job_addr(t, fu, s, d);
+                        nxt[u] = ld_nt(s);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t fu = f + (size_t)u * kPipeThreads;
+                if (fu < NV) {
+                    job_addr(t, fu, s, d);
+                    st_nt(d, cur[u]);
+                }
+            }
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            f = fn;
+        }
+    }
+    if (threadIdx.x < 16) {
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) {
+            const size_t o = (jb.len[j] & ~(size_t)15) + threadIdx.x;
+            if (o < jb.len[j]) jb.dst[j][o] = jb.src[j][o];
+        }
+    }
+}
+
+// Block-wide copy of nbytes from one source to every non-null destination.
+__device__ __forceinline__ void blk_copy_multi(const Dsts &d, const char *src, size_t nbytes) {
+    constexpr int U = 4;
+    const size_t nv = nbytes >> 4;
+    const v4u *s = (const v4u *)src;
+    size_t x = threadIdx.x;
+    if (x < nv) {
+        v4u cur[U], nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (x + (size_t)u * kPipeThreads < nv) cur[u] = ld_nt(s + x + (size_t)u * kPipeThreads);
+        for (;;) {
+            const size_t xn = x + (size_t)U * kPipeThreads;
+            const bool more = xn < nv;
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (xn + (size_t)u * kPipeThreads < nv) nxt[u] = ld_nt(s + xn + (size_t)u * kPipeThreads);
+            }
+#pragma unroll
+            for (int k = 0; k < kMaxRanks + 1; ++k) {
+                if (d.p[k]) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (x + (size_t)u * kPipeThreads < nv) st_nt((v4u *)d.p[k] + x + (size_t)u * kPipeThreads, cur[u]);
+                }
+            }
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            x = xn;
+        }
     }
     const size_t tb = nbytes & 15;
     if (threadIdx.x < tb) {
@@ -87,24 +198,44 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const size_t nv = nbytes >> 4;
-    for (size_t i = threadIdx.x; i < nv; i += (size_t)U * kThreads) {
-        v4u v[U][kMaxRanks];
+    size_t x = threadIdx.x;
+    if (x < nv) {
+        v4u cur[U][kMaxRanks], nxt[U][kMaxRanks];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t x = i + (size_t)u * kThreads;
+            const size_t xu = x + (size_t)u * kPipeThreads;
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
-                v[u][j] = (j < a.n && x < nv) ? ld_nt((const v4u *)src[j] + x) : v4u{0, 0, 0, 0};
+                cur[u][j] = (j < a.n && xu < nv) ? ld_nt((const v4u *)src[j] + xu) : v4u{0, 0, 0, 0};
         }
+        for (;;) {
+            const size_t xn = x + (size_t)U * kPipeThreads;
+            const bool more = xn < nv;
+            if (more) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t x = i + (size_t)u * kThreads;
-            if (x < nv) {
-                const v4u r = vreduce_n<Rd>(v[u], a.n, a.tp, ebase + x * N);
+                for (int u = 0; u < U; ++u) {
+                    const size_t xu = xn + (size_t)u * kPipeThreads;
 #pragma unroll
-                for (int k = 0; k < kMaxRanks + 1; ++k)
-                    if (d.p[k]) st_nt((v4u *)d.p[k] + x, r);
+                    for (int j = 0; j < kMaxRanks; ++j)
+                        nxt[u][j] = (j < a.n && xu < nv) ? ld_nt((const v4u *)src[j] + xu) : v4u{0, 0, 0, 0};
+                }
             }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t xu = x + (size_t)u * kPipeThreads;
+                if (xu < nv) {
+                    const v4u r = vreduce_n<Rd>(cur[u], a.n, a.tp, ebase + xu * N);
+#pragma unroll
+                    for (int k = 0; k < kMaxRanks + 1; ++k)
+                        if (d.p[k]) st_nt((v4u *)d.p[k] + xu, r);
+                }
+            }
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < kMaxRanks; ++j) cur[u][j] = nxt[u][j];
+            x = xn;
         }
     }
     const size_t tail = (nbytes & 15) / sizeof(T);
@@ -120,70 +251,113 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
     }
 }
 
+__device__ __forceinline__ size_t range_len(const PipeArgs &a, int j, size_t rbase) {
+    return rbase < a.seg_len[j] ? (a.seg_len[j] - rbase < a.tsub ? a.seg_len[j] - rbase : a.tsub) : 0;
+}
+
+// P3: my AG slots [par][j] -> recv segment j, for every j != me (and != skip)
+__device__ __forceinline__ void gather_slots(const PipeArgs &a, uint64_t par, size_t rbase, size_t soff, int skip) {
+    Jobs jb{};
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) {
+        if (j < a.n && j != a.me && j != skip) {
+            jb.src[j] = pslot(a.ag_peer.p[a.me], par, j) + soff;
+            jb.dst[j] = a.recv + a.recv_off[j] + rbase;
+            jb.len[j] = range_len(a, j, rbase);
+        }
+    }
+    blk_copy_jobs(jb);
+}
+
+// P1 of round k: my part of every other segment -> its owner's RS slot [par][me]
+// (all n-1 links at once)
+__device__ __forceinline__ void scatter_round(const PipeArgs &a, int k) {
+    const uint64_t par = (a.round0 + (uint64_t)k) & 1;
+    const size_t rbase = (size_t)k * a.tseg + (size_t)blockIdx.x * a.tsub;
+    const size_t soff = (size_t)blockIdx.x * a.tsub;
+    Jobs jb{};
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) {
+        if (j < a.n && j != a.me) {
+            jb.src[j] = a.send + a.seg_off[j] + rbase;
+            jb.dst[j] = pslot(a.rs_peer.p[j], par, a.me) + soff;
+            jb.len[j] = range_len(a, j, rbase);
+        }
+    }
+    blk_copy_jobs(jb);
+}
+
+// P2 of round k: reduce my segment's range from the n RS slots (own operand
+// straight from sendbuf); AR: result -> recv + every peer's AG slot [par][me];
+// RS: -> recv; RED: root -> recv, others -> the root's AG slot [par][me]
 template <class Rd>
-__global__ __launch_bounds__(kThreads) void k_pipe(PipeArgs a) {
+__device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
+    const uint64_t par = (a.round0 + (uint64_t)k) & 1;
+    const size_t rbase = (size_t)k * a.tseg + (size_t)blockIdx.x * a.tsub;
+    const size_t soff = (size_t)blockIdx.x * a.tsub;
+    const int me = a.me;
+    const size_t len = range_len(a, me, rbase);
+    if (!len) return;
+    const char *src[kMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j)
+        src[j] = (j == me || j >= a.n) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+    Dsts d{};
+    if (a.mode == PIPE_AR) {
+        d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j)
+            if (j < a.n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
+    } else if (a.mode == PIPE_RS || me == a.root) {
+        d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
+    } else {
+        d.p[0] = pslot(a.ag_peer.p[a.root], par, me) + soff;
+    }
+    // fewer sources -> more columns per thread, so >= 4 loads stay in flight
+    if (a.n <= 4) blk_reduce<Rd, 2>(a, src, d, len, (a.seg_off[me] + rbase) / (size_t)a.esize);
+    else blk_reduce<Rd, 1>(a, src, d, len, (a.seg_off[me] + rbase) / (size_t)a.esize);
+}
+
+template <class Rd>
+__global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
     const int b = blockIdx.x;
     const int n = a.n, me = a.me;
     const unsigned all = (1u << n) - 1u;
+    if (a.mode == PIPE_AR || a.mode == PIPE_RS || a.mode == PIPE_RED) {
+        if constexpr (!std::is_same<Rd, NoReduce>::value) {
+            // Rounds overlap: the scatter of round k+1 runs while the peers finish
+            // round k's reduction, and round k's gather follows it, so neither flag
+            // wait sits on an idle workgroup.
+            //   P1(0) E(0) | wait E(k); P2(k); E(k)+1; P1(k+1); E(k+1); wait E(k)+1; P3(k) |
+            const bool gathers = a.mode == PIPE_AR || (a.mode == PIPE_RED && me == a.root);
+            if (a.nrounds > 0) {
+                scatter_round(a, 0);
+                signal_peers(a.sig_peer, n, me, b, a.epoch0, a.light);
+            }
+            for (int k = 0; k < a.nrounds; ++k) {
+                const uint64_t E = a.epoch0 + 2 * (uint64_t)k;
+                if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout)) return;
+                reduce_round<Rd>(a, k);
+                if (a.mode != PIPE_RS) signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
+                if (k + 1 < a.nrounds) {
+                    scatter_round(a, k + 1);
+                    signal_peers(a.sig_peer, n, me, b, E + 2, a.light);
+                }
+                if (!gathers) continue;
+                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
+                const size_t rbase = (size_t)k * a.tseg + (size_t)b * a.tsub;
+                gather_slots(a, (a.round0 + (uint64_t)k) & 1, rbase, (size_t)b * a.tsub, -1);
+            }
+        }
+        return;
+    }
     for (int k = 0; k < a.nrounds; ++k) {
         const uint64_t par = (a.round0 + (uint64_t)k) & 1;
         const uint64_t E = a.epoch0 + 2 * (uint64_t)k;
         const size_t rbase = (size_t)k * a.tseg + (size_t)b * a.tsub;  // segment-relative
         const size_t soff = (size_t)b * a.tsub;                        // slot-relative
-        auto rlen = [&](int j) -> size_t {
-            return rbase < a.seg_len[j] ? (a.seg_len[j] - rbase < a.tsub ? a.seg_len[j] - rbase : a.tsub) : 0;
-        };
-        if (a.mode == PIPE_AR || a.mode == PIPE_RS || a.mode == PIPE_RED) {
-            if constexpr (!std::is_same<Rd, NoReduce>::value) {
-                // P1: scatter my part of every other segment (rotated so blocks spread over links)
-                for (int s = 0; s < n - 1; ++s) {
-                    const int j = (me + 1 + (b + s) % (n - 1)) % n;
-                    const size_t len = rlen(j);
-                    if (len) {
-                        Dsts d{};
-                        d.p[0] = pslot(a.rs_peer.p[j], par, me) + soff;
-                        blk_copy<4>(d, a.send + a.seg_off[j] + rbase, len);
-                    }
-                }
-                signal_peers(a.sig_peer, n, me, b, E);
-                if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout)) return;
-                // P2: reduce my segment
-                const size_t len = rlen(me);
-                if (len) {
-                    const char *src[kMaxRanks];
-#pragma unroll
-                    for (int j = 0; j < kMaxRanks; ++j)
-                        src[j] = (j == me || j >= n) ? a.send + a.seg_off[me] + rbase
-                                                     : pslot(a.rs_peer.p[me], par, j) + soff;
-                    Dsts d{};
-                    if (a.mode == PIPE_AR) {
-                        d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
-#pragma unroll
-                        for (int j = 0; j < kMaxRanks; ++j)
-                            if (j < n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
-                    } else if (a.mode == PIPE_RS || me == a.root) {
-                        d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
-                    } else {
-                        d.p[0] = pslot(a.ag_peer.p[a.root], par, me) + soff;
-                    }
-                    blk_reduce<Rd, 1>(a, src, d, len, (a.seg_off[me] + rbase) / (size_t)a.esize);
-                }
-                if (a.mode == PIPE_RS) continue;
-                signal_peers(a.sig_peer, n, me, b, E + 1);
-                if (a.mode == PIPE_RED && me != a.root) continue;
-                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
-                // P3: gather the other segments' results
-                for (int s = 0; s < n - 1; ++s) {
-                    const int j = (me + 1 + (b + s) % (n - 1)) % n;
-                    const size_t l = rlen(j);
-                    if (l) {
-                        Dsts d{};
-                        d.p[0] = a.recv + a.recv_off[j] + rbase;
-                        blk_copy<4>(d, pslot(a.ag_peer.p[me], par, j) + soff, l);
-                    }
-                }
-            }
-        } else if (a.mode == PIPE_AG) {
+        auto rlen = [&](int j) -> size_t { return range_len(a, j, rbase); };
+        if (a.mode == PIPE_AG) {
             const size_t len = rlen(me);
             if (len) {
                 Dsts d{};
@@ -191,30 +365,25 @@ __global__ __launch_bounds__(kThreads) void k_pipe(PipeArgs a) {
                 for (int j = 0; j < kMaxRanks; ++j)
                     if (j < n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
                 if (a.send != a.recv + a.recv_off[me]) d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
-                blk_copy<4>(d, a.send + rbase, len);
+                blk_copy_multi(d, a.send + rbase, len);
             }
-            signal_peers(a.sig_peer, n, me, b, E);
+            signal_peers(a.sig_peer, n, me, b, E, a.light);
             if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout)) return;
-            for (int s = 0; s < n - 1; ++s) {
-                const int j = (me + 1 + (b + s) % (n - 1)) % n;
-                const size_t l = rlen(j);
-                if (l) {
-                    Dsts d{};
-                    d.p[0] = a.recv + a.recv_off[j] + rbase;
-                    blk_copy<4>(d, pslot(a.ag_peer.p[me], par, j) + soff, l);
-                }
-            }
+            gather_slots(a, par, rbase, soff, -1);
         } else {  // PIPE_BC (send == recv == the buffer, seg_off == recv_off)
             const int root = a.root;
             if (me == root) {
-                for (int s = 0; s < n - 1; ++s) {
-                    const int j = (me + 1 + (b + s) % (n - 1)) % n;
-                    const size_t l = rlen(j);
-                    if (l) {
-                        Dsts d{};
-                        d.p[0] = pslot(a.rs_peer.p[j], par, root) + soff;
-                        blk_copy<4>(d, a.send + a.seg_off[j] + rbase, l);
+                {
+                    Jobs jb{};
+#pragma unroll
+                    for (int j = 0; j < kMaxRanks; ++j) {
+                        if (j < n && j != root) {
+                            jb.src[j] = a.send + a.seg_off[j] + rbase;
+                            jb.dst[j] = pslot(a.rs_peer.p[j], par, root) + soff;
+                            jb.len[j] = rlen(j);
+                        }
                     }
+                    blk_copy_jobs(jb);
                 }
                 const size_t l = rlen(root);
                 if (l) {
@@ -222,9 +391,9 @@ __global__ __launch_bounds__(kThreads) void k_pipe(PipeArgs a) {
 #pragma unroll
                     for (int j = 0; j < kMaxRanks; ++j)
                         if (j < n && j != root) d.p[j] = pslot(a.ag_peer.p[j], par, root) + soff;
-                    blk_copy<4>(d, a.send + a.seg_off[root] + rbase, l);
+                    blk_copy_multi(d, a.send + a.seg_off[root] + rbase, l);
                 }
-                signal_peers(a.sig_peer, n, me, b, E + 1);
+                signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
             } else {
                 if (!wait_mask(a.sig_own, 1u << root, b, E, a.err, a.timeout)) return;
@@ -235,19 +404,11 @@ __global__ __launch_bounds__(kThreads) void k_pipe(PipeArgs a) {
 #pragma unroll
                     for (int j = 0; j < kMaxRanks; ++j)
                         if (j < n && j != me && j != root) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
-                    blk_copy<4>(d, pslot(a.rs_peer.p[me], par, root) + soff, l);
+                    blk_copy_multi(d, pslot(a.rs_peer.p[me], par, root) + soff, l);
                 }
-                signal_peers(a.sig_peer, n, me, b, E + 1);
+                signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
-                for (int s = 0; s < n - 1; ++s) {
-                    const int j = (me + 1 + (b + s) % (n - 1)) % n;
-                    const size_t lj = rlen(j);
-                    if (lj) {
-                        Dsts d{};
-                        d.p[0] = a.recv + a.recv_off[j] + rbase;
-                        blk_copy<4>(d, pslot(a.ag_peer.p[me], par, j) + soff, lj);
-                    }
-                }
+                gather_slots(a, par, rbase, soff, -1);
             }
         }
     }
@@ -256,7 +417,7 @@ __global__ __launch_bounds__(kThreads) void k_pipe(PipeArgs a) {
 template <int OP, int K>
 struct LPipe {
     static int run(const PipeArgs &a, const LaunchCfg &cfg) {
-        hipLaunchKernelGGL((k_pipe<R<OP, K>>), dim3(cfg.grid), dim3(kThreads), 0, cfg.stream, a);
+        hipLaunchKernelGGL((k_pipe<R<OP, K>>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };

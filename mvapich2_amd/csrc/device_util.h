@@ -48,12 +48,14 @@ __device__ __forceinline__ uint64_t flag_load(uint64_t *p) {
 
 // Release this workgroup's prior global stores at system scope and raise
 // flag[me][blk] = epoch on every rank in [0, n).  Call from all threads.
+// light = true: the data the peers read is in uncached memory, so the
+// acknowledged stores (vmcnt(0)) are already visible; skip the L2 writeback.
 __device__ __forceinline__ void signal_peers(const SigTable &sig, int n, int me, int blk,
-                                             uint64_t epoch) {
+                                             uint64_t epoch, bool light = false) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < 64) {
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && !light) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }

@@ -192,6 +192,7 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
     w.epoch += 2 * (uint64_t)g.nrounds;
     a.err = w.h_err;
     a.timeout = w.timeout_ticks;
+    a.light = w.light_release;
     MV2_DEBUG("pipe mode %d grid %d tsub %zu rounds %d maxlen %zu", a.mode, g.grid, g.tsub, g.nrounds, maxlen);
     LaunchCfg cfg = coll_cfg(g.grid, st);
     tmark0(st);
@@ -255,6 +256,7 @@ int mv2h_set_tuning(const char *key, long value) {
     else if (!strcmp(key, "rl_grid")) w.rl_grid = (int)value;
     else if (!strcmp(key, "pipe_grid")) w.pipe_grid = (int)value;
     else if (!strcmp(key, "pipe_sub")) w.pipe_sub = (size_t)value;
+    else if (!strcmp(key, "light_release")) w.light_release = (int)value;
     else if (!strcmp(key, "oneshot_max")) {
         if ((size_t)value > w.slot_bytes && w.size > 1) return E_ARG;
         w.oneshot_max = (size_t)value;

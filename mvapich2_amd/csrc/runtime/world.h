@@ -83,6 +83,7 @@ struct World {
     int max_grid = 1024;
     int pipe_grid = kPipeMaxGrid;                 // pipelined collectives: workgroups (<= kPipeMaxGrid)
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
+    int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
     int rl_grid = 4096;       // reduce_local grid cap (tools/rl_variants.hip sweep)
 
     // timing (bench)

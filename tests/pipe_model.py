@@ -8,7 +8,7 @@ import numpy as np
 
 from oracle import oracle
 
-PIPE_MAX_GRID = 128
+PIPE_MAX_GRID = 256
 PIPE_MAX_SUB = 64 << 10
 PIPE_MIN_SUB = 16 << 10
 

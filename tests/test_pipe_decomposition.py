@@ -28,8 +28,8 @@ def inputs(t, count, rank, seed):
 
 
 def test_geometry_matches_runtime_rules():
-    # 256 MiB fp32 on 8 ranks: 32 MiB segments, 128 workgroups x 64 KiB, 4 rounds
-    assert pm.pipe_geom(32 << 20) == (128, 64 << 10, 8 << 20, 4)
+    # 256 MiB fp32 on 8 ranks: 32 MiB segments, 256 workgroups x 64 KiB, 2 rounds
+    assert pm.pipe_geom(32 << 20) == (256, 64 << 10, 16 << 20, 2)
     # 1 MiB segment: 64 workgroups x 16 KiB, one round
     assert pm.pipe_geom(1 << 20) == (64, 16 << 10, 1 << 20, 1)
     # tests sharing one GPU between 4 ranks: grid capped at cus / 4
