@@ -66,6 +66,31 @@ def cpu_baseline_reduce_local(seconds=10.0):
                       f"1 core of '{cpu_info()}'; reference device path adds D2H 2S + H2D S over PCIe"}
 
 
+def cpu_baseline_host_allreduce(seconds=10.0, ranks=8):
+    """The reference's host-buffer ch3 shared-memory MPI_Allreduce, fp32 SUM,
+    `ranks` processes pinned one per core (oracle/host_allreduce.c: the
+    reference-algorithm host restatement, BASELINE.json configs[0]).  Bounded
+    sample: 8 B .. 64 MiB, each size capped at ~seconds/12 s."""
+    exe = os.path.join(ROOT, "oracle", "host_allreduce")
+    if not os.path.exists(exe):
+        return {"error": "oracle/host_allreduce not built"}
+    cap = max(0.2, seconds / 12.0)
+    try:
+        out = subprocess.run([exe, "-n", str(ranks), "-m", "8:67108864", "-c", "-T", f"{cap:.2f}"],
+                             capture_output=True, text=True, timeout=max(60.0, 40 * cap)).stdout
+    except subprocess.TimeoutExpired:
+        return {"error": "host_allreduce timed out"}
+    rows = [json.loads(l[5:]) for l in out.splitlines() if l.startswith("JSON ")]
+    by = {r["bytes"]: r for r in rows}
+    if 8 not in by or (64 << 20) not in by:
+        return {"error": "incomplete host_allreduce output"}
+    return {"latency_8B_us": by[8]["lat_us"], "busbw_64MiB_GBps": by[64 << 20]["busbw_GBps"],
+            "busbw_1MiB_GBps": by[1 << 20]["busbw_GBps"], "all_ok": all(r["ok"] for r in rows), "cores": ranks,
+            "kind": "port", "cpu": cpu_info(),
+            "what": "reference host path (two-level shmem < 1 KiB, pt2pt_rs >= 1 KiB, single-copy exchange), "
+                    f"{ranks} ranks pinned 1/core, OSU loop, sizes 8 B..64 MiB, <= {cap:.2f} s per size"}
+
+
 def reduce_local_run(L, type_name, op_name, nbytes, steps, warmup):
     h, desc, size, ext = TYPES[type_name]
     count = nbytes // ext
@@ -128,75 +153,206 @@ def bench_n1(args, L):
         "cpu_baseline": cpu_baseline_reduce_local(args.cpu_seconds) if args.cpu_seconds > 0 else None,
         "extra": extra,
     }
+    if args.cpu_seconds > 0:
+        extra["cpu_host_allreduce_8rank"] = cpu_baseline_host_allreduce(args.cpu_seconds)
     return line
 
 
-def bench_nranks(args, L, rank, size):
-    h = TYPES["MPI_FLOAT"][0]
-    op = OPS["MPI_SUM"]
-    world = 0x44000000
-    count = S_BYTES // 4
-    sb = m.DeviceBuffer(S_BYTES)
-    rb = m.DeviceBuffer(S_BYTES)
-    x = np.full(count, float(rank + 1), dtype=np.float32)
-    sb.upload(x)
-    for _ in range(args.warmup):
-        m.check(L.MPI_Allreduce(sb.ptr, rb.ptr, count, h, op, world), "MPI_Allreduce")
+def _timed(L, world, call, steps, warmup):
+    """OSU loop on resident device buffers: warmup, barrier + device sync,
+    `steps` calls, device sync + barrier.  Returns (s per call, mean kernel ms)."""
+    for _ in range(warmup):
+        m.check(call(), "warmup")
     L.mv2h_timing_enable(1)
     kms = []
-    # contract: barrier + device sync, K timed steps, barrier + device sync
     L.MPI_Barrier(world)
     L.mv2h_device_synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m.check(L.MPI_Allreduce(sb.ptr, rb.ptr, count, h, op, world), "MPI_Allreduce")
+    for _ in range(steps):
+        m.check(call(), "timed call")
         kms.append(L.mv2h_last_kernel_ms())
     L.mv2h_device_synchronize()
     L.MPI_Barrier(world)
-    tot = time.perf_counter() - t0
+    t = time.perf_counter() - t0
     L.mv2h_timing_enable(0)
-    got = rb.download(np.float32, count=1024)
-    ok = bool(np.all(got == size * (size + 1) / 2))
-    # 8-byte latency (OSU: 1000 iterations, 100 skip for small messages)
+    return t / steps, float(np.mean(kms))
+
+
+def _pattern(count, rank):
+    """Exact-in-fp32 operand: x_r[i] = (7i + 13r) mod 1024 (sums of <= 8 ranks are exact)."""
+    i = np.arange(count, dtype=np.int64)
+    return ((7 * i + 13 * rank) % 1024).astype(np.float32)
+
+
+def _expected_sum(count, size):
+    i = np.arange(count, dtype=np.int64)
+    acc = np.zeros(count, dtype=np.int64)
+    for r in range(size):
+        acc += (7 * i + 13 * r) % 1024
+    return acc.astype(np.float32)
+
+
+def rccl_child():
+    """Child process of one bench rank: RCCL ncclAllReduce on the same 256 MiB
+    fp32 SUM (torch.distributed "nccl" backend = RCCL), timed like
+    osu_nccl_allreduce.c:107-131.  A comparator number only: never a code path
+    of the library.  Runs in its own process group (own port) so a stuck
+    comparator can be killed without losing the bench line."""
+    import torch
+    import torch.distributed as dist
+    rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    x = torch.ones(S_BYTES // 4, dtype=torch.float32, device=dev)
+    steps = int(os.environ.get("MV2AMD_RCCL_STEPS", "10"))
+    for _ in range(3):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt.item())
+    dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"busbw_GBps": round(2.0 * (size - 1) / size * S_BYTES / t / 1e9, 2), "ms": round(t * 1e3, 4),
+                          "what": "torch.distributed all_reduce (RCCL) fp32 SUM 256 MiB, comparator only"}), flush=True)
+
+
+def rccl_comparator(L, world, rank, size, steps, timeout=240):
+    """Every rank starts one rccl_child; rank 0 reads its line."""
+    import socket
+    port = np.zeros(1, dtype=np.int32)
+    if rank == 0:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port[0] = s.getsockname()[1]
+        s.close()
+    m.check(L.MPI_Bcast(port.ctypes.data, 1, TYPES["MPI_INT"][0], 0, world), "MPI_Bcast(port)")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(int(port[0])), RANK=str(rank),
+               WORLD_SIZE=str(size), MV2AMD_RCCL_STEPS=str(steps))
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--rccl-child"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return {"error": f"comparator timed out after {timeout} s"}
+    if p.returncode != 0:
+        return {"error": (err or "")[-200:]}
+    if rank == 0:
+        try:
+            return json.loads(out.strip().splitlines()[-1])
+        except Exception:
+            return {"error": "no comparator line"}
+    return None
+
+
+def bench_nranks(args, L, rank, size):
+    world = 0x44000000
+    F32, F64, DINT = TYPES["MPI_FLOAT"][0], TYPES["MPI_DOUBLE"][0], TYPES["MPI_DOUBLE_INT"][0]
+    CHAR = TYPES["MPI_CHAR"][0]
+    SUM, MAX, MAXLOC = OPS["MPI_SUM"], OPS["MPI_MAX"], OPS["MPI_MAXLOC"]
+    count = S_BYTES // 4
+    sb = m.DeviceBuffer(S_BYTES)
+    rb = m.DeviceBuffer(S_BYTES)
+    sb.upload(_pattern(count, rank))
+
+    # headline: allreduce fp32 SUM 256 MiB, validated over the whole buffer
+    ar = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, count, F32, SUM, world)  # noqa: E731
+    rb.upload(np.zeros(count, dtype=np.float32))
+    m.check(ar(), "MPI_Allreduce")
+    want = _expected_sum(count, size)
+    ok = bool(np.array_equal(rb.download(np.float32, count=count), want))
+    step_s, kms = _timed(L, world, ar, args.steps, args.warmup)
+    ok = ok and bool(np.array_equal(rb.download(np.float32, count=count), want))
+    del want
+
+    # config 4 / config 5 lines at 256 MiB (fewer steps)
+    ks = max(3, args.steps // 2)
+    rcnt = count // size
+    rsb = m.DeviceBuffer(rcnt * 4)
+    rcounts = (ctypes.c_int * size)(*([rcnt] * size))
+    rs_s, rs_k = _timed(L, world, lambda: L.MPI_Reduce_scatter(sb.ptr, rsb.ptr, rcounts, F32, SUM, world), ks, 2)
+    agb = S_BYTES // size
+    ag_s, ag_k = _timed(L, world, lambda: L.MPI_Allgather(sb.ptr, agb, CHAR, rb.ptr, agb, CHAR, world), ks, 2)
+    bc_s, bc_k = _timed(L, world, lambda: L.MPI_Bcast(rb.ptr, S_BYTES, CHAR, 0, world), ks, 2)
+    nrec = S_BYTES // 16
+    rec = np.zeros(nrec, dtype=[("v", "<f8"), ("i", "<i4"), ("pad", "<i4")])
+    rng = np.random.default_rng(1000 + rank)
+    rec["v"] = np.floor(rng.random(nrec) * 1000.0)
+    rec["i"] = rank
+    sb.upload(rec.view(np.uint8))
+    ml = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, nrec, DINT, MAXLOC, world)  # noqa: E731
+    ml_s, ml_k = _timed(L, world, ml, ks, 2)
+
+    # 8-byte latency (OSU: small-message iterations, skip 100)
     s8 = m.DeviceBuffer(8)
     r8 = m.DeviceBuffer(8)
     s8.upload(np.ones(2, dtype=np.float32))
     for _ in range(100):
-        L.MPI_Allreduce(s8.ptr, r8.ptr, 2, h, op, world)
+        L.MPI_Allreduce(s8.ptr, r8.ptr, 2, F32, SUM, world)
     lat = 0.0
     lat_k = []
     L.mv2h_timing_enable(1)
     for _ in range(args.lat_iters):
         L.MPI_Barrier(world)
         t0 = time.perf_counter()
-        L.MPI_Allreduce(s8.ptr, r8.ptr, 2, h, op, world)
+        L.MPI_Allreduce(s8.ptr, r8.ptr, 2, F32, SUM, world)
         lat += time.perf_counter() - t0
         lat_k.append(L.mv2h_last_kernel_ms())
     L.mv2h_timing_enable(0)
-    # max over ranks via a tiny device allreduce (MAX)
-    mx = np.array([tot, lat, float(np.mean(kms)), 0.0 if ok else 1.0], dtype=np.float64)
-    dm = m.DeviceBuffer(mx.nbytes)
-    dm.upload(mx)
-    dr = m.DeviceBuffer(mx.nbytes)
-    m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, 4, TYPES["MPI_DOUBLE"][0], OPS["MPI_MAX"], world), "max")
-    tot, lat, kms_max, bad = dr.download(np.float64, count=4)
-    step_s = tot / args.steps
-    busbw = 2.0 * (size - 1) / size * S_BYTES / step_s / 1e9
-    kbus = 2.0 * (size - 1) / size * S_BYTES / (kms_max / 1e3) / 1e9
+    lat_ok = bool(np.all(r8.download(np.float32, count=2) == size))
+
+    # max over ranks through the library itself (device allreduce MAX)
+    vals = np.array([step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat / args.lat_iters,
+                     float(np.median(lat_k)), 0.0 if (ok and lat_ok) else 1.0], dtype=np.float64)
+    dm = m.DeviceBuffer(vals.nbytes)
+    dm.upload(vals)
+    dr = m.DeviceBuffer(vals.nbytes)
+    m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, len(vals), F64, MAX, world), "max")
+    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad) = dr.download(np.float64)
+    f = (size - 1) / size
+    busbw = 2.0 * f * S_BYTES / step_s / 1e9
+    kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
     peak_all = (size - 1) * XGMI_LINK
+
+    def line4(t, k, bytes_bus):
+        return {"busbw_GBps": round(bytes_bus / t / 1e9, 2), "kernel_busbw_GBps": round(bytes_bus / (k / 1e3) / 1e9, 2),
+                "ms": round(t * 1e3, 4)}
+
+    extra = {
+        "reduce_scatter_f32_sum": line4(rs_s, rs_k, f * S_BYTES),
+        "allgather_char": line4(ag_s, ag_k, f * S_BYTES),
+        "bcast_char": line4(bc_s, bc_k, S_BYTES),
+        "allreduce_maxloc_double_int": line4(ml_s, ml_k, 2.0 * f * nrec * 12),
+    }
+    del sb, rb, rsb
+    if args.rccl:
+        try:
+            extra["rccl_comparator"] = rccl_comparator(L, world, rank, size, max(5, args.steps // 2))
+        except Exception as e:  # comparator only: never fail the bench line on it
+            extra["rccl_comparator"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     line = {
         "metric": METRIC, "value": round(busbw, 2), "unit": "GB/s", "n_gpus": size, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "configs[2]: osu_allreduce -d rocm fp32 SUM 256 MiB, 1 rank per GPU over xGMI",
                    "count": count, "bytes": S_BYTES, "algorithm": "pipelined direct RS+AG (pushes into peer arenas over xGMI)",
-                   "latency_8B_us": round(lat / args.lat_iters * 1e6, 2),
-                   "latency_8B_kernel_us": round(float(np.median(lat_k)) * 1e3, 2), "correct": not bool(bad)},
+                   "latency_8B_us": round(lat_s * 1e6, 2), "latency_8B_kernel_us": round(lat_k_ms * 1e3, 2),
+                   "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing"},
         "roofline": {"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
                      "frac": round(kbus / peak_all, 4), "traffic": None,
                      "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
-                     "kernel_ms": round(kms_max, 4)},
+                     "kernel_ms": round(kms, 4)},
         "cpu_baseline": None,
+        "extra": extra,
     }
     return line
 
@@ -208,7 +364,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--lat-iters", type=int, default=1000)
+    ap.add_argument("--rccl", type=int, default=1, help="N > 1: also time RCCL all_reduce as a comparator")
+    ap.add_argument("--rccl-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.rccl_child:
+        rccl_child()
+        return
     L = m.lib()
     size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -1,0 +1,374 @@
+/*
+ * host_allreduce.c — CPU BASELINE.  TEST / MEASUREMENT INFRASTRUCTURE ONLY.
+ *
+ * The reference's host-buffer MPI_Allreduce as MVAPICH2 2.3.7 runs it on one
+ * node over ch3 shared memory, restated as a standalone multi-process program
+ * (the reference itself cannot be built here: see DESIGN.md §2).  bench.py's
+ * cpu_baseline leg runs it on the GPU box's host cores; the product never
+ * links or calls it.
+ *
+ * What is restated (single node, generic tuning table,
+ * allreduce_tuning.c:2734-2750, allreduce_osu.c:3146-3375):
+ *   nbytes <  1 KiB: two-level shared memory — every rank copies its operand
+ *                    into its shmem slot, the leader reduces the slots in rank
+ *                    order (reduce_shmem, allreduce_osu.c:1482-1614: recv = x0;
+ *                    uop(slot_i, recv) for i = 1..L-1), then the shmem bcast
+ *                    (bcast_osu.c:1356: leader writes one slot, the others copy
+ *                    it out).
+ *   nbytes >= 1 KiB: MPIR_Allreduce_pt2pt_rs_MV2 (:633-1054): non-pof2 fold,
+ *                    recursive-halving reduce-scatter, recursive-doubling
+ *                    allgather, non-pof2 post-step; recursive doubling when
+ *                    count < pof2 (:802).
+ * The op loops are the oracle's (mv2_oracle.c, compiled -O2 like the
+ * reference).  Message exchange (MPIC_Sendrecv) is modelled as MVAPICH2's
+ * single-copy intra-node path (CMA/LiMIC rendezvous, the default for large
+ * messages on Linux): the receiver copies straight out of the sender's buffer,
+ * which lives in a MAP_SHARED region, after a ready/done handshake that keeps
+ * MPI's send-buffer semantics.  One process per core, pinned.
+ *
+ * Timing follows osu_allreduce (osu_benchmarks/mpi/collective/osu_allreduce.c):
+ * per size, `skip` untimed then `iters` timed iterations of
+ * barrier; t0; allreduce; t1 — average over ranks of the per-rank mean.
+ *
+ * Usage: host_allreduce [-n ranks] [-m min:max] [-i iters_small] [-I iters_large]
+ *                       [-c (validate)] [-T seconds per size cap]
+ * Prints an OSU-style table and one JSON line (prefix "JSON ").
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <sched.h>
+#include <signal.h>
+#include <sys/prctl.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+int oracle_reduce_local(const void *in, void *inout, long count, int h, int op_handle);
+
+#define H_FLOAT 0x4c00040a
+#define OP_SUM 0x58000003
+#define MAXR 64
+#define LARGE_MESSAGE_SIZE 8192 /* osu_util.h */
+
+typedef struct {
+    _Alignas(64) atomic_ulong v;
+} padded_t;
+
+typedef struct {
+    padded_t bar_count;
+    padded_t bar_gen;
+    padded_t ready[MAXR][MAXR]; /* ready[me][peer]: my buffer holds data for peer (gen) */
+    padded_t done[MAXR][MAXR];  /* done[me][peer]: I finished copying peer's data (gen) */
+    padded_t slot_flag[MAXR];   /* two-level: slot of rank r filled (gen) */
+    padded_t bc_flag;           /* two-level: leader's bcast slot filled (gen) */
+    padded_t bc_done[MAXR];     /* two-level: rank r copied the bcast slot (gen) */
+    double lat[MAXR];
+    int bad[MAXR];
+} ctrl_t;
+
+static ctrl_t *C;
+static int N, ME;
+static char *SHM_DATA;     /* per rank: [recv | tmp | slot] regions */
+static size_t RSTRIDE;     /* bytes per rank region */
+static size_t MAXB;
+static unsigned long gen_pair[MAXR];
+static unsigned long gen_bar, gen_slot;
+
+static inline void cpu_relax(void) { __builtin_ia32_pause(); }
+
+static void spin_until(atomic_ulong *p, unsigned long g) {
+    unsigned spins = 0;
+    while (atomic_load_explicit(p, memory_order_acquire) < g)
+        if (++spins > 4096) { sched_yield(); spins = 0; } else cpu_relax();
+}
+
+static void barrier(void) {
+    unsigned long g = ++gen_bar;
+    if (atomic_fetch_add_explicit(&C->bar_count.v, 1, memory_order_acq_rel) == (unsigned long)N - 1) {
+        atomic_store_explicit(&C->bar_count.v, 0, memory_order_relaxed);
+        atomic_store_explicit(&C->bar_gen.v, g, memory_order_release);
+    } else {
+        spin_until(&C->bar_gen.v, g);
+    }
+}
+
+static char *recv_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE; }
+static char *tmp_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE + MAXB; }
+static char *slot_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE + 2 * MAXB; }
+
+/* MPIC_Sendrecv(sendbuf+soff, sbytes -> peer; recvbuf <- peer's buffer at poff, rbytes)
+ * in the single-copy model: announce, wait for the peer's announcement, copy
+ * its bytes out of its buffer, acknowledge, wait for the peer's acknowledgement. */
+static void sendrecv(int peer, const char *peer_src, char *dst, size_t rbytes) {
+    unsigned long g = ++gen_pair[peer];
+    atomic_store_explicit(&C->ready[ME][peer].v, g, memory_order_release);
+    spin_until(&C->ready[peer][ME].v, g);
+    if (rbytes) memcpy(dst, peer_src, rbytes);
+    atomic_store_explicit(&C->done[ME][peer].v, g, memory_order_release);
+    spin_until(&C->done[peer][ME].v, g);
+}
+static void send_only(int peer) {
+    unsigned long g = ++gen_pair[peer];
+    atomic_store_explicit(&C->ready[ME][peer].v, g, memory_order_release);
+    spin_until(&C->done[peer][ME].v, g);
+}
+static void recv_only(int peer, const char *peer_src, char *dst, size_t rbytes) {
+    unsigned long g = ++gen_pair[peer];
+    spin_until(&C->ready[peer][ME].v, g);
+    if (rbytes) memcpy(dst, peer_src, rbytes);
+    atomic_store_explicit(&C->done[ME][peer].v, g, memory_order_release);
+}
+
+/* reduce_shmem + shmem bcast (allreduce_osu.c:1482-1614, bcast_osu.c:1356) */
+static void allreduce_two_level(const char *send, char *recv, long count) {
+    const size_t bytes = (size_t)count * 4;
+    unsigned long g = ++gen_slot;
+    if (ME != 0) {
+        memcpy(slot_of(ME), send, bytes);
+        atomic_store_explicit(&C->slot_flag[ME].v, g, memory_order_release);
+        spin_until(&C->bc_flag.v, g);
+        memcpy(recv, slot_of(0), bytes);
+        atomic_store_explicit(&C->bc_done[ME].v, g, memory_order_release);
+    } else {
+        memcpy(recv, send, bytes);
+        for (int i = 1; i < N; i++) {
+            spin_until(&C->slot_flag[i].v, g);
+            oracle_reduce_local(slot_of(i), recv, count, H_FLOAT, OP_SUM);
+        }
+        memcpy(slot_of(0), recv, bytes);
+        atomic_store_explicit(&C->bc_flag.v, g, memory_order_release);
+        for (int i = 1; i < N; i++) spin_until(&C->bc_done[i].v, g);
+    }
+}
+
+/* MPIR_Allreduce_pt2pt_rs_MV2 allreduce_osu.c:633-1054 on this rank.  The
+ * receive buffer of every rank is its shared region recv_of(rank). */
+static void allreduce_rs(const char *send, long count) {
+    const size_t ext = 4;
+    char *recv = recv_of(ME), *tmp = tmp_of(ME);
+    memcpy(recv, send, (size_t)count * ext); /* Localcopy (:712-718) */
+    int pof2 = 1;
+    while (pof2 * 2 <= N) pof2 *= 2;
+    const int rem = N - pof2;
+    int newrank;
+    if (ME < 2 * rem) {
+        if (ME % 2 == 0) { /* even: send to ME+1, sit out (:734-750) */
+            send_only(ME + 1);
+            newrank = -1;
+        } else {
+            recv_only(ME - 1, recv_of(ME - 1), tmp, (size_t)count * ext);
+            oracle_reduce_local(tmp, recv, count, H_FLOAT, OP_SUM);
+            newrank = ME / 2;
+        }
+    } else {
+        newrank = ME - rem;
+    }
+#define REAL(nr) ((nr) < rem ? (nr) * 2 + 1 : (nr) + rem)
+    if (newrank != -1) {
+        if (count < pof2) { /* recursive doubling (:787-851) */
+            for (int mask = 1; mask < pof2; mask <<= 1) {
+                int dst = REAL(newrank ^ mask);
+                sendrecv(dst, recv_of(dst), tmp, (size_t)count * ext);
+                oracle_reduce_local(tmp, recv, count, H_FLOAT, OP_SUM);
+            }
+        } else {
+            long cnts[MAXR], disps[MAXR];
+            for (int i = 0; i < pof2 - 1; i++) cnts[i] = count / pof2;
+            cnts[pof2 - 1] = count - (count / pof2) * (pof2 - 1);
+            disps[0] = 0;
+            for (int i = 1; i < pof2; i++) disps[i] = disps[i - 1] + cnts[i - 1];
+            int send_idx = 0, recv_idx = 0, last_idx = pof2;
+            int mask = 1;
+            /* the peer's send_idx at each step is derived the same way on its side;
+             * in the single-copy model I read the peer's region [its send range],
+             * which equals my recv range */
+            while (mask < pof2) {
+                int nd = newrank ^ mask, dst = REAL(nd);
+                long rc = 0;
+                if (newrank < nd) {
+                    send_idx = recv_idx + pof2 / (mask * 2);
+                    for (int i = recv_idx; i < send_idx; i++) rc += cnts[i];
+                } else {
+                    recv_idx = send_idx + pof2 / (mask * 2);
+                    for (int i = recv_idx; i < last_idx; i++) rc += cnts[i];
+                }
+                sendrecv(dst, recv_of(dst) + disps[recv_idx] * ext, tmp + disps[recv_idx] * ext, (size_t)rc * ext);
+                oracle_reduce_local(tmp + disps[recv_idx] * ext, recv + disps[recv_idx] * ext, rc, H_FLOAT, OP_SUM);
+                send_idx = recv_idx;
+                mask <<= 1;
+                if (mask < pof2) last_idx = recv_idx + pof2 / mask;
+            }
+            mask >>= 1;
+            while (mask > 0) { /* recursive-doubling allgather (:949-1000) */
+                int nd = newrank ^ mask, dst = REAL(nd);
+                long rc = 0;
+                if (newrank < nd) {
+                    if (mask != pof2 / 2) last_idx = last_idx + pof2 / (mask * 2);
+                    recv_idx = send_idx + pof2 / (mask * 2);
+                    for (int i = recv_idx; i < last_idx; i++) rc += cnts[i];
+                } else {
+                    recv_idx = send_idx - pof2 / (mask * 2);
+                    for (int i = recv_idx; i < send_idx; i++) rc += cnts[i];
+                }
+                sendrecv(dst, recv_of(dst) + disps[recv_idx] * ext, recv + disps[recv_idx] * ext, (size_t)rc * ext);
+                if (newrank > nd) send_idx = recv_idx;
+                mask >>= 1;
+            }
+        }
+    }
+    /* non-pof2 post-step (:1003-1030): odd sends the result to even */
+    if (ME < 2 * rem) {
+        if (ME % 2) send_only(ME - 1);
+        else recv_only(ME + 1, recv_of(ME + 1), recv, (size_t)count * ext);
+    }
+#undef REAL
+}
+
+static void allreduce(const char *send, char *recv_private, long count) {
+    if ((size_t)count * 4 < 1024) allreduce_two_level(send, recv_private, count);
+    else allreduce_rs(send, count);
+}
+
+static double now(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* pin to the k-th CPU of the inherited affinity mask (the job's cpuset) */
+static int pin(int k) {
+    cpu_set_t s, one;
+    if (sched_getaffinity(0, sizeof(s), &s)) return -1;
+    int cnt = CPU_COUNT(&s);
+    if (cnt <= 0) return -1;
+    k %= cnt;
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (!CPU_ISSET(c, &s)) continue;
+        if (k-- == 0) {
+            CPU_ZERO(&one);
+            CPU_SET(c, &one);
+            return sched_setaffinity(0, sizeof(one), &one) ? -1 : c;
+        }
+    }
+    return -1;
+}
+
+int main(int argc, char **argv) {
+    N = 8;
+    size_t mn = 4, mx = 64u << 20;
+    int it_small = 1000, it_large = 100, validate = 0;
+    double tcap = 3.0;
+    int first_core = 0;
+    int c;
+    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:")) != -1) {
+        switch (c) {
+        case 'n': N = atoi(optarg); break;
+        case 'm': sscanf(optarg, "%zu:%zu", &mn, &mx); break;
+        case 'i': it_small = atoi(optarg); break;
+        case 'I': it_large = atoi(optarg); break;
+        case 'c': validate = 1; break;
+        case 'T': tcap = atof(optarg); break;
+        case 'p': first_core = atoi(optarg); break;
+        default: fprintf(stderr, "usage: %s [-n ranks] [-m min:max] [-i it] [-I it] [-c] [-T s] [-p core0]\n", argv[0]); return 2;
+        }
+    }
+    if (N < 1 || N > MAXR || mn < 4) return 2;
+    MAXB = (mx + 63) & ~(size_t)63;
+    RSTRIDE = 3 * MAXB;
+    C = mmap(NULL, sizeof(ctrl_t), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    SHM_DATA = mmap(NULL, RSTRIDE * N, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    if (C == MAP_FAILED || SHM_DATA == MAP_FAILED) { perror("mmap"); return 1; }
+    memset(C, 0, sizeof(ctrl_t));
+    pid_t pids[MAXR];
+    for (int r = 0; r < N; r++) {
+        pid_t p = fork();
+        if (p < 0) { perror("fork"); return 1; }
+        if (p == 0) {
+            prctl(PR_SET_PDEATHSIG, SIGKILL);
+            ME = r;
+            const int core = pin(first_core + r);
+            float *send = malloc(mx);
+            float *recvp = malloc(mx);
+            memset(send, 0, mx);
+            memset(recv_of(ME), 0, RSTRIDE); /* first touch on this rank's core */
+            printf("# rank %d pinned to cpu %d\n", ME, core);
+            fflush(stdout);
+            barrier();
+            if (ME == 0) {
+                printf("# host_allreduce: %d ranks, MPI_FLOAT MPI_SUM, reference-algorithm host restatement\n", N);
+                printf("# %-12s %14s %14s %10s\n", "Size", "Avg Latency(us)", "busbw(GB/s)", "check");
+                fflush(stdout);
+            }
+            for (size_t sz = mn; sz <= mx; sz *= 2) {
+                long count = (long)(sz / 4);
+                int iters = sz > LARGE_MESSAGE_SIZE ? it_large : it_small;
+                int skip = sz > LARGE_MESSAGE_SIZE ? 10 : 100;
+                /* OSU fill: (i % 100 + 1) * (iter + 1) style; exact in fp32 */
+                for (long i = 0; i < count; i++) send[i] = (float)((i % 100) + 1) * (float)(ME + 1);
+                double tsum = 0;
+                int done_it = 0;
+                double t_start = now();
+                for (int i = 0; i < iters + skip; i++) {
+                    barrier();
+                    double t0 = now();
+                    allreduce((const char *)send, (char *)recvp, count);
+                    double t1 = now();
+                    if (i >= skip) { tsum += t1 - t0; done_it++; }
+                    /* bounded sample: all ranks agree through rank 0's clock */
+                    if (i >= skip && ME == 0 && now() - t_start > tcap) C->bad[MAXR - 1] = i + 1;
+                    barrier();
+                    if (C->bad[MAXR - 1] && i + 1 >= C->bad[MAXR - 1]) break;
+                }
+                barrier();
+                if (ME == 0) C->bad[MAXR - 1] = 0;
+                int bad = 0;
+                if (validate) {
+                    const float *res = (sz * 1 < 1024) ? recvp : (const float *)recv_of(ME);
+                    const float tot = (float)(N * (N + 1) / 2);
+                    for (long i = 0; i < count; i++)
+                        if (res[i] != (float)((i % 100) + 1) * tot) { bad = 1; break; }
+                }
+                C->lat[ME] = tsum / (done_it ? done_it : 1);
+                C->bad[ME] = bad;
+                barrier();
+                if (ME == 0) {
+                    double avg = 0;
+                    int anybad = 0;
+                    for (int j = 0; j < N; j++) { avg += C->lat[j]; anybad |= C->bad[j]; }
+                    avg /= N;
+                    double busbw = 2.0 * (N - 1) / N * (double)sz / avg / 1e9;
+                    printf("%-14zu %14.2f %14.3f %10s  (%d iters)\n", sz, avg * 1e6, busbw,
+                           validate ? (anybad ? "FAIL" : "ok") : "-", done_it);
+                    fflush(stdout);
+                    /* JSON row for bench.py */
+                    printf("JSON {\"bytes\": %zu, \"lat_us\": %.3f, \"busbw_GBps\": %.4f, \"ok\": %s, \"iters\": %d}\n",
+                           sz, avg * 1e6, busbw, (validate && anybad) ? "false" : "true", done_it);
+                    fflush(stdout);
+                }
+                barrier();
+            }
+            _exit(0);
+        }
+        pids[r] = p;
+    }
+    /* a rank that dies (signal, SIGPIPE on a closed stdout, ...) would leave the
+     * others spinning: kill the whole job on the first abnormal exit */
+    int rc = 0, left = N;
+    while (left > 0) {
+        int st = 0;
+        pid_t p = wait(&st);
+        if (p < 0) break;
+        --left;
+        if (!WIFEXITED(st) || WEXITSTATUS(st)) {
+            rc = 1;
+            for (int r = 0; r < N; r++) kill(pids[r], SIGKILL);
+        }
+    }
+    return rc;
+}
