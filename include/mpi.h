@@ -138,6 +138,10 @@ typedef void(MPI_User_function)(void *, void *, int *, MPI_Datatype *);
 #define MPI_REPLACE ((MPI_Op)0x5800000d)
 #define MPI_NO_OP ((MPI_Op)0x5800000e)
 
+/* ---- array orders (MPICH values, mpi.h.in) ---- */
+#define MPI_ORDER_C 56
+#define MPI_ORDER_FORTRAN 57
+
 /* ---- error classes ---- */
 #define MPI_SUCCESS 0
 #define MPI_ERR_BUFFER 1
@@ -212,6 +216,18 @@ int MPI_Type_create_hvector(int count, int blocklength, MPI_Aint stride, MPI_Dat
                             MPI_Datatype *newtype);
 int MPI_Type_create_indexed_block(int count, int blocklength, const int displacements[],
                                   MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_create_hindexed_block(int count, int blocklength, const MPI_Aint displacements[],
+                                   MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_indexed(int count, const int blocklengths[], const int displacements[],
+                     MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_create_hindexed(int count, const int blocklengths[], const MPI_Aint displacements[],
+                             MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_create_struct(int count, const int blocklengths[], const MPI_Aint displacements[],
+                           const MPI_Datatype types[], MPI_Datatype *newtype);
+int MPI_Type_create_resized(MPI_Datatype oldtype, MPI_Aint lb, MPI_Aint extent, MPI_Datatype *newtype);
+int MPI_Type_dup(MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_create_subarray(int ndims, const int sizes[], const int subsizes[], const int starts[],
+                             int order, MPI_Datatype oldtype, MPI_Datatype *newtype);
 int MPI_Type_commit(MPI_Datatype *datatype);
 int MPI_Type_free(MPI_Datatype *datatype);
 int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, int outsize,
@@ -264,6 +280,18 @@ int PMPI_Type_create_hvector(int count, int blocklength, MPI_Aint stride, MPI_Da
                              MPI_Datatype *newtype);
 int PMPI_Type_create_indexed_block(int count, int blocklength, const int displacements[],
                                    MPI_Datatype oldtype, MPI_Datatype *newtype);
+int PMPI_Type_create_hindexed_block(int count, int blocklength, const MPI_Aint displacements[],
+                                   MPI_Datatype oldtype, MPI_Datatype *newtype);
+int PMPI_Type_indexed(int count, const int blocklengths[], const int displacements[],
+                     MPI_Datatype oldtype, MPI_Datatype *newtype);
+int PMPI_Type_create_hindexed(int count, const int blocklengths[], const MPI_Aint displacements[],
+                             MPI_Datatype oldtype, MPI_Datatype *newtype);
+int PMPI_Type_create_struct(int count, const int blocklengths[], const MPI_Aint displacements[],
+                           const MPI_Datatype types[], MPI_Datatype *newtype);
+int PMPI_Type_create_resized(MPI_Datatype oldtype, MPI_Aint lb, MPI_Aint extent, MPI_Datatype *newtype);
+int PMPI_Type_dup(MPI_Datatype oldtype, MPI_Datatype *newtype);
+int PMPI_Type_create_subarray(int ndims, const int sizes[], const int subsizes[], const int starts[],
+                             int order, MPI_Datatype oldtype, MPI_Datatype *newtype);
 int PMPI_Type_commit(MPI_Datatype *datatype);
 int PMPI_Type_free(MPI_Datatype *datatype);
 int PMPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, int outsize,

@@ -80,6 +80,16 @@ int mv2h_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk_byt
                       size_t stride_bytes, void *stream);
 int mv2h_unpack_strided(const void *src, void *dst, size_t nblocks, size_t blk_bytes,
                         size_t stride_bytes, void *stream);
+/* Any flattened layout (pair types, indexed types, vectors with count > 1, nested types):
+ * one element = nseg byte segments (offs[s], lens[s]) in pack order, `count` elements
+ * `extent` bytes apart; packed element e holds its segments back to back at e * sum(lens).
+ *   pack:   packed[e*size + pos(s) + b] = src[e*extent + offs[s] + b]
+ *   unpack: the inverse; bytes outside the segments are never written.
+ * Replaces Segment_pack / Segment_unpack (segment_packunpack.c:70/96, m2m callbacks
+ * :124-388) and MPID_Segment_pack_device / _unpack_device (ibv_cuda_util.c:623 / :720). */
+int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent,
+                       const int64_t *offs, const int64_t *lens, int nseg, int unpack,
+                       void *stream);
 
 /* ---- runtime (bootstrap for COMM_WORLD) ---- */
 int mv2h_init(void);

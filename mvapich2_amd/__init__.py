@@ -57,6 +57,8 @@ def lib():
         "mv2h_barrier": ([], c_int),
         "mv2h_pack_strided": ([c_vp, c_vp, c_sz, c_sz, c_sz, c_vp], c_int),
         "mv2h_unpack_strided": ([c_vp, c_vp, c_sz, c_sz, c_sz, c_vp], c_int),
+        "mv2h_pack_segments": ([c_vp, c_vp, c_sz, c_sz, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                c_int, c_int, c_vp], c_int),
         "mv2h_init": ([], c_int),
         "mv2h_finalize": ([], c_int),
         "mv2h_rank": ([], c_int),
@@ -82,6 +84,21 @@ def lib():
         "MPI_Op_create": ([c_vp, c_int, ctypes.POINTER(c_int)], c_int),
         "MPI_Op_free": ([ctypes.POINTER(c_int)], c_int),
         "MPI_Type_vector": ([c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_contiguous": ([c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_hvector": ([c_int, c_int, ctypes.c_long, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_indexed_block": ([c_int, c_int, ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_hindexed_block": ([c_int, c_int, ctypes.POINTER(ctypes.c_long), c_int,
+                                            ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_indexed": ([c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_hindexed": ([c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_long), c_int,
+                                      ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_struct": ([c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_long), ctypes.POINTER(c_int),
+                                    ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_resized": ([c_int, ctypes.c_long, ctypes.c_long, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_dup": ([c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_create_subarray": ([c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int,
+                                      c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Type_get_true_extent": ([c_int, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)], c_int),
         "MPI_Type_commit": ([ctypes.POINTER(c_int)], c_int),
         "MPI_Type_free": ([ctypes.POINTER(c_int)], c_int),
         "MPI_Type_size": ([c_int, ctypes.POINTER(c_int)], c_int),

@@ -108,5 +108,7 @@ int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg
 int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg);
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride,
                         int unpack, hipStream_t stream);
+int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
+                     const int64_t *lens, int nseg, int unpack, hipStream_t stream);
 
 }  // namespace mv2

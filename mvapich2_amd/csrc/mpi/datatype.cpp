@@ -8,8 +8,10 @@
 // a regular layout (equal lengths at a constant stride, the MPI_Type_vector
 // case) is one strided pack/unpack launch (mv2h_pack_strided), replacing
 // MPID_Segment_pack_device (ibv_cuda_util.c:623) and its cudaMemcpy2DAsync /
-// pack_unpack_vector_kernel paths (pack_unpack.cu:419).  Host buffers are
-// copied on the host, as the reference does for host memory.
+// pack_unpack_vector_kernel paths (pack_unpack.cu:419); every other layout
+// (pair types, indexed blocks, vectors with count > 1, nested types) is one
+// run-table launch (mv2h_pack_segments).  Host buffers are copied on the
+// host, as the reference does for host memory.
 #include "datatype.h"
 
 #include <string.h>
@@ -29,6 +31,7 @@ struct Seg {
 struct Derived {
     bool live = false, committed = false;
     long size = 0, lb = 0, extent = 0, true_lb = 0, true_extent = 0;
+    long align = 1;         // alignsize (mpid_type_struct.c:42-124)
     std::vector<Seg> segs;  // one element, sorted by construction order, merged
 };
 
@@ -38,7 +41,7 @@ constexpr int kDerivedBase = (int)0x8c000010;
 
 Derived *derived(MPI_Datatype dt) {
     const unsigned idx = (unsigned)(dt - kDerivedBase);
-    if ((dt & 0xfc000000) != (int)0x8c000000 || idx >= g_types.size() || !g_types[idx].live) return nullptr;
+    if (((unsigned)dt & 0xfc000000u) != 0x8c000000u || idx >= g_types.size() || !g_types[idx].live) return nullptr;
     return &g_types[idx];
 }
 
@@ -71,44 +74,86 @@ void push_merge(std::vector<Seg> &v, Seg s) {
     else v.push_back(s);
 }
 
-int make_type(const std::vector<long> &block_offsets, int blocklen, MPI_Datatype old, MPI_Datatype *out) {
-    std::lock_guard<std::recursive_mutex> lk(g_mu);
-    std::vector<Seg> os;
-    long oext = 0, osize = 0;
-    if (!type_segs(old, os, oext, osize)) return MPI_ERR_TYPE;
-    if (blocklen < 0) return MPI_ERR_ARG;
-    Derived d;
-    d.live = true;
-    long lo = 0, hi = 0;
-    bool first = true;
-    for (long bo : block_offsets) {
-        for (int k = 0; k < blocklen; ++k) {
-            for (const Seg &s : os) {
-                const Seg t{bo + (long)k * oext + s.off, s.len};
-                push_merge(d.segs, t);
-                if (first || t.off < lo) lo = t.off;
-                if (first || t.off + t.len > hi) hi = t.off + t.len;
-                first = false;
-            }
+// One block of a type map: `blocklen` copies of `old` starting at byte `disp`.
+struct Block {
+    long disp;
+    long blocklen;
+    MPI_Datatype old;
+};
+
+// lb / ub of a (builtin or derived) type, as MPI_Type_get_extent reports them
+bool type_bounds(MPI_Datatype dt, long &lb, long &extent);
+
+// alignsize of a type (MPID_Type_struct_alignsize, mpid_type_struct.c:42-124,
+// with the x86-64 configure results: fp types aligned to their size up to 16,
+// everything else up to 8; pair types = the larger member, pairtype.c:26)
+long type_align(MPI_Datatype dt) {
+    if (const mv2::DtypeInfo *b = mv2::dtype_lookup(dt)) {
+        switch ((unsigned)dt) {
+        case 0x4c00040au: case 0x4c00080bu: case 0x4c00100cu: return b->size;  // FLOAT DOUBLE LONG_DOUBLE
+        case 0x8c000000u: return 4;   // FLOAT_INT
+        case 0x8c000001u: return 8;   // DOUBLE_INT
+        case 0x8c000002u: return 8;   // LONG_INT
+        case 0x8c000003u: return 4;   // SHORT_INT
+        case 0x8c000004u: return 16;  // LONG_DOUBLE_INT
+        default: return b->size < 8 ? b->size : 8;
         }
     }
-    d.size = (long)block_offsets.size() * blocklen * osize;
-    d.true_lb = first ? 0 : lo;
-    d.true_extent = first ? 0 : hi - lo;
-    // extent per MPI: lb = min block start, ub = max block end (old extent granularity)
-    long lb = 0, ub = 0;
-    first = true;
-    for (long bo : block_offsets) {
-        const long b0 = bo, b1 = bo + (long)blocklen * oext;
-        if (first || b0 < lb) lb = b0;
-        if (first || b1 > ub) ub = b1;
-        first = false;
+    Derived *d = derived(dt);
+    return d ? d->align : 1;
+}
+
+// General constructor (every MPI_Type_* constructor reduces to this, like the
+// reference's dataloop constructors reduce to DLOOP_Dataloop_create_struct,
+// dataloop_create_struct.c): the element's segments are the blocks' segments in
+// type-map order, merged when adjacent; lb/ub follow MPI-3.1 §4.1.6 (blocks
+// of length 0 do not count, zero-blklen-vector.c); size = sum of block sizes.
+int make_struct(const std::vector<Block> &blocks, MPI_Datatype *out, bool pad = false) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    Derived d;
+    d.live = true;
+    d.align = 1;
+    long lo = 0, hi = 0, lb = 0, ub = 0;
+    bool any_seg = false, any_blk = false;
+    for (const Block &b : blocks) {
+        if (b.blocklen < 0) return MPI_ERR_ARG;
+        std::vector<Seg> os;
+        long oext = 0, osize = 0, olb = 0, oext2 = 0;
+        if (!type_segs(b.old, os, oext, osize) || !type_bounds(b.old, olb, oext2)) return MPI_ERR_TYPE;
+        if (type_align(b.old) > d.align) d.align = type_align(b.old);
+        if (b.blocklen == 0) continue;
+        for (long k = 0; k < b.blocklen; ++k)
+            for (const Seg &sg : os) {
+                const Seg t{b.disp + k * oext + sg.off, sg.len};
+                if (t.len <= 0) continue;
+                push_merge(d.segs, t);
+                if (!any_seg || t.off < lo) lo = t.off;
+                if (!any_seg || t.off + t.len > hi) hi = t.off + t.len;
+                any_seg = true;
+            }
+        const long b0 = b.disp + olb, b1 = b.disp + olb + b.blocklen * oext;
+        if (!any_blk || b0 < lb) lb = b0;
+        if (!any_blk || b1 > ub) ub = b1;
+        any_blk = true;
+        d.size += b.blocklen * osize;
     }
-    d.lb = first ? 0 : lb;
-    d.extent = first ? 0 : ub - lb;
+    d.true_lb = any_seg ? lo : 0;
+    d.true_extent = any_seg ? hi - lo : 0;
+    if (d.true_lb < 0) return MPI_ERR_ARG;  // data below the buffer pointer: not supported
+    d.lb = any_blk ? lb : 0;
+    d.extent = any_blk ? ub - lb : 0;
+    if (pad && d.align > 1 && d.extent % d.align)  // struct padding (mpid_type_struct.c:400-411)
+        d.extent += d.align - d.extent % d.align;
     g_types.push_back(d);
     *out = kDerivedBase + (int)(g_types.size() - 1);
     return MPI_SUCCESS;
+}
+
+int make_type(const std::vector<long> &block_offsets, int blocklen, MPI_Datatype old, MPI_Datatype *out) {
+    std::vector<Block> blocks;
+    blocks.reserve(block_offsets.size());
+    for (long bo : block_offsets) blocks.push_back(Block{bo, blocklen, old});
+    return make_struct(blocks, out);
 }
 
 // regular layout of `count` elements: nblocks x blk bytes at constant stride
@@ -184,26 +229,18 @@ int pack_impl(const char *in, int count, MPI_Datatype dt, char *out, bool unpack
                         : mv2h_pack_strided(in, out, nb, blk, stride, nullptr);
         return rc ? MPI_ERR_OTHER : MPI_SUCCESS;
     }
-    if (d && count > 1 && regular(d, ext, 1, nb, blk, stride)) {
-        long pos = 0;
-        for (int e = 0; e < count; ++e) {
-            int rc = unpack ? mv2h_unpack_strided(in + pos, out + (long)e * ext, nb, blk, stride, nullptr)
-                            : mv2h_pack_strided(in + (long)e * ext, out + pos, nb, blk, stride, nullptr);
-            if (rc) return MPI_ERR_OTHER;
-            pos += size;
-        }
-        return MPI_SUCCESS;
+    if (segs.size() == 1 && segs[0].off == 0 && segs[0].len == ext)  // contiguous
+        return mv2h_memcpy_dtod(out, in, (size_t)count * ext) ? MPI_ERR_OTHER : MPI_SUCCESS;
+    // every other layout (pair types, indexed, vectors with count > 1, nested): one launch
+    std::vector<int64_t> offs(segs.size()), lens(segs.size());
+    for (size_t i = 0; i < segs.size(); ++i) {
+        offs[i] = segs[i].off;
+        lens[i] = segs[i].len;
     }
-    // irregular layouts: one device copy per segment
-    long pos = 0;
-    for (int e = 0; e < count; ++e)
-        for (const Seg &s : segs) {
-            int rc = unpack ? mv2h_memcpy_dtod(out + (long)e * ext + s.off, in + pos, s.len)
-                            : mv2h_memcpy_dtod(out + pos, in + (long)e * ext + s.off, s.len);
-            if (rc) return MPI_ERR_OTHER;
-            pos += s.len;
-        }
-    return MPI_SUCCESS;
+    return mv2h_pack_segments(in, out, (size_t)count, (size_t)ext, offs.data(), lens.data(), (int)segs.size(),
+                              unpack ? 1 : 0, nullptr)
+               ? MPI_ERR_OTHER
+               : MPI_SUCCESS;
 }
 
 }  // namespace
@@ -233,6 +270,21 @@ long dtype_span(MPI_Datatype dt, int count) {
     if (!d) return -1;
     return (long)(count - 1) * d->extent + d->true_lb + d->true_extent;
 }
+
+namespace {
+bool type_bounds(MPI_Datatype dt, long &lb, long &extent) {
+    if (const mv2::DtypeInfo *b = mv2::dtype_lookup(dt)) {
+        lb = 0;
+        extent = b->extent;
+        return true;
+    }
+    Derived *d = derived(dt);
+    if (!d) return false;
+    lb = d->lb;
+    extent = d->extent;
+    return true;
+}
+}  // namespace
 
 #define WEAK(name) __attribute__((weak, alias("P" #name)))
 
@@ -283,7 +335,6 @@ int MPI_Type_contiguous(int count, MPI_Datatype old, MPI_Datatype *nt) WEAK(MPI_
 
 int PMPI_Type_create_hvector(int count, int blocklen, MPI_Aint stride, MPI_Datatype old, MPI_Datatype *nt) {
     if (count < 0) return MPI_ERR_COUNT;
-    if (stride < 0) return MPI_ERR_ARG;  // negative strides: not supported yet
     std::vector<long> offs;
     for (int i = 0; i < count; ++i) offs.push_back((long)i * stride);
     return make_type(offs, blocklen, old, nt);
@@ -304,13 +355,121 @@ int PMPI_Type_create_indexed_block(int count, int blocklen, const int displs[], 
     long ext = 0, sz = 0;
     if (!type_segs(old, s, ext, sz)) return MPI_ERR_TYPE;
     std::vector<long> offs;
-    for (int i = 0; i < count; ++i) {
-        if (displs[i] < 0) return MPI_ERR_ARG;
-        offs.push_back((long)displs[i] * ext);
-    }
+    for (int i = 0; i < count; ++i) offs.push_back((long)displs[i] * ext);
     return make_type(offs, blocklen, old, nt);
 }
 int MPI_Type_create_indexed_block(int count, int blocklen, const int displs[], MPI_Datatype old, MPI_Datatype *nt) WEAK(MPI_Type_create_indexed_block);
+
+int PMPI_Type_create_hindexed_block(int count, int blocklen, const MPI_Aint displs[], MPI_Datatype old,
+                                    MPI_Datatype *nt) {
+    if (count < 0) return MPI_ERR_COUNT;
+    std::vector<long> offs(displs, displs + count);
+    return make_type(offs, blocklen, old, nt);
+}
+int MPI_Type_create_hindexed_block(int count, int blocklen, const MPI_Aint displs[], MPI_Datatype old,
+                                   MPI_Datatype *nt) WEAK(MPI_Type_create_hindexed_block);
+
+int PMPI_Type_indexed(int count, const int blocklens[], const int displs[], MPI_Datatype old, MPI_Datatype *nt) {
+    if (count < 0) return MPI_ERR_COUNT;
+    long lb = 0, ext = 0;
+    if (!type_bounds(old, lb, ext)) return MPI_ERR_TYPE;
+    std::vector<Block> blocks;
+    for (int i = 0; i < count; ++i) blocks.push_back(Block{(long)displs[i] * ext, blocklens[i], old});
+    return make_struct(blocks, nt);
+}
+int MPI_Type_indexed(int count, const int blocklens[], const int displs[], MPI_Datatype old, MPI_Datatype *nt) WEAK(MPI_Type_indexed);
+
+int PMPI_Type_create_hindexed(int count, const int blocklens[], const MPI_Aint displs[], MPI_Datatype old,
+                              MPI_Datatype *nt) {
+    if (count < 0) return MPI_ERR_COUNT;
+    if (!dtype_valid(old)) return MPI_ERR_TYPE;
+    std::vector<Block> blocks;
+    for (int i = 0; i < count; ++i) blocks.push_back(Block{(long)displs[i], blocklens[i], old});
+    return make_struct(blocks, nt);
+}
+int MPI_Type_create_hindexed(int count, const int blocklens[], const MPI_Aint displs[], MPI_Datatype old,
+                             MPI_Datatype *nt) WEAK(MPI_Type_create_hindexed);
+
+int PMPI_Type_create_struct(int count, const int blocklens[], const MPI_Aint displs[], const MPI_Datatype types[],
+                            MPI_Datatype *nt) {
+    if (count < 0) return MPI_ERR_COUNT;
+    std::vector<Block> blocks;
+    for (int i = 0; i < count; ++i) {
+        if (!dtype_valid(types[i])) return MPI_ERR_TYPE;
+        blocks.push_back(Block{(long)displs[i], blocklens[i], types[i]});
+    }
+    return make_struct(blocks, nt, true);
+}
+int MPI_Type_create_struct(int count, const int blocklens[], const MPI_Aint displs[], const MPI_Datatype types[],
+                           MPI_Datatype *nt) WEAK(MPI_Type_create_struct);
+
+int PMPI_Type_create_resized(MPI_Datatype old, MPI_Aint lb, MPI_Aint extent, MPI_Datatype *nt) {
+    std::vector<Block> one{Block{0, 1, old}};
+    if (!dtype_valid(old)) return MPI_ERR_TYPE;
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    int rc = make_struct(one, nt);
+    if (rc) return rc;
+    Derived *d = derived(*nt);
+    d->lb = (long)lb;
+    d->extent = (long)extent;
+    return MPI_SUCCESS;
+}
+int MPI_Type_create_resized(MPI_Datatype old, MPI_Aint lb, MPI_Aint extent, MPI_Datatype *nt) WEAK(MPI_Type_create_resized);
+
+int PMPI_Type_dup(MPI_Datatype old, MPI_Datatype *nt) {
+    long lb = 0, ext = 0;
+    if (!type_bounds(old, lb, ext)) return MPI_ERR_TYPE;
+    return PMPI_Type_create_resized(old, lb, ext, nt);
+}
+int MPI_Type_dup(MPI_Datatype old, MPI_Datatype *nt) WEAK(MPI_Type_dup);
+
+// Subarray (MPI-3.1 §4.1.3; the reference builds it from nested vectors,
+// create_subarray.c / dataloop pack_subarray kernel pack_unpack.cu:256):
+// one block per row of the fastest-varying dimension, then lb = 0 and
+// extent = prod(sizes) * extent(old).
+int PMPI_Type_create_subarray(int ndims, const int sizes[], const int subsizes[], const int starts[], int order,
+                              MPI_Datatype old, MPI_Datatype *nt) {
+    if (ndims <= 0) return MPI_ERR_DIMS;
+    if (order != MPI_ORDER_C && order != MPI_ORDER_FORTRAN) return MPI_ERR_ARG;
+    long olb = 0, oext = 0;
+    if (!type_bounds(old, olb, oext)) return MPI_ERR_TYPE;
+    std::vector<int> dim(ndims);  // dim[0] slowest ... dim[ndims-1] fastest
+    for (int i = 0; i < ndims; ++i) {
+        dim[i] = order == MPI_ORDER_C ? i : ndims - 1 - i;
+        const int k = dim[i];
+        if (sizes[k] <= 0 || subsizes[k] < 0 || starts[k] < 0 || starts[k] + subsizes[k] > sizes[k])
+            return MPI_ERR_ARG;
+    }
+    std::vector<long> elem_stride(ndims);
+    long total = 1;
+    for (int i = ndims - 1; i >= 0; --i) {
+        elem_stride[i] = total;
+        total *= sizes[dim[i]];
+    }
+    const int fast = dim[ndims - 1];
+    std::vector<Block> blocks;
+    long nrows = 1;
+    for (int i = 0; i + 1 < ndims; ++i) nrows *= subsizes[dim[i]];
+    if (subsizes[fast] > 0)
+        for (long r = 0; r < nrows; ++r) {
+            long rem = r, e = starts[fast];
+            for (int i = ndims - 2; i >= 0; --i) {
+                const int k = dim[i];
+                e += (starts[k] + rem % subsizes[k]) * elem_stride[i];
+                rem /= subsizes[k];
+            }
+            blocks.push_back(Block{e * oext, subsizes[fast], old});
+        }
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    int rc = make_struct(blocks, nt);
+    if (rc) return rc;
+    Derived *d = derived(*nt);
+    d->lb = 0;
+    d->extent = total * oext;
+    return MPI_SUCCESS;
+}
+int MPI_Type_create_subarray(int ndims, const int sizes[], const int subsizes[], const int starts[], int order,
+                             MPI_Datatype old, MPI_Datatype *nt) WEAK(MPI_Type_create_subarray);
 
 int PMPI_Type_commit(MPI_Datatype *dt) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);

@@ -451,6 +451,39 @@ int PMPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount,
 int MPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
                              MPI_Comm comm) WEAK(MPI_Reduce_scatter_block);
 
+// Allgather with a non-contiguous type on either side: pack this rank's
+// contribution on the device, gather the packed bytes, and unpack all n
+// blocks with one launch (block i of recvbuf starts i*recvcount extents in,
+// so the n blocks are n*recvcount consecutive elements of recvtype).  The
+// reference stages derived types through Localcopy / segment pack
+// (allgather_osu.c:2426, helper_fns.h:62-250).
+static int allgather_derived(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                             MPI_Datatype recvtype, MPI_Comm comm) {
+    const long rsize = dtype_size(recvtype), rext = dtype_extent(recvtype);
+    const long psize = rsize * recvcount;
+    if (sendbuf != MPI_IN_PLACE && dtype_size(sendtype) * sendcount != psize) return MPI_ERR_TRUNCATE;
+    if (psize == 0) return MPI_SUCCESS;
+    const int n = comm == MPI_COMM_SELF ? 1 : world().size, me = comm == MPI_COMM_SELF ? 0 : world().rank;
+    void *mine = nullptr, *all = nullptr;
+    if (mv2h_malloc(&mine, (size_t)psize)) return MPI_ERR_NO_MEM;
+    if (mv2h_malloc(&all, (size_t)psize * n)) {
+        mv2h_free(mine);
+        return MPI_ERR_NO_MEM;
+    }
+    int pos = 0, rc;
+    if (sendbuf == MPI_IN_PLACE)
+        rc = PMPI_Pack((const char *)recvbuf + (long)me * recvcount * rext, recvcount, recvtype, mine, (int)psize, &pos,
+                       comm);
+    else
+        rc = PMPI_Pack(sendbuf, sendcount, sendtype, mine, (int)psize, &pos, comm);
+    if (!rc) rc = n > 1 ? mv2h_allgather(mine, all, (size_t)psize, nullptr) : mv2h_memcpy_dtod(all, mine, (size_t)psize);
+    pos = 0;
+    if (!rc) rc = PMPI_Unpack(all, (int)(psize * n), &pos, recvbuf, recvcount * n, recvtype, comm);
+    mv2h_free(mine);
+    mv2h_free(all);
+    return rc;
+}
+
 int PMPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
                    MPI_Datatype recvtype, MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
@@ -461,7 +494,7 @@ int PMPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, vo
     if (!dtype_valid(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_valid(sendtype)))
         return err_return(comm, MPI_ERR_TYPE, fn);
     if (!dtype_is_contiguous(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_is_contiguous(sendtype)))
-        return err_return(comm, MPI_ERR_UNSUPPORTED_OPERATION, fn);
+        return err_return(comm, allgather_derived(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, comm), fn);
     const size_t rbytes = (size_t)dtype_span(recvtype, recvcount);
     if (sendbuf != MPI_IN_PLACE && (size_t)dtype_span(sendtype, sendcount) != rbytes)
         return err_return(comm, MPI_ERR_TRUNCATE, fn);

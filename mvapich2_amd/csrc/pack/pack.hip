@@ -14,6 +14,10 @@
 //    coalesced loads, then assembles 16 packed bytes per thread from LDS and
 //    writes them with one 16-byte store.  This is the LDS-staged gather.
 #include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
 
 #include "../coll/kernels.h"
 #include "../common.h"
@@ -76,6 +80,139 @@ __global__ __launch_bounds__(kThreads) void k_pack_lds(const char *__restrict__ 
         const uint32_t row = (uint32_t)(b / blk), col = (uint32_t)(b - (size_t)row * blk);
         o[b] = lds[lead + row * stride + col];
     }
+}
+
+// ---------------------------------------------------------------------------
+// Any flattened layout (pair types, indexed types, vectors with count > 1,
+// nested types): one element of the datatype is a list of RUNS in pack
+// order, run k = nrep blocks of blk units at off + i*stride units (a vector
+// is one run, an indexed type one run per block); `count` elements repeat
+// every `ext` units.  In a packed element, run k starts at unit pp[k] and
+// pp[nrun] = units per packed element.  One launch replaces the dataloop
+// segment walk (Segment_manipulate segment.c:344 with the contig / vector /
+// blkidx / index m2m callbacks, segment_packunpack.c:124-388) and the per-IOV
+// device copies of MPID_Segment_pack_device (ibv_cuda_util.c:37-49, :623).
+// The run table is staged in LDS when it fits; the packed side is read /
+// written coalesced in g-byte units, the strided side in the same units.
+// ---------------------------------------------------------------------------
+struct PackRun {
+    uint64_t pp;     // first packed unit of the run inside a packed element
+    uint64_t blk;    // units per block
+    uint64_t nrep;   // blocks in the run
+    int64_t off;     // unit offset of block 0 inside an element
+    int64_t stride;  // units between consecutive blocks
+};
+constexpr int kRunLds = 512;  // runs staged in LDS (20 KiB)
+
+__device__ __forceinline__ uint64_t udiv(uint64_t a, uint64_t b) {
+    return ((a | b) >> 32) ? a / b : (uint64_t)((uint32_t)a / (uint32_t)b);
+}
+
+template <typename G>
+__global__ __launch_bounds__(kThreads) void k_pack_runs(const G *__restrict__ src, G *__restrict__ dst,
+                                                        uint64_t count, uint64_t ext, uint64_t upe,
+                                                        const PackRun *__restrict__ runs, int nrun,
+                                                        int unpack) {
+    __shared__ PackRun lr[kRunLds];
+    const bool staged = nrun <= kRunLds;
+    if (staged) {
+        for (int k = threadIdx.x; k < nrun; k += kThreads) lr[k] = runs[k];
+        __syncthreads();
+    }
+    const uint64_t total = count * upe;
+    const uint64_t step = (uint64_t)gridDim.x * kThreads;
+    uint64_t u = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (u >= total) return;
+    // (element, unit-in-element) advanced incrementally: no per-unit 64-bit division
+    uint64_t e = udiv(u, upe), q = u - e * upe;
+    const uint64_t se = udiv(step, upe), sq = step - se * upe;
+    for (; u < total; u += step) {
+        int lo = 0, hi = nrun;  // largest k with pp[k] <= q
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            const uint64_t p = staged ? lr[mid].pp : runs[mid].pp;
+            if (p <= q) lo = mid;
+            else hi = mid;
+        }
+        const PackRun r = staged ? lr[lo] : runs[lo];
+        const uint64_t w = q - r.pp;
+        const uint64_t i = r.nrep > 1 ? udiv(w, r.blk) : 0;
+        const int64_t su = (int64_t)(e * ext) + r.off + (int64_t)i * r.stride + (int64_t)(w - i * r.blk);
+        if (!unpack) dst[u] = src[su];
+        else dst[su] = src[u];
+        q += sq;
+        e += se;
+        if (q >= upe) {
+            q -= upe;
+            ++e;
+        }
+    }
+}
+
+int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
+                     const int64_t *lens, int nseg, int unpack, hipStream_t stream) {
+    if (count == 0 || nseg <= 0) return 0;
+    if (!offs || !lens) return E_ARG;
+    uint64_t acc = (uint64_t)extent | (uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst;
+    for (int s = 0; s < nseg; ++s) {
+        if (lens[s] <= 0 || offs[s] < 0) return E_ARG;
+        acc |= (uint64_t)offs[s] | (uint64_t)lens[s];
+    }
+    int g = 16;
+    while (g > 1 && (acc % (uint64_t)g)) g >>= 1;
+    // equal-length blocks at a constant distance fold into one run
+    std::vector<PackRun> runs;
+    uint64_t pp = 0;
+    for (int s = 0; s < nseg; ++s) {
+        const int64_t off = offs[s] / g, len = lens[s] / g;
+        if (!runs.empty()) {
+            PackRun &r = runs.back();
+            const int64_t last = r.off + (int64_t)(r.nrep - 1) * r.stride;
+            if ((int64_t)r.blk == len && (r.nrep == 1 || off - last == r.stride)) {
+                if (r.nrep == 1) r.stride = off - last;
+                ++r.nrep;
+                pp += (uint64_t)len;
+                continue;
+            }
+        }
+        runs.push_back(PackRun{pp, (uint64_t)len, 1, off, 0});
+        pp += (uint64_t)len;
+    }
+    const int nrun = (int)runs.size();
+    // device copy of the run table: pinned staging + device buffer, grown on demand
+    // (every C-ABI call ends stream-synchronised, so the previous table is no longer read)
+    static PackRun *h_tab = nullptr, *d_tab = nullptr;
+    static size_t cap = 0;
+    if ((size_t)nrun > cap) {
+        (void)hipStreamSynchronize(stream);
+        if (h_tab) (void)hipHostFree(h_tab);
+        if (d_tab) (void)hipFree(d_tab);
+        h_tab = d_tab = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(64, 2 * (size_t)nrun);
+        if (hipHostMalloc((void **)&h_tab, want * sizeof(PackRun), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void **)&d_tab, want * sizeof(PackRun)) != hipSuccess)
+            return E_NO_MEM;
+        cap = want;
+    }
+    memcpy(h_tab, runs.data(), (size_t)nrun * sizeof(PackRun));
+    if (hipMemcpyAsync(d_tab, h_tab, (size_t)nrun * sizeof(PackRun), hipMemcpyHostToDevice, stream) != hipSuccess)
+        return E_INTERN;
+    const uint64_t upe = pp, ext_u = extent / (size_t)g, total = (uint64_t)count * upe;
+    size_t grid = (total + kThreads - 1) / kThreads;
+    if (grid > 4096) grid = 4096;
+#define MV2_RUNS(G)                                                                                          \
+    hipLaunchKernelGGL(k_pack_runs<G>, dim3(grid), dim3(kThreads), 0, stream, (const G *)src, (G *)dst,     \
+                       (uint64_t)count, ext_u, upe, d_tab, nrun, unpack)
+    switch (g) {
+    case 16: MV2_RUNS(v4u); break;
+    case 8: MV2_RUNS(uint64_t); break;
+    case 4: MV2_RUNS(uint32_t); break;
+    case 2: MV2_RUNS(uint16_t); break;
+    default: MV2_RUNS(uint8_t); break;
+    }
+#undef MV2_RUNS
+    return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
 }
 
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride, int unpack,

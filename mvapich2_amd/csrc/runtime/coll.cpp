@@ -711,4 +711,16 @@ int mv2h_unpack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
     return finish(st, world().timing);
 }
 
+int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
+                       const int64_t *lens, int nseg, int unpack, void *stream) {
+    int rc;
+    if ((rc = ensure_init_for_device())) return rc;
+    hipStream_t st = pick_stream(stream);
+    tmark0(st);
+    rc = launch_pack_runs(src, dst, count, extent, offs, lens, nseg, unpack ? 1 : 0, st);
+    tmark1(st);
+    if (rc) return rc;
+    return finish(st, world().timing);
+}
+
 }  // extern "C"

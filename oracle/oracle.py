@@ -36,6 +36,8 @@ def lib():
         L.oracle_pack_strided.restype = None
         L.oracle_unpack_strided.argtypes = [vp, vp, l, l, l]
         L.oracle_unpack_strided.restype = None
+        L.oracle_pack_segments.argtypes = [vp, vp, l, l, ctypes.POINTER(l), ctypes.POINTER(l), i, i]
+        L.oracle_pack_segments.restype = None
         L.oracle_time_reduce_local.argtypes = [vp, vp, l, i, i, i]
         L.oracle_time_reduce_local.restype = ctypes.c_double
         _lib = L
@@ -76,6 +78,15 @@ def reduce_linear(srcs, count, dtype_handle, op_handle):
 def pack_strided(src, nblocks, blk, stride):
     dst = np.zeros(nblocks * blk, dtype=np.uint8)
     lib().oracle_pack_strided(src.ctypes.data, dst.ctypes.data, nblocks, blk, stride)
+    return dst
+
+
+def pack_segments(src, dst, count, extent, offs, lens, unpack=False):
+    """Segment-walk pack (unpack=False: src strided -> dst packed) or unpack."""
+    n = len(offs)
+    lo = (ctypes.c_long * n)(*offs)
+    ll = (ctypes.c_long * n)(*lens)
+    lib().oracle_pack_segments(src.ctypes.data, dst.ctypes.data, count, extent, lo, ll, n, 1 if unpack else 0)
     return dst
 
 

@@ -76,3 +76,92 @@ def test_mpi_pack_vector_type_device_and_host():
     got = canvas.download(np.float32).reshape(N, 8)
     assert np.array_equal(got[:, :4].ravel(), want) and np.all(got[:, 4:] == -1.0)
     assert L.MPI_Type_free(ctypes.byref(vt)) == 0
+
+
+# ---- any flattened layout: the run-table kernel (mv2h_pack_segments) ----
+from oracle import typemap as tm  # noqa: E402
+from tests.typecases import CASES, Built, oracle_type  # noqa: E402
+
+
+def _segments(rng, nseg, align):
+    offs, lens, pos = [], [], int(rng.integers(0, 3)) * align
+    for _ in range(nseg):
+        pos += int(rng.integers(0, 4)) * align
+        ln = int(rng.integers(1, 6)) * align
+        offs.append(pos)
+        lens.append(ln)
+        pos += ln
+    return offs, lens, pos
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_pack_segments_random_tables(seed):
+    """Random run tables (unit sizes 1..16 B, 1..700 segments so that the LDS
+    table and the global-memory table are both used) vs the oracle walk."""
+    L = m.lib()
+    rng = np.random.default_rng(100 + seed)
+    align = [1, 2, 4, 8, 16, 16][seed % 6]
+    nseg = [1, 3, 40, 700][seed % 4]
+    offs, lens, end = _segments(rng, nseg, align)
+    extent = end + int(rng.integers(0, 3)) * align
+    count = int(rng.integers(1, 300))
+    span = (count - 1) * extent + end
+    src = rng.integers(0, 256, span + 32, dtype=np.uint8)
+    packed_n = count * sum(lens)
+    want = np.zeros(packed_n, dtype=np.uint8)
+    oracle.pack_segments(src, want, count, extent, offs, lens)
+    o64 = (ctypes.c_int64 * nseg)(*offs)
+    l64 = (ctypes.c_int64 * nseg)(*lens)
+    d_src = m.DeviceBuffer.from_array(src)
+    d_pk = m.DeviceBuffer(packed_n + 16)
+    assert L.mv2h_pack_segments(d_src.ptr, d_pk.ptr, count, extent, o64, l64, nseg, 0, None) == 0
+    assert np.array_equal(d_pk.download(np.uint8, count=packed_n), want), (seed, align, nseg)
+    canvas = rng.integers(0, 256, span + 32, dtype=np.uint8)
+    d_can = m.DeviceBuffer.from_array(canvas)
+    assert L.mv2h_pack_segments(d_pk.ptr, d_can.ptr, count, extent, o64, l64, nseg, 1, None) == 0
+    w2 = canvas.copy()
+    oracle.pack_segments(want, w2, count, extent, offs, lens, unpack=True)
+    assert np.array_equal(d_can.download(np.uint8), w2), ("unpack", seed)
+
+
+@pytest.mark.parametrize("name,spec,count", CASES, ids=[c[0] for c in CASES])
+def test_device_mpi_pack_unpack_all_type_shapes(name, spec, count):
+    """MPI_Pack / MPI_Unpack on device buffers for every derived-type shape of
+    the reference's datatype tests, vs the type-map oracle; also the mixed
+    host/device directions."""
+    L = m.lib()
+    b = Built(L)
+    try:
+        h = b.lib_type(spec)
+        assert L.MPI_Type_commit(ctypes.byref(ctypes.c_int(h))) == 0
+        t = oracle_type(spec)
+        if not t.size:
+            return
+        span = (count - 1) * t.extent + t.true_lb + t.true_extent
+        rng = np.random.default_rng(len(name) * 31)
+        src = rng.integers(0, 256, span + 16, dtype=np.uint8)
+        psize = count * t.size
+        want = tm.pack(src, t, count)
+        d_src = m.DeviceBuffer.from_array(src)
+        d_out = m.DeviceBuffer(psize + 8)
+        pos = ctypes.c_int(0)
+        assert L.MPI_Pack(d_src.ptr, count, h, d_out.ptr, psize + 8, ctypes.byref(pos), 0x44000000) == 0
+        assert pos.value == psize
+        assert np.array_equal(d_out.download(np.uint8, count=psize), want), name
+        # device source -> host packed
+        hout = np.zeros(psize, dtype=np.uint8)
+        pos = ctypes.c_int(0)
+        assert L.MPI_Pack(d_src.ptr, count, h, hout.ctypes.data, psize, ctypes.byref(pos), 0x44000000) == 0
+        assert np.array_equal(hout, want), ("d->h", name)
+        canvas = rng.integers(0, 256, span + 16, dtype=np.uint8)
+        d_can = m.DeviceBuffer.from_array(canvas)
+        pos = ctypes.c_int(0)
+        assert L.MPI_Unpack(d_out.ptr, psize, ctypes.byref(pos), d_can.ptr, count, h, 0x44000000) == 0
+        assert np.array_equal(d_can.download(np.uint8), tm.unpack(want, canvas, t, count)), ("unpack", name)
+        # host packed -> device destination
+        d_can2 = m.DeviceBuffer.from_array(canvas)
+        pos = ctypes.c_int(0)
+        assert L.MPI_Unpack(want.ctypes.data, psize, ctypes.byref(pos), d_can2.ptr, count, h, 0x44000000) == 0
+        assert np.array_equal(d_can2.download(np.uint8), tm.unpack(want, canvas, t, count)), ("h->d", name)
+    finally:
+        b.close()
