@@ -10,7 +10,8 @@ Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 A step is one MPI call on resident device buffers (OSU loop: barrier, t0,
 call, t1).  Kernel time comes from HIP events recorded on the library's own
-stream around the kernel launch (mv2h_timing_enable / mv2h_last_kernel_ms).
+stream around the kernel launch (mv2h_timing_enable / mv2h_last_kernel_ms),
+in a second loop so the events never sit inside the timed value loop.
 The CPU baseline (rank 0, N = 1 only) times the oracle's restatement of the
 reference op loop on a bounded host sample.
 """
@@ -108,15 +109,19 @@ def reduce_local_run(L, type_name, op_name, nbytes, steps, warmup):
     b.upload(y)
     for _ in range(warmup):
         m.check(L.MPI_Reduce_local(a.ptr, b.ptr, count, h, OPS[op_name]), "MPI_Reduce_local")
-    L.mv2h_timing_enable(1)
-    kms = []
+    # value: the blocking calls alone (no timing events in the stream)
     L.mv2h_device_synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         m.check(L.MPI_Reduce_local(a.ptr, b.ptr, count, h, OPS[op_name]), "MPI_Reduce_local")
-        kms.append(L.mv2h_last_kernel_ms())
     L.mv2h_device_synchronize()
     t = time.perf_counter() - t0
+    # kernel duration: HIP events around the launch on the library's stream, separate loop
+    L.mv2h_timing_enable(1)
+    kms = []
+    for _ in range(steps):
+        m.check(L.MPI_Reduce_local(a.ptr, b.ptr, count, h, OPS[op_name]), "MPI_Reduce_local")
+        kms.append(L.mv2h_last_kernel_ms())
     L.mv2h_timing_enable(0)
     # spot-check correctness of the last call on a slice (exact single-op fp/int)
     got = b.download(dt, count=4096)
@@ -163,17 +168,20 @@ def _timed(L, world, call, steps, warmup):
     `steps` calls, device sync + barrier.  Returns (s per call, mean kernel ms)."""
     for _ in range(warmup):
         m.check(call(), "warmup")
-    L.mv2h_timing_enable(1)
-    kms = []
     L.MPI_Barrier(world)
     L.mv2h_device_synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         m.check(call(), "timed call")
-        kms.append(L.mv2h_last_kernel_ms())
     L.mv2h_device_synchronize()
     L.MPI_Barrier(world)
     t = time.perf_counter() - t0
+    # kernel durations (HIP events on the library's stream) in a separate loop
+    L.mv2h_timing_enable(1)
+    kms = []
+    for _ in range(steps):
+        m.check(call(), "timed call")
+        kms.append(L.mv2h_last_kernel_ms())
     L.mv2h_timing_enable(0)
     return t / steps, float(np.mean(kms))
 

@@ -28,6 +28,7 @@ struct OneShotArgs {
     uint64_t epoch;
     int *err;
     uint64_t timeout;
+    Done done;
 };
 
 // ---------------------------------------------------------------------------
@@ -74,6 +75,7 @@ struct PipeArgs {
     TreeParams tp;
     int *err;
     uint64_t timeout;
+    Done done;
 };
 
 struct LaunchCfg {
@@ -82,6 +84,7 @@ struct LaunchCfg {
     hipStream_t stream;
     int cus = 256;    // compute units of the device
     int nshare = 1;   // max ranks sharing one GPU (same on every rank)
+    Done done{};      // completion word (reduce_local)
 };
 
 // Workgroups that are guaranteed co-resident for a kernel (the per-workgroup

@@ -23,7 +23,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_local(const v4u *__restrict
                                                            v4u *__restrict__ io, size_t nvec,
                                                            const typename Rd::T *__restrict__ tin,
                                                            typename Rd::T *__restrict__ tio,
-                                                           size_t tail_beg, size_t tail_end) {
+                                                           size_t tail_beg, size_t tail_end, Done dn) {
     const size_t stride = (size_t)gridDim.x * kThreads * U;
     for (size_t base = (size_t)blockIdx.x * kThreads * U + threadIdx.x; base < nvec; base += stride) {
         v4u a[U], b[U];
@@ -43,16 +43,18 @@ __global__ __launch_bounds__(kThreads) void k_reduce_local(const v4u *__restrict
     }
     if (blockIdx.x == 0)
         for (size_t e = tail_beg + threadIdx.x; e < tail_end; e += kThreads) tio[e] = Rd::apply(tio[e], tin[e]);
+    block_done(dn);
 }
 
 // element-granular variant for buffers that are not 16-byte aligned
 template <class Rd>
 __global__ __launch_bounds__(kThreads) void k_reduce_local_elem(const typename Rd::T *__restrict__ in,
                                                                 typename Rd::T *__restrict__ io,
-                                                                size_t count) {
+                                                                size_t count, Done dn) {
     const size_t stride = (size_t)gridDim.x * kThreads;
     for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < count; e += stride)
         io[e] = Rd::apply(io[e], in[e]);
+    block_done(dn);
 }
 
 template <int OP, int K>
@@ -67,7 +69,7 @@ struct LReduceLocal {
             if (g > (size_t)cfg.grid) g = cfg.grid;
             if (g == 0) g = 1;
             hipLaunchKernelGGL((k_reduce_local_elem<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream,
-                               (const T *)in, (T *)inout, count);
+                               (const T *)in, (T *)inout, count, cfg.done);
             return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
         }
         const size_t nvec = count / VPT;
@@ -77,7 +79,7 @@ struct LReduceLocal {
         if (g == 0) g = 1;
         hipLaunchKernelGGL((k_reduce_local<Rd, 4>), dim3(g), dim3(kThreads), 0, cfg.stream,
                            (const v4u *)in, (v4u *)inout, nvec, (const T *)in, (T *)inout,
-                           nvec * VPT, count);
+                           nvec * VPT, count, cfg.done);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };
@@ -209,7 +211,7 @@ struct LReduceN {
 // peer can only reach call i+2 after every rank finished call i.
 // ============================================================================
 template <class Rd>
-__global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
+__device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const int blk = blockIdx.x, G = gridDim.x;
@@ -253,6 +255,12 @@ __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
             ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
         }
     }
+}
+
+template <class Rd>
+__global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
+    oneshot_body<Rd>(a);
+    block_done(a.done);
 }
 
 template <int OP, int K>

@@ -319,7 +319,7 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
 }
 
 template <class Rd>
-__global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
+__device__ __forceinline__ void pipe_body(const PipeArgs &a) {
     const int b = blockIdx.x;
     const int n = a.n, me = a.me;
     const unsigned all = (1u << n) - 1u;
@@ -412,6 +412,12 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
             }
         }
     }
+}
+
+template <class Rd>
+__global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
+    pipe_body<Rd>(a);
+    block_done(a.done);
 }
 
 template <int OP, int K>

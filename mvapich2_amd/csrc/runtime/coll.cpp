@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "../../../include/mv2h.h"
 #include "log.h"
@@ -31,9 +32,54 @@ bool log_debug_on() {
 
 static hipStream_t pick_stream(void *s) { return s ? (hipStream_t)s : world().stream; }
 
+// Completion word for the kernel about to be launched on `st` as the call's
+// last stream operation (only the library's own stream; cleared again by
+// any copy enqueued after it, see enq_copy).
+static Done arm_done(hipStream_t st) {
+    World &w = world();
+    if (w.sync_mode != 0 || !w.done_flag || st != w.stream) return Done{nullptr, nullptr, 0};
+    w.pending = ++w.done_seq;
+    return Done{w.done_ctr, w.done_flag, w.pending};
+}
+
+static inline hipError_t enq_copy(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    world().pending = 0;
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
+}
+
+// Wait for the armed completion word; fall back to the stream when the
+// kernel ended without raising it (should not happen: counters are reset).
+static hipError_t wait_done(hipStream_t st, uint64_t want) {
+    World &w = world();
+    unsigned spins = 0;
+    for (;;) {
+        if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return hipSuccess;
+        if ((++spins & 1023u) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return hipSuccess;
+            if (q == hipSuccess) {
+                MV2_DEBUG("kernel finished without its completion word; resetting counters");
+                hipMemsetAsync(w.done_ctr, 0, kDoneBytes, st);
+                return hipStreamSynchronize(st);
+            }
+            return q;
+        }
+    }
+}
+
 static int finish(hipStream_t st, bool timed) {
     World &w = world();
-    if (hipStreamSynchronize(st) != hipSuccess) {
+    hipError_t e;
+    const uint64_t want = w.pending;
+    w.pending = 0;
+    if (want) {
+        e = wait_done(st, want);
+        if (e == hipSuccess && timed) e = hipEventSynchronize(w.ev1);
+    } else {
+        e = hipStreamSynchronize(st);
+    }
+    if (e != hipSuccess) {
         MV2_ERR("hipStreamSynchronize failed: %s", hipGetErrorString(hipGetLastError()));
         return E_INTERN;
     }
@@ -193,12 +239,88 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
     a.err = w.h_err;
     a.timeout = w.timeout_ticks;
     a.light = w.light_release;
+    a.done = arm_done(st);
     MV2_DEBUG("pipe mode %d grid %d tsub %zu rounds %d maxlen %zu", a.mode, g.grid, g.tsub, g.nrounds, maxlen);
     LaunchCfg cfg = coll_cfg(g.grid, st);
     tmark0(st);
     const int rc = dt ? launch_pipe_reduce(oi, dt->kind, a, cfg) : launch_pipe_copy(a, cfg);
     tmark1(st);
     return rc;
+}
+
+}  // namespace mv2
+
+namespace mv2 {
+
+// Init-time check of the cross-GPU publish protocol on this node's topology.
+// The pipelined kernels publish arena stores with the light release (stores
+// acknowledged, no L2 writeback), which is right only if peer-mapped
+// uncached arenas are not write-back cached by the writer.  One 4 MiB
+// pipelined int32 SUM allreduce (two calls: both slot parities) is checked
+// element by element on every rank; the verdict is agreed through a
+// one-shot allreduce (full release).  On a mismatch every rank falls back to
+// the full system-scope release and re-checks; a second failure fails
+// MPI_Init loudly instead of returning wrong sums later.
+int coll_selftest() {
+    World &w = world();
+    const int n = w.size;
+    const size_t count = (size_t)1 << 20;
+    const size_t bytes = count * 4;
+    std::vector<uint32_t> h(count), want(count), got(count);
+    for (size_t i = 0; i < count; ++i) {
+        h[i] = (uint32_t)(i * 2654435761u) ^ (uint32_t)(w.rank * 0x9E3779B9u + 17u);
+        uint32_t acc = 0;
+        for (int r = 0; r < n; ++r) acc += (uint32_t)(i * 2654435761u) ^ (uint32_t)(r * 0x9E3779B9u + 17u);
+        want[i] = acc;
+    }
+    void *sb = nullptr, *rb = nullptr, *fb = nullptr;
+    if (hipMalloc(&sb, bytes) != hipSuccess || hipMalloc(&rb, bytes) != hipSuccess ||
+        hipMalloc(&fb, 2 * sizeof(int)) != hipSuccess) {
+        MV2_ERR("self-test: device allocation failed");
+        return E_NO_MEM;
+    }
+    hipMemcpy(sb, h.data(), bytes, hipMemcpyHostToDevice);
+    const int MPI_INT_H = 0x4c000405, MPI_SUM_H = 0x58000003, MPI_MIN_H = 0x58000002;
+    int verdict = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        int ok = 1;
+        for (int call = 0; call < 2 && ok; ++call) {
+            hipMemset(rb, 0, bytes);
+            hipDeviceSynchronize();
+            if (mv2h_allreduce(sb, rb, count, MPI_INT_H, MPI_SUM_H, nullptr) != 0) {
+                ok = 0;
+                break;
+            }
+            hipMemcpy(got.data(), rb, bytes, hipMemcpyDeviceToHost);
+            ok = memcmp(got.data(), want.data(), bytes) == 0;
+        }
+        hipMemcpy(fb, &ok, sizeof(int), hipMemcpyHostToDevice);
+        int all_ok = 0;
+        if (mv2h_allreduce(fb, (int *)fb + 1, 1, MPI_INT_H, MPI_MIN_H, nullptr) != 0) {
+            verdict = E_OTHER;
+            break;
+        }
+        hipMemcpy(&all_ok, (int *)fb + 1, sizeof(int), hipMemcpyDeviceToHost);
+        if (all_ok) {
+            verdict = 0;
+            MV2_DEBUG("self-test passed (light_release=%d)", w.light_release);
+            break;
+        }
+        verdict = E_INTERN;
+        if (w.light_release) {
+            if (w.rank == 0)
+                fprintf(stderr, "[mv2amd] warning: pipelined allreduce self-test failed with the light release; "
+                                "using the full system-scope release\n");
+            w.light_release = 0;
+        } else {
+            break;
+        }
+    }
+    hipFree(sb);
+    hipFree(rb);
+    hipFree(fb);
+    if (verdict) MV2_ERR("device collective self-test failed at MPI_Init (ranks %d): cross-GPU protocol broken", n);
+    return verdict;
 }
 
 }  // namespace mv2
@@ -312,11 +434,12 @@ int mv2h_reduce_local(const void *in, void *inout, size_t count, int dtype, int 
         rc = hipMemcpyAsync(dio_p, din_p, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : E_INTERN;
     } else {
         LaunchCfg cfg{w.rl_grid, 4, st};
+        cfg.done = arm_done(st);
         rc = launch_reduce_local(oi, dt->kind, din_p, dio_p, count, dt->extent, cfg);
     }
     tmark1(st);
     if (rc) return rc;
-    if (!dio) hipMemcpyAsync(inout, dio_p, bytes, hipMemcpyDeviceToHost, st);
+    if (!dio) enq_copy(inout, dio_p, bytes, st);
     return finish(st, w.timing);
 }
 
@@ -409,7 +532,7 @@ static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, 
 }
 
 static void stage_out(const Staged &s, hipStream_t st) {
-    if (s.copy_back) hipMemcpyAsync(s.user_recv, s.recv, s.bytes, hipMemcpyDefault, st);
+    if (s.copy_back) enq_copy(s.user_recv, s.recv, s.bytes, st);
 }
 
 static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, const DtypeInfo *dt, int oi,
@@ -458,6 +581,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.epoch = epoch;
         a.err = w.h_err;
         a.timeout = w.timeout_ticks;
+        a.done = arm_done(st);
         int g = (int)((nvec + 511) / 512);
         g = std::max(1, std::min(g, std::min(gcap, 32)));
         LaunchCfg cfg = coll_cfg(g, st);
@@ -617,7 +741,7 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     tp.linear = 1;
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
-    if (!direct && mycnt) hipMemcpyAsync(recvbuf, dst, mycnt * ext, hipMemcpyDefault, st);
+    if (!direct && mycnt) enq_copy(recvbuf, dst, mycnt * ext, st);
     return finish(st, w.timing);
 }
 
@@ -655,7 +779,10 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
         a.recv_off[j] = (size_t)j * pitch;
     }
     if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
-    if (!direct) hipMemcpy2DAsync(recvbuf, bytes, dst, pitch, bytes, n, hipMemcpyDefault, st);
+    if (!direct) {
+        w.pending = 0;
+        hipMemcpy2DAsync(recvbuf, bytes, dst, pitch, bytes, n, hipMemcpyDefault, st);
+    }
     return finish(st, w.timing);
 }
 
@@ -682,7 +809,7 @@ int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
     a.esize = 1;
     even_segments(a, bytes, w.size);
     if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
-    if (!direct && w.rank != root) hipMemcpyAsync(buffer, buf, bytes, hipMemcpyDefault, st);
+    if (!direct && w.rank != root) enq_copy(buffer, buf, bytes, st);
     return finish(st, w.timing);
 }
 

@@ -122,10 +122,20 @@ static int setup_device_common() {
     const char *dn[] = {"MV2AMD_DEVICE", nullptr};
     w.device = env_int(dn, w.local_rank % ndev);
     if (hipSetDevice(w.device) != hipSuccess) return E_OTHER;
+    w.sync_mode = (int)env_long("MV2AMD_SYNC", w.sync_mode);
     // blocking stream: orders after legacy null-stream work (buffer readiness)
     if (hipStreamCreate(&w.stream) != hipSuccess) return E_OTHER;
     if (hipHostMalloc((void **)&w.h_err, 64, hipHostMallocDefault) != hipSuccess) return E_OTHER;
     memset(w.h_err, 0, 64);
+    if (hipMalloc((void **)&w.done_ctr, kDoneBytes) != hipSuccess || hipMemset(w.done_ctr, 0, kDoneBytes) != hipSuccess ||
+        hipHostMalloc((void **)&w.done_flag, 64, hipHostMallocDefault) != hipSuccess) {
+        w.done_ctr = nullptr;
+        w.done_flag = nullptr;
+        w.sync_mode = 1;
+    } else {
+        memset(w.done_flag, 0, 64);
+        hipDeviceSynchronize();
+    }
     hipDeviceGetAttribute(&w.cus, hipDeviceAttributeMultiprocessorCount, w.device);
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, w.device) == hipSuccess && khz > 0)
@@ -276,6 +286,13 @@ int world_init() {
         }
     }
     w.inited = true;
+    if (w.size > 1 && w.size <= kMaxRanks && !control_only && env_long("MV2AMD_SELFTEST", 1) != 0) {
+        const int rc = coll_selftest();
+        if (rc) {
+            w.inited = false;
+            return rc;
+        }
+    }
     MV2_DEBUG("init rank %d/%d local %d device %d nshare %d", w.rank, w.size, w.local_rank, w.device, w.nshare);
     return 0;
 }

@@ -85,6 +85,11 @@ struct World {
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
     int rl_grid = 4096;       // reduce_local grid cap (tools/rl_variants.hip sweep)
+    int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
+    uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
+    uint64_t *done_flag = nullptr;  // pinned host: last completed call's sequence number
+    uint64_t done_seq = 0;          // last sequence number armed
+    uint64_t pending = 0;           // seq the current call waits for (0: stream sync)
 
     // timing (bench)
     bool timing = false;
@@ -102,5 +107,6 @@ int world_finalize();
 void host_barrier();
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
+int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
 
 }  // namespace mv2
