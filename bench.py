@@ -139,7 +139,7 @@ def bench_n1(args, L):
         s, k, c, _ = reduce_local_run(L, t, op, S_BYTES, max(3, args.steps // 2), 2)
         extra[f"{t}:{op}"] = {"GB/s_call": round(3 * S_BYTES / s / 1e9, 1), "GB/s_kernel": round(3 * S_BYTES / k / 1e9, 1)}
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_reduce_local_r01.json")
+    tfile = os.path.join(ROOT, "profiles", "pmc_reduce_local_r01i.json")
     if os.path.exists(tfile):
         try:
             traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
@@ -154,7 +154,7 @@ def bench_n1(args, L):
                    "api": "MPI_Reduce_local via libmpi.so (MPICH ABI)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
-                     "kernel": "k_reduce_local<R<SUM,F32>,4>", "kernel_ms": round(kern_s * 1e3, 4)},
+                     "kernel": "k_reduce_local<R<SUM,F32>,2>", "kernel_ms": round(kern_s * 1e3, 4)},
         "cpu_baseline": cpu_baseline_reduce_local(args.cpu_seconds) if args.cpu_seconds > 0 else None,
         "extra": extra,
     }

@@ -18,18 +18,23 @@ namespace mv2 {
 // ============================================================================
 // MPI_Reduce_local: inout[i] = op(inout[i], in[i])   (reduce_local.c:139)
 // ============================================================================
+// Streamed shape chosen by tools/rl_variants.hip on MI355X (random fp32
+// operands, 256 MiB): non-temporal loads + plain stores, 512 threads x 2
+// vectors per thread, one tile per workgroup (full grid): 6.7 TB/s, against
+// 6.25 TB/s for non-temporal stores on a 4096-workgroup grid-stride grid.
+constexpr int kRLThreads = 512;
 template <class Rd, int U>
-__global__ __launch_bounds__(kThreads) void k_reduce_local(const v4u *__restrict__ in,
-                                                           v4u *__restrict__ io, size_t nvec,
-                                                           const typename Rd::T *__restrict__ tin,
-                                                           typename Rd::T *__restrict__ tio,
-                                                           size_t tail_beg, size_t tail_end, Done dn) {
-    const size_t stride = (size_t)gridDim.x * kThreads * U;
-    for (size_t base = (size_t)blockIdx.x * kThreads * U + threadIdx.x; base < nvec; base += stride) {
+__global__ __launch_bounds__(kRLThreads) void k_reduce_local(const v4u *__restrict__ in,
+                                                             v4u *__restrict__ io, size_t nvec,
+                                                             const typename Rd::T *__restrict__ tin,
+                                                             typename Rd::T *__restrict__ tio,
+                                                             size_t tail_beg, size_t tail_end, Done dn) {
+    const size_t stride = (size_t)gridDim.x * kRLThreads * U;
+    for (size_t base = (size_t)blockIdx.x * kRLThreads * U + threadIdx.x; base < nvec; base += stride) {
         v4u a[U], b[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t i = base + (size_t)u * kThreads;
+            const size_t i = base + (size_t)u * kRLThreads;
             if (i < nvec) {
                 a[u] = ld_nt(&io[i]);
                 b[u] = ld_nt(&in[i]);
@@ -37,12 +42,12 @@ __global__ __launch_bounds__(kThreads) void k_reduce_local(const v4u *__restrict
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t i = base + (size_t)u * kThreads;
-            if (i < nvec) st_nt(&io[i], vapply<Rd>(a[u], b[u]));
+            const size_t i = base + (size_t)u * kRLThreads;
+            if (i < nvec) io[i] = vapply<Rd>(a[u], b[u]);
         }
     }
     if (blockIdx.x == 0)
-        for (size_t e = tail_beg + threadIdx.x; e < tail_end; e += kThreads) tio[e] = Rd::apply(tio[e], tin[e]);
+        for (size_t e = tail_beg + threadIdx.x; e < tail_end; e += kRLThreads) tio[e] = Rd::apply(tio[e], tin[e]);
     block_done(dn);
 }
 
@@ -73,11 +78,11 @@ struct LReduceLocal {
             return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
         }
         const size_t nvec = count / VPT;
-        const size_t tile = (size_t)kThreads * 4;
+        const size_t tile = (size_t)kRLThreads * 2;
         size_t g = (nvec + tile - 1) / tile;
         if (g > (size_t)cfg.grid) g = cfg.grid;
         if (g == 0) g = 1;
-        hipLaunchKernelGGL((k_reduce_local<Rd, 4>), dim3(g), dim3(kThreads), 0, cfg.stream,
+        hipLaunchKernelGGL((k_reduce_local<Rd, 2>), dim3(g), dim3(kRLThreads), 0, cfg.stream,
                            (const v4u *)in, (v4u *)inout, nvec, (const T *)in, (T *)inout,
                            nvec * VPT, count, cfg.done);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;

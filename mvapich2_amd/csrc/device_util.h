@@ -36,10 +36,11 @@ struct SigTable {
 // host returns from the MPI call without the kernel-completion signal
 // round trip (runtime/coll.cpp finish()).
 constexpr int kDoneStride = 1024;  // counter spacing in words (4 KiB: separate memory channels)
-constexpr size_t kDoneBytes = 9 * kDoneStride * sizeof(uint32_t);
+constexpr int kDoneSub = 64;       // first-level counters (blockIdx % 64)
+constexpr int kDoneCtrs = kDoneSub + 8 + 1;  // + per-XCD group (blockIdx % 8) + groups done
+constexpr size_t kDoneBytes = (size_t)kDoneCtrs * kDoneStride * sizeof(uint32_t);
 struct Done {
-    uint32_t *ctr;   // 9 counters, kDoneStride words apart: arrivals per XCD group (blockIdx % 8),
-                     // then groups done; all 0 between launches
+    uint32_t *ctr;   // kDoneCtrs counters, kDoneStride words apart; all 0 between launches
     uint64_t *flag;  // pinned host word
     uint64_t seq;
 };
@@ -119,32 +120,38 @@ __device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, ui
 
 // Arrive at the call's completion word (all threads of the block).  Each
 // block waits for its own stores to be acknowledged and counts itself,
-// relaxed, in its XCD group's counter (blockIdx % 8: round-robin workgroup
-// placement over the 8 XCDs); the last arrival of a group writes back that
-// XCD's L2 (one agent-scope release per XCD, not per block: a release per
-// block cost 20-220 us on a 256 MiB Reduce_local) and counts the group; the
-// last group resets the counters for the next launch and publishes seq to
-// the host at system scope.  Stream-ordered consumers of the result wait for
-// the kernel's end anyway; the release makes the data visible to work on
-// other streams of this GPU as soon as the host returns.
+// relaxed, in sub-counter blockIdx % 64 (spreads the arrivals of a large
+// grid over 64 addresses); the last arrival of a sub-counter counts it in its
+// XCD group blockIdx % 8 (round-robin workgroup placement over the 8 XCDs);
+// the last arrival of a group writes back that XCD's L2 (one agent-scope
+// release per XCD, not per block: a release per block cost 20-220 us on a
+// 256 MiB Reduce_local) and counts the group; the last group resets the
+// counters for the next launch and publishes seq to the host at system
+// scope.  Stream-ordered consumers of the result wait for the kernel's end
+// anyway; the release makes the data visible to work on other streams of
+// this GPU as soon as the host returns.
 __device__ __forceinline__ void block_done(const Done &d) {
     if (!d.flag) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned nb = gridDim.x, x = blockIdx.x & 7u;
-        const unsigned members = (nb - x + 7u) / 8u;  // blocks b < nb with b % 8 == x
+        const unsigned nb = gridDim.x, b = blockIdx.x;
+        const unsigned i = b % kDoneSub, x = b & 7u;
+        const unsigned members = (nb - i + kDoneSub - 1) / kDoneSub;  // blocks with b % 64 == i
+        const unsigned nsub = nb < (unsigned)kDoneSub ? nb : (unsigned)kDoneSub;
+        const unsigned subs = (nsub - x + 7u) / 8u;                    // sub-counters i < nsub with i % 8 == x
         const unsigned groups = nb < 8u ? nb : 8u;
-        const unsigned old = __hip_atomic_fetch_add(d.ctr + x * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1u == members) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-            const unsigned g = __hip_atomic_fetch_add(d.ctr + 8 * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (g + 1u == groups) {
-                for (int i = 0; i < 9; ++i)
-                    __hip_atomic_store(d.ctr + i * kDoneStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
+        uint32_t *c = d.ctr;
+        if (__hip_atomic_fetch_add(c + i * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != members)
+            return;
+        if (__hip_atomic_fetch_add(c + (kDoneSub + x) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != subs)
+            return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        if (__hip_atomic_fetch_add(c + (kDoneSub + 8) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups)
+            return;
+        for (int k = 0; k < kDoneCtrs; ++k)
+            __hip_atomic_store(c + k * kDoneStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

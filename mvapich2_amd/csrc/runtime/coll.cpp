@@ -468,7 +468,7 @@ int mv2h_reduce_n(const void *const *srcs, int nsrc, void *dst, size_t count, in
         tp.owner_fixed = -1;
         tp.rs_blk = count / pof2;
     }
-    LaunchCfg cfg{world().rl_grid, 2, st};
+    LaunchCfg cfg{std::min(world().rl_grid, 4096), 2, st};
     tmark0(st);
     rc = launch_reduce_n(oi, dt->kind, srcs, nsrc, dst, count, dt->extent, tp, cfg);
     tmark1(st);

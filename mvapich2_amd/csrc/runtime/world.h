@@ -84,7 +84,7 @@ struct World {
     int pipe_grid = kPipeMaxGrid;                 // pipelined collectives: workgroups (<= kPipeMaxGrid)
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
-    int rl_grid = 4096;       // reduce_local grid cap (tools/rl_variants.hip sweep)
+    int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
     uint64_t *done_flag = nullptr;  // pinned host: last completed call's sequence number

@@ -48,7 +48,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         child()
     else:
-        for mode, grid in ((1, 4096), (0, 4096), (0, 2048), (0, 1024), (0, 512)):
+        for mode, grid in ((1, 1 << 20), (0, 1 << 20), (0, 8192), (0, 4096)):
             env = dict(os.environ, MV2AMD_SYNC=str(mode), MV2AMD_RL_GRID=str(grid))
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, timeout=120,
                                capture_output=True, text=True)
