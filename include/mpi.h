@@ -58,6 +58,12 @@ typedef void(MPI_User_function)(void *, void *, int *, MPI_Datatype *);
 #define MPI_BOTTOM ((void *)0)
 #define MPI_UNDEFINED (-32766)
 #define MPI_STATUS_IGNORE ((MPI_Status *)1)
+#define MPI_STATUSES_IGNORE ((MPI_Status *)1)
+#define MPI_REQUEST_NULL ((MPI_Request)0x2c000000)
+#define MPI_ANY_SOURCE (-2)
+#define MPI_ANY_TAG (-1)
+#define MPI_PROC_NULL (-1)
+#define MPI_TAG_UB_VALUE 0x7fffffff
 #define MPI_MAX_PROCESSOR_NAME 128
 #define MPI_MAX_ERROR_STRING 512
 #define MPI_MAX_OBJECT_NAME 128
@@ -160,6 +166,9 @@ typedef void(MPI_User_function)(void *, void *, int *, MPI_Datatype *);
 #define MPI_ERR_TRUNCATE 14
 #define MPI_ERR_OTHER 15
 #define MPI_ERR_INTERN 16
+#define MPI_ERR_IN_STATUS 17
+#define MPI_ERR_PENDING 18
+#define MPI_ERR_REQUEST 19
 #define MPI_ERR_NO_MEM 34
 #define MPI_ERR_UNSUPPORTED_OPERATION 44
 #define MPI_ERR_LASTCODE 0x3fffffff
@@ -199,6 +208,40 @@ int MPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount,
 int MPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf,
                   int recvcount, MPI_Datatype recvtype, MPI_Comm comm);
 int MPI_Bcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm);
+
+/* ---- nonblocking collectives + request completion (MPI-3.1 5.12, 3.7.3) ---- */
+int MPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                   MPI_Op op, MPI_Comm comm, MPI_Request *request);
+int MPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                int root, MPI_Comm comm, MPI_Request *request);
+int MPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[],
+                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, MPI_Request *request);
+int MPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount,
+                              MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                              MPI_Request *request);
+int MPI_Iallgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf,
+                   int recvcount, MPI_Datatype recvtype, MPI_Comm comm, MPI_Request *request);
+int MPI_Ibcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm,
+               MPI_Request *request);
+int MPI_Ibarrier(MPI_Comm comm, MPI_Request *request);
+int MPI_Wait(MPI_Request *request, MPI_Status *status);
+int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status);
+int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]);
+int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]);
+int MPI_Request_free(MPI_Request *request);
+
+/* ---- point-to-point on device or host buffers, COMM_WORLD of one node (MPI-3.1 3.2-3.7) ---- */
+int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+             MPI_Status *status);
+int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag,
+                 void *recvbuf, int recvcount, MPI_Datatype recvtype, int source, int recvtag,
+                 MPI_Comm comm, MPI_Status *status);
+int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+              MPI_Request *request);
+int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+              MPI_Request *request);
+int MPI_Get_count(const MPI_Status *status, MPI_Datatype datatype, int *count);
 
 /* ---- user operations ---- */
 int MPI_Op_create(MPI_User_function *user_fn, int commute, MPI_Op *op);
@@ -267,6 +310,37 @@ int PMPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount,
 int PMPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf,
                    int recvcount, MPI_Datatype recvtype, MPI_Comm comm);
 int PMPI_Bcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm);
+int PMPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                   MPI_Op op, MPI_Comm comm, MPI_Request *request);
+int PMPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                int root, MPI_Comm comm, MPI_Request *request);
+int PMPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[],
+                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, MPI_Request *request);
+int PMPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount,
+                              MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                              MPI_Request *request);
+int PMPI_Iallgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf,
+                   int recvcount, MPI_Datatype recvtype, MPI_Comm comm, MPI_Request *request);
+int PMPI_Ibcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm,
+               MPI_Request *request);
+int PMPI_Ibarrier(MPI_Comm comm, MPI_Request *request);
+int PMPI_Wait(MPI_Request *request, MPI_Status *status);
+int PMPI_Test(MPI_Request *request, int *flag, MPI_Status *status);
+int PMPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]);
+int PMPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]);
+int PMPI_Request_free(MPI_Request *request);
+
+int PMPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int PMPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+             MPI_Status *status);
+int PMPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag,
+                 void *recvbuf, int recvcount, MPI_Datatype recvtype, int source, int recvtag,
+                 MPI_Comm comm, MPI_Status *status);
+int PMPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+              MPI_Request *request);
+int PMPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+              MPI_Request *request);
+int PMPI_Get_count(const MPI_Status *status, MPI_Datatype datatype, int *count);
 int PMPI_Op_create(MPI_User_function *user_fn, int commute, MPI_Op *op);
 int PMPI_Op_free(MPI_Op *op);
 int PMPI_Op_commutative(MPI_Op op, int *commute);

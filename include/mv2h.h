@@ -73,6 +73,33 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes_per_rank, vo
 int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream);
 int mv2h_barrier(void);
 
+/* ---- nonblocking collectives (MPI_Iallreduce family, reference iallreduce_osu.c) ----
+ * Between mv2h_defer_begin() and mv2h_defer_end(&ticket) the device collectives above
+ * return right after their kernel is enqueued instead of waiting for it.  ticket > 0:
+ * the call's completion word; ticket == 0: the call already completed (host-staged or
+ * copy-back paths complete at initiation, which MPI allows).  Tickets complete in issue
+ * order (one stream).  mv2h_wait_ticket blocks; mv2h_test_ticket sets *done.  Both return
+ * the collective's error class (e.g. a peer timeout), 0 on success. */
+/* ---- point-to-point (runtime/p2p.cpp; reference ch3 eager/IPC path, ch3u_recvq.c matching) ----
+ * Byte messages between the ranks of the node; buffers may be device or host memory.
+ * A send completes when its last chunk is in the receiver's arena (buffer reusable); a
+ * receive completes when the matched message is in `buf` (E_TRUNCATE if it was longer
+ * than cap: the first cap bytes are delivered).  Matching: posting order against arrival
+ * order, MV2H_ANY_SOURCE / MV2H_ANY_TAG wildcards, non-overtaking per (source, tag).
+ * Progress happens inside every isend/irecv/test/wait call. */
+#define MV2H_ANY_SOURCE (-2)
+#define MV2H_ANY_TAG (-1)
+int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req);
+int mv2h_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req);
+int mv2h_p2p_test(unsigned long long req, int *done, int *source, int *tag, size_t *bytes);
+int mv2h_p2p_wait(unsigned long long req, int *source, int *tag, size_t *bytes);
+int mv2h_p2p_progress(void);
+
+int mv2h_defer_begin(void);
+int mv2h_defer_end(unsigned long long *ticket);
+int mv2h_wait_ticket(unsigned long long ticket);
+int mv2h_test_ticket(unsigned long long ticket, int *done);
+
 /* ---- part (3): strided pack / unpack (MPI_Type_vector family) ----
  * pack:   dst[i*blk + j] = src[i*stride + j],  i < nblocks, j < blk  (bytes)
  * unpack: dst[i*stride + j] = src[i*blk + j] */

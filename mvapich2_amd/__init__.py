@@ -106,6 +106,22 @@ def lib():
         "MPI_Pack": ([c_vp, c_int, c_int, c_vp, c_int, ctypes.POINTER(c_int), c_int], c_int),
         "MPI_Unpack": ([c_vp, c_int, ctypes.POINTER(c_int), c_vp, c_int, c_int, c_int], c_int),
         "MPI_Pack_size": ([c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        # nonblocking collectives / requests / point-to-point
+        "MPI_Iallreduce": ([c_vp, c_vp, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Ireduce": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Ireduce_scatter_block": ([c_vp, c_vp, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Iallgather": ([c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Ibcast": ([c_vp, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Ibarrier": ([c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Wait": ([ctypes.POINTER(c_int), c_vp], c_int),
+        "MPI_Test": ([ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_vp], c_int),
+        "MPI_Waitall": ([c_int, ctypes.POINTER(c_int), c_vp], c_int),
+        "MPI_Send": ([c_vp, c_int, c_int, c_int, c_int, c_int], c_int),
+        "MPI_Recv": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "MPI_Isend": ([c_vp, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Irecv": ([c_vp, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
+        "MPI_Sendrecv": ([c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "MPI_Get_count": ([c_vp, c_int, ctypes.POINTER(c_int)], c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

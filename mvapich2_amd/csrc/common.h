@@ -71,7 +71,7 @@ inline int op_index(int handle) { return (handle & 0xf) - 1; }
 inline bool is_builtin_op(int handle) { return (handle & 0xfffffff0) == 0x58000000 && op_index(handle) >= 0 && op_index(handle) < OP_COUNT; }
 
 // MPI error classes used by the HIP layer (mirror include/mpi.h)
-enum { E_SUCCESS = 0, E_BUFFER = 1, E_COUNT = 2, E_TYPE = 3, E_COMM = 5, E_ROOT = 7, E_OP = 9,
-       E_ARG = 12, E_OTHER = 15, E_INTERN = 16, E_NO_MEM = 34, E_UNSUPPORTED = 44 };
+enum { E_SUCCESS = 0, E_BUFFER = 1, E_COUNT = 2, E_TYPE = 3, E_TAG = 4, E_COMM = 5, E_RANK = 6, E_ROOT = 7, E_OP = 9,
+       E_ARG = 12, E_TRUNCATE = 14, E_OTHER = 15, E_INTERN = 16, E_REQUEST = 19, E_NO_MEM = 34, E_UNSUPPORTED = 44 };
 
 }  // namespace mv2

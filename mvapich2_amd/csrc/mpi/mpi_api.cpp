@@ -6,6 +6,7 @@
 // (default MPI_ERRORS_ARE_FATAL).  Every MPI_X is a weak alias of PMPI_X
 // (allreduce.c:80-84).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -534,5 +535,443 @@ int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm
     return err_return(comm, rc, fn);
 }
 int MPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm) WEAK(MPI_Bcast);
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- requests
+// One table for nonblocking collectives (completion-word tickets, mv2h_defer_*)
+// and point-to-point requests (mv2h_isend / mv2h_irecv ids).  Handles are
+// kReqBase | slot; MPI_REQUEST_NULL is MPICH's 0x2c000000.
+namespace {
+enum ReqKind { RQ_COLL = 1, RQ_P2P = 2, RQ_DONE = 3 };
+struct MReq {
+    int kind = 0;
+    unsigned long long id = 0;
+    bool live = false;
+    bool is_recv = false;
+    int src = MPI_ANY_SOURCE, tag = MPI_ANY_TAG;  // RQ_DONE status
+    // derived-type staging: send keeps its packed copy, receive unpacks at completion
+    void *tmp = nullptr;
+    bool tmp_dev = false;
+    int tmp_bytes = 0;
+    void *ubuf = nullptr;
+    MPI_Datatype dt = MPI_DATATYPE_NULL;
+};
+std::vector<MReq> g_mreqs;
+constexpr MPI_Request kReqBase = (MPI_Request)0xac000000;
+
+MPI_Request req_new(const MReq &r) {
+    for (size_t i = 0; i < g_mreqs.size(); ++i)
+        if (!g_mreqs[i].live) {
+            g_mreqs[i] = r;
+            g_mreqs[i].live = true;
+            return kReqBase | (MPI_Request)i;
+        }
+    g_mreqs.push_back(r);
+    g_mreqs.back().live = true;
+    return kReqBase | (MPI_Request)(g_mreqs.size() - 1);
+}
+
+MReq *req_get(MPI_Request h) {
+    if ((h & 0xfc000000) != (kReqBase & 0xfc000000)) return nullptr;
+    const size_t i = (size_t)(h & 0x03ffffff);
+    return i < g_mreqs.size() && g_mreqs[i].live ? &g_mreqs[i] : nullptr;
+}
+
+void status_set(MPI_Status *st, int src, int tag, size_t bytes, int err) {
+    if (!st || st == MPI_STATUS_IGNORE) return;
+    st->MPI_SOURCE = src;
+    st->MPI_TAG = tag;
+    st->MPI_ERROR = err;
+    st->count_lo = (int)(bytes & 0xffffffffu);
+    st->count_hi_and_cancelled = (int)((bytes >> 32) << 1);
+}
+
+void tmp_free(MReq &r) {
+    if (!r.tmp) return;
+    if (r.tmp_dev) mv2h_free(r.tmp);
+    else free(r.tmp);
+    r.tmp = nullptr;
+}
+
+// finish a request whose underlying operation completed (rc = its error class)
+int req_finish(MReq &r, int rc, int src, int tag, size_t bytes, MPI_Status *st) {
+    if (r.kind == RQ_P2P && r.is_recv && r.tmp && (rc == MPI_SUCCESS || rc == MPI_ERR_TRUNCATE)) {
+        const long tsz = dtype_size(r.dt);
+        const int nel = tsz > 0 ? (int)(bytes / (size_t)tsz) : 0;
+        int pos = 0;
+        const int urc = PMPI_Unpack(r.tmp, (int)bytes, &pos, r.ubuf, nel, r.dt, MPI_COMM_WORLD);
+        if (rc == MPI_SUCCESS) rc = urc;
+    }
+    tmp_free(r);
+    if (r.kind == RQ_COLL) status_set(st, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, rc);
+    else if (r.kind == RQ_DONE) status_set(st, r.src, r.tag, 0, rc);
+    else if (r.is_recv) status_set(st, src, tag, bytes, rc);
+    else status_set(st, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, rc);
+    r.live = false;
+    return rc;
+}
+
+int req_wait(MReq &r, MPI_Status *st) {
+    int src = MPI_ANY_SOURCE, tag = MPI_ANY_TAG, rc = MPI_SUCCESS;
+    size_t bytes = 0;
+    if (r.kind == RQ_COLL) rc = mv2h_wait_ticket(r.id);
+    else if (r.kind == RQ_P2P) rc = mv2h_p2p_wait(r.id, &src, &tag, &bytes);
+    return req_finish(r, rc, src, tag, bytes, st);
+}
+
+int req_test(MReq &r, int *flag, MPI_Status *st) {
+    int src = MPI_ANY_SOURCE, tag = MPI_ANY_TAG, rc = MPI_SUCCESS, done = 1;
+    size_t bytes = 0;
+    if (r.kind == RQ_COLL) rc = mv2h_test_ticket(r.id, &done);
+    else if (r.kind == RQ_P2P) rc = mv2h_p2p_test(r.id, &done, &src, &tag, &bytes);
+    *flag = done;
+    if (!done && rc == MPI_SUCCESS) return MPI_SUCCESS;
+    *flag = 1;
+    return req_finish(r, rc, src, tag, bytes, st);
+}
+
+// nonblocking collective = the blocking implementation initiated with
+// deferred completion (the kernel is enqueued, the ticket waits later)
+template <class F>
+int start_coll(MPI_Request *request, const char *fn, F &&call) {
+    if (!request) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, fn);
+    mv2h_defer_begin();
+    const int rc = call();
+    unsigned long long t = 0;
+    mv2h_defer_end(&t);
+    if (rc) return rc;  // already passed through the error handler
+    MReq r;
+    r.kind = RQ_COLL;
+    r.id = t;
+    *request = req_new(r);
+    return MPI_SUCCESS;
+}
+
+int p2p_checks(MPI_Comm comm, int count, MPI_Datatype dt, int tag, bool recv) {
+    if (!g_initialized) return MPI_ERR_OTHER;
+    if (comm != MPI_COMM_WORLD) return comm_index(comm) < 0 ? MPI_ERR_COMM : MPI_ERR_UNSUPPORTED_OPERATION;
+    if (count < 0) return MPI_ERR_COUNT;
+    if (!dtype_valid(dt)) return MPI_ERR_TYPE;
+    if (recv ? (tag < 0 && tag != MPI_ANY_TAG) : tag < 0) return MPI_ERR_TAG;
+    return MPI_SUCCESS;
+}
+
+int isend_impl(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Request *request) {
+    MReq r;
+    if (dest == MPI_PROC_NULL) {
+        r.kind = RQ_DONE;
+        r.src = MPI_PROC_NULL;
+        *request = req_new(r);
+        return MPI_SUCCESS;
+    }
+    if (dest < 0 || dest >= world().size) return MPI_ERR_RANK;
+    r.kind = RQ_P2P;
+    const void *src = buf;
+    size_t bytes = (size_t)dtype_span(dt, count);
+    if (!dtype_is_contiguous(dt)) {  // device (or host) pack first, the packed copy travels
+        int psize = 0, pos = 0;
+        PMPI_Pack_size(count, dt, MPI_COMM_WORLD, &psize);
+        r.tmp_dev = is_dev(buf);
+        if (r.tmp_dev) {
+            if (mv2h_malloc(&r.tmp, (size_t)psize)) return MPI_ERR_NO_MEM;
+        } else if (!(r.tmp = malloc((size_t)psize + 1))) {
+            return MPI_ERR_NO_MEM;
+        }
+        const int rc = PMPI_Pack(buf, count, dt, r.tmp, psize, &pos, MPI_COMM_WORLD);
+        if (rc) {
+            tmp_free(r);
+            return rc;
+        }
+        src = r.tmp;
+        bytes = (size_t)pos;
+    }
+    const int rc = mv2h_isend(src, bytes, dest, tag, &r.id);
+    if (rc) {
+        tmp_free(r);
+        return rc;
+    }
+    *request = req_new(r);
+    return MPI_SUCCESS;
+}
+
+int irecv_impl(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Request *request) {
+    MReq r;
+    r.is_recv = true;
+    if (source == MPI_PROC_NULL) {
+        r.kind = RQ_DONE;
+        r.src = MPI_PROC_NULL;
+        *request = req_new(r);
+        return MPI_SUCCESS;
+    }
+    if (source != MPI_ANY_SOURCE && (source < 0 || source >= world().size)) return MPI_ERR_RANK;
+    r.kind = RQ_P2P;
+    void *dst = buf;
+    size_t cap = (size_t)dtype_span(dt, count);
+    if (!dtype_is_contiguous(dt)) {  // receive packed, unpack at completion
+        int psize = 0;
+        PMPI_Pack_size(count, dt, MPI_COMM_WORLD, &psize);
+        r.tmp_dev = is_dev(buf);
+        if (r.tmp_dev) {
+            if (mv2h_malloc(&r.tmp, (size_t)psize)) return MPI_ERR_NO_MEM;
+        } else if (!(r.tmp = malloc((size_t)psize + 1))) {
+            return MPI_ERR_NO_MEM;
+        }
+        r.ubuf = buf;
+        r.dt = dt;
+        dst = r.tmp;
+        cap = (size_t)psize;
+    }
+    const int rc = mv2h_irecv(dst, cap, source, tag, &r.id);
+    if (rc) {
+        tmp_free(r);
+        return rc;
+    }
+    *request = req_new(r);
+    return MPI_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int PMPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm,
+                    MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Iallreduce", [&] { return PMPI_Allreduce(sendbuf, recvbuf, count, dt, op, comm); });
+}
+int MPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm,
+                   MPI_Request *request) WEAK(MPI_Iallreduce);
+
+int PMPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm,
+                 MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Ireduce", [&] { return PMPI_Reduce(sendbuf, recvbuf, count, dt, op, root, comm); });
+}
+int MPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm,
+                MPI_Request *request) WEAK(MPI_Ireduce);
+
+int PMPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
+                         MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Ireduce_scatter",
+                      [&] { return PMPI_Reduce_scatter(sendbuf, recvbuf, recvcounts, dt, op, comm); });
+}
+int MPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
+                        MPI_Comm comm, MPI_Request *request) WEAK(MPI_Ireduce_scatter);
+
+int PMPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
+                               MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Ireduce_scatter_block",
+                      [&] { return PMPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, dt, op, comm); });
+}
+int MPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
+                              MPI_Comm comm, MPI_Request *request) WEAK(MPI_Ireduce_scatter_block);
+
+int PMPI_Iallgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                    MPI_Datatype recvtype, MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Iallgather", [&] {
+        return PMPI_Allgather(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, comm);
+    });
+}
+int MPI_Iallgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                   MPI_Datatype recvtype, MPI_Comm comm, MPI_Request *request) WEAK(MPI_Iallgather);
+
+int PMPI_Ibcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Ibcast", [&] { return PMPI_Bcast(buffer, count, dt, root, comm); });
+}
+int MPI_Ibcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm, MPI_Request *request)
+    WEAK(MPI_Ibcast);
+
+int PMPI_Ibarrier(MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    return start_coll(request, "MPI_Ibarrier", [&] { return PMPI_Barrier(comm); });
+}
+int MPI_Ibarrier(MPI_Comm comm, MPI_Request *request) WEAK(MPI_Ibarrier);
+
+int PMPI_Wait(MPI_Request *request, MPI_Status *status) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (!request) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Wait");
+    if (*request == MPI_REQUEST_NULL) {
+        status_set(status, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, MPI_SUCCESS);
+        return MPI_SUCCESS;
+    }
+    MReq *r = req_get(*request);
+    if (!r) return err_return(MPI_COMM_WORLD, MPI_ERR_REQUEST, "MPI_Wait");
+    const int rc = req_wait(*r, status);
+    *request = MPI_REQUEST_NULL;
+    return err_return(MPI_COMM_WORLD, rc, "MPI_Wait");
+}
+int MPI_Wait(MPI_Request *request, MPI_Status *status) WEAK(MPI_Wait);
+
+int PMPI_Test(MPI_Request *request, int *flag, MPI_Status *status) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (!request || !flag) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Test");
+    if (*request == MPI_REQUEST_NULL) {
+        *flag = 1;
+        status_set(status, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, MPI_SUCCESS);
+        return MPI_SUCCESS;
+    }
+    MReq *r = req_get(*request);
+    if (!r) return err_return(MPI_COMM_WORLD, MPI_ERR_REQUEST, "MPI_Test");
+    const int rc = req_test(*r, flag, status);
+    if (*flag) *request = MPI_REQUEST_NULL;
+    return err_return(MPI_COMM_WORLD, rc, "MPI_Test");
+}
+int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status) WEAK(MPI_Test);
+
+int PMPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (count < 0 || (count && !requests)) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Waitall");
+    // progress every request together (a receive may need a send of this rank to move)
+    int rc_all = MPI_SUCCESS;
+    for (;;) {
+        bool pending = false;
+        for (int i = 0; i < count; ++i) {
+            if (requests[i] == MPI_REQUEST_NULL) continue;
+            MReq *r = req_get(requests[i]);
+            MPI_Status *st = (!statuses || statuses == MPI_STATUSES_IGNORE) ? MPI_STATUS_IGNORE : &statuses[i];
+            if (!r) {
+                status_set(st, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, MPI_ERR_REQUEST);
+                rc_all = MPI_ERR_IN_STATUS;
+                requests[i] = MPI_REQUEST_NULL;
+                continue;
+            }
+            int flag = 0;
+            const int rc = req_test(*r, &flag, st);
+            if (flag) {
+                requests[i] = MPI_REQUEST_NULL;
+                if (rc) rc_all = MPI_ERR_IN_STATUS;
+            } else {
+                pending = true;
+            }
+        }
+        if (!pending) break;
+        sched_yield();
+    }
+    return err_return(MPI_COMM_WORLD, rc_all, "MPI_Waitall");
+}
+int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]) WEAK(MPI_Waitall);
+
+int PMPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (count < 0 || !flag || (count && !requests)) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Testall");
+    // Requests found complete are completed (set to MPI_REQUEST_NULL) even when
+    // others are still pending: a point-to-point request cannot be peeked
+    // without completing it.  *flag = 1 once all of them are complete.
+    int rc_all = MPI_SUCCESS;
+    bool any_pending = false;
+    for (int i = 0; i < count; ++i) {
+        if (requests[i] == MPI_REQUEST_NULL) continue;
+        MReq *r = req_get(requests[i]);
+        int f = 0;
+        MPI_Status *st = (!statuses || statuses == MPI_STATUSES_IGNORE) ? MPI_STATUS_IGNORE : &statuses[i];
+        if (!r) {
+            status_set(st, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, MPI_ERR_REQUEST);
+            requests[i] = MPI_REQUEST_NULL;
+            rc_all = MPI_ERR_IN_STATUS;
+            continue;
+        }
+        const int rc = req_test(*r, &f, st);
+        if (f) {
+            requests[i] = MPI_REQUEST_NULL;
+            if (rc) rc_all = MPI_ERR_IN_STATUS;
+        } else {
+            any_pending = true;
+        }
+    }
+    *flag = any_pending ? 0 : 1;
+    return err_return(MPI_COMM_WORLD, rc_all, "MPI_Testall");
+}
+int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]) WEAK(MPI_Testall);
+
+int PMPI_Request_free(MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (!request) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Request_free");
+    MReq *r = req_get(*request);
+    if (!r) return err_return(MPI_COMM_WORLD, MPI_ERR_REQUEST, "MPI_Request_free");
+    // the operation still completes; this library waits for it here
+    req_wait(*r, MPI_STATUS_IGNORE);
+    *request = MPI_REQUEST_NULL;
+    return MPI_SUCCESS;
+}
+int MPI_Request_free(MPI_Request *request) WEAK(MPI_Request_free);
+
+// ---------------------------------------------------------------- point-to-point
+int PMPI_Isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    int rc = p2p_checks(comm, count, dt, tag, false);
+    if (!rc && !request) rc = MPI_ERR_ARG;
+    if (!rc) rc = isend_impl(buf, count, dt, dest, tag, request);
+    return err_return(comm, rc, "MPI_Isend");
+}
+int MPI_Isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *request)
+    WEAK(MPI_Isend);
+
+int PMPI_Irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *request) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    int rc = p2p_checks(comm, count, dt, tag, true);
+    if (!rc && !request) rc = MPI_ERR_ARG;
+    if (!rc) rc = irecv_impl(buf, count, dt, source, tag, request);
+    return err_return(comm, rc, "MPI_Irecv");
+}
+int MPI_Irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *request)
+    WEAK(MPI_Irecv);
+
+int PMPI_Send(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    MPI_Request rq = MPI_REQUEST_NULL;
+    int rc = p2p_checks(comm, count, dt, tag, false);
+    if (!rc) rc = isend_impl(buf, count, dt, dest, tag, &rq);
+    if (!rc) rc = req_wait(*req_get(rq), MPI_STATUS_IGNORE);
+    return err_return(comm, rc, "MPI_Send");
+}
+int MPI_Send(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm) WEAK(MPI_Send);
+
+int PMPI_Recv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Status *status) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    MPI_Request rq = MPI_REQUEST_NULL;
+    int rc = p2p_checks(comm, count, dt, tag, true);
+    if (!rc) rc = irecv_impl(buf, count, dt, source, tag, &rq);
+    if (!rc) rc = req_wait(*req_get(rq), status);
+    return err_return(comm, rc, "MPI_Recv");
+}
+int MPI_Recv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Status *status)
+    WEAK(MPI_Recv);
+
+int PMPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag, void *recvbuf,
+                  int recvcount, MPI_Datatype recvtype, int source, int recvtag, MPI_Comm comm, MPI_Status *status) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    MPI_Request rr = MPI_REQUEST_NULL, sr = MPI_REQUEST_NULL;
+    int rc = p2p_checks(comm, recvcount, recvtype, recvtag, true);
+    if (!rc) rc = p2p_checks(comm, sendcount, sendtype, sendtag, false);
+    if (!rc) rc = irecv_impl(recvbuf, recvcount, recvtype, source, recvtag, &rr);
+    if (!rc) rc = isend_impl(sendbuf, sendcount, sendtype, dest, sendtag, &sr);
+    if (rc) return err_return(comm, rc, "MPI_Sendrecv");
+    MPI_Request both[2] = {rr, sr};
+    MPI_Status sts[2];
+    rc = PMPI_Waitall(2, both, sts);
+    if (status && status != MPI_STATUS_IGNORE) *status = sts[0];
+    if (rc == MPI_ERR_IN_STATUS) rc = sts[0].MPI_ERROR ? sts[0].MPI_ERROR : sts[1].MPI_ERROR;
+    return err_return(comm, rc, "MPI_Sendrecv");
+}
+int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag, void *recvbuf,
+                 int recvcount, MPI_Datatype recvtype, int source, int recvtag, MPI_Comm comm, MPI_Status *status)
+    WEAK(MPI_Sendrecv);
+
+int PMPI_Get_count(const MPI_Status *status, MPI_Datatype dt, int *count) {
+    if (!status || !count) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Get_count");
+    const long tsz = dtype_size(dt);
+    if (tsz < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_TYPE, "MPI_Get_count");
+    const unsigned long long bytes = (unsigned long long)(unsigned)status->count_lo |
+                                     ((unsigned long long)((unsigned)status->count_hi_and_cancelled >> 1) << 32);
+    if (tsz == 0) *count = 0;
+    else *count = bytes % (unsigned long long)tsz ? MPI_UNDEFINED : (int)(bytes / (unsigned long long)tsz);
+    return MPI_SUCCESS;
+}
+int MPI_Get_count(const MPI_Status *status, MPI_Datatype dt, int *count) WEAK(MPI_Get_count);
 
 }  // extern "C"

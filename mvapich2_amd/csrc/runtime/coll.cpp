@@ -68,11 +68,26 @@ static hipError_t wait_done(hipStream_t st, uint64_t want) {
     }
 }
 
+static int check_err_word() {
+    World &w = world();
+    if (w.h_err && __atomic_load_n(w.h_err, __ATOMIC_ACQUIRE)) {
+        MV2_ERR("device collective timed out waiting for a peer (MV2AMD_TIMEOUT_S)");
+        __atomic_store_n(w.h_err, 0, __ATOMIC_RELEASE);
+        return E_OTHER;
+    }
+    return 0;
+}
+
 static int finish(hipStream_t st, bool timed) {
     World &w = world();
     hipError_t e;
     const uint64_t want = w.pending;
     w.pending = 0;
+    if (w.defer && want) {  // nonblocking initiation: the ticket waits later
+        w.deferred = want;
+        return 0;
+    }
+    if (w.defer) w.deferred = 0;
     if (want) {
         e = wait_done(st, want);
         if (e == hipSuccess && timed) e = hipEventSynchronize(w.ev1);
@@ -395,6 +410,47 @@ int mv2h_local_rank(void) { return world().local_rank; }
 int mv2h_barrier(void) {
     host_barrier();
     return 0;
+}
+
+int mv2h_defer_begin(void) {
+    World &w = world();
+    w.defer = true;
+    w.deferred = 0;
+    return 0;
+}
+
+int mv2h_defer_end(unsigned long long *ticket) {
+    World &w = world();
+    w.defer = false;
+    if (ticket) *ticket = w.deferred;
+    w.deferred = 0;
+    return 0;
+}
+
+int mv2h_test_ticket(unsigned long long ticket, int *done) {
+    World &w = world();
+    if (done) *done = 1;
+    if (ticket == 0 || !w.done_flag) return 0;
+    if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) < ticket) {
+        const hipError_t q = hipStreamQuery(w.stream);
+        if (q == hipErrorNotReady) {
+            if (done) *done = 0;
+            return 0;
+        }
+        if (q != hipSuccess) return E_INTERN;
+    }
+    return check_err_word();
+}
+
+int mv2h_wait_ticket(unsigned long long ticket) {
+    World &w = world();
+    if (ticket == 0 || !w.done_flag) return 0;
+    const hipError_t e = wait_done(w.stream, ticket);
+    if (e != hipSuccess) {
+        MV2_ERR("waiting for a nonblocking collective failed: %s", hipGetErrorString(e));
+        return E_INTERN;
+    }
+    return check_err_word();
 }
 
 // ---------------------------------------------------------------------------

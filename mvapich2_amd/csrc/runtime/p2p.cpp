@@ -1,0 +1,355 @@
+// p2p.cpp — point-to-point messages on device (or host) buffers between the
+// ranks of one node: MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv.
+//
+// Reference: the ch3 device-buffer pt2pt path (MPIDI_CH3_EagerContigSend,
+// ch3u_eager.c:153, with CUDA IPC eager/rendezvous in ibv_cuda_ipc.c and the
+// matching queues of ch3u_recvq.c: posted + unexpected, non-overtaking
+// per (source, tag, comm)).
+//
+// Here:
+//   * one FIFO channel per ordered pair (src -> dst): kP2PSlots chunk records
+//     in the /dev/shm control segment (world.h P2PChan) and kP2PSlots data
+//     slots of kP2PChunk bytes in dst's uncached, IPC-exported P2P arena;
+//   * the sender copies a chunk straight into the destination GPU's slot
+//     (hipMemcpyAsync over xGMI into the peer mapping), waits for the copy,
+//     then publishes the record (release) — a send completes once its last
+//     chunk is in the receiver's arena (eager through the ring; messages
+//     larger than the ring flow as the receiver frees slots);
+//   * the receiver matches a message when its first chunk arrives against the
+//     posted receives in posting order (MPI_ANY_SOURCE / MPI_ANY_TAG), else
+//     drains it into an unexpected-message buffer so later messages keep
+//     flowing; a receive posted later takes the earliest matching unexpected
+//     message (arrival order), so per-(source, tag) order is preserved;
+//   * progress is made inside Wait/Test of any request (and blocking calls).
+// Copies run on their own stream so a pending nonblocking collective never
+// blocks point-to-point progress.
+#include <hip/hip_runtime.h>
+#include <sched.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <deque>
+#include <list>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/mv2h.h"
+#include "log.h"
+#include "world.h"
+
+namespace mv2 {
+
+namespace {
+
+struct Req {
+    bool send;
+    bool done = false;
+    int err = 0;
+    // send
+    const char *sbuf = nullptr;
+    size_t bytes = 0, off = 0;
+    int peer = -1, tag = 0;
+    uint64_t msg = 0;
+    // receive
+    char *rbuf = nullptr;
+    size_t cap = 0;
+    int src_want = 0, tag_want = 0;
+    int src = -1, rtag = -1;
+    size_t total = 0;
+};
+
+struct Unexp {
+    int src, tag;
+    size_t total;
+    size_t got = 0;  // bytes landed in `data` (copies synchronised)
+    bool complete = false;
+    std::vector<char> data;
+};
+
+// message currently arriving on the channel from one source
+struct Arrival {
+    bool active = false;
+    size_t total = 0, got = 0;  // got: chunks issued (bytes)
+    Req *req = nullptr;         // matched receive, or
+    Unexp *ux = nullptr;        // unexpected buffer
+};
+
+std::unordered_map<uint64_t, Req *> g_reqs;
+uint64_t g_next_id = 1;
+uint64_t g_msg_seq = 0;
+std::deque<Req *> g_sendq[kMaxRanks];  // per destination, FIFO (one message at a time per channel)
+std::list<Req *> g_posted;             // unmatched receives in posting order
+std::list<Unexp *> g_unexp;            // unexpected messages in arrival order
+Arrival g_in[kMaxRanks];
+
+bool matches(const Req *r, int src, int tag) {
+    return (r->src_want == MV2H_ANY_SOURCE || r->src_want == src) && (r->tag_want == MV2H_ANY_TAG || r->tag_want == tag);
+}
+
+char *slot_ptr(char *arena, int src, uint64_t pos) {
+    return arena + ((size_t)src * kP2PSlots + (size_t)(pos % kP2PSlots)) * kP2PChunk;
+}
+
+int ready() {
+    World &w = world();
+    if (!w.inited || !w.shm || !w.p2p || !w.p2p_stream) {
+        MV2_ERR("point-to-point needs MPI_Init and at most %d ranks on the node", kMaxRanks);
+        return E_OTHER;
+    }
+    return 0;
+}
+
+// One progress pass: push queued send chunks into free slots, drain arrived
+// chunks into matched receives / unexpected buffers.  Returns an error class
+// or 0; *moved = whether anything happened.
+int progress(bool *moved) {
+    World &w = world();
+    const int n = w.size, me = w.rank;
+    *moved = false;
+
+    struct SendPub {
+        P2PChan *c;
+        uint64_t pos;
+        P2PRec rec;
+        Req *r;
+        bool last;
+    };
+    struct RecvPub {
+        P2PChan *c;
+        uint64_t head;  // new head after this chunk
+        int src;
+        size_t len;
+        bool last;
+        Req *r;
+        Unexp *ux;
+    };
+    std::vector<SendPub> sp;
+    std::vector<RecvPub> rp;
+
+    for (int d = 0; d < n; ++d) {
+        if (g_sendq[d].empty()) continue;
+        P2PChan &c = w.shm->chan[me][d];
+        uint64_t tail = c.tail.load(std::memory_order_relaxed);
+        const uint64_t head = c.head.load(std::memory_order_acquire);
+        while (!g_sendq[d].empty() && tail - head < (uint64_t)kP2PSlots) {
+            Req *r = g_sendq[d].front();
+            const size_t len = std::min(kP2PChunk, r->bytes - r->off);
+            if (len && hipMemcpyAsync(slot_ptr(w.peer_p2p[d], me, tail), r->sbuf + r->off, len, hipMemcpyDefault,
+                                      w.p2p_stream) != hipSuccess) {
+                MV2_ERR("point-to-point chunk copy to rank %d failed", d);
+                return E_INTERN;
+            }
+            P2PRec rec{r->msg, r->tag, 0, r->bytes, r->off, len};
+            r->off += len;
+            const bool last = r->off >= r->bytes;
+            sp.push_back({&c, tail, rec, r, last});
+            ++tail;
+            if (last) g_sendq[d].pop_front();
+        }
+    }
+
+    for (int s = 0; s < n; ++s) {
+        P2PChan &c = w.shm->chan[s][me];
+        uint64_t head = c.head.load(std::memory_order_relaxed);
+        const uint64_t tail = c.tail.load(std::memory_order_acquire);
+        Arrival &a = g_in[s];
+        while (head < tail) {
+            const P2PRec rec = c.rec[head % kP2PSlots];
+            if (!a.active) {
+                if (rec.off != 0) {
+                    MV2_ERR("point-to-point channel from rank %d out of sequence", s);
+                    return E_INTERN;
+                }
+                a = Arrival{};
+                a.active = true;
+                a.total = rec.total;
+                for (auto it = g_posted.begin(); it != g_posted.end(); ++it) {
+                    if (matches(*it, s, rec.tag)) {
+                        a.req = *it;
+                        g_posted.erase(it);
+                        break;
+                    }
+                }
+                if (a.req) {
+                    a.req->src = s;
+                    a.req->rtag = rec.tag;
+                    a.req->total = rec.total;
+                } else {
+                    a.ux = new Unexp{s, rec.tag, (size_t)rec.total};
+                    a.ux->data.resize(rec.total ? rec.total : 1);
+                    g_unexp.push_back(a.ux);
+                }
+            }
+            const char *src = slot_ptr(w.p2p, s, head);
+            hipError_t e = hipSuccess;
+            if (a.req) {
+                const size_t room = a.req->cap > rec.off ? std::min<size_t>(rec.len, a.req->cap - rec.off) : 0;
+                if (room) e = hipMemcpyAsync(a.req->rbuf + rec.off, src, room, hipMemcpyDefault, w.p2p_stream);
+            } else if (rec.len) {
+                e = hipMemcpyAsync(a.ux->data.data() + rec.off, src, rec.len, hipMemcpyDefault, w.p2p_stream);
+            }
+            if (e != hipSuccess) {
+                MV2_ERR("point-to-point chunk copy from rank %d failed", s);
+                return E_INTERN;
+            }
+            a.got += rec.len;
+            ++head;
+            const bool last = a.got >= a.total;
+            rp.push_back({&c, head, s, (size_t)rec.len, last, a.req, a.ux});
+            if (last) a.active = false;
+        }
+    }
+
+    if (sp.empty() && rp.empty()) return 0;
+    *moved = true;
+    if (hipStreamSynchronize(w.p2p_stream) != hipSuccess) {
+        MV2_ERR("point-to-point copies failed: %s", hipGetErrorString(hipGetLastError()));
+        return E_INTERN;
+    }
+    // data is in place: publish records / free slots, complete requests
+    for (const SendPub &p : sp) {
+        p.c->rec[p.pos % kP2PSlots] = p.rec;
+        p.c->tail.store(p.pos + 1, std::memory_order_release);
+        if (p.last) p.r->done = true;
+    }
+    for (const RecvPub &p : rp) {
+        p.c->head.store(p.head, std::memory_order_release);
+        if (p.ux) {
+            p.ux->got += p.len;
+            if (p.last) p.ux->complete = true;
+        }
+        if (p.r && p.last) {
+            if (p.r->total > p.r->cap) p.r->err = E_TRUNCATE;
+            p.r->done = true;
+        }
+    }
+    return 0;
+}
+
+uint64_t add_req(Req *r) {
+    const uint64_t id = g_next_id++;
+    g_reqs[id] = r;
+    return id;
+}
+
+}  // namespace
+}  // namespace mv2
+
+using namespace mv2;
+
+extern "C" {
+
+int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req) {
+    int rc = ready();
+    if (rc) return rc;
+    World &w = world();
+    if (dest < 0 || dest >= w.size) return E_RANK;
+    if (tag < 0) return E_TAG;
+    if (bytes && !buf) return E_BUFFER;
+    Req *r = new Req{};
+    r->send = true;
+    r->sbuf = (const char *)buf;
+    r->bytes = bytes;
+    r->peer = dest;
+    r->tag = tag;
+    r->msg = ++g_msg_seq;
+    g_sendq[dest].push_back(r);
+    *req = add_req(r);
+    bool moved;
+    return progress(&moved);  // eager: start pushing right away
+}
+
+int mv2h_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req) {
+    int rc = ready();
+    if (rc) return rc;
+    World &w = world();
+    if (source != MV2H_ANY_SOURCE && (source < 0 || source >= w.size)) return E_RANK;
+    if (tag < 0 && tag != MV2H_ANY_TAG) return E_TAG;
+    if (cap && !buf) return E_BUFFER;
+    Req *r = new Req{};
+    r->send = false;
+    r->rbuf = (char *)buf;
+    r->cap = cap;
+    r->src_want = source;
+    r->tag_want = tag;
+    *req = add_req(r);
+    // earliest matching unexpected message first (arrival order)
+    for (auto it = g_unexp.begin(); it != g_unexp.end(); ++it) {
+        Unexp *u = *it;
+        if (!matches(r, u->src, u->tag)) continue;
+        r->src = u->src;
+        r->rtag = u->tag;
+        r->total = u->total;
+        const size_t have = std::min(u->got, cap);
+        if (have && hipMemcpy(buf, u->data.data(), have, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+        g_unexp.erase(it);
+        if (u->complete) {
+            if (u->total > cap) r->err = E_TRUNCATE;
+            r->done = true;
+        } else {
+            // still arriving: the rest of its chunks go straight to the user buffer
+            Arrival &a = g_in[u->src];
+            a.ux = nullptr;
+            a.req = r;
+        }
+        delete u;
+        bool moved;
+        return progress(&moved);
+    }
+    g_posted.push_back(r);
+    bool moved;
+    return progress(&moved);
+}
+
+int mv2h_p2p_test(unsigned long long id, int *done, int *source, int *tag, size_t *bytes) {
+    auto it = g_reqs.find(id);
+    if (it == g_reqs.end()) return E_REQUEST;
+    Req *r = it->second;
+    if (!r->done) {
+        bool moved;
+        const int rc = progress(&moved);
+        if (rc) return rc;
+    }
+    *done = r->done ? 1 : 0;
+    if (!r->done) return 0;
+    if (!r->send) {
+        if (source) *source = r->src;
+        if (tag) *tag = r->rtag;
+        if (bytes) *bytes = std::min(r->total, r->cap);
+    }
+    const int err = r->err;
+    g_reqs.erase(it);
+    delete r;
+    return err;
+}
+
+int mv2h_p2p_wait(unsigned long long id, int *source, int *tag, size_t *bytes) {
+    if (g_reqs.find(id) == g_reqs.end()) return E_REQUEST;
+    const auto t0 = std::chrono::steady_clock::now();
+    const char *tv = getenv("MV2AMD_TIMEOUT_S");
+    const double limit = (tv && *tv) ? atof(tv) : 120.0;
+    unsigned idle = 0;
+    for (;;) {
+        int done = 0;
+        const int rc = mv2h_p2p_test(id, &done, source, tag, bytes);
+        if (done || rc) return rc;
+        if (++idle > 64) {
+            sched_yield();
+            if ((idle & 1023) == 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+                MV2_ERR("point-to-point request not matched within %.0f s (MV2AMD_TIMEOUT_S)", limit);
+                return E_OTHER;
+            }
+        }
+    }
+}
+
+int mv2h_p2p_progress(void) {
+    if (ready()) return 0;
+    bool moved;
+    return progress(&moved);
+}
+
+}  // extern "C"

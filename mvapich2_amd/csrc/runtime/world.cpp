@@ -240,6 +240,10 @@ int world_init() {
                 MV2_ERR("hipExtMallocWithFlags(uncached) for the one-shot arena failed");
                 return E_NO_MEM;
             }
+            if (hipExtMallocWithFlags((void **)&w.p2p, kP2PArena, hipDeviceMallocUncached) != hipSuccess) {
+                MV2_ERR("hipExtMallocWithFlags(uncached) for the point-to-point arena failed");
+                return E_NO_MEM;
+            }
             if (hipExtMallocWithFlags((void **)&w.pipe_rs, kPipeRegion, hipDeviceMallocUncached) != hipSuccess ||
                 hipExtMallocWithFlags((void **)&w.pipe_ag, kPipeRegion, hipDeviceMallocUncached) != hipSuccess) {
                 MV2_ERR("hipExtMallocWithFlags(uncached) for the pipeline arenas (2 x %zu MiB) failed",
@@ -250,7 +254,8 @@ int world_init() {
             if (hipIpcGetMemHandle(&me.sig_handle, w.sig) != hipSuccess ||
                 hipIpcGetMemHandle(&me.arena_handle, w.arena) != hipSuccess ||
                 hipIpcGetMemHandle(&me.pipe_rs_handle, w.pipe_rs) != hipSuccess ||
-                hipIpcGetMemHandle(&me.pipe_ag_handle, w.pipe_ag) != hipSuccess) {
+                hipIpcGetMemHandle(&me.pipe_ag_handle, w.pipe_ag) != hipSuccess ||
+                hipIpcGetMemHandle(&me.p2p_handle, w.p2p) != hipSuccess) {
                 MV2_ERR("hipIpcGetMemHandle failed for the signal page / arenas");
                 return E_OTHER;
             }
@@ -263,17 +268,19 @@ int world_init() {
                     w.peer_arena[j] = w.arena;
                     w.peer_rs.p[j] = w.pipe_rs;
                     w.peer_ag.p[j] = w.pipe_ag;
+                    w.peer_p2p[j] = w.p2p;
                     continue;
                 }
                 if (w.shm->r[j].slot_bytes != w.slot_bytes) {
                     MV2_ERR("MV2AMD_ONESHOT_MAX differs between ranks");
                     return E_OTHER;
                 }
-                void *ps = nullptr, *pa = nullptr, *pr = nullptr, *pg = nullptr;
+                void *ps = nullptr, *pa = nullptr, *pr = nullptr, *pg = nullptr, *pp = nullptr;
                 if (hipIpcOpenMemHandle(&ps, w.shm->r[j].sig_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
                     hipIpcOpenMemHandle(&pa, w.shm->r[j].arena_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
                     hipIpcOpenMemHandle(&pr, w.shm->r[j].pipe_rs_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
-                    hipIpcOpenMemHandle(&pg, w.shm->r[j].pipe_ag_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    hipIpcOpenMemHandle(&pg, w.shm->r[j].pipe_ag_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                    hipIpcOpenMemHandle(&pp, w.shm->r[j].p2p_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                     MV2_ERR("hipIpcOpenMemHandle failed for rank %d (peer access over xGMI?)", j);
                     return E_OTHER;
                 }
@@ -281,10 +288,22 @@ int world_init() {
                 w.peer_arena[j] = (char *)pa;
                 w.peer_rs.p[j] = (char *)pr;
                 w.peer_ag.p[j] = (char *)pg;
+                w.peer_p2p[j] = (char *)pp;
             }
             host_barrier();
         }
     }
+    if (w.size == 1 && !control_only) {
+        void *p = mmap(nullptr, sizeof(ShmSeg), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) return E_NO_MEM;
+        w.shm = (ShmSeg *)p;
+        if (hipExtMallocWithFlags((void **)&w.p2p, kP2PArena, hipDeviceMallocUncached) != hipSuccess) {
+            MV2_ERR("hipExtMallocWithFlags(uncached) for the point-to-point arena failed");
+            return E_NO_MEM;
+        }
+        w.peer_p2p[0] = w.p2p;
+    }
+    if (!control_only && hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
     w.inited = true;
     if (w.size > 1 && w.size <= kMaxRanks && !control_only && env_long("MV2AMD_SELFTEST", 1) != 0) {
         const int rc = coll_selftest();
@@ -309,6 +328,7 @@ int world_finalize() {
                 if (w.peer_arena[j]) hipIpcCloseMemHandle(w.peer_arena[j]);
                 if (w.peer_rs.p[j]) hipIpcCloseMemHandle(w.peer_rs.p[j]);
                 if (w.peer_ag.p[j]) hipIpcCloseMemHandle(w.peer_ag.p[j]);
+                if (w.peer_p2p[j]) hipIpcCloseMemHandle(w.peer_p2p[j]);
             }
         }
         host_barrier();  // nobody maps our pages any more
@@ -322,6 +342,7 @@ int world_finalize() {
     if (w.arena) hipFree(w.arena);
     if (w.pipe_rs) hipFree(w.pipe_rs);
     if (w.pipe_ag) hipFree(w.pipe_ag);
+    if (w.p2p) hipFree(w.p2p);
     w.finalized = true;
     return 0;
 }

@@ -27,6 +27,30 @@ namespace mv2 {
 
 constexpr int kShmMaxRanks = 64;
 
+// Point-to-point channels (runtime/p2p.cpp): per ordered pair (src -> dst) a
+// FIFO of kP2PSlots chunk records in the control segment and kP2PSlots data
+// slots of kP2PChunk bytes in dst's IPC-exported, uncached P2P arena.
+constexpr int kP2PSlots = 16;
+constexpr size_t kP2PChunk = (size_t)1 << 20;
+constexpr size_t kP2PArena = (size_t)kMaxRanks * kP2PSlots * kP2PChunk;  // 128 MiB per rank
+
+struct P2PRec {
+    uint64_t msg;    // sender's message sequence number
+    int32_t tag;
+    int32_t pad;
+    uint64_t total;  // message bytes
+    uint64_t off;    // byte offset of this chunk
+    uint64_t len;    // bytes in this chunk (0 only for an empty message)
+};
+
+struct alignas(64) P2PChan {
+    std::atomic<uint64_t> tail;  // chunk records published by the sender
+    char pad0[56];
+    std::atomic<uint64_t> head;  // chunk records consumed by the receiver (slot freed)
+    char pad1[56];
+    P2PRec rec[kP2PSlots];
+};
+
 struct alignas(64) ShmRank {
     std::atomic<uint64_t> arrive;  // host barrier generation
     char pad0[56];
@@ -40,6 +64,7 @@ struct alignas(64) ShmRank {
     uint64_t slot_bytes;
     hipIpcMemHandle_t pipe_rs_handle;
     hipIpcMemHandle_t pipe_ag_handle;
+    hipIpcMemHandle_t p2p_handle;
 };
 
 struct ShmSeg {
@@ -48,6 +73,7 @@ struct ShmSeg {
     int size;
     int pad;
     ShmRank r[kShmMaxRanks];
+    P2PChan chan[kMaxRanks][kMaxRanks];  // [src][dst]
 };
 
 struct World {
@@ -74,6 +100,11 @@ struct World {
     uint64_t round = 0;       // pipeline rounds issued (slot parity)
     uint64_t os_calls = 0;    // one-shot calls issued (arena parity)
 
+    // point-to-point (runtime/p2p.cpp)
+    char *p2p = nullptr;                  // my P2P arena: [src][slot] chunks
+    char *peer_p2p[kMaxRanks] = {};       // rank j's P2P arena (mapped; entry me = mine)
+    hipStream_t p2p_stream = nullptr;     // chunk copies (separate from the collectives' stream)
+
     int *h_err = nullptr;     // pinned host error word written by kernels on timeout
     uint64_t timeout_ticks = 0;
     double wall_clock_khz = 100000.0;
@@ -90,6 +121,8 @@ struct World {
     uint64_t *done_flag = nullptr;  // pinned host: last completed call's sequence number
     uint64_t done_seq = 0;          // last sequence number armed
     uint64_t pending = 0;           // seq the current call waits for (0: stream sync)
+    bool defer = false;             // nonblocking initiation: finish() leaves the wait to a ticket
+    uint64_t deferred = 0;          // ticket of the last deferred call (0: completed at initiation)
 
     // timing (bench)
     bool timing = false;
