@@ -232,7 +232,7 @@ def rccl_child():
                           "what": "torch.distributed all_reduce (RCCL) fp32 SUM 256 MiB, comparator only"}), flush=True)
 
 
-def rccl_comparator(L, world, rank, size, steps, timeout=240):
+def rccl_comparator(L, world, rank, size, steps, timeout=150):
     """Every rank starts one rccl_child; rank 0 reads its line."""
     import socket
     port = np.zeros(1, dtype=np.int32)
@@ -253,7 +253,8 @@ def rccl_comparator(L, world, rank, size, steps, timeout=240):
         p.communicate()
         return {"error": f"comparator timed out after {timeout} s"}
     if p.returncode != 0:
-        return {"error": (err or "")[-200:]}
+        lines = [l for l in (err or "").splitlines() if "rror" in l and "destroy_process_group" not in l]
+        return {"error": (lines[-1] if lines else (err or "")[-200:])[-300:], "returncode": p.returncode}
     if rank == 0:
         try:
             return json.loads(out.strip().splitlines()[-1])
@@ -318,14 +319,42 @@ def bench_nranks(args, L, rank, size):
     L.mv2h_timing_enable(0)
     lat_ok = bool(np.all(r8.download(np.float32, count=2) == size))
 
+    # device point-to-point bandwidth, rank 0 -> rank 1 (osu_bw pattern: a window of
+    # Isends, one Waitall; the receiver posts the matching Irecvs)
+    pbytes, win = 16 << 20, 8
+    BYTE = TYPES["MPI_BYTE"][0]
+    pb = m.DeviceBuffer(pbytes * win)
+    p2p_s = 0.0
+    for it in range(1 + max(2, ks)):
+        L.MPI_Barrier(world)
+        t0 = time.perf_counter()
+        if rank in (0, 1):
+            reqs = (ctypes.c_int * win)()
+            for w_ in range(win):
+                q = ctypes.c_int()
+                if rank == 0:
+                    m.check(L.MPI_Isend(pb.ptr + w_ * pbytes, pbytes, BYTE, 1, 50, world, ctypes.byref(q)), "Isend")
+                else:
+                    m.check(L.MPI_Irecv(pb.ptr + w_ * pbytes, pbytes, BYTE, 0, 50, world, ctypes.byref(q)), "Irecv")
+                reqs[w_] = q.value
+            m.check(L.MPI_Waitall(win, reqs, None), "Waitall")
+            if rank == 1:  # osu_bw: the receiver's ack closes the window
+                m.check(L.MPI_Send(pb.ptr, 4, BYTE, 0, 51, world), "ack")
+            else:
+                m.check(L.MPI_Recv(pb.ptr, 4, BYTE, 1, 51, world, None), "ack")
+        if it:
+            p2p_s += time.perf_counter() - t0
+    p2p_s /= max(2, ks)
+    del pb
+
     # max over ranks through the library itself (device allreduce MAX)
     vals = np.array([step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat / args.lat_iters,
-                     float(np.median(lat_k)), 0.0 if (ok and lat_ok) else 1.0], dtype=np.float64)
+                     float(np.median(lat_k)), 0.0 if (ok and lat_ok) else 1.0, p2p_s], dtype=np.float64)
     dm = m.DeviceBuffer(vals.nbytes)
     dm.upload(vals)
     dr = m.DeviceBuffer(vals.nbytes)
     m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, len(vals), F64, MAX, world), "max")
-    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad) = dr.download(np.float64)
+    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad, p2p_s) = dr.download(np.float64)
     f = (size - 1) / size
     busbw = 2.0 * f * S_BYTES / step_s / 1e9
     kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
@@ -340,6 +369,8 @@ def bench_nranks(args, L, rank, size):
         "allgather_char": line4(ag_s, ag_k, f * S_BYTES),
         "bcast_char": line4(bc_s, bc_k, S_BYTES),
         "allreduce_maxloc_double_int": line4(ml_s, ml_k, 2.0 * f * nrec * 12),
+        "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
+                              "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
     del sb, rb, rsb
     if args.rccl:

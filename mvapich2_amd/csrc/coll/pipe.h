@@ -80,6 +80,10 @@ __device__ __forceinline__ void job_addr(const JobTable &t, size_t f, const v4u 
     d = (v4u *)t.dst[j] + (f - t.pre[j]);
 }
 
+// LocalDst: destinations are this GPU's own buffers -> plain stores (the HBM
+// write path the Reduce_local sweep measured fastest); arena destinations on
+// peers keep non-temporal stores.
+template <bool LocalDst>
 __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
     constexpr int U = 4;
     __shared__ JobTable t;
@@ -128,7 +132,8 @@ __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
                 const size_t fu = f + (size_t)u * kPipeThreads;
                 if (fu < NV) {
                     job_addr(t, fu, s, d);
-                    st_nt(d, cur[u]);
+                    if (LocalDst) *d = cur[u];
+                    else st_nt(d, cur[u]);
                 }
             }
             if (!more) break;
@@ -170,7 +175,11 @@ __device__ __forceinline__ void blk_copy_multi(const Dsts &d, const char *src, s
                 if (d.p[k]) {
 #pragma unroll
                     for (int u = 0; u < U; ++u)
-                        if (x + (size_t)u * kPipeThreads < nv) st_nt((v4u *)d.p[k] + x + (size_t)u * kPipeThreads, cur[u]);
+                        if (x + (size_t)u * kPipeThreads < nv) {
+                            v4u *q = (v4u *)d.p[k] + x + (size_t)u * kPipeThreads;
+                            if (k == kMaxRanks) *q = cur[u];  // own recv buffer
+                            else st_nt(q, cur[u]);
+                        }
                 }
             }
             if (!more) break;
@@ -227,7 +236,10 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
                     const v4u r = vreduce_n<Rd>(cur[u], a.n, a.tp, ebase + xu * N);
 #pragma unroll
                     for (int k = 0; k < kMaxRanks + 1; ++k)
-                        if (d.p[k]) st_nt((v4u *)d.p[k] + xu, r);
+                        if (d.p[k]) {
+                            if (k == kMaxRanks) ((v4u *)d.p[k])[xu] = r;  // own recv buffer
+                            else st_nt((v4u *)d.p[k] + xu, r);
+                        }
                 }
             }
             if (!more) break;
@@ -266,7 +278,7 @@ __device__ __forceinline__ void gather_slots(const PipeArgs &a, uint64_t par, si
             jb.len[j] = range_len(a, j, rbase);
         }
     }
-    blk_copy_jobs(jb);
+    blk_copy_jobs<true>(jb);
 }
 
 // P1 of round k: my part of every other segment -> its owner's RS slot [par][me]
@@ -284,7 +296,7 @@ __device__ __forceinline__ void scatter_round(const PipeArgs &a, int k) {
             jb.len[j] = range_len(a, j, rbase);
         }
     }
-    blk_copy_jobs(jb);
+    blk_copy_jobs<false>(jb);
 }
 
 // P2 of round k: reduce my segment's range from the n RS slots (own operand
@@ -383,7 +395,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
                             jb.len[j] = rlen(j);
                         }
                     }
-                    blk_copy_jobs(jb);
+                    blk_copy_jobs<false>(jb);
                 }
                 const size_t l = rlen(root);
                 if (l) {

@@ -303,7 +303,6 @@ int world_init() {
         }
         w.peer_p2p[0] = w.p2p;
     }
-    if (!control_only && hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
     w.inited = true;
     if (w.size > 1 && w.size <= kMaxRanks && !control_only && env_long("MV2AMD_SELFTEST", 1) != 0) {
         const int rc = coll_selftest();
