@@ -67,7 +67,8 @@ BASIC = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_F
 COUNTS = [1, 3, 100, 4099, 70001, 300007]  # one-shot (<=256 KiB) and pipelined sizes, ragged tails
 
 
-@pytest.mark.parametrize("n,geom", [(2, "default"), (3, "default"), (4, "default"), (3, "small"), (4, "small")])
+@pytest.mark.parametrize("n,geom", [(2, "default"), (3, "default"), (4, "default"), (3, "small"), (4, "small"),
+                                    (7, "small"), (8, "default")])
 def test_collectives_multiprocess(n, geom, tmp_path, golden):
     cases = []
     seed = 1
