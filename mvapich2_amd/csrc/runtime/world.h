@@ -30,9 +30,9 @@ constexpr int kShmMaxRanks = 64;
 // Point-to-point channels (runtime/p2p.cpp): per ordered pair (src -> dst) a
 // FIFO of kP2PSlots chunk records in the control segment and kP2PSlots data
 // slots of kP2PChunk bytes in dst's IPC-exported, uncached P2P arena.
-constexpr int kP2PSlots = 16;
-constexpr size_t kP2PChunk = (size_t)1 << 20;
-constexpr size_t kP2PArena = (size_t)kMaxRanks * kP2PSlots * kP2PChunk;  // 128 MiB per rank
+constexpr int kP2PSlots = 4;
+constexpr size_t kP2PChunk = (size_t)8 << 20;
+constexpr size_t kP2PArena = (size_t)kMaxRanks * kP2PSlots * kP2PChunk;  // 256 MiB per rank
 
 struct P2PRec {
     uint64_t msg;    // sender's message sequence number

@@ -42,8 +42,8 @@ def main():
     L.MPI_Comm_set_errhandler(WORLD, 0x54000001)
     right, left = (rank + 1) % n, (rank - 1) % n
 
-    # 1. ring exchange with Sendrecv at sizes below, at and above the 16 MiB channel ring
-    for nbytes in (0, 1, 4093, 1 << 20, (1 << 20) + 17, 40 << 20):
+    # 1. ring exchange with Sendrecv at sizes below, at and above the 32 MiB channel ring (8 MiB chunks)
+    for nbytes in (0, 1, 4093, 8 << 20, (8 << 20) + 17, 40 << 20):
         sb = m.DeviceBuffer.from_array(pattern(nbytes, rank, right, 5)) if nbytes else m.DeviceBuffer(1)
         rb = m.DeviceBuffer(max(nbytes, 1))
         st = Status()
@@ -85,7 +85,7 @@ def main():
         assert seen == set(range(1, n))
 
     # 3. Isend/Irecv both directions with Waitall (must not deadlock above the ring size)
-    nbytes = 24 << 20
+    nbytes = 48 << 20
     sb = m.DeviceBuffer.from_array(pattern(nbytes, rank, right, 9))
     rb = m.DeviceBuffer(nbytes)
     q0, q1 = ctypes.c_int(), ctypes.c_int()
