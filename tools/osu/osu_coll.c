@@ -6,7 +6,7 @@
  * report the average over ranks of per-rank mean latency), with `-d rocm`
  * device buffers and busbw columns added (OMB prints latency only).
  *
- *   osu_coll -c allreduce|reduce|reduce_scatter|allgather|bcast|reduce_local
+ *   osu_coll -c allreduce|reduce|reduce_scatter|allgather|bcast|reduce_local|latency|bw
  *            [-m min:max bytes] [-i iters] [-x warmup] [-d rocm|host] [-v]
  */
 #include <hip/hip_runtime.h>
@@ -39,6 +39,48 @@ static void fill(void *p, size_t count, int rank) {
     free(h);
 }
 
+/* osu_latency / osu_bw patterns between ranks 0 and 1 (osu_latency.c, osu_bw.c):
+ * latency = half the ping-pong round trip; bw = a window of 64 Isend/Irecv then
+ * the receiver's 4-byte ack, bytes / time. */
+static int run_pt2pt(int rank, void *sbuf, void *rbuf) {
+    const int window = 64;
+    MPI_Request reqs[64];
+    for (size_t sz = min_sz; sz <= max_sz; sz *= 2) {
+        const int large = sz > 8192;
+        const int iters = large ? iters_large : iters_small, skip = large ? skip_large : skip_small;
+        double t0 = 0.0;
+        MPI_Barrier(MPI_COMM_WORLD);
+        for (int it = 0; it < iters + skip; ++it) {
+            if (it == skip) t0 = MPI_Wtime();
+            if (!strcmp(coll, "latency")) {
+                if (rank == 0) {
+                    MPI_Send(sbuf, (int)sz, MPI_CHAR, 1, 1, MPI_COMM_WORLD);
+                    MPI_Recv(rbuf, (int)sz, MPI_CHAR, 1, 1, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+                } else if (rank == 1) {
+                    MPI_Recv(rbuf, (int)sz, MPI_CHAR, 0, 1, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+                    MPI_Send(sbuf, (int)sz, MPI_CHAR, 0, 1, MPI_COMM_WORLD);
+                }
+            } else {
+                if (rank == 0) {
+                    for (int w = 0; w < window; ++w) MPI_Isend(sbuf, (int)sz, MPI_CHAR, 1, 100, MPI_COMM_WORLD, &reqs[w]);
+                    MPI_Waitall(window, reqs, MPI_STATUSES_IGNORE);
+                    MPI_Recv(rbuf, 4, MPI_CHAR, 1, 101, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+                } else if (rank == 1) {
+                    for (int w = 0; w < window; ++w) MPI_Irecv(rbuf, (int)sz, MPI_CHAR, 0, 100, MPI_COMM_WORLD, &reqs[w]);
+                    MPI_Waitall(window, reqs, MPI_STATUSES_IGNORE);
+                    MPI_Send(sbuf, 4, MPI_CHAR, 0, 101, MPI_COMM_WORLD);
+                }
+            }
+        }
+        const double t = MPI_Wtime() - t0;
+        if (rank == 0) {
+            if (!strcmp(coll, "latency")) printf("%-12zu %14.2f\n", sz, t / iters / 2 * 1e6);
+            else printf("%-12zu %14.2f\n", sz, (double)sz * window * iters / t / 1e9);
+        }
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "-c") && i + 1 < argc) coll = argv[++i];
@@ -58,6 +100,15 @@ int main(int argc, char **argv) {
     const size_t maxb = max_sz * (size_t)size;
     void *sbuf = alloc_buf(maxb), *rbuf = alloc_buf(maxb);
     if (!sbuf || !rbuf) { fprintf(stderr, "allocation failed\n"); MPI_Abort(MPI_COMM_WORLD, 1); }
+    if (!strcmp(coll, "latency") || !strcmp(coll, "bw")) {
+        if (size < 2) { fprintf(stderr, "-c %s needs 2 ranks\n", coll); MPI_Abort(MPI_COMM_WORLD, 1); }
+        if (rank == 0)
+            printf("# mvapich2_amd osu_%s (pt2pt, ranks 0 <-> 1), %s buffers\n%-12s %14s\n", coll,
+                   device ? "ROCm device" : "host", "# Size(B)", !strcmp(coll, "latency") ? "Latency(us)" : "BW(GB/s)");
+        run_pt2pt(rank, sbuf, rbuf);
+        MPI_Finalize();
+        return 0;
+    }
     if (rank == 0) {
         printf("# mvapich2_amd osu_coll -c %s, %d ranks, %s buffers\n", coll, size, device ? "ROCm device" : "host");
         printf("%-12s %14s %14s %14s %12s\n", "# Size(B)", "Avg Lat(us)", "algbw(GB/s)", "busbw(GB/s)", "valid");
