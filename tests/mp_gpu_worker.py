@@ -38,7 +38,7 @@ def main():
         h, ext = TYPES[t][0], TYPES[t][3]
         count = case.get("count", 0)
         res = None
-        if k in ("allreduce", "allreduce_inplace", "reduce"):
+        if k in ("allreduce", "allreduce_inplace", "reduce", "iallreduce"):
             if "golden" in case:
                 if golden is None:
                     golden = np.load(os.path.join(ROOT, "tests", "golden", "golden.npz"), allow_pickle=False)
@@ -54,6 +54,11 @@ def main():
             elif k == "allreduce_inplace":
                 rc = L.MPI_Allreduce(ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF), sb.ptr, count, h, op, WORLD)
                 rb = sb
+            elif k == "iallreduce":  # nonblocking: initiate, then MPI_Wait (completion word)
+                req = ctypes.c_int()
+                rc = L.MPI_Iallreduce(sb.ptr, rb.ptr, count, h, op, WORLD, ctypes.byref(req))
+                if rc == 0:
+                    rc = L.MPI_Wait(ctypes.byref(req), None)
             else:
                 rc = L.MPI_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)

@@ -79,6 +79,10 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             cases.append({"id": f"ar{seed}", "kind": "allreduce", "type": t, "op": op, "count": count,
                           "seed": seed, "small": op == "MPI_PROD"})
             seed += 1
+    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_MAXLOC", "MPI_DOUBLE_INT"), ("MPI_BXOR", "MPI_INT")):
+        for count in (5, 70001):
+            cases.append({"id": f"ia{seed}", "kind": "iallreduce", "type": t, "op": op, "count": count, "seed": seed})
+            seed += 1
     for count in (10, 70001, 300007):
         cases.append({"id": f"ip{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
                       "count": count, "seed": seed})
@@ -125,7 +129,7 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             sol = arrs[case["golden"] + "__sol"]
             for r in range(n):
                 assert_bytes_equal(res(cid, r), sol, t, case["count"], f"{cid} {case['golden']} rank {r}")
-        elif k in ("allreduce", "allreduce_inplace"):
+        elif k in ("allreduce", "allreduce_inplace", "iallreduce"):
             want = expected_allreduce(case, n)
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {case['op']} n={n} rank {r}")
