@@ -311,9 +311,19 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
     const size_t len = range_len(a, me, rbase);
     if (!len) return;
     const char *src[kMaxRanks];
+    if (a.tp.linear == 2) {
+        // ring order: source k is rank me+1+k (mod n), so the chain ends with my own operand
 #pragma unroll
-    for (int j = 0; j < kMaxRanks; ++j)
-        src[j] = (j == me || j >= a.n) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+        for (int k = 0; k < kMaxRanks; ++k) {
+            int j = me + 1 + k;
+            while (j >= a.n) j -= a.n;
+            src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j)
+            src[j] = (j == me || j >= a.n) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+    }
     Dsts d{};
     if (a.mode == PIPE_AR) {
         d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;

@@ -171,6 +171,7 @@ __device__ __forceinline__ v4u vapply(v4u a, v4u b) {
 
 // ---- n-input reduction tree on one element (n <= 8, all indices constant) ----
 // LINEAR   : ((v0 . v1) . v2) ...                (two-level reduce_shmem order)
+// RING     : v_{n-1} . (... (v2 . (v1 . v0)))    (linear == 2; reduce-scatter ring, rotated sources)
 // BUTTERFLY: non-pof2 fold w[i] = v[2i+1] . v[2i] for i < rem, then levels
 //            m = 1, 2, 4 pairing (j, j+m); the left operand is the subtree
 //            containing `owner` (recursive halving / doubling order).
@@ -178,6 +179,15 @@ template <class Rd>
 __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[kMaxRanks], int n,
                                                       int linear, int pof2, int rem, int owner) {
     using T = typename Rd::T;
+    if (linear == 2) {
+        // RING (MPIR_Reduce_scatter_ring red_scat_osu.c:1121-1141): sources pre-rotated so
+        // v[0] = x_{b+1}, v[k] = x_{b+1+k}; each hop's own operand is the accumulator (inout)
+        T acc = v[0];
+#pragma unroll
+        for (int i = 1; i < kMaxRanks; ++i)
+            if (i < n) acc = Rd::apply(v[i], acc);
+        return acc;
+    }
     if (linear) {
         T acc = v[0];
 #pragma unroll

@@ -794,7 +794,11 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     tp.pof2 = pof2;
     tp.lg = lg;
     tp.rem = n - pof2;
-    tp.linear = 1;
+    // MPIR_Reduce_scatter_MV2 (red_scat_osu.c:1869-1880): commutative ops (every builtin) take the
+    // ring at total bytes >= mv2_red_scat_ring_algo_threshold (131072, ch3_shmem_coll.c:498);
+    // below it the tuning table's recursive halving / pairwise run, restated here as linear order
+    // (exact for integer / logical / bitwise / LOC ops, reduction-order tolerance for fp)
+    tp.linear = (total * (size_t)dt->size >= 131072) ? 2 : 1;
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
     if (!direct && mycnt) enq_copy(recvbuf, dst, mycnt * ext, st);

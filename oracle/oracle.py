@@ -32,6 +32,7 @@ def lib():
         L.oracle_allreduce.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, l, i, i, i]
         L.oracle_allreduce_algo.argtypes = [i, l, i]
         L.oracle_reduce_linear.argtypes = [ctypes.POINTER(vp), i, vp, l, i, i]
+        L.oracle_reduce_scatter_ring.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(l), vp, i, i]
         L.oracle_pack_strided.argtypes = [vp, vp, l, l, l]
         L.oracle_pack_strided.restype = None
         L.oracle_unpack_strided.argtypes = [vp, vp, l, l, l]
@@ -72,6 +73,18 @@ def reduce_linear(srcs, count, dtype_handle, op_handle):
     rc = lib().oracle_reduce_linear(sp, n, dst.ctypes.data, count, dtype_handle, op_handle)
     if rc:
         raise RuntimeError(f"oracle_reduce_linear rc={rc}")
+    return dst
+
+
+def reduce_scatter_ring(srcs, counts, dtype_handle, op_handle):
+    """Every block of MPIR_Reduce_scatter_ring's result (red_scat_osu.c:1026-1180), concatenated."""
+    n = len(srcs)
+    dst = np.zeros_like(srcs[0])
+    sp = (ctypes.c_void_p * n)(*[s.ctypes.data for s in srcs])
+    cn = (ctypes.c_long * n)(*counts)
+    rc = lib().oracle_reduce_scatter_ring(sp, n, cn, dst.ctypes.data, dtype_handle, op_handle)
+    if rc:
+        raise RuntimeError(f"oracle_reduce_scatter_ring rc={rc}")
     return dst
 
 

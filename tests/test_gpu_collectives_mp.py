@@ -98,6 +98,13 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
                       "recvcounts": counts, "count": sum(counts), "seed": seed})
         seed += 1
+    # floating point: ring order above 128 KiB total (red_scat_osu.c:1869-1880), linear below
+    for t, op, counts in (("MPI_FLOAT", "MPI_SUM", [70001] * n), ("MPI_DOUBLE", "MPI_SUM", [20000 + r for r in range(n)]),
+                          ("MPI_FLOAT", "MPI_MAX", [40000] * n), ("MPI_DOUBLE", "MPI_SUM", [100] * n),
+                          ("MPI_DOUBLE_INT", "MPI_MINLOC", [9000] * n)):
+        cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": t, "op": op,
+                      "recvcounts": counts, "count": sum(counts), "seed": seed})
+        seed += 1
     for count in (1, 13, 4096, 100003, 1 << 20):
         cases.append({"id": f"ag{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": count,
                       "seed": seed})
@@ -140,11 +147,16 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
         elif k == "reduce_scatter":
             counts = case["recvcounts"]
             sends = [inputs(dict(case, count=sum(counts)), r) for r in range(n)]
-            full = oracle.reduce_linear(sends, sum(counts), TYPES[t][0], OPS[case["op"]]).view(np.int32)
+            if sum(counts) * TYPES[t][2] >= 131072:
+                full = oracle.reduce_scatter_ring(sends, counts, TYPES[t][0], OPS[case["op"]])
+            else:
+                full = oracle.reduce_linear(sends, sum(counts), TYPES[t][0], OPS[case["op"]])
+            full = as_bytes(full)
+            ext = TYPES[t][3]
             off = 0
             for r in range(n):
-                got = res(cid, r).view(np.int32)
-                assert np.array_equal(got, full[off:off + counts[r]]), (cid, r)
+                assert_bytes_equal(res(cid, r), full[off * ext:(off + counts[r]) * ext], t, counts[r],
+                                   f"{cid} {t} {case['op']} rank {r}")
                 off += counts[r]
         elif k == "allgather":
             want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])

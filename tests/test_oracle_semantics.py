@@ -103,3 +103,30 @@ def test_pack_roundtrip():
     oracle.unpack_strided(p, dst, 4, 4, 16)
     assert np.array_equal(dst.reshape(4, 16)[:, :4], src.reshape(4, 16)[:, :4])
     assert not dst.reshape(4, 16)[:, 4:].any()
+
+
+def test_reduce_scatter_ring_order():
+    """MPIR_Reduce_scatter_ring (red_scat_osu.c:1026-1180): block b = op(x_b, op(x_{b-1}, ...
+    op(x_{b+2}, x_{b+1}))) with each hop's own operand as the accumulator."""
+    import numpy as np
+    from mvapich2_amd.consts import OPS, TYPES
+    from oracle import oracle
+    n, c = 3, 2
+    # fp32 values whose sum depends on association order
+    xs = [np.array([1e8, 1.0, 1.0, -1e8, 3.0, 7.0], dtype=np.float32),
+          np.array([1.0, 1e8, -1e8, 1.0, 5.0, 11.0], dtype=np.float32),
+          np.array([-1e8, -1e8, 1e8, 1e8, 13.0, 17.0], dtype=np.float32)]
+    got = oracle.reduce_scatter_ring(xs, [c] * n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"])
+    want = np.zeros(n * c, dtype=np.float32)
+    for b in range(n):
+        blk = slice(b * c, (b + 1) * c)
+        acc = xs[(b + 1) % n][blk].copy()
+        for k in range(2, n + 1):
+            acc = (xs[(b + k) % n][blk] + acc).astype(np.float32)
+        want[blk] = acc
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    # integers: any order gives the linear result
+    xi = [np.arange(12, dtype=np.int32) * (r + 1) for r in range(4)]
+    ring = oracle.reduce_scatter_ring(xi, [3] * 4, TYPES["MPI_INT"][0], OPS["MPI_SUM"])
+    lin = oracle.reduce_linear(xi, 12, TYPES["MPI_INT"][0], OPS["MPI_SUM"])
+    assert np.array_equal(ring, lin)
