@@ -183,6 +183,61 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
 
 }  // namespace
 
+extern "C" int PMPI_Type_get_extent(MPI_Datatype dt, MPI_Aint *lb, MPI_Aint *extent);
+
+namespace {
+
+// Reduce_scatter with a user op (host callbacks on host copies, like every
+// user op here): gather the operands, then the reference's orders for this
+// rank's block: commutative and >= 128 KiB total -> ring (red_scat_osu.c:
+// 1026-1180, selected :1869-1880): block b = fn chain starting at rank b+1
+// with each hop's own operand as inout; otherwise the canonical rank-ordered
+// x_0 op x_1 op ... op x_{n-1} (what non-commutative ops must yield,
+// MPI-3.1 §5.9.1), applied right to left as fn(in = x_i, inout = acc).
+int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u) {
+    World &w = world();
+    const int n = w.size, me = w.rank;
+    MPI_Aint lb = 0, extent = 0;
+    if (PMPI_Type_get_extent(dt, &lb, &extent) || extent <= 0) return MPI_ERR_TYPE;
+    long total = 0, disp = 0;
+    for (int j = 0; j < n; ++j) {
+        if (j == me) disp = total;
+        total += counts[j];
+    }
+    const long span = dtype_span(dt, (int)total);
+    if (span < 0) return MPI_ERR_TYPE;
+    const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+    std::vector<char> mine, all((size_t)span * n + 1);
+    if (copy_to_host(mine, src, span)) return MPI_ERR_OTHER;
+    if (n > 1) {
+        const int rc = mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
+        if (rc) return rc;
+    } else {
+        memcpy(all.data(), mine.data(), span);
+    }
+    const int c = counts[me];
+    if (c == 0) return MPI_SUCCESS;
+    const long bspan = dtype_span(dt, c);
+    auto X = [&](int r) { return all.data() + (size_t)r * span + (size_t)disp * extent; };
+    int cc = c;
+    MPI_Datatype d = dt;
+    std::vector<char> acc((size_t)bspan + 1), own((size_t)bspan + 1);
+    if (u->commute && total * dtype_size(dt) >= 131072) {
+        memcpy(acc.data(), X((me + 1) % n), bspan);
+        for (int k = 2; k <= n; ++k) {
+            memcpy(own.data(), X((me + k) % n), bspan);
+            u->fn(acc.data(), own.data(), &cc, &d);
+            acc.swap(own);
+        }
+    } else {
+        memcpy(acc.data(), X(n - 1), bspan);
+        for (int i = n - 2; i >= 0; --i) u->fn(X(i), acc.data(), &cc, &d);
+    }
+    return copy_from_host(recvbuf, acc, bspan) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+}  // namespace
+
 #define WEAK(name) __attribute__((weak, alias("P" #name)))
 
 extern "C" {
@@ -431,7 +486,8 @@ int PMPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts
         total += rc_sz[j];
     }
     if (total == 0) return MPI_SUCCESS;
-    if (user_op(op)) return err_return(comm, MPI_ERR_UNSUPPORTED_OPERATION, fn);
+    if (UserOp *u = user_op(op))
+        if (comm != MPI_COMM_SELF) return err_return(comm, user_reduce_scatter(sendbuf, recvbuf, recvcounts, dt, u), fn);
     if (comm == MPI_COMM_SELF) {
         if (sendbuf != MPI_IN_PLACE)
             rc = mv2h_memcpy_dtod(recvbuf, sendbuf, dtype_span(dt, recvcounts[0]));

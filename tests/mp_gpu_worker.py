@@ -104,6 +104,27 @@ def main():
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * 4)
             L.MPI_Op_free(ctypes.byref(op))
+        elif k == "user_reduce_scatter":
+            FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(ctypes.c_int))
+
+            def uop(inp, io, ln, dt):
+                c = ln[0]
+                a = np.ctypeslib.as_array((ctypes.c_int * c).from_address(inp))
+                b = np.ctypeslib.as_array((ctypes.c_int * c).from_address(io))
+                b[:] = a * 2 + b * 3
+            cb = FN(uop)
+            op = ctypes.c_int()
+            L.MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), case["commute"], ctypes.byref(op))
+            counts = case["recvcounts"]
+            x = ((np.arange(sum(counts)) + rank) % 7).astype(np.int32)
+            sb = m.DeviceBuffer.from_array(x)
+            rb = m.DeviceBuffer(max(1, counts[rank]) * 4)
+            arr = (ctypes.c_int * n)(*counts)
+            rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, TYPES["MPI_INT"][0], op.value, WORLD)
+            assert rc == 0, (case["id"], rc)
+            res = rb.download(np.uint8, count=counts[rank] * 4)
+            L.MPI_Op_free(ctypes.byref(op))
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)
             vt = ctypes.c_int()

@@ -118,6 +118,11 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             cases.append({"id": f"uo{seed}", "kind": "user_allreduce", "count": count, "commute": commute,
                           "seed": seed, "type": "MPI_INT", "op": "MPI_SUM"})
             seed += 1
+    for commute in (0, 1):
+        for counts in ([10] * n, [50000 + r for r in range(n)]):
+            cases.append({"id": f"ur{seed}", "kind": "user_reduce_scatter", "recvcounts": counts, "count": sum(counts),
+                          "commute": commute, "seed": seed, "type": "MPI_INT", "op": "MPI_SUM"})
+            seed += 1
     cases.append({"id": f"vb{seed}", "kind": "vector_bcast", "nblocks": 1000, "root": 0, "count": 8000,
                   "seed": seed, "type": "MPI_FLOAT", "op": "MPI_SUM"})
     seed += 1
@@ -170,6 +175,10 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             want = user_allreduce_expected(n, case["count"], case["commute"])
             for r in range(n):
                 assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
+        elif k == "user_reduce_scatter":
+            want = user_reduce_scatter_expected(n, case["recvcounts"], case["commute"])
+            for r in range(n):
+                assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
         elif k == "vector_bcast":
             nb = case["nblocks"]
             src = np.arange(nb * 8, dtype=np.float32).reshape(nb, 8)
@@ -220,3 +229,27 @@ def user_allreduce_expected(n, count, commute):
     for r in range(0, 2 * rem, 2):
         rb[r] = rb[r + 1]
     return rb
+
+
+def user_reduce_scatter_expected(n, counts, commute):
+    """User-op reduce-scatter orders (mpi_api.cpp user_reduce_scatter): commutative and
+    >= 128 KiB total -> MPIR_Reduce_scatter_ring (red_scat_osu.c:1026-1180, own operand is
+    inout at every hop); otherwise x_0 op x_1 op ... op x_{n-1} right to left."""
+    def fn(inp, io):
+        return (inp * 2 + io * 3).astype(np.int32)
+    total = sum(counts)
+    xs = [((np.arange(total) + r) % 7).astype(np.int32) for r in range(n)]
+    out, off = [], 0
+    for b in range(n):
+        blk = slice(off, off + counts[b])
+        if commute and total * 4 >= 131072:
+            acc = xs[(b + 1) % n][blk]
+            for k in range(2, n + 1):
+                acc = fn(acc, xs[(b + k) % n][blk])
+        else:
+            acc = xs[n - 1][blk]
+            for i in range(n - 2, -1, -1):
+                acc = fn(xs[i][blk], acc)
+        out.append(acc)
+        off += counts[b]
+    return out
