@@ -101,7 +101,7 @@ __device__ __forceinline__ int elem_owner(const TreeParams &tp, size_t e) {
 }
 
 // reduce n 16-byte vectors (v[j] from rank j) whose first element index is e0
-template <class Rd>
+template <class Rd, int ORD = -1>
 __device__ __forceinline__ v4u vreduce_n(const v4u (&v)[kMaxRanks], int n, const TreeParams &tp,
                                          size_t e0) {
     using T = typename Rd::T;
@@ -110,15 +110,16 @@ __device__ __forceinline__ v4u vreduce_n(const v4u (&v)[kMaxRanks], int n, const
 #pragma unroll
     for (int j = 0; j < kMaxRanks; ++j) __builtin_memcpy(t[j], &v[j], 16);
     T out[N];
-    const int own0 = tp.linear ? 0 : elem_owner<Rd>(tp, e0);
-    const int ownN = tp.linear ? 0 : elem_owner<Rd>(tp, e0 + N - 1);
+    const int lin = ORD >= 0 ? ORD : tp.linear;
+    const int own0 = lin ? 0 : elem_owner<Rd>(tp, e0);
+    const int ownN = lin ? 0 : elem_owner<Rd>(tp, e0 + N - 1);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         T col[kMaxRanks];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) col[j] = t[j][i];
         const int own = (own0 == ownN) ? own0 : elem_owner<Rd>(tp, e0 + i);
-        out[i] = tree_reduce<Rd>(col, n, tp.linear, tp.pof2, tp.rem, own);
+        out[i] = tree_reduce<Rd, ORD>(col, n, tp.linear, tp.pof2, tp.rem, own);
     }
     v4u r;
     __builtin_memcpy(&r, out, 16);

@@ -201,7 +201,7 @@ __device__ __forceinline__ void blk_copy_multi(const Dsts &d, const char *src, s
 // Block-wide n-source reduction of nbytes (whole elements) into every
 // non-null destination.  src[j] = rank j's operand for this range; `ebase` =
 // global element index of the first element (reduction-order owner).
-template <class Rd, int U>
+template <class Rd, int U, int ORD>
 __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const (&src)[kMaxRanks], const Dsts &d,
                                            size_t nbytes, size_t ebase) {
     using T = typename Rd::T;
@@ -233,7 +233,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
             for (int u = 0; u < U; ++u) {
                 const size_t xu = x + (size_t)u * kPipeThreads;
                 if (xu < nv) {
-                    const v4u r = vreduce_n<Rd>(cur[u], a.n, a.tp, ebase + xu * N);
+                    const v4u r = vreduce_n<Rd, ORD>(cur[u], a.n, a.tp, ebase + xu * N);
 #pragma unroll
                     for (int k = 0; k < kMaxRanks + 1; ++k)
                         if (d.p[k]) {
@@ -256,7 +256,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
         T col[kMaxRanks];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) col[j] = ((const T *)(j < a.n ? src[j] : src[0]))[e];
-        const T r = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, ebase + e));
+        const T r = tree_reduce<Rd, ORD>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, ebase + e));
 #pragma unroll
         for (int k = 0; k < kMaxRanks + 1; ++k)
             if (d.p[k]) ((T *)d.p[k])[e] = r;
@@ -336,8 +336,17 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
         d.p[0] = pslot(a.ag_peer.p[a.root], par, me) + soff;
     }
     // fewer sources -> more columns per thread, so >= 4 loads stay in flight
-    if (a.n <= 4) blk_reduce<Rd, 2>(a, src, d, len, (a.seg_off[me] + rbase) / (size_t)a.esize);
-    else blk_reduce<Rd, 1>(a, src, d, len, (a.seg_off[me] + rbase) / (size_t)a.esize);
+    // one specialised loop per (unroll, order); the order is uniform over the call
+    const size_t e0 = (a.seg_off[me] + rbase) / (size_t)a.esize;
+    if (a.n <= 4) {
+        if (a.tp.linear == 2) blk_reduce<Rd, 2, 2>(a, src, d, len, e0);
+        else if (a.tp.linear) blk_reduce<Rd, 2, 1>(a, src, d, len, e0);
+        else blk_reduce<Rd, 2, 0>(a, src, d, len, e0);
+    } else {
+        if (a.tp.linear == 2) blk_reduce<Rd, 1, 2>(a, src, d, len, e0);
+        else if (a.tp.linear) blk_reduce<Rd, 1, 1>(a, src, d, len, e0);
+        else blk_reduce<Rd, 1, 0>(a, src, d, len, e0);
+    }
 }
 
 template <class Rd>

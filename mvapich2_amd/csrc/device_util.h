@@ -175,10 +175,13 @@ __device__ __forceinline__ v4u vapply(v4u a, v4u b) {
 // BUTTERFLY: non-pof2 fold w[i] = v[2i+1] . v[2i] for i < rem, then levels
 //            m = 1, 2, 4 pairing (j, j+m); the left operand is the subtree
 //            containing `owner` (recursive halving / doubling order).
-template <class Rd>
+// ORD >= 0 fixes the order at compile time (hot loops: one specialised body per
+// order); ORD = -1 reads it from `linear` at run time.
+template <class Rd, int ORD = -1>
 __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[kMaxRanks], int n,
                                                       int linear, int pof2, int rem, int owner) {
     using T = typename Rd::T;
+    if (ORD >= 0) linear = ORD;
     if (linear == 2) {
         // RING (MPIR_Reduce_scatter_ring red_scat_osu.c:1121-1141): sources pre-rotated so
         // v[0] = x_{b+1}, v[k] = x_{b+1+k}; each hop's own operand is the accumulator (inout)
