@@ -28,6 +28,7 @@ struct OneShotArgs {
     uint64_t epoch;
     int *err;
     uint64_t timeout;
+    int light;    // 1: signal without the L2 writeback (peers read only uncached arena data)
     Done done;
 };
 

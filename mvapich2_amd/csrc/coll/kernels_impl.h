@@ -241,7 +241,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
                 if (j < a.n && j != a.me) ((T *)(a.arena_peer.p[j] + (size_t)a.me * a.slot_bytes))[e] = x;
         }
     }
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch);
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
     if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
     // phase B: reduce the n slots (own data straight from sendbuf)
     for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {

@@ -268,14 +268,15 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
 namespace mv2 {
 
 // Init-time check of the cross-GPU publish protocol on this node's topology.
-// The pipelined kernels publish arena stores with the light release (stores
-// acknowledged, no L2 writeback), which is right only if peer-mapped
-// uncached arenas are not write-back cached by the writer.  One 4 MiB
-// pipelined int32 SUM allreduce (two calls: both slot parities) is checked
-// element by element on every rank; the verdict is agreed through a
-// one-shot allreduce (full release).  On a mismatch every rank falls back to
-// the full system-scope release and re-checks; a second failure fails
-// MPI_Init loudly instead of returning wrong sums later.
+// The pipelined and one-shot kernels publish arena stores with the light
+// release (stores acknowledged, no L2 writeback), which is right only if
+// peer-mapped uncached arenas are not write-back cached by the writer.  A
+// 4 MiB pipelined int32 SUM allreduce (two calls: both slot parities) and a
+// 4 KiB one-shot one are checked element by element on every rank; the
+// verdict is agreed through the host control segment (no GPU path involved).
+// On a mismatch every rank falls back to the full system-scope release and
+// re-checks; a second failure fails MPI_Init loudly instead of returning
+// wrong sums later.
 int coll_selftest() {
     World &w = world();
     const int n = w.size;
@@ -288,34 +289,34 @@ int coll_selftest() {
         for (int r = 0; r < n; ++r) acc += (uint32_t)(i * 2654435761u) ^ (uint32_t)(r * 0x9E3779B9u + 17u);
         want[i] = acc;
     }
-    void *sb = nullptr, *rb = nullptr, *fb = nullptr;
-    if (hipMalloc(&sb, bytes) != hipSuccess || hipMalloc(&rb, bytes) != hipSuccess ||
-        hipMalloc(&fb, 2 * sizeof(int)) != hipSuccess) {
+    void *sb = nullptr, *rb = nullptr;
+    if (hipMalloc(&sb, bytes) != hipSuccess || hipMalloc(&rb, bytes) != hipSuccess) {
         MV2_ERR("self-test: device allocation failed");
         return E_NO_MEM;
     }
     hipMemcpy(sb, h.data(), bytes, hipMemcpyHostToDevice);
-    const int MPI_INT_H = 0x4c000405, MPI_SUM_H = 0x58000003, MPI_MIN_H = 0x58000002;
+    const int MPI_INT_H = 0x4c000405, MPI_SUM_H = 0x58000003;
     int verdict = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         int ok = 1;
-        for (int call = 0; call < 2 && ok; ++call) {
+        // pipelined (4 MiB, both parities) then one-shot (first 1024 elements)
+        const size_t sizes[3] = {count, count, 1024};
+        for (int call = 0; call < 3 && ok; ++call) {
+            const size_t c = sizes[call];
             hipMemset(rb, 0, bytes);
             hipDeviceSynchronize();
-            if (mv2h_allreduce(sb, rb, count, MPI_INT_H, MPI_SUM_H, nullptr) != 0) {
+            if (mv2h_allreduce(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr) != 0) {
                 ok = 0;
                 break;
             }
-            hipMemcpy(got.data(), rb, bytes, hipMemcpyDeviceToHost);
-            ok = memcmp(got.data(), want.data(), bytes) == 0;
+            hipMemcpy(got.data(), rb, c * 4, hipMemcpyDeviceToHost);
+            ok = memcmp(got.data(), want.data(), c * 4) == 0;
         }
-        hipMemcpy(fb, &ok, sizeof(int), hipMemcpyHostToDevice);
-        int all_ok = 0;
-        if (mv2h_allreduce(fb, (int *)fb + 1, 1, MPI_INT_H, MPI_MIN_H, nullptr) != 0) {
-            verdict = E_OTHER;
-            break;
-        }
-        hipMemcpy(&all_ok, (int *)fb + 1, sizeof(int), hipMemcpyDeviceToHost);
+        w.shm->r[w.rank].selftest_ok = ok;
+        host_barrier();
+        int all_ok = 1;
+        for (int j = 0; j < n; ++j) all_ok &= w.shm->r[j].selftest_ok;
+        host_barrier();  // every rank has read every verdict
         if (all_ok) {
             verdict = 0;
             MV2_DEBUG("self-test passed (light_release=%d)", w.light_release);
@@ -324,7 +325,7 @@ int coll_selftest() {
         verdict = E_INTERN;
         if (w.light_release) {
             if (w.rank == 0)
-                fprintf(stderr, "[mv2amd] warning: pipelined allreduce self-test failed with the light release; "
+                fprintf(stderr, "[mv2amd] warning: device collective self-test failed with the light release; "
                                 "using the full system-scope release\n");
             w.light_release = 0;
         } else {
@@ -333,7 +334,6 @@ int coll_selftest() {
     }
     hipFree(sb);
     hipFree(rb);
-    hipFree(fb);
     if (verdict) MV2_ERR("device collective self-test failed at MPI_Init (ranks %d): cross-GPU protocol broken", n);
     return verdict;
 }
@@ -637,6 +637,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.epoch = epoch;
         a.err = w.h_err;
         a.timeout = w.timeout_ticks;
+        a.light = w.light_release;
         a.done = arm_done(st);
         int g = (int)((nvec + 511) / 512);
         g = std::max(1, std::min(g, std::min(gcap, 32)));

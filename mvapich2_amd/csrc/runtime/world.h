@@ -65,6 +65,7 @@ struct alignas(64) ShmRank {
     hipIpcMemHandle_t pipe_rs_handle;
     hipIpcMemHandle_t pipe_ag_handle;
     hipIpcMemHandle_t p2p_handle;
+    int selftest_ok;  // coll_selftest verdict of this rank (agreed through host_barrier)
 };
 
 struct ShmSeg {
