@@ -138,6 +138,16 @@ def bench_n1(args, L):
     for t, op in (("MPI_FLOAT", "MPI_MAX"), ("MPI_INT", "MPI_SUM"), ("MPI_DOUBLE", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX")):
         s, k, c, _ = reduce_local_run(L, t, op, S_BYTES, max(3, args.steps // 2), 2)
         extra[f"{t}:{op}"] = {"GB/s_call": round(3 * S_BYTES / s / 1e9, 1), "GB/s_kernel": round(3 * S_BYTES / k / 1e9, 1)}
+    # host (pageable) operands: the library stages them to the GPU and back — the
+    # PCIe-inclusive rate of the same call (never the headline value)
+    hx = np.random.default_rng(3).uniform(-1, 1, count).astype(np.float32)
+    hy = np.random.default_rng(4).uniform(-1, 1, count).astype(np.float32)
+    m.check(L.MPI_Reduce_local(hx.ctypes.data, hy.ctypes.data, count, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]), "host")
+    t0 = time.perf_counter()
+    for _ in range(3):
+        m.check(L.MPI_Reduce_local(hx.ctypes.data, hy.ctypes.data, count, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]), "host")
+    extra["MPI_FLOAT:MPI_SUM host buffers (PCIe-inclusive)"] = {"GB/s_call": round(3 * S_BYTES * 3 / (time.perf_counter() - t0) / 1e9, 2)}
+    del hx, hy
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_reduce_local_r01i.json")
     if os.path.exists(tfile):
