@@ -319,6 +319,16 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
             while (j >= a.n) j -= a.n;
             src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
         }
+    } else if (a.tp.linear == 3) {
+        // flat ring allreduce (MPIR_Allreduce_pt2pt_ring_MV2 allreduce_osu.c:3925-3958): segment
+        // me is ring chunk me, which starts at rank me and gathers rank me+k at hop k with the
+        // received partial as the accumulator -> linear order over sources rotated by me
+#pragma unroll
+        for (int k = 0; k < kMaxRanks; ++k) {
+            int j = me + k;
+            while (j >= a.n) j -= a.n;
+            src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)

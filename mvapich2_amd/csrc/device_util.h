@@ -170,7 +170,8 @@ __device__ __forceinline__ v4u vapply(v4u a, v4u b) {
 }
 
 // ---- n-input reduction tree on one element (n <= 8, all indices constant) ----
-// LINEAR   : ((v0 . v1) . v2) ...                (two-level reduce_shmem order)
+// LINEAR   : ((v0 . v1) . v2) ...                (two-level reduce_shmem order; linear == 3 is
+//                                                  the flat ring allreduce on rotated sources)
 // RING     : v_{n-1} . (... (v2 . (v1 . v0)))    (linear == 2; reduce-scatter ring, rotated sources)
 // BUTTERFLY: non-pof2 fold w[i] = v[2i+1] . v[2i] for i < rem, then levels
 //            m = 1, 2, 4 pairing (j, j+m); the left operand is the subtree

@@ -2,10 +2,13 @@
 // host orchestration of the device collectives.
 //
 // Algorithm / order selection restates the reference's single-node choice
-// (generic table allreduce_tuning.c:2734-2750, selection allreduce_osu.c:
-// 3146-3375): nbytes < 1024 -> two-level reduce_shmem order (LINEAR),
-// otherwise pt2pt_rs order (BUTTERFLY; recursive-doubling owner when
-// count < pof2, allreduce_osu.c:802).  The data path is MI355X-native:
+// (MPIR_Allreduce_index_tuned_intra_MV2, allreduce_osu.c:3144-3160): nbytes <=
+// 1024 (mv2_coll_skip_table_threshold, coll_shmem.h:191) -> two-level
+// reduce_shmem order (LINEAR); nbytes >= 2 MiB -> the flat ring wrapper
+// (allreduce_osu.c:163-170, :3758-3818: ring order over count/n chunks, the
+// remainder and every IN_PLACE call through pt2pt_rs); otherwise pt2pt_rs
+// order (BUTTERFLY; recursive-doubling owner when count < pof2,
+// allreduce_osu.c:802).  The data path is MI355X-native:
 // one-shot push through uncached IPC arenas for small messages, direct
 // reduce-scatter + all-gather over xGMI peer mappings for large ones.
 #include <hip/hip_runtime.h>
@@ -157,7 +160,7 @@ static TreeParams make_tree(int n, size_t count, const DtypeInfo *dt, int me) {
     tp.pof2 = pof2;
     tp.lg = lg;
     tp.rem = n - pof2;
-    tp.linear = (count * (size_t)dt->size < 1024) ? 1 : 0;
+    tp.linear = (count * (size_t)dt->size <= 1024) ? 1 : 0;
     tp.owner_fixed = 0;
     tp.rs_blk = 0;
     if (!tp.linear) {
@@ -591,8 +594,13 @@ static void stage_out(const Staged &s, hipStream_t st) {
     if (s.copy_back) enq_copy(s.user_recv, s.recv, s.bytes, st);
 }
 
+// order: AR_AUTO (size selection), AR_RS (pt2pt_rs whatever the size: the ring
+// wrapper's IN_PLACE body and remainder), AR_RING (flat ring over count/n chunks;
+// count is a multiple of n)
+enum { AR_AUTO = 0, AR_RS = 1, AR_RING = 2 };
+
 static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, const DtypeInfo *dt, int oi,
-                          hipStream_t st) {
+                          hipStream_t st, int order = AR_AUTO) {
     World &w = world();
     const size_t bytes = count * (size_t)dt->extent;
     const bool in_place = sendbuf == (const void *)-1 || sendbuf == recvbuf;
@@ -614,10 +622,22 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         if (rc) return rc;
         return mv2h_bcast(recvbuf, bytes, n - 1, nullptr);
     }
-    const TreeParams tp = make_tree(n, count, dt, w.rank);
+    TreeParams tp = make_tree(n, count, dt, w.rank);
+    if (order != AR_AUTO && tp.linear) {
+        // pt2pt_rs on a small range: butterfly, or recursive doubling below pof2
+        tp.linear = 0;
+        if (count >= (size_t)tp.pof2) {
+            tp.owner_fixed = -1;
+            tp.rs_blk = count / tp.pof2;
+        } else {
+            int r = w.rank;
+            if (r < 2 * tp.rem && r % 2 == 0) r = r + 1;
+            tp.owner_fixed = (r < 2 * tp.rem) ? r / 2 : r - tp.rem;
+        }
+    }
     const size_t nvec = bytes / 16;
     const int gcap = grid_cap();
-    if (bytes <= w.oneshot_max && bytes <= w.slot_bytes) {
+    if (order != AR_RING && bytes <= w.oneshot_max && bytes <= w.slot_bytes) {
         OneShotArgs a{};
         a.send = s.send;
         a.recv = s.recv;
@@ -655,11 +675,63 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     a.send = s.send;
     a.recv = s.recv;
     a.esize = dt->extent;
+    if (order == AR_RING) {
+        // segment j = ring chunk j; chunks that are not 16-byte multiples go through
+        // padded copies of the operand and the result
+        tp.linear = 3;
+        const size_t cb = (count / n) * (size_t)dt->extent;
+        if (cb % 16 == 0) {
+            for (int j = 0; j < n; ++j) {
+                a.seg_off[j] = a.recv_off[j] = (size_t)j * cb;
+                a.seg_len[j] = cb;
+            }
+        } else {
+            const size_t pcb = (cb + 15) & ~(size_t)15;
+            char *ps = (char *)get_scratch(3, pcb * n), *pr = (char *)get_scratch(4, pcb * n);
+            if (!ps || !pr) return E_NO_MEM;
+            if (hipMemcpy2DAsync(ps, pcb, s.send, cb, cb, n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                return E_INTERN;
+            for (int j = 0; j < n; ++j) {
+                a.seg_off[j] = a.recv_off[j] = (size_t)j * pcb;
+                a.seg_len[j] = cb;
+            }
+            a.send = ps;
+            a.recv = pr;
+            a.tp = tp;
+            if ((rc = run_pipe(a, oi, dt, st))) return rc;
+            if (hipMemcpy2DAsync(s.recv, cb, pr, pcb, cb, n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                return E_INTERN;
+            world().pending = 0;
+            stage_out(s, st);
+            return finish(st, w.timing);
+        }
+    } else {
+        even_segments(a, bytes, n);
+    }
     a.tp = tp;
-    even_segments(a, bytes, n);
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
     stage_out(s, st);
     return finish(st, w.timing);
+}
+
+// MPIR_Allreduce_pt2pt_ring_wrapper_MV2 (allreduce_osu.c:3758-3818), taken for
+// nbytes >= MV2_ALLREDUCE_RING_ALGO_THRESHOLD with <= 8 ranks per node
+// (allreduce_osu.c:163-170): ring over the first (count/n)*n elements, then
+// pt2pt_rs over the remainder; with MPI_IN_PLACE the ring body itself falls
+// back to pt2pt_rs (:4095-4100), still over the two ranges separately.
+static int allreduce_select(const void *sendbuf, void *recvbuf, size_t count, const DtypeInfo *dt, int oi,
+                            hipStream_t st) {
+    World &w = world();
+    const int n = w.size;
+    const bool reducing = n > 1 && oi != OP_NO_OP && oi != OP_REPLACE;
+    if (!reducing || !w.allred_use_ring || count * (size_t)dt->size < w.allred_ring_thr || count < (size_t)n)
+        return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st);
+    const bool in_place = sendbuf == (const void *)-1;
+    const size_t main = (count / n) * n, rest = count - main, off = main * (size_t)dt->extent;
+    int rc = allreduce_impl(sendbuf, recvbuf, main, dt, oi, st, in_place ? AR_RS : AR_RING);
+    if (rc || !rest) return rc;
+    return allreduce_impl(in_place ? sendbuf : (const char *)sendbuf + off, (char *)recvbuf + off, rest, dt, oi, st,
+                          AR_RS);
 }
 
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
@@ -669,7 +741,7 @@ int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, 
     if (count == 0) return 0;  // allreduce_osu.c:3730
     if ((rc = kind_supported(dt))) return rc;
     if ((rc = require_world())) return rc;
-    return allreduce_impl(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
+    return allreduce_select(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
 }
 
 int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {

@@ -38,6 +38,19 @@ static long env_long(const char *name, long dflt) {
     return (v && *v) ? atol(v) : dflt;
 }
 
+// MV2_* byte-size knobs with the reference's K/M/G suffixes (user_val_to_bytes,
+// ch3_shmem_coll.c); negative values clamp to 0 like :3097
+static long env_bytes(const char *name, long dflt) {
+    const char *v = getenv(name);
+    if (!v || !*v) return dflt;
+    char *end = nullptr;
+    long x = strtol(v, &end, 10);
+    if (end && (*end == 'k' || *end == 'K')) x <<= 10;
+    else if (end && (*end == 'm' || *end == 'M')) x <<= 20;
+    else if (end && (*end == 'g' || *end == 'G')) x <<= 30;
+    return x < 0 ? 0 : x;
+}
+
 // start time of the parent process (jiffies since boot): with the parent pid
 // it names one launch of one launcher (torchrun agent, mv2run, pytest)
 static unsigned long long parent_start_time(pid_t ppid) {
@@ -147,6 +160,8 @@ static int setup_device_common() {
     w.pipe_sub = (size_t)env_long("MV2AMD_PIPE_SUB", (long)w.pipe_sub);
     w.light_release = (int)env_long("MV2AMD_LIGHT_RELEASE", w.light_release);
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
+    w.allred_use_ring = env_long("MV2_ALLRED_USE_RING", 1) != 0;
+    w.allred_ring_thr = (size_t)env_bytes("MV2_ALLREDUCE_RING_ALGO_THRESHOLD", (long)w.allred_ring_thr);
     hipEventCreate(&w.ev0);
     hipEventCreate(&w.ev1);
     return 0;
@@ -335,7 +350,7 @@ int world_finalize() {
         munmap(w.shm, sizeof(ShmSeg));
         w.shm = nullptr;
     }
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 5; ++i)
         if (w.scratch[i]) hipFree(w.scratch[i]);
     if (w.sig) hipFree(w.sig);
     if (w.arena) hipFree(w.arena);

@@ -116,6 +116,10 @@ struct World {
     int pipe_grid = kPipeMaxGrid;                 // pipelined collectives: workgroups (<= kPipeMaxGrid)
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
+    // flat ring allreduce (allreduce_osu.c:163-170): MV2_ALLRED_USE_RING (default 1,
+    // ch3_shmem_coll.c:513) and MV2_ALLREDUCE_RING_ALGO_THRESHOLD (2 MiB, :492)
+    int allred_use_ring = 1;
+    size_t allred_ring_thr = (size_t)2 << 20;
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
@@ -131,8 +135,8 @@ struct World {
     double last_ms = 0.0;
 
     // scratch device buffers (host-buffer staging, misalignment, Reduce non-roots)
-    void *scratch[3] = {};
-    size_t scratch_bytes[3] = {};
+    void *scratch[5] = {};
+    size_t scratch_bytes[5] = {};
 };
 
 World &world();

@@ -39,8 +39,14 @@ def tree_params(n, count, size):
     while pof2 * 2 <= n:
         pof2 *= 2
     lg = pof2.bit_length() - 1
-    return {"pof2": pof2, "rem": n - pof2, "lg": lg, "linear": count * size < 1024,
+    return {"pof2": pof2, "rem": n - pof2, "lg": lg, "linear": count * size <= 1024,
             "rs_blk": count // pof2 if count >= pof2 else 0}
+
+
+def ring_segments(count, ext, n):
+    """coll.cpp AR_RING: segment j = ring chunk j of count/n elements (count % n == 0)."""
+    cb = (count // n) * ext
+    return [(j * cb, cb) for j in range(n)]
 
 
 def bitrev(b, lg):
@@ -59,6 +65,13 @@ def reduce_range(seg, e0, ext, h, oh, tp):
     cnt = len(seg[0]) // ext
     if cnt == 0:
         return np.zeros(0, dtype=np.uint8)
+    if tp.get("ring") is not None:
+        # flat ring allreduce: chunk `ring` starts at rank ring, the partial is the accumulator
+        r0 = tp["ring"]
+        acc = seg[r0]
+        for k in range(1, n):
+            acc = _ap(acc, seg[(r0 + k) % n], ext, h, oh)
+        return acc
     if tp["linear"]:
         acc = seg[0]
         for i in range(1, n):
@@ -89,7 +102,8 @@ def allreduce(xs, count, ext, h, oh, tp, geom_kw=None):
     arena slots.  Returns the n recv buffers."""
     n = len(xs)
     nbytes = count * ext
-    segs = even_segments(nbytes, n)
+    ring = tp.get("ring_mode", False)
+    segs = ring_segments(count, ext, n) if ring else even_segments(nbytes, n)
     g, tsub, tseg, nrounds = pipe_geom(max(l for _, l in segs), **(geom_kw or {}))
     rs = [{} for _ in range(n)]  # rs[dst][(par, src)] -> bytearray slot
     ag = [{} for _ in range(n)]
@@ -117,7 +131,7 @@ def allreduce(xs, count, ext, h, oh, tp, geom_kw=None):
                 if not ln:
                     continue
                 ops = [xs[r][o:o + ln] if j == r else slot(rs, r, par, j)[soff:soff + ln] for j in range(n)]
-                res = reduce_range(ops, o // ext, ext, h, oh, tp)
+                res = reduce_range(ops, o // ext, ext, h, oh, dict(tp, ring=r) if ring else tp)
                 recv[r][o:o + ln] = res
                 for j in range(n):
                     if j != r:

@@ -57,7 +57,10 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
 
 def expected_allreduce(case, n):
     sends = [inputs(case, r) for r in range(n)]
-    return oracle.allreduce([s.copy() for s in sends], case["count"], TYPES[case["type"]][0], OPS[case["op"]])
+    # IN_PLACE: the ring wrapper runs pt2pt_rs; MPI_Reduce keeps the pt2pt_rs order at every size
+    algo = {"allreduce_inplace": 6, "reduce": 2}.get(case["kind"], -1)
+    return oracle.allreduce([s.copy() for s in sends], case["count"], TYPES[case["type"]][0], OPS[case["op"]],
+                            algo=algo)
 
 
 BASIC = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_FLOAT"), ("MPI_MIN", "MPI_DOUBLE"),
@@ -94,6 +97,13 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
     cases.append({"id": f"ar{seed}", "kind": "allreduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": 1 << 21,
                   "seed": seed})
     seed += 1
+    # flat ring wrapper from 2 MiB (allreduce_osu.c:163-170): ragged remainders, chunks that are
+    # not 16-byte multiples (padded staging), pair types, and IN_PLACE (pt2pt_rs on both ranges)
+    for kind, t, op, count in (("allreduce", "MPI_FLOAT", "MPI_SUM", 524291), ("allreduce", "MPI_DOUBLE", "MPI_MAX", 262147),
+                               ("allreduce", "MPI_DOUBLE_INT", "MPI_MAXLOC", 200003),
+                               ("allreduce_inplace", "MPI_FLOAT", "MPI_SUM", 524291)):
+        cases.append({"id": f"rg{seed}", "kind": kind, "type": t, "op": op, "count": count, "seed": seed})
+        seed += 1
     for counts in ([1] * n, [1000 + r for r in range(n)], [70001] * n, [65536] * n, [0] + [33] * (n - 1)):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
                       "recvcounts": counts, "count": sum(counts), "seed": seed})
@@ -196,7 +206,7 @@ def user_allreduce_expected(n, count, commute):
     def fn(inp, io):
         return (inp * 2 + io * 3).astype(np.int32)
     xs = [((np.arange(count) + r) % 7).astype(np.int32) for r in range(n)]
-    if commute and count * 4 < 1024:
+    if commute and count * 4 <= 1024:
         acc = xs[0].copy()
         for i in range(1, n):
             acc = fn(xs[i], acc)

@@ -76,7 +76,7 @@ def test_golden_allred_cases_through_device_tree(golden):
         sol = arrs[c["id"] + "__sol"]
         size = TYPES[c["type"]][2]
         srcs = [ins[r] for r in range(n)]
-        if count * size < 1024:
+        if count * size <= 1024:
             got = reduce_n(srcs, c["type"], c["op"], count, 0, 0)
         else:
             got = reduce_n(srcs, c["type"], c["op"], count, 1, -1)

@@ -51,6 +51,53 @@ def test_pipe_allreduce_model_matches_oracle(n):
             assert_bytes_equal(got[r], want[r], t, count, f"n={n} rank {r} {t} {op}")
 
 
+RING_CASES = [("MPI_FLOAT", "MPI_SUM", 4099), ("MPI_DOUBLE", "MPI_MAX", 2003), ("MPI_DOUBLE_INT", "MPI_MINLOC", 1001),
+              ("MPI_FLOAT", "MPI_MIN", 3001)]
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_ring_wrapper_model_matches_oracle(n):
+    """MV2_ALLRED_USE_RING path (allreduce_osu.c:163-170, :3758-3818): ring over
+    (count/n)*n elements as the pipe with ring segments, pt2pt_rs on the remainder."""
+    for seed, (t, op, c0) in enumerate(RING_CASES):
+        h, _, size, ext = TYPES[t]
+        count = c0 * n + (n - 1)          # ragged: a remainder of n-1 elements
+        xs = [inputs(t, count, r, seed + 50) for r in range(n)]
+        main, rest = (count // n) * n, count - (count // n) * n
+        tp = dict(pm.tree_params(n, main, size), ring_mode=True)
+        got = pm.allreduce([x[:main * ext] for x in xs], main, ext, h, OPS[op], tp,
+                           geom_kw={"pipe_grid": 3, "pipe_sub": 4096})
+        # the remainder (< n elements) is a separate pt2pt_rs call (RD below pof2)
+        tail = oracle.allreduce([x[main * ext:].copy() for x in xs], rest, h, OPS[op], algo=2)
+        want = oracle.allreduce([x.copy() for x in xs], count, h, OPS[op], algo=4)
+        for r in range(n):
+            assert_bytes_equal(np.concatenate([got[r], tail[r]]), want[r], t, count, f"ring n={n} r{r} {t} {op}")
+
+
+def test_ring_selection_thresholds():
+    lib = oracle.lib()
+    h = TYPES["MPI_FLOAT"][0]
+    assert lib.oracle_allreduce_algo(8, 256, h) == 1          # 1024 B: skip-table two-level
+    assert lib.oracle_allreduce_algo(8, 257, h) == 2
+    assert lib.oracle_allreduce_algo(8, (2 << 20) // 4 - 1, h) == 2
+    assert lib.oracle_allreduce_algo(8, (2 << 20) // 4, h) == 4   # ring wrapper from 2 MiB
+    assert lib.oracle_allreduce_algo(8, 64 << 20, h) == 4          # the 256 MiB bench case
+
+
+def test_ring_differs_from_butterfly_in_fp():
+    """The selection matters for parity: at >= 2 MiB fp32 SUM the ring order and the
+    pt2pt_rs butterfly give different bits for random operands."""
+    n, count = 8, 1 << 19
+    h = TYPES["MPI_FLOAT"][0]
+    xs = [np.random.default_rng(r).standard_normal(count).astype(np.float32) for r in range(n)]
+    ring = oracle.allreduce([x.copy() for x in xs], count, h, OPS["MPI_SUM"], algo=4)
+    bfly = oracle.allreduce([x.copy() for x in xs], count, h, OPS["MPI_SUM"], algo=2)
+    auto = oracle.allreduce([x.copy() for x in xs], count, h, OPS["MPI_SUM"])
+    assert not np.array_equal(ring[0], bfly[0])
+    assert np.array_equal(auto[0], ring[0])
+    assert all(np.array_equal(ring[0], ring[r]) for r in range(n))
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
