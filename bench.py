@@ -88,7 +88,7 @@ def cpu_baseline_host_allreduce(seconds=10.0, ranks=8):
     return {"latency_8B_us": by[8]["lat_us"], "busbw_64MiB_GBps": by[64 << 20]["busbw_GBps"],
             "busbw_1MiB_GBps": by[1 << 20]["busbw_GBps"], "all_ok": all(r["ok"] for r in rows), "cores": ranks,
             "kind": "port", "cpu": cpu_info(),
-            "what": "reference host path (two-level shmem < 1 KiB, pt2pt_rs >= 1 KiB, single-copy exchange), "
+            "what": "reference host path (two-level shmem <= 1 KiB, pt2pt_rs to 2 MiB, flat ring from 2 MiB, single-copy exchange), "
                     f"{ranks} ranks pinned 1/core, OSU loop, sizes 8 B..64 MiB, <= {cap:.2f} s per size"}
 
 

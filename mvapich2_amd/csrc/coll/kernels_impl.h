@@ -243,14 +243,20 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
     }
     signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
     if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
-    // phase B: reduce the n slots (own data straight from sendbuf)
+    // phase B: reduce the n slots (own data straight from sendbuf); a butterfly owner that
+    // is constant over this workgroup's range is fixed once (no per-vector 64-bit division)
+    TreeParams tp = a.tp;
+    if (!tp.linear && tp.owner_fixed < 0 && ve > vb) {
+        const int o0 = elem_owner<Rd>(tp, vb * N), o1 = elem_owner<Rd>(tp, ve * N - 1);
+        if (o0 == o1) tp.owner_fixed = o0;
+    }
     for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
         v4u v[kMaxRanks];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) {
             v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ((const v4u *)(a.arena_own + (size_t)j * a.slot_bytes))[i];
         }
-        ((v4u *)a.recv)[i] = vreduce_n<Rd>(v, a.n, a.tp, i * N);
+        ((v4u *)a.recv)[i] = vreduce_n<Rd>(v, a.n, tp, i * N);
     }
     if (blk == 0) {
         for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {

@@ -207,6 +207,13 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const size_t nv = nbytes >> 4;
+    // butterfly owner: constant over a range inside one pt2pt_rs block (all but at most
+    // pof2-1 ranges of a call), so the per-vector 64-bit division is hoisted out of the loop
+    TreeParams tp = a.tp;
+    if (ORD == 0 && tp.owner_fixed < 0 && nbytes >= sizeof(T)) {
+        const int o0 = elem_owner<Rd>(tp, ebase), o1 = elem_owner<Rd>(tp, ebase + nbytes / sizeof(T) - 1);
+        if (o0 == o1) tp.owner_fixed = o0;
+    }
     size_t x = threadIdx.x;
     if (x < nv) {
         v4u cur[U][kMaxRanks], nxt[U][kMaxRanks];
@@ -233,7 +240,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
             for (int u = 0; u < U; ++u) {
                 const size_t xu = x + (size_t)u * kPipeThreads;
                 if (xu < nv) {
-                    const v4u r = vreduce_n<Rd, ORD>(cur[u], a.n, a.tp, ebase + xu * N);
+                    const v4u r = vreduce_n<Rd, ORD>(cur[u], a.n, tp, ebase + xu * N);
 #pragma unroll
                     for (int k = 0; k < kMaxRanks + 1; ++k)
                         if (d.p[k]) {
@@ -256,7 +263,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
         T col[kMaxRanks];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) col[j] = ((const T *)(j < a.n ? src[j] : src[0]))[e];
-        const T r = tree_reduce<Rd, ORD>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, ebase + e));
+        const T r = tree_reduce<Rd, ORD>(col, a.n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, ebase + e));
 #pragma unroll
         for (int k = 0; k < kMaxRanks + 1; ++k)
             if (d.p[k]) ((T *)d.p[k])[e] = r;

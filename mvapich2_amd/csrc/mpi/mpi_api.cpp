@@ -25,6 +25,8 @@
 
 using namespace mv2;
 
+extern "C" int PMPI_Type_get_extent(MPI_Datatype dt, MPI_Aint *lb, MPI_Aint *extent);
+
 namespace {
 
 std::recursive_mutex g_cs;  // global critical section (allreduce.c:838)
@@ -141,7 +143,7 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
     std::vector<char> result((size_t)span + 1);
     if (n == 1) {
         memcpy(result.data(), X(0), span);
-    } else if (u->commute && (long)count * tsize < 1024) {
+    } else if (u->commute && (long)count * tsize <= 1024) {
         memcpy(result.data(), X(0), span);
         for (int i = 1; i < n; ++i) u->fn(X(i), result.data(), &c, &d);
     } else {
@@ -177,6 +179,23 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
         }
         for (int r = 0; r < 2 * rem; r += 2) rb[r] = rb[r + 1];
         memcpy(result.data(), rb[me].data(), span);
+    }
+    // flat ring wrapper (allreduce_osu.c:163-170, :3758-3818) from 2 MiB for commutative ops
+    // not called IN_PLACE: chunk c of the first (count/n)*n elements is fn(x_{c+k}, acc) along
+    // the ring starting at rank c (:3925-3958); the remainder keeps the pt2pt_rs (RD) result
+    MPI_Aint lb = 0, extent = 0;
+    if (n > 1 && u->commute && sendbuf != MPI_IN_PLACE && w.allred_use_ring &&
+        (size_t)count * (size_t)tsize >= w.allred_ring_thr && count >= n &&
+        PMPI_Type_get_extent(dt, &lb, &extent) == MPI_SUCCESS && extent > 0) {
+        int cc = count / n;
+        const long cspan = dtype_span(dt, cc);
+        std::vector<char> acc((size_t)cspan + 1);
+        for (int c = 0; c < n; ++c) {
+            const size_t off = (size_t)c * (size_t)cc * (size_t)extent;
+            memcpy(acc.data(), X(c) + off, cspan);
+            for (int k = 1; k < n; ++k) u->fn(X((c + k) % n) + off, acc.data(), &cc, &d);
+            memcpy(result.data() + off, acc.data(), cspan);
+        }
     }
     return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }

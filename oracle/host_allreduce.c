@@ -101,6 +101,7 @@ static void barrier(void) {
 static char *recv_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE; }
 static char *tmp_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE + MAXB; }
 static char *slot_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE + 2 * MAXB; }
+static char *send_of(int r) { return SHM_DATA + (size_t)r * RSTRIDE + 3 * MAXB; }
 
 /* MPIC_Sendrecv(sendbuf+soff, sbytes -> peer; recvbuf <- peer's buffer at poff, rbytes)
  * in the single-copy model: announce, wait for the peer's announcement, copy
@@ -230,8 +231,47 @@ static void allreduce_rs(const char *send, long count) {
 #undef REAL
 }
 
+/* one ring hop: announce to the right neighbour, copy the left neighbour's chunk, then
+ * wait until the right neighbour has copied mine (MPID_Irecv/Isend + waits, :3939-3968) */
+static void ring_xfer(int left, int right, const char *src, char *dst, size_t bytes) {
+    if (left == right) {
+        sendrecv(left, src, dst, bytes);
+        return;
+    }
+    unsigned long gs = ++gen_pair[right], gr = ++gen_pair[left];
+    atomic_store_explicit(&C->ready[ME][right].v, gs, memory_order_release);
+    spin_until(&C->ready[left][ME].v, gr);
+    if (bytes) memcpy(dst, src, bytes);
+    atomic_store_explicit(&C->done[ME][left].v, gr, memory_order_release);
+    spin_until(&C->done[right][ME].v, gs);
+}
+
+/* MPIR_Allreduce_pt2pt_ring_MV2 allreduce_osu.c:3824-4025 (count % N == 0): N-1
+ * reduce-scatter hops uop(in = own send chunk, inout = received chunk), then N-1
+ * allgather hops.  The send buffer lives in the shared region (single-copy model). */
+static void allreduce_ring(long count) {
+    const long cc = count / N;
+    const size_t cb = (size_t)cc * 4;
+    char *recv = recv_of(ME);
+    const int left = (ME - 1 + N) % N, right = (ME + 1) % N;
+    for (int i = 1; i < N; i++) {
+        const int c = (ME - i + N) % N; /* chunk received from the left this hop */
+        const char *src = (i == 1 ? send_of(left) : recv_of(left)) + (size_t)c * cb;
+        ring_xfer(left, right, src, recv + (size_t)c * cb, cb);
+        oracle_reduce_local(send_of(ME) + (size_t)c * cb, recv + (size_t)c * cb, cc, H_FLOAT, OP_SUM);
+    }
+    for (int i = 1; i < N; i++) {
+        const int c = (ME - i + 1 + N) % N;
+        ring_xfer(left, right, recv_of(left) + (size_t)c * cb, recv + (size_t)c * cb, cb);
+    }
+}
+
+/* single-node selection (MPIR_Allreduce_index_tuned_intra_MV2 allreduce_osu.c:3144-3160):
+ * <= 1024 B two-level, >= 2 MiB the ring wrapper (:163-170; power-of-two sizes divide
+ * evenly over the ranks, so no pt2pt_rs remainder), pt2pt_rs between */
 static void allreduce(const char *send, char *recv_private, long count) {
-    if ((size_t)count * 4 < 1024) allreduce_two_level(send, recv_private, count);
+    if ((size_t)count * 4 <= 1024) allreduce_two_level(send, recv_private, count);
+    else if ((size_t)count * 4 >= (2u << 20) && N > 1 && count % N == 0) allreduce_ring(count);
     else allreduce_rs(send, count);
 }
 
@@ -280,7 +320,7 @@ int main(int argc, char **argv) {
     }
     if (N < 1 || N > MAXR || mn < 4) return 2;
     MAXB = (mx + 63) & ~(size_t)63;
-    RSTRIDE = 3 * MAXB;
+    RSTRIDE = 4 * MAXB;
     C = mmap(NULL, sizeof(ctrl_t), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     SHM_DATA = mmap(NULL, RSTRIDE * N, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (C == MAP_FAILED || SHM_DATA == MAP_FAILED) { perror("mmap"); return 1; }
@@ -293,7 +333,7 @@ int main(int argc, char **argv) {
             prctl(PR_SET_PDEATHSIG, SIGKILL);
             ME = r;
             const int core = pin(first_core + r);
-            float *send = malloc(mx);
+            float *send = (float *)send_of(r);
             float *recvp = malloc(mx);
             memset(send, 0, mx);
             memset(recv_of(ME), 0, RSTRIDE); /* first touch on this rank's core */
@@ -329,7 +369,7 @@ int main(int argc, char **argv) {
                 if (ME == 0) C->bad[MAXR - 1] = 0;
                 int bad = 0;
                 if (validate) {
-                    const float *res = (sz * 1 < 1024) ? recvp : (const float *)recv_of(ME);
+                    const float *res = (sz <= 1024) ? recvp : (const float *)recv_of(ME);
                     const float tot = (float)(N * (N + 1) / 2);
                     for (long i = 0; i < count; i++)
                         if (res[i] != (float)((i % 100) + 1) * tot) { bad = 1; break; }

@@ -124,7 +124,7 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
                       "seed": seed, "root": 1 % n})
         seed += 1
     for commute in (0, 1):
-        for count in (10, 1000):
+        for count in (10, 1000, 524291):  # the last: ring wrapper for commutative ops (>= 2 MiB)
             cases.append({"id": f"uo{seed}", "kind": "user_allreduce", "count": count, "commute": commute,
                           "seed": seed, "type": "MPI_INT", "op": "MPI_SUM"})
             seed += 1
@@ -200,7 +200,7 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
 
 
 def user_allreduce_expected(n, count, commute):
-    """Reference order for user ops (allreduce_osu.c): commutative & < 1 KB ->
+    """Reference order for user ops (allreduce_osu.c): commutative & <= 1 KB ->
     two-level chain fn(x_i, acc); else recursive doubling with the
     dst < rank operand swap (:824-845) and the non-pof2 fold (:734-777)."""
     def fn(inp, io):
@@ -238,6 +238,18 @@ def user_allreduce_expected(n, count, commute):
         mask <<= 1
     for r in range(0, 2 * rem, 2):
         rb[r] = rb[r + 1]
+    if commute and count * 4 >= (2 << 20) and count >= n:
+        # ring wrapper (allreduce_osu.c:3758-3818): chunk c = fn chain from rank c along the
+        # ring, received partial as inout; the remainder keeps the RD result above
+        cc = count // n
+        for c in range(n):
+            blk = slice(c * cc, (c + 1) * cc)
+            acc = xs[c][blk].copy()
+            for k in range(1, n):
+                acc = fn(xs[(c + k) % n][blk], acc)
+            for r in range(n):
+                rb[r] = rb[r].copy()
+                rb[r][blk] = acc
     return rb
 
 
