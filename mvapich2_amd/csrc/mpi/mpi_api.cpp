@@ -143,7 +143,7 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
     std::vector<char> result((size_t)span + 1);
     if (n == 1) {
         memcpy(result.data(), X(0), span);
-    } else if (u->commute && (long)count * tsize <= 1024) {
+    } else if (u->commute && (size_t)count * (size_t)tsize <= w.coll_skip_thr) {
         memcpy(result.data(), X(0), span);
         for (int i = 1; i < n; ++i) u->fn(X(i), result.data(), &c, &d);
     } else {
@@ -241,7 +241,7 @@ int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     int cc = c;
     MPI_Datatype d = dt;
     std::vector<char> acc((size_t)bspan + 1), own((size_t)bspan + 1);
-    if (u->commute && total * dtype_size(dt) >= 131072) {
+    if (u->commute && (size_t)(total * dtype_size(dt)) >= w.red_scat_ring_thr) {
         memcpy(acc.data(), X((me + 1) % n), bspan);
         for (int k = 2; k <= n; ++k) {
             memcpy(own.data(), X((me + k) % n), bspan);

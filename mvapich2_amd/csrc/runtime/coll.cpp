@@ -160,7 +160,7 @@ static TreeParams make_tree(int n, size_t count, const DtypeInfo *dt, int me) {
     tp.pof2 = pof2;
     tp.lg = lg;
     tp.rem = n - pof2;
-    tp.linear = (count * (size_t)dt->size <= 1024) ? 1 : 0;
+    tp.linear = (count * (size_t)dt->size <= world().coll_skip_thr) ? 1 : 0;
     tp.owner_fixed = 0;
     tp.rs_blk = 0;
     if (!tp.linear) {
@@ -871,7 +871,7 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     // ring at total bytes >= mv2_red_scat_ring_algo_threshold (131072, ch3_shmem_coll.c:498);
     // below it the tuning table's recursive halving / pairwise run, restated here as linear order
     // (exact for integer / logical / bitwise / LOC ops, reduction-order tolerance for fp)
-    tp.linear = (total * (size_t)dt->size >= 131072) ? 2 : 1;
+    tp.linear = (total * (size_t)dt->size >= w.red_scat_ring_thr) ? 2 : 1;
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
     if (!direct && mycnt) enq_copy(recvbuf, dst, mycnt * ext, st);

@@ -162,6 +162,8 @@ static int setup_device_common() {
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
     w.allred_use_ring = env_long("MV2_ALLRED_USE_RING", 1) != 0;
     w.allred_ring_thr = (size_t)env_bytes("MV2_ALLREDUCE_RING_ALGO_THRESHOLD", (long)w.allred_ring_thr);
+    w.coll_skip_thr = (size_t)env_bytes("MV2_COLL_SKIP_TABLE_THRESHOLD", (long)w.coll_skip_thr);
+    w.red_scat_ring_thr = (size_t)env_bytes("MV2_RED_SCAT_RING_ALGO_THRESHOLD", (long)w.red_scat_ring_thr);
     hipEventCreate(&w.ev0);
     hipEventCreate(&w.ev1);
     return 0;

@@ -275,3 +275,37 @@ def user_reduce_scatter_expected(n, counts, commute):
         out.append(acc)
         off += counts[b]
     return out
+
+
+KNOB_RUNS = [
+    # MV2_ALLRED_USE_RING=0 (ch3_shmem_coll.c:2665-2670): >= 2 MiB stays in pt2pt_rs
+    ({"MV2_ALLRED_USE_RING": "0"}, [("MPI_FLOAT", "MPI_SUM", 524291, 2)]),
+    # MV2_ALLREDUCE_RING_ALGO_THRESHOLD (:3094-3098, K/M suffixes): the ring wrapper from 64 KiB
+    ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "64K"}, [("MPI_FLOAT", "MPI_SUM", 70001, 4),
+                                                    ("MPI_DOUBLE", "MPI_MAX", 10007, 4)]),
+    # MV2_COLL_SKIP_TABLE_THRESHOLD=0: no two-level shortcut, small calls take pt2pt_rs / RD
+    ({"MV2_COLL_SKIP_TABLE_THRESHOLD": "0"}, [("MPI_FLOAT", "MPI_SUM", 10, 2), ("MPI_FLOAT", "MPI_SUM", 1, 2)]),
+]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_mv2_selection_knobs(n, tmp_path):
+    """The reference's MV2_* selection knobs move the algorithm (and so the reduction-order)
+    boundaries; each run is checked bit-exactly against the oracle's algorithm for it."""
+    seed = 900
+    for i, (env, specs) in enumerate(KNOB_RUNS):
+        cases = []
+        for t, op, count, algo in specs:
+            cases.append({"id": f"kn{seed}", "kind": "allreduce", "type": t, "op": op, "count": count,
+                          "seed": seed, "algo": algo})
+            seed += 1
+        d = tmp_path / f"run{i}"
+        d.mkdir()
+        res = run_workers(n, cases, d, extra_env=env)
+        for case in cases:
+            sends = [inputs(case, r) for r in range(n)]
+            want = oracle.allreduce([s.copy() for s in sends], case["count"], TYPES[case["type"]][0],
+                                    OPS[case["op"]], algo=case["algo"])
+            for r in range(n):
+                assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"],
+                                   f"{case['id']} {env} rank {r}")
