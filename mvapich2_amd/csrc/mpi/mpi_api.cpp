@@ -185,7 +185,8 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
     // the ring starting at rank c (:3925-3958); the remainder keeps the pt2pt_rs (RD) result
     MPI_Aint lb = 0, extent = 0;
     if (n > 1 && u->commute && sendbuf != MPI_IN_PLACE && w.allred_use_ring &&
-        (size_t)count * (size_t)tsize >= w.allred_ring_thr && count >= n &&
+        (size_t)count * (size_t)tsize >= w.allred_ring_thr && (size_t)count * (size_t)tsize > w.coll_skip_thr &&
+        count >= n &&
         PMPI_Type_get_extent(dt, &lb, &extent) == MPI_SUCCESS && extent > 0) {
         int cc = count / n;
         const long cspan = dtype_span(dt, cc);

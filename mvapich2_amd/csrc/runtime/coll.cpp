@@ -724,8 +724,12 @@ static int allreduce_select(const void *sendbuf, void *recvbuf, size_t count, co
     World &w = world();
     const int n = w.size;
     const bool reducing = n > 1 && oi != OP_NO_OP && oi != OP_REPLACE;
-    if (!reducing || !w.allred_use_ring || count * (size_t)dt->size < w.allred_ring_thr || count < (size_t)n)
+    const size_t nbytes = count * (size_t)dt->size;
+    // the small-message shortcut is tested first (allreduce_osu.c:3155-3160)
+    if (!reducing || !w.allred_use_ring || nbytes <= w.coll_skip_thr || nbytes < w.allred_ring_thr)
         return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st);
+    // count < n: the ring gets no whole chunk and the wrapper's pt2pt_rs takes everything
+    if (count < (size_t)n) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, AR_RS);
     const bool in_place = sendbuf == (const void *)-1;
     const size_t main = (count / n) * n, rest = count - main, off = main * (size_t)dt->extent;
     int rc = allreduce_impl(sendbuf, recvbuf, main, dt, oi, st, in_place ? AR_RS : AR_RING);

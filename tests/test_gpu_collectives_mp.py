@@ -283,6 +283,9 @@ KNOB_RUNS = [
     # MV2_ALLREDUCE_RING_ALGO_THRESHOLD (:3094-3098, K/M suffixes): the ring wrapper from 64 KiB
     ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "64K"}, [("MPI_FLOAT", "MPI_SUM", 70001, 4),
                                                     ("MPI_DOUBLE", "MPI_MAX", 10007, 4)]),
+    # ring threshold 0: the small-message shortcut still wins up to 1 KiB (allreduce_osu.c:3155-3160),
+    # everything above takes the ring wrapper (301 elements: padded chunks at n = 2, a remainder)
+    ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "0"}, [("MPI_FLOAT", "MPI_SUM", 10, 1), ("MPI_FLOAT", "MPI_SUM", 301, 4)]),
     # MV2_COLL_SKIP_TABLE_THRESHOLD=0: no two-level shortcut, small calls take pt2pt_rs / RD
     ({"MV2_COLL_SKIP_TABLE_THRESHOLD": "0"}, [("MPI_FLOAT", "MPI_SUM", 10, 2), ("MPI_FLOAT", "MPI_SUM", 1, 2)]),
 ]
