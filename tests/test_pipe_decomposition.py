@@ -165,3 +165,24 @@ def test_pipe_decomposition_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert all(v == "ok" for v in res.values()), res
+
+
+@pytest.mark.parametrize("n", [3, 8])
+def test_ring_wrapper_in_place_is_two_rs_calls(n):
+    """MPI_IN_PLACE at >= 2 MiB: the ring body rejects IN_PLACE (allreduce_osu.c:4095-4100), so
+    the wrapper's result is pt2pt_rs over (count/n)*n elements followed by pt2pt_rs over the rest
+    (for MAX/MIN the operand sides can differ from one whole-count call: ±0 ties, NaN payloads)."""
+    count = (1 << 19) + n - 1
+    h = TYPES["MPI_FLOAT"][0]
+    xs = [np.random.default_rng(40 + r).standard_normal(count).astype(np.float32) for r in range(n)]
+    main = (count // n) * n
+    got = oracle.allreduce([x.copy() for x in xs], count, h, OPS["MPI_SUM"], algo=6)
+    head = oracle.allreduce([x[:main].copy() for x in xs], main, h, OPS["MPI_SUM"], algo=2)
+    tail = oracle.allreduce([x[main:].copy() for x in xs], count - main, h, OPS["MPI_SUM"], algo=2)
+    whole = oracle.allreduce([x.copy() for x in xs], count, h, OPS["MPI_SUM"], algo=2)
+    for r in range(n):
+        assert np.array_equal(got[r], np.concatenate([head[r], tail[r]]))
+    # for SUM the split changes only operand sides within the same pairing tree, and fp add is
+    # commutative bit for bit, so the whole-count pt2pt_rs result agrees here
+    for r in range(n):
+        assert np.array_equal(got[r], whole[r])
