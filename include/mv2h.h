@@ -118,6 +118,42 @@ int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent,
                        const int64_t *offs, const int64_t *lens, int nseg, int unpack,
                        void *stream);
 
+/* ---- reduction-order plans (host only: no GPU needed) ----
+ * The algorithm MVAPICH2 2.3.7 selects for a one-node collective and the
+ * reduction order it gives each element, as register programs:
+ * registers w[j] = rank j's operand; step s: w[dst[s]] = uop(in = w[src[s]],
+ * inout = w[dst[s]]); result w[res].  Element e uses p[min(e / blk, nprog-1)].
+ * Replaces the selection in MPIR_Allreduce_index_tuned_intra_MV2
+ * (allreduce_osu.c:3015-3420), MPIR_Reduce_index_tuned_intra_MV2
+ * (reduce_osu.c:2391-2660) and MPIR_Reduce_scatter_MV2 (red_scat_osu.c:1771). */
+typedef struct {
+    uint8_t nsteps, res;
+    uint8_t dst[7];
+    uint8_t src[7];
+} mv2h_prog;
+typedef struct {
+    int32_t nprog, pad;
+    uint64_t blk;
+    mv2h_prog p[8];
+} mv2h_progset;
+enum mv2h_coll {
+    MV2H_COLL_ALLREDUCE = 0,      /* count; in_place */
+    MV2H_COLL_REDUCE = 1,         /* count; root */
+    MV2H_COLL_REDUCE_SCATTER = 2, /* counts[n] */
+    MV2H_COLL_ALLREDUCE_RS = 3,   /* pt2pt_rs forced (ring wrapper remainder / IN_PLACE body) */
+};
+/* opkind: 0 builtin, 1 commutative user op, 2 non-commutative user op.
+ * *algo: 0 none, 1 shmem_linear, 2 pt2pt_rs, 3 pt2pt_rd, 4 ring_wrapper,
+ * 5 topo_tree, 6 two_level_p2p, 7 binomial, 8 knomial, 9 redscat_gather,
+ * 10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic, 14 reduce_topo.
+ * *unpinned = 1 when the reference's own result depends on message arrival. */
+int mv2h_plan(int coll, int n, int rank, int root, size_t count, const size_t *counts, int dtype, int opkind,
+              int in_place, int *algo, int *inner, int *unpinned, mv2h_progset *ps);
+int mv2h_knobs_reload(void);
+/* dst = reduce(srcs[0..nsrc-1]) by the programs of *ps (single GPU; order tests) */
+int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t count, int dtype, int op,
+                       const mv2h_progset *ps, void *stream);
+
 /* ---- runtime (bootstrap for COMM_WORLD) ---- */
 int mv2h_init(void);
 int mv2h_finalize(void);

@@ -67,6 +67,10 @@ def lib():
         "mv2h_timing_enable": ([c_int], c_int),
         "mv2h_last_kernel_ms": ([], ctypes.c_double),
         "mv2h_set_tuning": ([ctypes.c_char_p, ctypes.c_long], c_int),
+        "mv2h_plan": ([c_int, c_int, c_int, c_int, c_sz, ctypes.POINTER(c_sz), c_int, c_int, c_int,
+                       ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_vp], c_int),
+        "mv2h_knobs_reload": ([], c_int),
+        "mv2h_reduce_n_prog": ([ctypes.POINTER(c_vp), c_int, c_vp, c_sz, c_int, c_int, c_vp, c_vp], c_int),
         "MPI_Init": ([c_vp, c_vp], c_int),
         "MPI_Finalize": ([], c_int),
         "MPI_Comm_rank": ([c_int, ctypes.POINTER(c_int)], c_int),
@@ -191,3 +195,33 @@ def reduce_local(inbuf, inoutbuf, count, type_name, op_name, offset_in=0, offset
 
 
 __all__ = ["lib", "check", "DeviceBuffer", "MPIError", "reduce_local", "np_dtype", "consts", "OPS", "TYPES"]
+
+
+# ---- reduction-order plans (host only) ----
+class Prog(ctypes.Structure):
+    _fields_ = [("nsteps", ctypes.c_uint8), ("res", ctypes.c_uint8), ("dst", ctypes.c_uint8 * 7),
+                ("src", ctypes.c_uint8 * 7)]
+
+
+class ProgSet(ctypes.Structure):
+    _fields_ = [("nprog", ctypes.c_int32), ("pad", ctypes.c_int32), ("blk", ctypes.c_uint64), ("p", Prog * 8)]
+
+
+COLL = {"allreduce": 0, "reduce": 1, "reduce_scatter": 2, "allreduce_rs": 3}
+
+
+def plan(coll, n, rank, dtype_handle, count=0, counts=None, root=0, opkind=0, in_place=False):
+    """(algo, inner, unpinned, programs, blk): the algorithm MVAPICH2 picks for this call
+    and its per-block reduction programs [(steps[(dst, src)...], res), ...]."""
+    L = lib()
+    algo, inner, unp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    ps = ProgSet()
+    cz = (ctypes.c_size_t * n)(*counts) if counts is not None else None
+    check(L.mv2h_plan(COLL[coll], n, rank, root, count, cz, dtype_handle, opkind, int(in_place), ctypes.byref(algo),
+                      ctypes.byref(inner), ctypes.byref(unp), ctypes.byref(ps)), "mv2h_plan")
+    progs = [([(p.dst[i], p.src[i]) for i in range(p.nsteps)], p.res) for p in ps.p[:ps.nprog]]
+    return algo.value, inner.value, unp.value, progs, ps.blk
+
+
+def knobs_reload():
+    check(lib().mv2h_knobs_reload(), "mv2h_knobs_reload")

@@ -9,10 +9,11 @@
 namespace mv2 {
 
 struct TreeParams {
-    int linear;      // 1: LINEAR order, 0: BUTTERFLY
+    int linear;      // 1: LINEAR, 0: BUTTERFLY, 2: RS ring, 3: AR ring (rotated), 4: PROGRAM (ps)
     int pof2, rem, lg;
     int owner_fixed; // >= 0: fixed owner newrank; -1: reduce-scatter block owner
     size_t rs_blk;   // elements per reduce-scatter block (count / pof2)
+    ProgSet ps;      // linear == 4
 };
 
 struct OneShotArgs {
@@ -69,6 +70,7 @@ struct PipeArgs {
     uint64_t round0;                // global round counter at launch (slot parity)
     int nrounds;
     int esize;                      // element extent (reducing modes)
+    int64_t eshift;                 // program order: global element index = (seg_off[me] + r) / esize + eshift
     SigTable sig_peer;
     uint64_t *sig_own;
     uint64_t epoch0;                // round k uses epochs epoch0 + 2k and epoch0 + 2k + 1

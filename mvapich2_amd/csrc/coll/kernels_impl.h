@@ -100,10 +100,12 @@ __device__ __forceinline__ int elem_owner(const TreeParams &tp, size_t e) {
     return brev_bits((int)b, tp.lg);
 }
 
-// reduce n 16-byte vectors (v[j] from rank j) whose first element index is e0
+// reduce n 16-byte vectors (v[j] from rank j) whose first element index is e0.
+// Program order (linear == 4): fixed_blk >= 0 is the program block of the
+// whole vector when the caller knows it (hoisted out of the loop).
 template <class Rd, int ORD = -1>
 __device__ __forceinline__ v4u vreduce_n(const v4u (&v)[kMaxRanks], int n, const TreeParams &tp,
-                                         size_t e0) {
+                                         size_t e0, int fixed_blk = -1) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     T t[kMaxRanks][N];
@@ -111,19 +113,44 @@ __device__ __forceinline__ v4u vreduce_n(const v4u (&v)[kMaxRanks], int n, const
     for (int j = 0; j < kMaxRanks; ++j) __builtin_memcpy(t[j], &v[j], 16);
     T out[N];
     const int lin = ORD >= 0 ? ORD : tp.linear;
-    const int own0 = lin ? 0 : elem_owner<Rd>(tp, e0);
-    const int ownN = lin ? 0 : elem_owner<Rd>(tp, e0 + N - 1);
+    if constexpr (ORD == 4) {  // callers dispatch program order explicitly (no copy of tp.ps)
+        const ProgSet &ps = tp.ps;
+        const int b0 = fixed_blk >= 0 ? fixed_blk : prog_block(ps, e0);
+        const int bN = fixed_blk >= 0 ? fixed_blk : prog_block(ps, e0 + N - 1);
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-        T col[kMaxRanks];
+        for (int i = 0; i < N; ++i) {
+            T col[kMaxRanks];
 #pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) col[j] = t[j][i];
-        const int own = (own0 == ownN) ? own0 : elem_owner<Rd>(tp, e0 + i);
-        out[i] = tree_reduce<Rd, ORD>(col, n, tp.linear, tp.pof2, tp.rem, own);
+            for (int j = 0; j < kMaxRanks; ++j) col[j] = t[j][i];
+            const int b = (b0 == bN) ? b0 : prog_block(ps, e0 + i);
+            out[i] = prog_eval<Rd>(col, ps.p[b]);
+        }
+        v4u r;
+        __builtin_memcpy(&r, out, 16);
+        return r;
+    } else {
+        const int own0 = lin ? 0 : elem_owner<Rd>(tp, e0);
+        const int ownN = lin ? 0 : elem_owner<Rd>(tp, e0 + N - 1);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            T col[kMaxRanks];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j) col[j] = t[j][i];
+            const int own = (own0 == ownN) ? own0 : elem_owner<Rd>(tp, e0 + i);
+            out[i] = tree_reduce<Rd, ORD>(col, n, tp.linear, tp.pof2, tp.rem, own);
+        }
+        v4u r;
+        __builtin_memcpy(&r, out, 16);
+        return r;
     }
-    v4u r;
-    __builtin_memcpy(&r, out, 16);
-    return r;
+}
+
+// one element's reduction in the call's order (scalar tails)
+template <class Rd>
+__device__ __forceinline__ typename Rd::T col_reduce(const typename Rd::T (&col)[kMaxRanks], int n,
+                                                     const TreeParams &tp, size_t e) {
+    if (tp.linear == 4) return prog_eval<Rd>(col, tp.ps.p[prog_block(tp.ps, e)]);
+    return tree_reduce<Rd>(col, n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, e));
 }
 
 template <class Rd>
@@ -133,7 +160,7 @@ __device__ __forceinline__ typename Rd::T sreduce_n(const typename Rd::T *const 
     T col[kMaxRanks];
 #pragma unroll
     for (int j = 0; j < kMaxRanks; ++j) col[j] = (j < n) ? src[j][e] : src[0][e];
-    return tree_reduce<Rd>(col, n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, e));
+    return col_reduce<Rd>(col, n, tp, e);
 }
 
 // plain n-source reduction into dst (single process; used by mv2h_reduce_n and tests)
@@ -155,7 +182,9 @@ __global__ __launch_bounds__(kThreads) void k_reduce_n(PeerTable src, int n, cha
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * kThreads;
-            if (i < nvec) st_nt((v4u *)dst + i, vreduce_n<Rd>(v[u], n, tp, i * N));
+            if (i < nvec)
+                st_nt((v4u *)dst + i, tp.linear == 4 ? vreduce_n<Rd, 4>(v[u], n, tp, i * N)
+                                                     : vreduce_n<Rd>(v[u], n, tp, i * N));
         }
     }
     if (blockIdx.x == 0) {
@@ -216,7 +245,7 @@ struct LReduceN {
 // No exit barrier: the arena half used alternates per call (parity), and a
 // peer can only reach call i+2 after every rank finished call i.
 // ============================================================================
-template <class Rd>
+template <class Rd, bool PROG>
 __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
@@ -243,20 +272,37 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
     }
     signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
     if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
-    // phase B: reduce the n slots (own data straight from sendbuf); a butterfly owner that
-    // is constant over this workgroup's range is fixed once (no per-vector 64-bit division)
-    TreeParams tp = a.tp;
-    if (!tp.linear && tp.owner_fixed < 0 && ve > vb) {
-        const int o0 = elem_owner<Rd>(tp, vb * N), o1 = elem_owner<Rd>(tp, ve * N - 1);
-        if (o0 == o1) tp.owner_fixed = o0;
-    }
-    for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
-        v4u v[kMaxRanks];
+    // phase B: reduce the n slots (own data straight from sendbuf)
+    auto load = [&](size_t i, v4u (&v)[kMaxRanks]) {
 #pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) {
+        for (int j = 0; j < kMaxRanks; ++j)
             v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ((const v4u *)(a.arena_own + (size_t)j * a.slot_bytes))[i];
+    };
+    if constexpr (PROG) {
+        // program order: the block of a range that lies in one block is fixed once
+        int fb = -1;
+        if (ve > vb) {
+            const int b0 = prog_block(a.tp.ps, vb * N), b1 = prog_block(a.tp.ps, ve * N - 1);
+            if (b0 == b1) fb = b0;
         }
-        ((v4u *)a.recv)[i] = vreduce_n<Rd>(v, a.n, tp, i * N);
+        for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
+            v4u v[kMaxRanks];
+            load(i, v);
+            ((v4u *)a.recv)[i] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
+        }
+    } else {
+        // a butterfly owner that is constant over this workgroup's range is fixed once (no
+        // per-vector 64-bit division)
+        TreeParams tp = a.tp;
+        if (!tp.linear && tp.owner_fixed < 0 && ve > vb) {
+            const int o0 = elem_owner<Rd>(tp, vb * N), o1 = elem_owner<Rd>(tp, ve * N - 1);
+            if (o0 == o1) tp.owner_fixed = o0;
+        }
+        for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
+            v4u v[kMaxRanks];
+            load(i, v);
+            ((v4u *)a.recv)[i] = vreduce_n<Rd>(v, a.n, tp, i * N);
+        }
     }
     if (blk == 0) {
         for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {
@@ -264,23 +310,28 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
                 col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e] : ((const T *)(a.arena_own + (size_t)j * a.slot_bytes))[e];
-            ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
+            if constexpr (PROG) ((T *)a.recv)[e] = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, e)]);
+            else ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
         }
     }
 }
 
-template <class Rd>
+template <class Rd, bool PROG>
 __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
-    oneshot_body<Rd>(a);
+    oneshot_body<Rd, PROG>(a);
     block_done(a.done);
 }
 
 template <int OP, int K>
 struct LOneShot {
     static int run(const OneShotArgs &a, const LaunchCfg &cfg) {
-        static const int cap = resident_grid((const void *)k_oneshot<R<OP, K>>, cfg);
+        const bool prog = a.tp.linear == 4;
+        static const int cap0 = resident_grid((const void *)k_oneshot<R<OP, K>, false>, cfg);
+        static const int cap1 = resident_grid((const void *)k_oneshot<R<OP, K>, true>, cfg);
+        const int cap = prog ? cap1 : cap0;
         const int g = cfg.grid < cap ? cfg.grid : cap;
-        hipLaunchKernelGGL((k_oneshot<R<OP, K>>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+        if (prog) hipLaunchKernelGGL((k_oneshot<R<OP, K>, true>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+        else hipLaunchKernelGGL((k_oneshot<R<OP, K>, false>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };

@@ -207,12 +207,23 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const size_t nv = nbytes >> 4;
-    // butterfly owner: constant over a range inside one pt2pt_rs block (all but at most
-    // pof2-1 ranges of a call), so the per-vector 64-bit division is hoisted out of the loop
-    TreeParams tp = a.tp;
-    if (ORD == 0 && tp.owner_fixed < 0 && nbytes >= sizeof(T)) {
-        const int o0 = elem_owner<Rd>(tp, ebase), o1 = elem_owner<Rd>(tp, ebase + nbytes / sizeof(T) - 1);
-        if (o0 == o1) tp.owner_fixed = o0;
+    // butterfly owner / program block: constant over a range inside one block (all but at
+    // most nblocks-1 ranges of a call), so the per-vector 64-bit division is hoisted out
+    // of the loop.  Program order reads the programs in place (a.tp), never a copy.
+    const TreeParams &tpa = a.tp;
+    TreeParams tp;
+    int fb = -1;
+    if constexpr (ORD == 4) {
+        if (nbytes >= sizeof(T)) {
+            const int b0 = prog_block(tpa.ps, ebase), b1 = prog_block(tpa.ps, ebase + nbytes / sizeof(T) - 1);
+            if (b0 == b1) fb = b0;
+        }
+    } else {
+        tp = a.tp;
+        if (ORD == 0 && tp.owner_fixed < 0 && nbytes >= sizeof(T)) {
+            const int o0 = elem_owner<Rd>(tp, ebase), o1 = elem_owner<Rd>(tp, ebase + nbytes / sizeof(T) - 1);
+            if (o0 == o1) tp.owner_fixed = o0;
+        }
     }
     size_t x = threadIdx.x;
     if (x < nv) {
@@ -240,7 +251,9 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
             for (int u = 0; u < U; ++u) {
                 const size_t xu = x + (size_t)u * kPipeThreads;
                 if (xu < nv) {
-                    const v4u r = vreduce_n<Rd, ORD>(cur[u], a.n, tp, ebase + xu * N);
+                    v4u r;
+                    if constexpr (ORD == 4) r = vreduce_n<Rd, 4>(cur[u], a.n, tpa, ebase + xu * N, fb);
+                    else r = vreduce_n<Rd, ORD>(cur[u], a.n, tp, ebase + xu * N);
 #pragma unroll
                     for (int k = 0; k < kMaxRanks + 1; ++k)
                         if (d.p[k]) {
@@ -263,7 +276,9 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
         T col[kMaxRanks];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) col[j] = ((const T *)(j < a.n ? src[j] : src[0]))[e];
-        const T r = tree_reduce<Rd, ORD>(col, a.n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, ebase + e));
+        T r;
+        if constexpr (ORD == 4) r = prog_eval<Rd>(col, tpa.ps.p[prog_block(tpa.ps, ebase + e)]);
+        else r = tree_reduce<Rd, ORD>(col, a.n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, ebase + e));
 #pragma unroll
         for (int k = 0; k < kMaxRanks + 1; ++k)
             if (d.p[k]) ((T *)d.p[k])[e] = r;
@@ -309,7 +324,10 @@ __device__ __forceinline__ void scatter_round(const PipeArgs &a, int k) {
 // P2 of round k: reduce my segment's range from the n RS slots (own operand
 // straight from sendbuf); AR: result -> recv + every peer's AG slot [par][me];
 // RS: -> recv; RED: root -> recv, others -> the root's AG slot [par][me]
-template <class Rd>
+// PROG: the program-order variant (tp.linear == 4) is a kernel of its own so
+// that its register demand never lowers the occupancy of the hot ring /
+// butterfly kernel.
+template <class Rd, bool PROG>
 __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
     const uint64_t par = (a.round0 + (uint64_t)k) & 1;
     const size_t rbase = (size_t)k * a.tseg + (size_t)blockIdx.x * a.tsub;
@@ -355,7 +373,9 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
     // fewer sources -> more columns per thread, so >= 4 loads stay in flight
     // one specialised loop per (unroll, order); the order is uniform over the call
     const size_t e0 = (a.seg_off[me] + rbase) / (size_t)a.esize;
-    if (a.n <= 4) {
+    if constexpr (PROG) {
+        blk_reduce<Rd, 1, 4>(a, src, d, len, (size_t)((int64_t)e0 + a.eshift));
+    } else if (a.n <= 4) {
         if (a.tp.linear == 2) blk_reduce<Rd, 2, 2>(a, src, d, len, e0);
         else if (a.tp.linear) blk_reduce<Rd, 2, 1>(a, src, d, len, e0);
         else blk_reduce<Rd, 2, 0>(a, src, d, len, e0);
@@ -366,7 +386,7 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
     }
 }
 
-template <class Rd>
+template <class Rd, bool PROG = false>
 __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
     const int b = blockIdx.x;
     const int n = a.n, me = a.me;
@@ -385,7 +405,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
             for (int k = 0; k < a.nrounds; ++k) {
                 const uint64_t E = a.epoch0 + 2 * (uint64_t)k;
                 if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout)) return;
-                reduce_round<Rd>(a, k);
+                reduce_round<Rd, PROG>(a, k);
                 if (a.mode != PIPE_RS) signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (k + 1 < a.nrounds) {
                     scatter_round(a, k + 1);
@@ -462,16 +482,19 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
     }
 }
 
-template <class Rd>
+template <class Rd, bool PROG = false>
 __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
-    pipe_body<Rd>(a);
+    pipe_body<Rd, PROG>(a);
     block_done(a.done);
 }
 
 template <int OP, int K>
 struct LPipe {
     static int run(const PipeArgs &a, const LaunchCfg &cfg) {
-        hipLaunchKernelGGL((k_pipe<R<OP, K>>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
+        if (a.tp.linear == 4)
+            hipLaunchKernelGGL((k_pipe<R<OP, K>, true>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
+        else
+            hipLaunchKernelGGL((k_pipe<R<OP, K>, false>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };

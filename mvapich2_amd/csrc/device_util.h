@@ -31,6 +31,27 @@ struct SigTable {
     uint64_t *p[kMaxRanks];
 };
 
+// One reduction program over the n rank operands of an element: registers
+// w[j] start as rank j's value; step s computes w[dst[s]] = w[dst[s]] op
+// w[src[s]] (dst is the accumulator, the reference's inoutvec); the result is
+// w[res].  Any binary reduction tree of an MV2 algorithm compiles to one
+// (runtime/orders.cpp).  The fields are uniform over a workgroup range, so
+// prog_eval selects registers with uniform compares: no scratch memory.
+struct Prog {
+    uint8_t nsteps, res;
+    uint8_t dst[kMaxRanks - 1];
+    uint8_t src[kMaxRanks - 1];
+};
+// Programs by element block: element e uses p[min(e / blk, nprog - 1)]
+// (the pof2 blocks of a recursive-halving reduce-scatter, last block takes
+// the remainder, reduce_osu.c:908-910; the n chunks of the ring).
+struct ProgSet {
+    int32_t nprog;
+    int32_t pad;
+    uint64_t blk;
+    Prog p[kMaxRanks];
+};
+
 // Completion word of one blocking call (flag == nullptr: not armed).  The
 // last workgroup to finish raises *flag = seq in pinned host memory, so the
 // host returns from the MPI call without the kernel-completion signal
@@ -225,6 +246,45 @@ __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[
         }
     }
     return w[0];
+}
+
+// Evaluate a reduction program on one element's operands.  All register
+// indices are compile-time constants; the program's fields only drive
+// selects, so w[] stays in VGPRs whatever the program.
+template <class Rd>
+__device__ __forceinline__ typename Rd::T prog_eval(const typename Rd::T (&v)[kMaxRanks], const Prog &p) {
+    using T = typename Rd::T;
+    T w[kMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) w[j] = v[j];
+    const int ns = p.nsteps;
+#pragma unroll
+    for (int s = 0; s < kMaxRanks - 1; ++s) {
+        if (s < ns) {
+            const int d = p.dst[s], q = p.src[s];
+            T a = w[0], b = w[0];
+#pragma unroll
+            for (int j = 1; j < kMaxRanks; ++j) {
+                if (d == j) a = w[j];
+                if (q == j) b = w[j];
+            }
+            const T r = Rd::apply(a, b);
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                if (d == j) w[j] = r;
+        }
+    }
+    T out = w[0];
+#pragma unroll
+    for (int j = 1; j < kMaxRanks; ++j)
+        if (p.res == j) out = w[j];
+    return out;
+}
+
+__device__ __forceinline__ int prog_block(const ProgSet &ps, size_t e) {
+    if (ps.nprog <= 1) return 0;
+    const size_t b = e / ps.blk;
+    return b >= (size_t)ps.nprog ? ps.nprog - 1 : (int)b;
 }
 
 // bit-reverse of b over lg bits (owner newrank of reduce-scatter block b)

@@ -263,6 +263,14 @@ long dtype_extent(MPI_Datatype dt) {
     Derived *d = derived(dt);
     return d ? d->extent : -1;
 }
+void dtype_merge_typemap(char *dst, const char *src, MPI_Datatype dt, long count) {
+    std::vector<Seg> segs;
+    long extent = 0, size = 0;
+    if (!type_segs(dt, segs, extent, size)) return;
+    for (long e = 0; e < count; ++e)
+        for (const Seg &sg : segs) memcpy(dst + e * extent + sg.off, src + e * extent + sg.off, (size_t)sg.len);
+}
+
 long dtype_span(MPI_Datatype dt, int count) {
     if (count <= 0) return 0;
     if (const mv2::DtypeInfo *b = mv2::dtype_lookup(dt)) return (long)count * b->extent;

@@ -9,3 +9,6 @@ long dtype_size(MPI_Datatype dt);
 long dtype_extent(MPI_Datatype dt);
 // bytes from the first to one past the last byte touched by `count` elements (lb = 0)
 long dtype_span(MPI_Datatype dt, int count);
+// copy only the type-map bytes of `count` elements from src to dst (both laid out from
+// element 0 at offset 0): what MPIR_Localcopy / Segment_unpack write into a buffer
+void dtype_merge_typemap(char *dst, const char *src, MPI_Datatype dt, long count);

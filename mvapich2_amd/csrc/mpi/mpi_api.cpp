@@ -13,6 +13,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -20,6 +21,7 @@
 #include "../../../include/mv2h.h"
 #include "../common.h"
 #include "../runtime/log.h"
+#include "../runtime/orders.h"
 #include "../runtime/world.h"
 #include "datatype.h"
 
@@ -116,87 +118,102 @@ int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, U
     return copy_from_host(inout, hio, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
 
-// Allreduce with a user op: gather every rank's operand, then apply the
-// reference's order on host: two-level linear chain for commutative ops
-// below 1 KB (allreduce_osu.c:1569-1583), recursive doubling otherwise
-// (pt2pt_rs falls back to RD for user ops, allreduce_osu.c:802;
-// operand order :824-845, non-pof2 fold :734-777).
-int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u) {
+// ---- user ops through the reference's algorithm orders (orders.cpp plans) ----
+// Every rank's operand is gathered to host memory; the plan's programs then
+// run with the user function, step dst <- src being fn(in = W[src], inout =
+// W[dst]) on the block's elements, exactly the uop calls the reference makes
+// (its own user-op path also runs on host copies of device buffers).  Only
+// the type-map bytes of the result are written back (MPIR_Localcopy /
+// Segment_unpack semantics): gap bytes of a strided recvbuf stay untouched.
+int gather_operands(const void *src, long span, std::vector<char> &all) {
     World &w = world();
-    const long span = dtype_span(dt, count);
-    if (span < 0) return MPI_ERR_TYPE;
-    const int n = w.size, me = w.rank;
-    const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
-    std::vector<char> all((size_t)span * n + 1);
+    const int n = w.size;
     std::vector<char> mine;
     if (copy_to_host(mine, src, span)) return MPI_ERR_OTHER;
-    if (n > 1) {
-        int rc = mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
-        if (rc) return rc;
-    } else {
-        memcpy(all.data(), mine.data(), span);
+    all.assign((size_t)span * n + 1, 0);
+    if (n > 1) return mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
+    memcpy(all.data(), mine.data(), span);
+    return MPI_SUCCESS;
+}
+
+// Run ps over elements [e_begin, e_end) of the n operands in W (span bytes
+// each, element e at e*extent); merge the type-map bytes of the result into
+// out, whose element 0 is element e_begin.
+void eval_plan(const ProgSet &ps, std::vector<char> &W, long span, long e_begin, long e_end, MPI_Datatype dt,
+               long extent, UserOp *u, char *out) {
+    long e = e_begin;
+    while (e < e_end) {
+        int b = 0;
+        long be = e_end;
+        if (ps.nprog > 1) {
+            b = (int)std::min<long>((long)(e / (long)ps.blk), ps.nprog - 1);
+            if (b < ps.nprog - 1) be = std::min<long>(e_end, (long)(b + 1) * (long)ps.blk);
+        }
+        const Prog &p = ps.p[b];
+        int cnt = (int)(be - e);
+        MPI_Datatype d = dt;
+        const size_t off = (size_t)e * extent;
+        for (int s = 0; s < p.nsteps; ++s)
+            u->fn(W.data() + (size_t)p.src[s] * span + off, W.data() + (size_t)p.dst[s] * span + off, &cnt, &d);
+        dtype_merge_typemap(out + (size_t)(e - e_begin) * extent, W.data() + (size_t)p.res * span + off, dt, cnt);
+        e = be;
     }
-    auto X = [&](int r) { return all.data() + (size_t)r * span; };
-    int c = count;
-    MPI_Datatype d = dt;
-    long tsize = dtype_size(dt);
-    std::vector<char> result((size_t)span + 1);
+}
+
+int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u) {
+    World &w = world();
+    const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
+    if (span < 0) return MPI_ERR_TYPE;
+    const int n = w.size, me = w.rank;
+    const bool in_place = sendbuf == MPI_IN_PLACE;
+    std::vector<char> W, result;
+    int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
+    if (rc) return rc;
+    if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
+    const int opk = u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM;
+    Plan p;
     if (n == 1) {
-        memcpy(result.data(), X(0), span);
-    } else if (u->commute && (size_t)count * (size_t)tsize <= w.coll_skip_thr) {
-        memcpy(result.data(), X(0), span);
-        for (int i = 1; i < n; ++i) u->fn(X(i), result.data(), &c, &d);
+        dtype_merge_typemap(result.data(), W.data(), dt, count);
+    } else if ((rc = plan_allreduce(n, me, (size_t)count, (int)tsize, (int)extent, in_place, 0, &p, opk))) {
+        return rc;
+    } else if (p.algo != ALG_RING) {
+        eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
     } else {
-        int pof2 = 1;
-        while (pof2 * 2 <= n) pof2 *= 2;
-        const int rem = n - pof2;
-        std::vector<std::vector<char>> rb(n, std::vector<char>((size_t)span + 1));
-        for (int r = 0; r < n; ++r) memcpy(rb[r].data(), X(r), span);
-        std::vector<int> newrank(n), real(pof2);
-        for (int r = 0; r < n; ++r) {
-            if (r < 2 * rem) {
-                if (r % 2 == 0) newrank[r] = -1;
-                else {
-                    u->fn(X(r - 1), rb[r].data(), &c, &d);
-                    newrank[r] = r / 2;
-                }
-            } else newrank[r] = r - rem;
-            if (newrank[r] >= 0) real[newrank[r]] = r;
+        // ring wrapper (allreduce_osu.c:3758-3818): ring over (count/n)*n elements unless
+        // IN_PLACE or count < n, pt2pt_rs (recursive doubling for user ops) on the rest
+        const long main = in_place ? 0 : (long)(count / n) * n;
+        if (main) eval_plan(p.ps, W, span, 0, main, dt, extent, u, result.data());
+        if (main < count) {
+            Plan r;
+            if ((rc = plan_allreduce(n, me, (size_t)(count - main), (int)tsize, (int)extent, in_place, ALG_PT2PT_RS,
+                                     &r, opk)))
+                return rc;
+            eval_plan(r.ps, W, span, main, count, dt, extent, u, result.data() + (size_t)main * extent);
         }
-        for (int mask = 1; mask < pof2; mask <<= 1) {
-            std::vector<std::vector<char>> prev(pof2);
-            for (int nr = 0; nr < pof2; ++nr) prev[nr] = rb[real[nr]];
-            for (int nr = 0; nr < pof2; ++nr) {
-                const int r = real[nr], dst = real[nr ^ mask];
-                std::vector<char> tmp = prev[nr ^ mask];
-                if (u->commute || dst < r) {
-                    u->fn(tmp.data(), rb[r].data(), &c, &d);
-                } else {
-                    u->fn(rb[r].data(), tmp.data(), &c, &d);
-                    rb[r] = tmp;
-                }
-            }
-        }
-        for (int r = 0; r < 2 * rem; r += 2) rb[r] = rb[r + 1];
-        memcpy(result.data(), rb[me].data(), span);
     }
-    // flat ring wrapper (allreduce_osu.c:163-170, :3758-3818) from 2 MiB for commutative ops
-    // not called IN_PLACE: chunk c of the first (count/n)*n elements is fn(x_{c+k}, acc) along
-    // the ring starting at rank c (:3925-3958); the remainder keeps the pt2pt_rs (RD) result
-    MPI_Aint lb = 0, extent = 0;
-    if (n > 1 && u->commute && sendbuf != MPI_IN_PLACE && w.allred_use_ring &&
-        (size_t)count * (size_t)tsize >= w.allred_ring_thr && (size_t)count * (size_t)tsize > w.coll_skip_thr &&
-        count >= n &&
-        PMPI_Type_get_extent(dt, &lb, &extent) == MPI_SUCCESS && extent > 0) {
-        int cc = count / n;
-        const long cspan = dtype_span(dt, cc);
-        std::vector<char> acc((size_t)cspan + 1);
-        for (int c = 0; c < n; ++c) {
-            const size_t off = (size_t)c * (size_t)cc * (size_t)extent;
-            memcpy(acc.data(), X(c) + off, cspan);
-            for (int k = 1; k < n; ++k) u->fn(X((c + k) % n) + off, acc.data(), &cc, &d);
-            memcpy(result.data() + off, acc.data(), cspan);
-        }
+    return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+// MPI_Reduce with a user op: the root evaluates the plan of
+// MPIR_Reduce_index_tuned_intra_MV2 (binomial / knomial / shmem / ...)
+int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root) {
+    World &w = world();
+    const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
+    if (span < 0) return MPI_ERR_TYPE;
+    const int n = w.size, me = w.rank;
+    const bool in_place = sendbuf == MPI_IN_PLACE;
+    std::vector<char> W, result;
+    int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
+    if (rc || me != root) return rc;
+    if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
+    Plan p;
+    if (n == 1) {
+        dtype_merge_typemap(result.data(), W.data(), dt, count);
+    } else {
+        if ((rc = plan_reduce(n, me, root, (size_t)count, (int)tsize, (int)extent, &p,
+                              u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM)))
+            return rc;
+        eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
     }
     return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
@@ -207,53 +224,46 @@ extern "C" int PMPI_Type_get_extent(MPI_Datatype dt, MPI_Aint *lb, MPI_Aint *ext
 
 namespace {
 
-// Reduce_scatter with a user op (host callbacks on host copies, like every
-// user op here): gather the operands, then the reference's orders for this
-// rank's block: commutative and >= 128 KiB total -> ring (red_scat_osu.c:
-// 1026-1180, selected :1869-1880): block b = fn chain starting at rank b+1
-// with each hop's own operand as inout; otherwise the canonical rank-ordered
-// x_0 op x_1 op ... op x_{n-1} (what non-commutative ops must yield,
-// MPI-3.1 §5.9.1), applied right to left as fn(in = x_i, inout = acc).
+// Reduce_scatter with a user op.  Commutative: the order of
+// MPIR_Reduce_scatter_MV2's choice for this rank's block (ring, recursive
+// halving, pairwise or reduce + scatter).  Non-commutative
+// (MPIR_Reduce_scatter_non_comm_MV2, not restated): the canonical rank order
+// x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
+// associative op, applied as fn(in = x_i, inout = acc).
 int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u) {
     World &w = world();
     const int n = w.size, me = w.rank;
-    MPI_Aint lb = 0, extent = 0;
-    if (PMPI_Type_get_extent(dt, &lb, &extent) || extent <= 0) return MPI_ERR_TYPE;
+    const long extent = dtype_extent(dt), tsize = dtype_size(dt);
+    if (extent <= 0) return MPI_ERR_TYPE;
     long total = 0, disp = 0;
+    std::vector<size_t> cz(n);
     for (int j = 0; j < n; ++j) {
         if (j == me) disp = total;
         total += counts[j];
+        cz[j] = (size_t)counts[j];
     }
     const long span = dtype_span(dt, (int)total);
     if (span < 0) return MPI_ERR_TYPE;
-    const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
-    std::vector<char> mine, all((size_t)span * n + 1);
-    if (copy_to_host(mine, src, span)) return MPI_ERR_OTHER;
-    if (n > 1) {
-        const int rc = mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
-        if (rc) return rc;
-    } else {
-        memcpy(all.data(), mine.data(), span);
-    }
+    std::vector<char> W, result;
+    int rc = gather_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, span, W);
+    if (rc) return rc;
     const int c = counts[me];
     if (c == 0) return MPI_SUCCESS;
     const long bspan = dtype_span(dt, c);
-    auto X = [&](int r) { return all.data() + (size_t)r * span + (size_t)disp * extent; };
-    int cc = c;
-    MPI_Datatype d = dt;
-    std::vector<char> acc((size_t)bspan + 1), own((size_t)bspan + 1);
-    if (u->commute && (size_t)(total * dtype_size(dt)) >= w.red_scat_ring_thr) {
-        memcpy(acc.data(), X((me + 1) % n), bspan);
-        for (int k = 2; k <= n; ++k) {
-            memcpy(own.data(), X((me + k) % n), bspan);
-            u->fn(acc.data(), own.data(), &cc, &d);
-            acc.swap(own);
-        }
+    if (copy_to_host(result, recvbuf, bspan)) return MPI_ERR_OTHER;
+    if (u->commute) {
+        Plan p;
+        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)tsize, (int)extent, &p, OPK_USER_COMM))) return rc;
+        eval_plan(p.ps, W, span, disp, disp + c, dt, extent, u, result.data());
     } else {
-        memcpy(acc.data(), X(n - 1), bspan);
+        auto X = [&](int r) { return W.data() + (size_t)r * span + (size_t)disp * extent; };
+        int cc = c;
+        MPI_Datatype d = dt;
+        std::vector<char> acc(X(n - 1), X(n - 1) + bspan);
         for (int i = n - 2; i >= 0; --i) u->fn(X(i), acc.data(), &cc, &d);
+        dtype_merge_typemap(result.data(), acc.data(), dt, c);
     }
-    return copy_from_host(recvbuf, acc, bspan) ? MPI_ERR_OTHER : MPI_SUCCESS;
+    return copy_from_host(recvbuf, result, bspan) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
 
 }  // namespace
@@ -476,16 +486,7 @@ int PMPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
         }
         return err_return(comm, rc, fn);
     }
-    if (UserOp *u = user_op(op)) {
-        // result needed only at root; every rank computes it (same order as allreduce)
-        std::vector<char> scratch;
-        void *dst = recvbuf;
-        if (world().rank != root) {
-            scratch.resize(dtype_span(dt, count) + 1);
-            dst = scratch.data();
-        }
-        return err_return(comm, user_allreduce(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, dst, count, dt, u), fn);
-    }
+    if (UserOp *u = user_op(op)) return err_return(comm, user_reduce(sendbuf, recvbuf, count, dt, u, root), fn);
     rc = mv2h_reduce(sendbuf, recvbuf, (size_t)count, dt, op, root, nullptr);
     return err_return(comm, rc, fn);
 }

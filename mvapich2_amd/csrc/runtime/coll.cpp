@@ -19,6 +19,7 @@
 
 #include "../../../include/mv2h.h"
 #include "log.h"
+#include "orders.h"
 #include "world.h"
 
 namespace mv2 {
@@ -151,31 +152,57 @@ static int check_op_dtype(int op, int dtype, const DtypeInfo **out) {
 }
 
 // ---------------------------------------------------------------------------
-// reduction order
+// reduction order (algorithm choice and programs: orders.cpp)
 // ---------------------------------------------------------------------------
-static TreeParams make_tree(int n, size_t count, const DtypeInfo *dt, int me) {
+static TreeParams tree_base(int n) {
     TreeParams tp{};
     int pof2 = 1, lg = 0;
     while (pof2 * 2 <= n) { pof2 *= 2; ++lg; }
     tp.pof2 = pof2;
     tp.lg = lg;
     tp.rem = n - pof2;
-    tp.linear = (count * (size_t)dt->size <= world().coll_skip_thr) ? 1 : 0;
-    tp.owner_fixed = 0;
-    tp.rs_blk = 0;
-    if (!tp.linear) {
-        if (count >= (size_t)pof2) {
-            tp.owner_fixed = -1;
-            tp.rs_blk = count / pof2;
-        } else {
-            // recursive doubling: each rank keeps its own result; even ranks
-            // below 2*rem receive their odd partner's (allreduce_osu.c:585-600)
-            int r = me;
-            if (r < 2 * tp.rem && r % 2 == 0) r = r + 1;
-            tp.owner_fixed = (r < 2 * tp.rem) ? r / 2 : r - tp.rem;
-        }
+    return tp;
+}
+
+// pt2pt_rs order on the specialised butterfly evaluator: recursive halving
+// with owner bitrev(block), or recursive doubling (count < pof2, or the
+// pt2pt_rd algorithm) where each rank keeps its own result and even ranks
+// below 2*rem take their odd partner's (allreduce_osu.c:585-600, :1003-1030)
+static TreeParams tree_rs(int n, size_t count, int me, bool force_rd) {
+    TreeParams tp = tree_base(n);
+    tp.linear = 0;
+    if (!force_rd && count >= (size_t)tp.pof2) {
+        tp.owner_fixed = -1;
+        tp.rs_blk = count / tp.pof2;
+    } else {
+        int r = me;
+        if (r < 2 * tp.rem && r % 2 == 0) r = r + 1;
+        tp.owner_fixed = (r < 2 * tp.rem) ? r / 2 : r - tp.rem;
     }
     return tp;
+}
+
+static TreeParams tree_from_plan(const Plan &p, int n, size_t count, int me) {
+    switch (p.algo) {
+    case ALG_PT2PT_RS: return tree_rs(n, count, me, false);
+    case ALG_PT2PT_RD: return tree_rs(n, count, me, true);
+    case ALG_SHMEM_LINEAR: {
+        TreeParams tp = tree_base(n);
+        tp.linear = 1;
+        return tp;
+    }
+    default: {
+        TreeParams tp = tree_base(n);
+        tp.linear = 4;
+        tp.ps = p.ps;
+        return tp;
+    }
+    }
+}
+
+static void log_plan(const char *coll, const Plan &p, size_t count) {
+    MV2_DEBUG("%s count %zu -> %s%s%s", coll, count, algo_name(p.algo), p.inner ? " / " : "",
+              p.inner ? algo_name(p.inner) : "");
 }
 
 static int grid_cap() {
@@ -535,6 +562,74 @@ int mv2h_reduce_n(const void *const *srcs, int nsrc, void *dst, size_t count, in
     return finish(st, world().timing);
 }
 
+static_assert(sizeof(mv2h_progset) == sizeof(ProgSet), "mv2h_progset mirrors ProgSet");
+
+int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t count, int dtype, int op,
+                       const mv2h_progset *ps, void *stream) {
+    const DtypeInfo *dt = nullptr;
+    int rc = check_op_dtype(op, dtype, &dt);
+    if (rc) return rc;
+    if ((rc = kind_supported(dt))) return rc;
+    if (nsrc < 1 || nsrc > kMaxRanks || !ps || ps->nprog < 1 || ps->nprog > kMaxRanks || ps->blk == 0) return E_ARG;
+    for (int b = 0; b < ps->nprog; ++b) {
+        const mv2h_prog &p = ps->p[b];
+        if (p.nsteps > kMaxRanks - 1 || p.res >= nsrc) return E_ARG;
+        for (int i = 0; i < p.nsteps; ++i)
+            if (p.dst[i] >= nsrc || p.src[i] >= nsrc) return E_ARG;
+    }
+    if (count == 0) return 0;
+    if ((rc = ensure_init_for_device())) return rc;
+    const int oi = op_index(op);
+    if (oi >= OP_REPLACE) return E_OP;
+    hipStream_t st = pick_stream(stream);
+    TreeParams tp = tree_base(nsrc);
+    tp.linear = 4;
+    memcpy(&tp.ps, ps, sizeof(ProgSet));
+    LaunchCfg cfg{std::min(world().rl_grid, 4096), 2, st};
+    tmark0(st);
+    rc = launch_reduce_n(oi, dt->kind, srcs, nsrc, dst, count, dt->extent, tp, cfg);
+    tmark1(st);
+    if (rc) return rc;
+    return finish(st, world().timing);
+}
+
+int mv2h_knobs_reload(void) {
+    knobs_reload();
+    return 0;
+}
+
+int mv2h_plan(int coll, int n, int rank, int root, size_t count, const size_t *counts, int dtype, int opkind,
+              int in_place, int *algo, int *inner, int *unpinned, mv2h_progset *ps) {
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    if (!dt) return E_TYPE;
+    if (n < 1 || n > kMaxRanks || rank < 0 || rank >= n || opkind < 0 || opkind > 2) return E_ARG;
+    Plan p;
+    int rc;
+    switch (coll) {
+    case MV2H_COLL_ALLREDUCE:
+        rc = plan_allreduce(n, rank, count, dt->size, dt->extent, in_place != 0, 0, &p, opkind);
+        break;
+    case MV2H_COLL_ALLREDUCE_RS:
+        rc = plan_allreduce(n, rank, count, dt->size, dt->extent, in_place != 0, ALG_PT2PT_RS, &p, opkind);
+        break;
+    case MV2H_COLL_REDUCE:
+        if (root < 0 || root >= n) return E_ROOT;
+        rc = plan_reduce(n, rank, root, count, dt->size, dt->extent, &p, opkind);
+        break;
+    case MV2H_COLL_REDUCE_SCATTER:
+        if (!counts) return E_ARG;
+        rc = plan_reduce_scatter(n, rank, counts, dt->size, dt->extent, &p, opkind);
+        break;
+    default: return E_ARG;
+    }
+    if (rc) return rc;
+    if (algo) *algo = p.algo;
+    if (inner) *inner = p.inner;
+    if (unpinned) *unpinned = p.unpinned;
+    if (ps) memcpy(ps, &p.ps, sizeof(ProgSet));
+    return 0;
+}
+
 // ---------------------------------------------------------------------------
 // part (2): device collectives
 // ---------------------------------------------------------------------------
@@ -594,13 +689,10 @@ static void stage_out(const Staged &s, hipStream_t st) {
     if (s.copy_back) enq_copy(s.user_recv, s.recv, s.bytes, st);
 }
 
-// order: AR_AUTO (size selection), AR_RS (pt2pt_rs whatever the size: the ring
-// wrapper's IN_PLACE body and remainder), AR_RING (flat ring over count/n chunks;
-// count is a multiple of n)
-enum { AR_AUTO = 0, AR_RS = 1, AR_RING = 2 };
-
+// One allreduce over `count` elements in the order `tp` (ring = true: the flat
+// ring's chunking, segment j = ring chunk j; count is a multiple of n).
 static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, const DtypeInfo *dt, int oi,
-                          hipStream_t st, int order = AR_AUTO) {
+                          hipStream_t st, const TreeParams &tp_in, bool ring = false) {
     World &w = world();
     const size_t bytes = count * (size_t)dt->extent;
     const bool in_place = sendbuf == (const void *)-1 || sendbuf == recvbuf;
@@ -622,22 +714,10 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         if (rc) return rc;
         return mv2h_bcast(recvbuf, bytes, n - 1, nullptr);
     }
-    TreeParams tp = make_tree(n, count, dt, w.rank);
-    if (order != AR_AUTO && tp.linear) {
-        // pt2pt_rs on a small range: butterfly, or recursive doubling below pof2
-        tp.linear = 0;
-        if (count >= (size_t)tp.pof2) {
-            tp.owner_fixed = -1;
-            tp.rs_blk = count / tp.pof2;
-        } else {
-            int r = w.rank;
-            if (r < 2 * tp.rem && r % 2 == 0) r = r + 1;
-            tp.owner_fixed = (r < 2 * tp.rem) ? r / 2 : r - tp.rem;
-        }
-    }
+    TreeParams tp = tp_in;
     const size_t nvec = bytes / 16;
     const int gcap = grid_cap();
-    if (order != AR_RING && bytes <= w.oneshot_max && bytes <= w.slot_bytes) {
+    if (!ring && bytes <= w.oneshot_max && bytes <= w.slot_bytes) {
         OneShotArgs a{};
         a.send = s.send;
         a.recv = s.recv;
@@ -675,7 +755,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     a.send = s.send;
     a.recv = s.recv;
     a.esize = dt->extent;
-    if (order == AR_RING) {
+    if (ring) {
         // segment j = ring chunk j; chunks that are not 16-byte multiples go through
         // padded copies of the operand and the result
         tp.linear = 3;
@@ -714,30 +794,31 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     return finish(st, w.timing);
 }
 
-// MPIR_Allreduce_pt2pt_ring_wrapper_MV2 (allreduce_osu.c:3758-3818), taken for
-// nbytes >= MV2_ALLREDUCE_RING_ALGO_THRESHOLD with <= 8 ranks per node
-// (allreduce_osu.c:163-170): ring over the first (count/n)*n elements, then
-// pt2pt_rs over the remainder; with MPI_IN_PLACE the ring body itself falls
-// back to pt2pt_rs (:4095-4100), still over the two ranges separately.
+// MPIR_Allreduce_index_tuned_intra_MV2's one-node choice (orders.cpp
+// plan_allreduce).  The ring wrapper (allreduce_osu.c:3758-3818) runs the
+// ring over the first (count/n)*n elements and pt2pt_rs over the remainder;
+// with MPI_IN_PLACE the ring body itself falls back to pt2pt_rs (:4095-4100),
+// still over the two ranges separately; count < n leaves the ring nothing.
 static int allreduce_select(const void *sendbuf, void *recvbuf, size_t count, const DtypeInfo *dt, int oi,
                             hipStream_t st) {
     World &w = world();
-    const int n = w.size;
+    const int n = w.size, me = w.rank;
     const bool reducing = n > 1 && oi != OP_NO_OP && oi != OP_REPLACE;
-    const size_t nbytes = count * (size_t)dt->size;
-    // the small-message shortcut is tested first (allreduce_osu.c:3155-3160)
-    if (!reducing || !w.allred_use_ring || nbytes <= w.coll_skip_thr || nbytes < w.allred_ring_thr)
-        return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st);
-    // count < n: the ring gets no whole chunk and the wrapper's pt2pt_rs takes everything
-    if (count < (size_t)n) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, AR_RS);
     const bool in_place = sendbuf == (const void *)-1;
+    Plan p;
+    if (!reducing) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tree_base(n));
+    int rc = plan_allreduce(n, me, count, dt->size, dt->extent, in_place, 0, &p);
+    if (rc) return rc;
+    log_plan("allreduce", p, count);
+    if (p.algo != ALG_RING) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tree_from_plan(p, n, count, me));
+    if (count < (size_t)n) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tree_rs(n, count, me, false));
     const size_t main = (count / n) * n, rest = count - main, off = main * (size_t)dt->extent;
-    int rc = allreduce_impl(sendbuf, recvbuf, main, dt, oi, st, in_place ? AR_RS : AR_RING);
+    rc = in_place ? allreduce_impl(sendbuf, recvbuf, main, dt, oi, st, tree_rs(n, main, me, false))
+                  : allreduce_impl(sendbuf, recvbuf, main, dt, oi, st, tree_base(n), true);
     if (rc || !rest) return rc;
     return allreduce_impl(in_place ? sendbuf : (const char *)sendbuf + off, (char *)recvbuf + off, rest, dt, oi, st,
-                          AR_RS);
+                          tree_rs(n, rest, me, false));
 }
-
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
@@ -762,13 +843,18 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
     const int oi = op_index(op);
     const bool is_root = w.rank == root;
     const bool in_place = sendbuf == (const void *)-1 || (is_root && sendbuf == recvbuf);
-    // small messages, REPLACE / NO_OP, one rank: every rank computes the result
+    // MPIR_Reduce_index_tuned_intra_MV2's one-node choice (orders.cpp plan_reduce)
+    Plan p;
+    if ((rc = plan_reduce(w.size, w.rank, root, count, dt->size, dt->extent, &p))) return rc;
+    log_plan("reduce", p, count);
+    const TreeParams tp = tree_from_plan(p, w.size, count, w.rank);
+    // small messages, REPLACE / NO_OP, one rank: every rank computes the root's result
     // (one-shot); non-roots discard theirs
     if (w.size == 1 || oi >= OP_REPLACE || (bytes <= w.oneshot_max && bytes <= w.slot_bytes)) {
-        if (is_root) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st);
+        if (is_root) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tp);
         void *tmp = get_scratch(2, bytes);
         if (!tmp) return E_NO_MEM;
-        return allreduce_impl(in_place ? recvbuf : sendbuf, tmp, count, dt, oi, st);
+        return allreduce_impl(in_place ? recvbuf : sendbuf, tmp, count, dt, oi, st, tp);
     }
     // pipelined: scatter -> reduce -> push to the root -> root gathers
     Staged s{};
@@ -793,7 +879,7 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
     a.send = s.send;
     a.recv = s.recv;
     a.esize = dt->extent;
-    a.tp = make_tree(w.size, count, dt, root);
+    a.tp = tp;
     even_segments(a, bytes, w.size);
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
     if (is_root) stage_out(s, st);
@@ -865,17 +951,19 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     }
     a.recv = dst;
     a.recv_off[w.rank] = 0;
-    TreeParams tp{};
-    int pof2 = 1, lg = 0;
-    while (pof2 * 2 <= n) { pof2 *= 2; ++lg; }
-    tp.pof2 = pof2;
-    tp.lg = lg;
-    tp.rem = n - pof2;
-    // MPIR_Reduce_scatter_MV2 (red_scat_osu.c:1869-1880): commutative ops (every builtin) take the
-    // ring at total bytes >= mv2_red_scat_ring_algo_threshold (131072, ch3_shmem_coll.c:498);
-    // below it the tuning table's recursive halving / pairwise run, restated here as linear order
-    // (exact for integer / logical / bitwise / LOC ops, reduction-order tolerance for fp)
-    tp.linear = (total * (size_t)dt->size >= w.red_scat_ring_thr) ? 2 : 1;
+    // MPIR_Reduce_scatter_MV2's one-node choice (orders.cpp plan_reduce_scatter): ring,
+    // recursive halving, pairwise or reduce + scatter, each in its own order
+    Plan p;
+    if ((rc = plan_reduce_scatter(n, w.rank, recvcounts, dt->size, dt->extent, &p))) return rc;
+    log_plan("reduce_scatter", p, total);
+    TreeParams tp = tree_base(n);
+    if (p.algo == ALG_RS_RING) {
+        tp.linear = 2;  // rotated sources, specialised chain (coll/pipe.h reduce_round)
+    } else {
+        tp.linear = 4;
+        tp.ps = p.ps;
+        a.eshift = (int64_t)off - (int64_t)(a.seg_off[w.rank] / ext);
+    }
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
     if (!direct && mycnt) enq_copy(recvbuf, dst, mycnt * ext, st);

@@ -1,0 +1,698 @@
+// orders.cpp — one-node algorithm selection and reduction-order programs
+// (see orders.h).  Each algorithm is restated as a symbolic run of its
+// message schedule: every rank's partial result for every block is an
+// expression tree whose internal nodes are uop(in, inout) calls, with the
+// inout operand (the reference's accumulator) on the left.  compile() turns
+// the final tree of each block into a Prog: each subtree's value lives in
+// the register of its leftmost leaf, so a tree over distinct ranks needs no
+// temporaries.
+#include "orders.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../common.h"
+
+namespace mv2 {
+
+// ---------------------------------------------------------------------------
+// knobs
+// ---------------------------------------------------------------------------
+static Knobs g_knobs;
+static bool g_knobs_ok = false;
+
+static bool env_set(const char *name, const char **v) {
+    *v = getenv(name);
+    return *v && **v;
+}
+
+// user_val_to_bytes (mv2_utils.c:27-70): a trailing K/M/G multiplies, as an int
+static int64_t val_to_bytes(const char *v) {
+    const size_t len = strlen(v);
+    int64_t f = 1;
+    const char last = v[len - 1];
+    if (last == 'k' || last == 'K') f = 1 << 10;
+    else if (last == 'm' || last == 'M') f = 1 << 20;
+    else if (last == 'g' || last == 'G') f = 1 << 30;
+    return (int64_t)(int)((int64_t)atoi(v) * f);
+}
+
+void knobs_reload() {
+    Knobs k{};
+    k.enable_shmem_collectives = 1;
+    k.enable_shmem_allreduce = 1;
+    k.enable_shmem_reduce = 1;
+    k.enable_skip_search = 1;
+    k.coll_skip_thr = 1024;
+    k.allred_skip_small = 1;
+    k.allred_skip_large = 1;
+    k.enable_topo = 1;
+    k.use_topo_allreduce = 1;
+    k.topo_allred_min = 1;
+    k.topo_allred_max = 2048;
+    k.topo_allred_ppn = 1;
+    k.use_topo_reduce = 0;
+    k.topo_red_min = 1;
+    k.topo_red_max = 2048;
+    k.topo_red_ppn = 1;
+    k.topo_red_nodes = 1;
+    k.tree_degree = 4;
+    k.allred_use_ring = 1;
+    k.allred_ring_thr = (int64_t)2 << 20;
+    k.allred_ring_ppn = 8;
+    k.smp_use_cma = 1;
+    k.use_knomial_reduce = 1;
+    k.reduce_inter_k = -1;
+    k.shmem_coll_max_msg = 32 * 1024;
+    k.shmem_intra_reduce_msg = 1 << 11;
+    k.red_scat_ring_thr = 131072;
+    const char *v;
+    int flag;
+    // ch3_shmem_coll.c MV2_Read_env_vars, in its order where order matters
+    if (env_set("MV2_USE_SHARED_MEM", &v) && atoi(v) <= 0) k.enable_shmem_collectives = 0;
+    if (env_set("MV2_USE_SHMEM_ALLREDUCE", &v)) k.enable_shmem_allreduce = atoi(v);
+    if (env_set("MV2_USE_SHMEM_REDUCE", &v)) k.enable_shmem_reduce = atoi(v);
+    if (env_set("MV2_ENABLE_SKIP_TUNING_TABLE_SEARCH", &v)) k.enable_skip_search = !!atoi(v);
+    if (env_set("MV2_COLL_SKIP_TABLE_THRESHOLD", &v)) {
+        k.coll_skip_thr = atoi(v);  // a negative value keeps the threshold negative (:2328-2331)
+    }
+    if (env_set("MV2_ENABLE_ALLREDUCE_SKIP_LARGE_MESSAGE_TUNING_TABLE_SEARCH", &v)) k.allred_skip_large = !!atoi(v);
+    if (env_set("MV2_ENABLE_ALLREDUCE_SKIP_SMALL_MESSAGE_TUNING_TABLE_SEARCH", &v)) k.allred_skip_small = !!atoi(v);
+    if (env_set("MV2_USE_KNOMIAL_REDUCE", &v) && (flag = atoi(v)) >= 0) k.use_knomial_reduce = flag;
+    if (env_set("MV2_USE_INTER_KNOMIAL_REDUCE_FACTOR", &v) && (flag = atoi(v)) >= 0) k.reduce_inter_k = flag;
+    if (env_set("MV2_SHMEM_COLL_MAX_MSG_SIZE", &v) && (flag = atoi(v)) > 0) k.shmem_coll_max_msg = flag;
+    if (env_set("MV2_INTRA_SHMEM_REDUCE_MSG", &v) && (flag = atoi(v)) >= 0) k.shmem_intra_reduce_msg = flag;
+    if (env_set("MV2_ALLRED_USE_RING", &v)) k.allred_use_ring = atoi(v) > 0 ? 1 : 0;
+    if (env_set("MV2_ALLREDUCE_RING_ALGO_PPN_THRESHOLD", &v) && (flag = atoi(v)) >= 1) k.allred_ring_ppn = flag;
+    if (env_set("MV2_ALLREDUCE_RING_ALGO_THRESHOLD", &v)) {
+        k.allred_ring_thr = val_to_bytes(v);
+        if (k.allred_ring_thr < 0) k.allred_ring_thr = 0;
+    }
+    if (env_set("MV2_RED_SCAT_RING_ALGO_THRESHOLD", &v)) {
+        k.red_scat_ring_thr = val_to_bytes(v);
+        if (k.red_scat_ring_thr < 0) k.red_scat_ring_thr = 0;
+    }
+    if (env_set("MV2_SHMEM_REDUCE_TREE_DEGREE", &v)) k.tree_degree = atoi(v);
+    // socket-aware collectives switch the topology-aware ones off (:3304-3320)
+    if (env_set("MV2_ENABLE_SOCKET_AWARE_COLLECTIVES", &v) && atoi(v)) k.enable_topo = 0;
+    if (env_set("MV2_ENABLE_TOPO_AWARE_COLLECTIVES", &v)) k.enable_topo = !!atoi(v);
+    if (env_set("MV2_USE_TOPO_AWARE_ALLREDUCE", &v)) k.use_topo_allreduce = !!atoi(v);
+    if (env_set("MV2_USE_TOPO_AWARE_REDUCE", &v)) k.use_topo_reduce = !!atoi(v);
+    if (env_set("MV2_TOPO_AWARE_ALLREDUCE_MAX_MSG", &v)) k.topo_allred_max = atoi(v);
+    if (env_set("MV2_TOPO_AWARE_ALLREDUCE_MIN_MSG", &v)) k.topo_allred_min = atoi(v);
+    if (env_set("MV2_TOPO_AWARE_REDUCE_MAX_MSG", &v)) k.topo_red_max = atoi(v);
+    if (env_set("MV2_TOPO_AWARE_REDUCE_MIN_MSG", &v)) k.topo_red_min = atoi(v);
+    if (env_set("MV2_TOPO_AWARE_REDUCE_PPN_THRESHOLD", &v)) k.topo_red_ppn = atoi(v);
+    if (env_set("MV2_TOPO_AWARE_REDUCE_NODE_THRESHOLD", &v)) k.topo_red_nodes = atoi(v);
+    // CMA selects the reduce tables (reduce_tuning.c:1578-1629; ibv_param.c:716)
+    if (env_set("MV2_SMP_USE_CMA", &v)) k.smp_use_cma = !!atoi(v);
+    g_knobs = k;
+    g_knobs_ok = true;
+}
+
+const Knobs &knobs() {
+    if (!g_knobs_ok) knobs_reload();
+    return g_knobs;
+}
+
+const char *algo_name(int a) {
+    static const char *names[ALG_COUNT] = {
+        "none", "shmem_linear", "pt2pt_rs", "pt2pt_rd", "ring_wrapper", "topo_tree", "two_level_p2p",
+        "binomial", "knomial", "redscat_gather", "rs_ring", "rs_rec_halving", "rs_pairwise", "rs_basic",
+        "reduce_topo"};
+    return (a >= 0 && a < ALG_COUNT) ? names[a] : "?";
+}
+
+// ---------------------------------------------------------------------------
+// symbolic expressions and their compilation to programs
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Sym {
+    struct Node {
+        int leaf;  // >= 0: rank operand
+        int a, b;  // op(a = inout, b = in)
+    };
+    std::vector<Node> nodes;
+    int leaf(int r) {
+        nodes.push_back({r, -1, -1});
+        return (int)nodes.size() - 1;
+    }
+    int op(int acc, int in) {
+        nodes.push_back({-1, acc, in});
+        return (int)nodes.size() - 1;
+    }
+    // returns the register holding e's value, or -1 on a malformed tree
+    int emit(int e, Prog &p, unsigned &used) const {
+        const Node &nd = nodes[e];
+        if (nd.leaf >= 0) {
+            if (used & (1u << nd.leaf)) return -1;
+            used |= 1u << nd.leaf;
+            return nd.leaf;
+        }
+        const int ra = emit(nd.a, p, used);
+        const int rb = emit(nd.b, p, used);
+        if (ra < 0 || rb < 0 || p.nsteps >= kMaxRanks - 1) return -1;
+        p.dst[p.nsteps] = (uint8_t)ra;
+        p.src[p.nsteps] = (uint8_t)rb;
+        ++p.nsteps;
+        return ra;
+    }
+    bool compile(int e, Prog &p) const {
+        memset(&p, 0, sizeof(p));
+        unsigned used = 0;
+        const int r = emit(e, p, used);
+        if (r < 0) return false;
+        p.res = (uint8_t)r;
+        return true;
+    }
+};
+
+int pof2_of(int n) {
+    int p = 1;
+    while (p * 2 <= n) p *= 2;
+    return p;
+}
+
+void single(ProgSet &ps, const Prog &p) {
+    memset(&ps, 0, sizeof(ps));
+    ps.nprog = 1;
+    ps.blk = ~(uint64_t)0 >> 1;
+    ps.p[0] = p;
+}
+
+bool single_expr(const Sym &s, int e, ProgSet &ps) {
+    Prog p;
+    if (!s.compile(e, p)) return false;
+    single(ps, p);
+    return true;
+}
+
+// LINEAR: ((x0 . x1) . x2) ... (reduce_shmem allreduce_osu.c:1569-1583,
+// MPIR_Reduce_shmem_MV2 reduce_osu.c:1517-1532)
+bool prog_linear(int n, ProgSet &ps) {
+    Sym s;
+    int acc = s.leaf(0);
+    for (int i = 1; i < n; ++i) acc = s.op(acc, s.leaf(i));
+    return single_expr(s, acc, ps);
+}
+
+// mv2_shm_tree_reduce (ch3_shmem_coll.c:4272-4359) rooted at local rank 0:
+// every rank with local_rank % deg == 0 reduces members g+1 .. g+deg-1 in
+// order; the root then reduces the group leaders deg, 2deg, ... in order
+bool prog_tree(int n, int deg, ProgSet &ps) {
+    if (deg < 1) deg = 1;
+    Sym s;
+    std::vector<int> grp(n, -1);
+    for (int g = 0; g < n; g += deg) {
+        int acc = s.leaf(g);
+        for (int i = g + 1; i < g + deg && i < n; ++i) acc = s.op(acc, s.leaf(i));
+        grp[g] = acc;
+    }
+    int acc = grp[0];
+    for (int g = deg; g < n; g += deg) acc = s.op(acc, grp[g]);
+    return single_expr(s, acc, ps);
+}
+
+// MPIR_Reduce_binomial_MV2 (reduce_osu.c:577-643), commutative: relrank =
+// (rank - root) mod n; at mask m a rank without bits below m receives from
+// relrank | m and computes uop(tmp, recvbuf) (own value is inout)
+// Non-commutative ops use lroot = 0 (the result is then sent to the root,
+// :645-663) and uop(recvbuf, tmp): the received higher ranks are the inout.
+bool prog_binomial(int n, int root, bool noncomm, ProgSet &ps) {
+    if (noncomm) root = 0;
+    Sym s;
+    std::vector<int> cur(n);
+    for (int r = 0; r < n; ++r) cur[r] = s.leaf((r + root) % n);
+    for (int mask = 1; mask < n; mask <<= 1)
+        for (int r = 0; r < n; ++r)
+            if ((r & (2 * mask - 1)) == 0 && (r | mask) < n)
+                cur[r] = noncomm ? s.op(cur[r | mask], cur[r]) : s.op(cur[r], cur[r | mask]);
+    return single_expr(s, cur[0], ps);
+}
+
+// MPIR_Reduce_knomial_MV2 (reduce_osu.c:1639-1835) with the children of
+// MPIR_Reduce_knomial_trace (:1569-1633).  Receives are posted in reverse
+// src_array order and reduced in PMPI_Waitany completion order (:1747-1786);
+// the order used here is the request-index order, which is what Waitany
+// returns when the children's messages have all arrived.
+int knomial_expr(Sym &s, int n, int root, int k, int r) {
+    int mask = 1;
+    while (mask < n) {
+        if (r % (k * mask)) break;
+        mask *= k;
+    }
+    mask /= k;
+    std::vector<int> src;
+    for (int m = mask; m > 0; m /= k)
+        for (int j = 1; j < k; ++j)
+            if (r + m * j < n) src.push_back(r + m * j);
+    int acc = s.leaf((r + root) % n);
+    for (int i = (int)src.size() - 1; i >= 0; --i) acc = s.op(acc, knomial_expr(s, n, root, k, src[i]));
+    return acc;
+}
+
+bool prog_knomial(int n, int root, int k, ProgSet &ps) {
+    Sym s;
+    return single_expr(s, knomial_expr(s, n, root, k, 0), ps);
+}
+
+// Recursive-halving reduce-scatter over pof2 blocks as in
+// MPIR_Allreduce_pt2pt_rs_MV2 (allreduce_osu.c:853-947) and
+// MPIR_Reduce_redscat_gather_MV2 (reduce_osu.c:907-991): mask = 1, 2, ...;
+// the lower newrank keeps the lower half of its index range; the received
+// part is reduced as uop(tmp, recvbuf).  cur[nr][i] is newrank nr's partial
+// of block i; returns the final owner's expression of each block.
+void rs_halving(Sym &s, int pof2, std::vector<std::vector<int>> &cur, std::vector<int> &block_expr) {
+    std::vector<int> send_idx(pof2, 0), recv_idx(pof2, 0), last_idx(pof2, pof2);
+    std::vector<int> lo(pof2, 0), hi(pof2, pof2);
+    for (int mask = 1; mask < pof2; mask <<= 1) {
+        std::vector<std::vector<int>> prev = cur;
+        for (int nr = 0; nr < pof2; ++nr) {
+            const int nd = nr ^ mask;
+            if (nr < nd) {
+                send_idx[nr] = recv_idx[nr] + pof2 / (mask * 2);
+                lo[nr] = recv_idx[nr];
+                hi[nr] = send_idx[nr];
+            } else {
+                recv_idx[nr] = send_idx[nr] + pof2 / (mask * 2);
+                lo[nr] = recv_idx[nr];
+                hi[nr] = last_idx[nr];
+            }
+        }
+        for (int nr = 0; nr < pof2; ++nr)
+            for (int i = lo[nr]; i < hi[nr]; ++i) cur[nr][i] = s.op(prev[nr][i], prev[nr ^ mask][i]);
+        for (int nr = 0; nr < pof2; ++nr) {
+            send_idx[nr] = recv_idx[nr];
+            if ((mask << 1) < pof2) last_idx[nr] = recv_idx[nr] + pof2 / (mask << 1);
+        }
+    }
+    block_expr.assign(pof2, -1);
+    for (int nr = 0; nr < pof2; ++nr) {
+        // after the last step newrank nr holds exactly one block: [lo, hi)
+        const int b = pof2 == 1 ? 0 : lo[nr];
+        block_expr[b] = cur[nr][b];
+    }
+}
+
+bool blocks_to_progset(const Sym &s, const std::vector<int> &blk_expr, size_t count, ProgSet &ps) {
+    const int nb = (int)blk_expr.size();
+    memset(&ps, 0, sizeof(ps));
+    ps.nprog = nb;
+    ps.blk = count / (size_t)nb;
+    if (ps.blk == 0) ps.blk = 1;
+    for (int b = 0; b < nb; ++b)
+        if (blk_expr[b] < 0 || !s.compile(blk_expr[b], ps.p[b])) return false;
+    return true;
+}
+
+// MPIR_Allreduce_pt2pt_rs_MV2 (allreduce_osu.c:633-1054) for builtin ops.
+// Non-pof2 pre-step (:734-777): even r < 2rem sends to r+1, odd r computes
+// uop(tmp = x_{r-1}, recv = x_r).  count < pof2 (:802): recursive doubling
+// (every rank's own result); else recursive halving + doubling allgather.
+// Non-commutative (user) ops always take recursive doubling; a step keeps the
+// lower real rank on the left (:824-845: uop(recvbuf, tmp) when dst > rank).
+bool prog_pt2pt_rs(int n, int me, size_t count, bool force_rd, ProgSet &ps, bool noncomm = false) {
+    const int pof2 = pof2_of(n), rem = n - pof2;
+    Sym s;
+    std::vector<int> x(n);
+    for (int r = 0; r < n; ++r) x[r] = s.leaf(r);
+    std::vector<int> base(pof2);
+    for (int nr = 0; nr < pof2; ++nr) base[nr] = nr < rem ? s.op(x[2 * nr + 1], x[2 * nr]) : x[nr + rem];
+    if (force_rd || count < (size_t)pof2) {
+        std::vector<int> cur = base;
+        auto real = [&](int nr) { return nr < rem ? 2 * nr + 1 : nr + rem; };
+        for (int mask = 1; mask < pof2; mask <<= 1) {
+            std::vector<int> prev = cur;
+            for (int nr = 0; nr < pof2; ++nr) {
+                const int nd = nr ^ mask;
+                cur[nr] = (!noncomm || real(nd) < real(nr)) ? s.op(prev[nr], prev[nd]) : s.op(prev[nd], prev[nr]);
+            }
+        }
+        // post-step (:1003-1030): even r < 2rem takes the result of r+1
+        const int r = (me < 2 * rem && me % 2 == 0) ? me + 1 : me;
+        const int nr = r < 2 * rem ? r / 2 : r - rem;
+        return single_expr(s, cur[nr], ps);
+    }
+    std::vector<std::vector<int>> cur(pof2, std::vector<int>(pof2));
+    for (int nr = 0; nr < pof2; ++nr)
+        for (int i = 0; i < pof2; ++i) cur[nr][i] = base[nr];
+    std::vector<int> be;
+    rs_halving(s, pof2, cur, be);
+    return blocks_to_progset(s, be, count, ps);
+}
+
+// MPIR_Reduce_redscat_gather_MV2 (reduce_osu.c:718-1135): the pre-step runs
+// the other way round (:849-894: odd r < 2rem sends to r-1, even r computes
+// uop(tmp = x_{r+1}, recv = x_r)); the gather to the root only moves data.
+bool prog_redscat_gather(int n, size_t count, ProgSet &ps) {
+    const int pof2 = pof2_of(n), rem = n - pof2;
+    Sym s;
+    std::vector<int> x(n);
+    for (int r = 0; r < n; ++r) x[r] = s.leaf(r);
+    std::vector<std::vector<int>> cur(pof2, std::vector<int>(pof2));
+    for (int nr = 0; nr < pof2; ++nr) {
+        const int b = nr < rem ? s.op(x[2 * nr], x[2 * nr + 1]) : x[nr + rem];
+        for (int i = 0; i < pof2; ++i) cur[nr][i] = b;
+    }
+    std::vector<int> be;
+    rs_halving(s, pof2, cur, be);
+    return blocks_to_progset(s, be, count, ps);
+}
+
+// MPIR_Allreduce_pt2pt_ring_MV2 (allreduce_osu.c:3925-3958): chunk c starts at
+// rank c; hop k runs uop(in = own chunk of rank c+k, inout = received partial)
+bool prog_ring_allreduce(int n, size_t count, ProgSet &ps) {
+    Sym s;
+    std::vector<int> be(n);
+    for (int c = 0; c < n; ++c) {
+        int acc = s.leaf(c);
+        for (int k = 1; k < n; ++k) acc = s.op(acc, s.leaf((c + k) % n));
+        be[c] = acc;
+    }
+    if (!blocks_to_progset(s, be, count, ps)) return false;
+    ps.blk = count / (size_t)n;
+    return true;
+}
+
+// MPIR_Reduce_scatter_ring(_2lvl) (red_scat_osu.c:1290-1336): block b starts at
+// rank b+1; each later rank runs Reduce_local(in = received, inout = own chunk)
+int rs_ring_expr(Sym &s, int n, int b) {
+    int acc = s.leaf((b + 1) % n);
+    for (int k = 2; k <= n; ++k) acc = s.op(s.leaf((b + k) % n), acc);
+    return acc;
+}
+
+// MPIR_Reduce_scatter_Rec_Halving_MV2 (red_scat_osu.c:537-760): pre-step
+// even r < 2rem sends to r+1, odd r: uop(tmp = x_{r-1}, results = x_r);
+// new block i = old blocks of the ranks it stands for; halving from
+// mask = pof2/2 down to 1, the lower newrank keeping the lower half.
+int rs_rec_halving_expr(Sym &s, int n, int me) {
+    const int pof2 = pof2_of(n), rem = n - pof2;
+    std::vector<int> x(n);
+    for (int r = 0; r < n; ++r) x[r] = s.leaf(r);
+    std::vector<std::vector<int>> cur(pof2, std::vector<int>(pof2));
+    for (int nr = 0; nr < pof2; ++nr) {
+        const int b = nr < rem ? s.op(x[2 * nr + 1], x[2 * nr]) : x[nr + rem];
+        for (int i = 0; i < pof2; ++i) cur[nr][i] = b;
+    }
+    std::vector<int> send_idx(pof2, 0), recv_idx(pof2, 0), last_idx(pof2, pof2), lo(pof2), hi(pof2);
+    for (int mask = pof2 >> 1; mask > 0; mask >>= 1) {
+        std::vector<std::vector<int>> prev = cur;
+        for (int nr = 0; nr < pof2; ++nr) {
+            const int nd = nr ^ mask;
+            if (nr < nd) {
+                send_idx[nr] = recv_idx[nr] + mask;
+                lo[nr] = recv_idx[nr];
+                hi[nr] = send_idx[nr];
+            } else {
+                recv_idx[nr] = send_idx[nr] + mask;
+                lo[nr] = recv_idx[nr];
+                hi[nr] = last_idx[nr];
+            }
+        }
+        for (int nr = 0; nr < pof2; ++nr)
+            for (int i = lo[nr]; i < hi[nr]; ++i) cur[nr][i] = s.op(prev[nr][i], prev[nr ^ mask][i]);
+        for (int nr = 0; nr < pof2; ++nr) {
+            send_idx[nr] = recv_idx[nr];
+            last_idx[nr] = recv_idx[nr] + mask;
+        }
+    }
+    const int nb = me < 2 * rem ? me / 2 : me - rem;  // new block holding my old block
+    // the newrank whose final single-block range is nb
+    for (int nr = 0; nr < pof2; ++nr)
+        if ((pof2 == 1 ? 0 : lo[nr]) == nb) return cur[nr][nb];
+    return -1;
+}
+
+// MPIR_Reduce_scatter_Pair_Wise_MV2 (red_scat_osu.c:867-989), commutative:
+// own block, then uop(tmp = x_{me-i}, recvbuf) for i = 1 .. n-1
+int rs_pairwise_expr(Sym &s, int n, int me) {
+    int acc = s.leaf(me);
+    for (int i = 1; i < n; ++i) acc = s.op(acc, s.leaf((me - i + n) % n));
+    return acc;
+}
+
+// tuning-table index of a message size (allreduce_osu.c:3241-3277,
+// reduce_osu.c:2556-2586): 0 below the smallest entry, the last entry above
+// the largest, else log2 of the largest power of two <= nbytes over the smallest
+int table_index(long nbytes, long minsz, int size_table) {
+    const long maxsz = minsz << (size_table - 1);
+    if (nbytes < minsz) return 0;
+    if (nbytes > maxsz) return size_table - 1;
+    int idx = 0;
+    long v = nbytes / minsz;
+    while (v > 1) {
+        v >>= 1;
+        ++idx;
+    }
+    return idx;
+}
+
+// FIND_PPN_INDEX (common_tuning.h:91-115) over the default tables' ppn
+// configurations {1, 2, 16}: one node with n ranks -> 0 (n = 1), 1 (n = 2), 2 (n >= 3)
+int ppn_conf(int n) { return n <= 1 ? 0 : (n == 2 ? 1 : 2); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// MPI_Reduce
+// ---------------------------------------------------------------------------
+enum { R_BINOM = 0, R_KNOM = 1, R_RSG = 2 };
+
+// First entries (numproc <= n) of the default reduce tables
+// (reduce_tuning.c:1563-1649, "Stampede" fall-back for an unlisted
+// architecture): tuning/reduce/gen2{_cma}_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{2,16}ppn.h
+struct ReduceEntry {
+    int minsz, size;        // smallest inter-leader message size, size_inter_table
+    int k;                  // inter_k_degree
+    int two_level[19];
+    int inter[19];
+};
+static const ReduceEntry kRedCma2 = {
+    4, 19, 4, {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 1, 1, 1, 1, 1, 1},
+    {R_RSG, R_BINOM, R_KNOM, R_KNOM, R_RSG, R_BINOM, R_BINOM, R_KNOM, R_KNOM, R_BINOM, R_BINOM, R_RSG, R_BINOM,
+     R_RSG, R_KNOM, R_KNOM, R_BINOM, R_BINOM, R_BINOM}};
+static const ReduceEntry kRedCma16 = {
+    4, 19, 4, {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 0, 0, 0, 0},
+    {R_KNOM, R_RSG, R_BINOM, R_RSG, R_RSG, R_BINOM, R_BINOM, R_KNOM, R_RSG, R_RSG, R_KNOM, R_RSG, R_BINOM, R_BINOM,
+     R_KNOM, R_RSG, R_RSG, R_RSG, R_RSG}};
+static const ReduceEntry kRed2 = {
+    1, 18, 4, {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1},
+    {R_RSG, R_KNOM, R_KNOM, R_BINOM, R_BINOM, R_BINOM, R_BINOM, R_KNOM, R_BINOM, R_RSG, R_BINOM, R_BINOM, R_BINOM,
+     R_BINOM, R_BINOM, R_BINOM, R_BINOM, R_BINOM, R_RSG}};
+static const ReduceEntry kRed16 = {
+    1, 18, 4, {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0},
+    {R_BINOM, R_KNOM, R_BINOM, R_BINOM, R_RSG, R_RSG, R_RSG, R_RSG, R_RSG, R_RSG, R_KNOM, R_KNOM, R_KNOM, R_KNOM,
+     R_KNOM, R_KNOM, R_KNOM, R_BINOM, R_BINOM}};
+
+static int reduce_k(const Knobs &K, const ReduceEntry *e) {
+    int k = K.reduce_inter_k >= 0 ? K.reduce_inter_k : (e ? e->k : 4);
+    return k < 2 ? 2 : k;  // factors 0 and 1 never terminate the reference's trace loop
+}
+
+static int reduce_fill(Plan *p, int algo, int n, int root, size_t count, int k, bool noncomm = false) {
+    p->algo = algo;
+    p->k = k;
+    bool ok = false;
+    switch (algo) {
+    case ALG_SHMEM_LINEAR: ok = prog_linear(n, p->ps); break;
+    case ALG_BINOMIAL: ok = prog_binomial(n, root, noncomm, p->ps); break;
+    case ALG_KNOMIAL: ok = prog_knomial(n, root, k, p->ps); p->unpinned = n > 2; break;
+    case ALG_REDSCAT_GATHER: ok = prog_redscat_gather(n, count, p->ps); break;
+    case ALG_REDUCE_TOPO: ok = prog_tree(n, k, p->ps); break;
+    default: break;
+    }
+    return ok ? 0 : E_INTERN;
+}
+
+// MPIR_Reduce_two_level_helper_MV2, one-node branch (reduce_osu.c:2082-2166)
+static int reduce_helper(const Knobs &K, Plan *p, int n, int root, size_t count, int textent,
+                         const ReduceEntry *e) {
+    const long stride = (long)count * textent;
+    const int k = reduce_k(K, e);
+    if (stride <= K.shmem_intra_reduce_msg && K.enable_shmem_reduce) {
+        // MPIR_Reduce_shmem_MV2 at local root 0 (then sent to the root), or the intra knomial
+        // wrapper at 0 from the shmem slot size on (:2125-2133)
+        if (stride < K.shmem_coll_max_msg) return reduce_fill(p, ALG_SHMEM_LINEAR, n, 0, count, k);
+        return reduce_fill(p, ALG_KNOMIAL, n, 0, count, k);
+    }
+    return reduce_fill(p, K.use_knomial_reduce == 1 ? ALG_KNOMIAL : ALG_BINOMIAL, n, root, count, k);
+}
+
+int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *p, int opk) {
+    (void)me;
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    const Knobs &K = knobs();
+    const bool comm = opk != OPK_USER_NONCOMM, builtin = opk == OPK_BUILTIN;
+    const long nbytes = (long)count * tsize;
+    // topology-aware reduce (reduce_osu.c:2498-2506), off by default
+    if (nbytes <= K.topo_red_max && nbytes >= K.topo_red_min && K.enable_skip_search && nbytes <= K.coll_skip_thr &&
+        K.enable_topo && K.use_topo_reduce && comm && n >= K.topo_red_ppn && K.topo_red_nodes <= 1)
+        return reduce_fill(p, ALG_REDUCE_TOPO, n, root, count, K.tree_degree < 1 ? 1 : K.tree_degree);
+    // small messages: shmem + binomial two-level (:2508-2514); two-level needs a
+    // commutative op, else binomial (:2628-2636)
+    if (K.enable_shmem_reduce && K.enable_skip_search && nbytes <= K.coll_skip_thr)
+        return comm ? reduce_helper(K, p, n, root, count, textent, nullptr)
+                    : reduce_fill(p, ALG_BINOMIAL, n, root, count, 0, true);
+    const ReduceEntry *e = ppn_conf(n) == 1 ? (K.smp_use_cma ? &kRedCma2 : &kRed2)
+                                            : (K.smp_use_cma ? &kRedCma16 : &kRed16);
+    const int idx = table_index(nbytes, e->minsz, e->size);
+    const int k = reduce_k(K, e);
+    if (e->two_level[idx])
+        return comm ? reduce_helper(K, p, n, root, count, textent, e)
+                    : reduce_fill(p, ALG_BINOMIAL, n, root, count, k, true);
+    switch (e->inter[idx]) {
+    case R_KNOM:  // commutative only (:2637-2644)
+        return reduce_fill(p, comm ? ALG_KNOMIAL : ALG_BINOMIAL, n, root, count, k, !comm);
+    case R_RSG:  // builtin op and count >= pof2 (:2645-2652)
+        return reduce_fill(p, builtin && count >= (size_t)pof2_of(n) ? ALG_REDSCAT_GATHER : ALG_BINOMIAL, n, root,
+                           count, k, !comm);
+    default: return reduce_fill(p, ALG_BINOMIAL, n, root, count, k, !comm);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MPI_Allreduce
+// ---------------------------------------------------------------------------
+enum { A_RS = 0, A_RD = 1 };
+enum { I_SHMEM = 0, I_P2P = 1 };
+// First entries of the default allreduce tables (allreduce_tuning.c:1714-1762,
+// tuning/allreduce/nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{2,16}ppn.h): 18
+// entries of 1 B .. 128 KiB for both the inter-leader and the intra-node lists
+struct AllreduceEntry {
+    int two_level[19];
+    int inter[18];
+    int intra[18];
+};
+static const AllreduceEntry kAr2 = {
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0},
+    {A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS},
+    {I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM,
+     I_P2P, I_P2P, I_P2P, I_P2P, I_P2P, I_P2P}};
+static const AllreduceEntry kAr16 = {
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS},
+    {I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_SHMEM, I_P2P, I_P2P, I_P2P, I_P2P, I_P2P, I_P2P,
+     I_P2P, I_P2P, I_P2P, I_P2P}};
+
+// pt2pt_rs falls back to recursive doubling for user ops and count < pof2 (:802)
+static int allreduce_fill(Plan *p, int algo, int n, int me, size_t count, int opk = OPK_BUILTIN) {
+    if (algo == ALG_PT2PT_RS && (opk != OPK_BUILTIN || count < (size_t)pof2_of(n))) algo = ALG_PT2PT_RD;
+    p->algo = algo;
+    bool ok = false;
+    switch (algo) {
+    case ALG_SHMEM_LINEAR: ok = prog_linear(n, p->ps); break;
+    case ALG_PT2PT_RS: ok = prog_pt2pt_rs(n, me, count, false, p->ps); break;
+    case ALG_PT2PT_RD: ok = prog_pt2pt_rs(n, me, count, true, p->ps, opk == OPK_USER_NONCOMM); break;
+    case ALG_RING: ok = count >= (size_t)n && prog_ring_allreduce(n, (count / n) * n, p->ps); break;
+    default: break;
+    }
+    return ok ? 0 : E_INTERN;
+}
+
+int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *p,
+                   int opk) {
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    const Knobs &K = knobs();
+    if (forced == ALG_PT2PT_RS || forced == ALG_PT2PT_RD || forced == ALG_RING || forced == ALG_SHMEM_LINEAR)
+        return allreduce_fill(p, forced, n, me, count, opk);
+    // a non-commutative op fails every shortcut's is_commutative test and ends in
+    // recursive doubling whatever the size (allreduce_osu.c:3359-3368, :3893-3898, :802)
+    if (opk == OPK_USER_NONCOMM) return allreduce_fill(p, ALG_PT2PT_RD, n, me, count, opk);
+    const long nbytes = (long)count * tsize;
+    // ALLREDUCE_SKIP_SMALL_MESSAGE_TUNING_TABLES (allreduce_osu.c:118-160)
+    bool tables = false;
+    if (K.allred_skip_small) {
+        if (nbytes <= K.topo_allred_max && nbytes >= K.topo_allred_min && K.enable_topo && K.use_topo_allreduce) {
+            if (n < K.topo_allred_ppn) {
+                tables = true;  // goto use_tables
+            } else {
+                p->algo = ALG_TOPO_TREE;
+                p->k = K.tree_degree < 1 ? 1 : K.tree_degree;
+                return prog_tree(n, p->k, p->ps) ? 0 : E_INTERN;
+            }
+        }
+        if (!tables && K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr)
+            return allreduce_fill(p, ALG_SHMEM_LINEAR, n, me, count, opk);
+    }
+    // ALLREDUCE_SKIP_LARGE_MESSAGE_TUNING_TABLES (:163-188): the flat ring wrapper at low ppn
+    if (!tables && K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes &&
+        n <= K.allred_ring_ppn) {
+        p->algo = ALG_RING;
+        if (count >= (size_t)n && !in_place) return prog_ring_allreduce(n, (count / n) * n, p->ps) ? 0 : E_INTERN;
+        return 0;  // the wrapper runs pt2pt_rs (count < n, or MPI_IN_PLACE): see coll.cpp
+    }
+    // tuning tables (:3162-3373)
+    const AllreduceEntry &e = ppn_conf(n) == 1 ? kAr2 : kAr16;
+    const int idx = table_index(nbytes, 1, 18);
+    if (e.two_level[idx]) {
+        // MPIR_Allreduce_two_level_MV2 (:1687-1830) when shmem is usable, else recursive doubling
+        if (!(K.enable_shmem_allreduce && K.enable_shmem_collectives))
+            return allreduce_fill(p, ALG_PT2PT_RD, n, me, count, opk);
+        const int iidx = table_index(nbytes, 1, 18);
+        if (e.intra[iidx] == I_SHMEM) {
+            const int rc = allreduce_fill(p, ALG_SHMEM_LINEAR, n, me, count, opk);
+            // from the shmem slot size on reduce_shmem runs MPICH's MPIR_Reduce_intra (:1521-1526),
+            // whose order is not restated; only reachable through raised thresholds
+            if ((long)count * textent >= K.shmem_coll_max_msg) p->unpinned = 1;
+            return rc;
+        }
+        // reduce_p2p (:1616-1684): MPIR_Reduce_MV2 to local rank 0, then the shmem bcast
+        Plan r;
+        const int rc = plan_reduce(n, me, 0, count, tsize, textent, &r, opk);
+        if (rc) return rc;
+        *p = r;
+        p->inner = r.algo;
+        p->algo = ALG_TWO_LEVEL_P2P;
+        return 0;
+    }
+    return allreduce_fill(p, e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS, n, me, count, opk);
+}
+
+// ---------------------------------------------------------------------------
+// MPI_Reduce_scatter (commutative ops; red_scat_osu.c:1859-1896)
+// ---------------------------------------------------------------------------
+int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *p, int opk) {
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    if (opk == OPK_USER_NONCOMM) return E_INTERN;  // MPIR_Reduce_scatter_non_comm_MV2: not restated here
+    const Knobs &K = knobs();
+    size_t total = 0;
+    for (int j = 0; j < n; ++j) total += counts[j];
+    const long nbytes = (long)total * tsize;
+    // default table (red_scat_tuning.c:214-287), first entry (numproc 8) for n <= 8
+    int algo;
+    if (K.red_scat_ring_thr <= nbytes) algo = ALG_RS_RING;
+    else if (nbytes <= 256) algo = ALG_RS_BASIC;
+    else if (nbytes <= 16384) algo = ALG_RS_REC_HALVING;
+    else if (nbytes <= 65536) algo = ALG_RS_PAIRWISE;
+    else algo = ALG_RS_RING;
+    p->algo = algo;
+    Sym s;
+    switch (algo) {
+    case ALG_RS_RING: return single_expr(s, rs_ring_expr(s, n, me), p->ps) ? 0 : E_INTERN;
+    case ALG_RS_PAIRWISE: return single_expr(s, rs_pairwise_expr(s, n, me), p->ps) ? 0 : E_INTERN;
+    case ALG_RS_REC_HALVING: {
+        const int e = rs_rec_halving_expr(s, n, me);
+        return (e >= 0 && single_expr(s, e, p->ps)) ? 0 : E_INTERN;
+    }
+    default: {
+        // MPIR_Reduce_MV2(total, root 0) then a scatter (:326-413)
+        Plan r;
+        const int rc = plan_reduce(n, 0, 0, total, tsize, textent, &r, opk);
+        if (rc) return rc;
+        p->ps = r.ps;
+        p->inner = r.algo;
+        p->k = r.k;
+        p->unpinned = r.unpinned;
+        return 0;
+    }
+    }
+}
+
+}  // namespace mv2

@@ -1,0 +1,103 @@
+// orders.h — which MV2 algorithm a one-node collective runs, and the
+// reduction order that algorithm gives every element (as Prog programs).
+//
+// The reference picks an algorithm per call from size thresholds, MV2_*
+// knobs and tuning tables (MPIR_Allreduce_index_tuned_intra_MV2
+// allreduce_osu.c:3015-3420, MPIR_Reduce_index_tuned_intra_MV2
+// reduce_osu.c:2391-2660, MPIR_Reduce_scatter_MV2 red_scat_osu.c:1771-1900),
+// and the fp result depends on that algorithm's operand order.  This module
+// restates the selection for one node (shmem_coll_ok, is_uniform, blocked
+// placement, one topology level: see DESIGN.md §4) and turns each algorithm
+// into per-element programs by a symbolic run of its message schedule: the
+// device kernels then evaluate the same binary tree in registers.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../coll/kernels.h"
+
+namespace mv2 {
+
+enum Algo : int {
+    ALG_NONE = 0,            // one rank / REPLACE / NO_OP: no reduction order
+    ALG_SHMEM_LINEAR = 1,    // reduce_shmem / MPIR_Reduce_shmem_MV2: ((x0 . x1) . x2) ...
+    ALG_PT2PT_RS = 2,        // MPIR_Allreduce_pt2pt_rs_MV2 (allreduce_osu.c:633)
+    ALG_PT2PT_RD = 3,        // MPIR_Allreduce_pt2pt_rd_MV2 (:360), also pt2pt_rs with count < pof2
+    ALG_RING = 4,            // MPIR_Allreduce_pt2pt_ring_wrapper_MV2 (:3758)
+    ALG_TOPO_TREE = 5,       // MPIR_Allreduce_topo_aware_hierarchical_MV2 (:2272) -> mv2_shm_tree_reduce
+    ALG_TWO_LEVEL_P2P = 6,   // two-level with intra reduce_p2p: MPIR_Reduce_MV2 to local rank 0 (:1616)
+    ALG_BINOMIAL = 7,        // MPIR_Reduce_binomial_MV2 (reduce_osu.c:425)
+    ALG_KNOMIAL = 8,         // MPIR_Reduce_knomial_MV2 (:1639)
+    ALG_REDSCAT_GATHER = 9,  // MPIR_Reduce_redscat_gather_MV2 (:718)
+    ALG_RS_RING = 10,        // MPIR_Reduce_scatter_ring(_2lvl) (red_scat_osu.c:1026/1190)
+    ALG_RS_REC_HALVING = 11, // MPIR_Reduce_scatter_Rec_Halving_MV2 (:428)
+    ALG_RS_PAIRWISE = 12,    // MPIR_Reduce_scatter_Pair_Wise_MV2 (:786)
+    ALG_RS_BASIC = 13,       // MPIR_Reduce_Scatter_Basic_MV2 (:300): MPIR_Reduce_MV2 to 0 + scatter
+    ALG_REDUCE_TOPO = 14,    // MPIR_Reduce_topo_aware_hierarchical_MV2 (reduce_osu.c:206)
+    ALG_COUNT
+};
+
+// MV2_* knobs that move the one-node selection, parsed like the reference
+// (ch3_shmem_coll.c MV2_Read_env_vars; atoi unless the reference uses
+// user_val_to_bytes).  Defaults: ch3_shmem_coll.c:283-541, coll_shmem.h:35/191,
+// mpiimpl.h:3954, ch3_smp_progress.c:221.
+struct Knobs {
+    int32_t enable_shmem_collectives;   // MV2_USE_SHARED_MEM (1)
+    int32_t enable_shmem_allreduce;     // MV2_USE_SHMEM_ALLREDUCE (1)
+    int32_t enable_shmem_reduce;        // MV2_USE_SHMEM_REDUCE (1)
+    int32_t enable_skip_search;         // MV2_ENABLE_SKIP_TUNING_TABLE_SEARCH (1)
+    int32_t coll_skip_thr;              // MV2_COLL_SKIP_TABLE_THRESHOLD (1024, atoi)
+    int32_t allred_skip_small;          // MV2_ENABLE_ALLREDUCE_SKIP_SMALL_MESSAGE_TUNING_TABLE_SEARCH (1)
+    int32_t allred_skip_large;          // MV2_ENABLE_ALLREDUCE_SKIP_LARGE_MESSAGE_TUNING_TABLE_SEARCH (1)
+    int32_t enable_topo;                // MV2_ENABLE_TOPO_AWARE_COLLECTIVES (1; 0 if socket-aware is enabled)
+    int32_t use_topo_allreduce;         // MV2_USE_TOPO_AWARE_ALLREDUCE (1)
+    int32_t topo_allred_min, topo_allred_max;   // MV2_TOPO_AWARE_ALLREDUCE_{MIN,MAX}_MSG (1, 2048)
+    int32_t topo_allred_ppn;            // mv2_topo_aware_allreduce_ppn_threshold (1)
+    int32_t use_topo_reduce;            // MV2_USE_TOPO_AWARE_REDUCE (0)
+    int32_t topo_red_min, topo_red_max; // MV2_TOPO_AWARE_REDUCE_{MIN,MAX}_MSG (1, 2048)
+    int32_t topo_red_ppn;               // MV2_TOPO_AWARE_REDUCE_PPN_THRESHOLD (1)
+    int32_t topo_red_nodes;             // MV2_TOPO_AWARE_REDUCE_NODE_THRESHOLD (1)
+    int32_t tree_degree;                // MV2_SHMEM_REDUCE_TREE_DEGREE (4)
+    int32_t allred_use_ring;            // MV2_ALLRED_USE_RING (1; flag > 0)
+    int32_t pad0;                       // (explicit: the struct is compared bytewise across ranks)
+    int64_t allred_ring_thr;            // MV2_ALLREDUCE_RING_ALGO_THRESHOLD (2 MiB, user_val_to_bytes)
+    int32_t allred_ring_ppn;            // MV2_ALLREDUCE_RING_ALGO_PPN_THRESHOLD (8)
+    int32_t smp_use_cma;                // MV2_SMP_USE_CMA (1): selects the CMA reduce tables
+    int32_t use_knomial_reduce;         // MV2_USE_KNOMIAL_REDUCE (1)
+    int32_t reduce_inter_k;             // MV2_USE_INTER_KNOMIAL_REDUCE_FACTOR (-1: the table's inter_k_degree)
+    int32_t shmem_coll_max_msg;         // MV2_SHMEM_COLL_MAX_MSG_SIZE (32 KiB)
+    int32_t shmem_intra_reduce_msg;     // MV2_INTRA_SHMEM_REDUCE_MSG (2048)
+    int64_t red_scat_ring_thr;          // MV2_RED_SCAT_RING_ALGO_THRESHOLD (131072, user_val_to_bytes)
+};
+
+const Knobs &knobs();  // parsed from the environment on first use
+void knobs_reload();   // re-read the environment (tests)
+
+struct Plan {
+    int algo;    // Algo
+    int inner;   // ALG_TWO_LEVEL_P2P / ALG_RS_BASIC: the MPIR_Reduce_MV2 algorithm inside
+    int k;       // knomial factor / shm tree degree
+    int unpinned;// 1: the reference result depends on message arrival (knomial Waitany)
+    ProgSet ps;  // order of every element of this rank's result (global element index)
+};
+
+// Kind of op: builtin ops are commutative; user ops are commutative or not
+// (MPI_Op_create); several algorithms branch on HANDLE_KIND_BUILTIN and on
+// is_commutative.  A program step dst <- src is uop(in = w[src], inout = w[dst])
+// for every kind, so a non-commutative order is expressed by which operand
+// is the accumulator.
+enum OpKind : int { OPK_BUILTIN = 0, OPK_USER_COMM = 1, OPK_USER_NONCOMM = 2 };
+
+// All functions: n ranks on one node, tsize = MPI_Type_size, textent = extent.
+// Return 0, or E_INTERN when the order cannot be expressed.  forced: 0 = the
+// reference's selection, else an Algo to run (ring wrapper parts).
+int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *out,
+                   int opk = OPK_BUILTIN);
+int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *out, int opk = OPK_BUILTIN);
+// counts[n] per-rank block counts; elements are indexed over the whole operand
+int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *out,
+                        int opk = OPK_BUILTIN);
+
+const char *algo_name(int algo);
+
+}  // namespace mv2

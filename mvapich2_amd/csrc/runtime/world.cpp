@@ -19,6 +19,7 @@
 #include <thread>
 
 #include "log.h"
+#include "orders.h"
 
 namespace mv2 {
 
@@ -36,19 +37,6 @@ static int env_int(const char *const *names, int dflt) {
 static long env_long(const char *name, long dflt) {
     const char *v = getenv(name);
     return (v && *v) ? atol(v) : dflt;
-}
-
-// MV2_* byte-size knobs with the reference's K/M/G suffixes (user_val_to_bytes,
-// ch3_shmem_coll.c); negative values clamp to 0 like :3097
-static long env_bytes(const char *name, long dflt) {
-    const char *v = getenv(name);
-    if (!v || !*v) return dflt;
-    char *end = nullptr;
-    long x = strtol(v, &end, 10);
-    if (end && (*end == 'k' || *end == 'K')) x <<= 10;
-    else if (end && (*end == 'm' || *end == 'M')) x <<= 20;
-    else if (end && (*end == 'g' || *end == 'G')) x <<= 30;
-    return x < 0 ? 0 : x;
 }
 
 // start time of the parent process (jiffies since boot): with the parent pid
@@ -160,10 +148,7 @@ static int setup_device_common() {
     w.pipe_sub = (size_t)env_long("MV2AMD_PIPE_SUB", (long)w.pipe_sub);
     w.light_release = (int)env_long("MV2AMD_LIGHT_RELEASE", w.light_release);
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
-    w.allred_use_ring = env_long("MV2_ALLRED_USE_RING", 1) != 0;
-    w.allred_ring_thr = (size_t)env_bytes("MV2_ALLREDUCE_RING_ALGO_THRESHOLD", (long)w.allred_ring_thr);
-    w.coll_skip_thr = (size_t)env_bytes("MV2_COLL_SKIP_TABLE_THRESHOLD", (long)w.coll_skip_thr);
-    w.red_scat_ring_thr = (size_t)env_bytes("MV2_RED_SCAT_RING_ALGO_THRESHOLD", (long)w.red_scat_ring_thr);
+    knobs_reload();  // MV2_* algorithm-selection knobs (orders.cpp)
     hipEventCreate(&w.ev0);
     hipEventCreate(&w.ev1);
     return 0;
@@ -230,8 +215,16 @@ int world_init() {
             hipDeviceGetAttribute(&me.pci_bus, hipDeviceAttributePciBusId, w.device);
             hipDeviceGetAttribute(&me.pci_device, hipDeviceAttributePciDeviceId, w.device);
         }
+        memcpy(&me.knobs, &knobs(), sizeof(Knobs));
         w.shm->attached.fetch_add(1);
-        host_barrier();  // everyone attached and published pid/device
+        host_barrier();  // everyone attached and published pid/device/knobs
+        // the algorithm choice (and with it the kernels' flag pairing) must agree on every
+        // rank: a rank started with different MV2_* selection knobs would hang the job
+        for (int j = 0; j < w.size; ++j)
+            if (memcmp(&w.shm->r[j].knobs, &knobs(), sizeof(Knobs)) != 0) {
+                MV2_ERR("MV2_* collective selection knobs differ between rank %d and rank %d", w.rank, j);
+                return E_OTHER;
+            }
 
         // ranks sharing one GPU (tests run several ranks on one device): the
         // maximum over all GPUs, so every rank derives the same kernel grids

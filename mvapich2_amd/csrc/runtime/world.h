@@ -22,6 +22,7 @@
 
 #include "../common.h"
 #include "../coll/kernels.h"
+#include "orders.h"
 
 namespace mv2 {
 
@@ -66,6 +67,7 @@ struct alignas(64) ShmRank {
     hipIpcMemHandle_t pipe_ag_handle;
     hipIpcMemHandle_t p2p_handle;
     int selftest_ok;  // coll_selftest verdict of this rank (agreed through host_barrier)
+    Knobs knobs;      // MV2_* selection knobs as this rank parsed them (must agree)
 };
 
 struct ShmSeg {
@@ -116,14 +118,6 @@ struct World {
     int pipe_grid = kPipeMaxGrid;                 // pipelined collectives: workgroups (<= kPipeMaxGrid)
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
-    // flat ring allreduce (allreduce_osu.c:163-170): MV2_ALLRED_USE_RING (default 1,
-    // ch3_shmem_coll.c:513) and MV2_ALLREDUCE_RING_ALGO_THRESHOLD (2 MiB, :492)
-    int allred_use_ring = 1;
-    size_t allred_ring_thr = (size_t)2 << 20;
-    // two-level (reduce_shmem) below MV2_COLL_SKIP_TABLE_THRESHOLD (1024, coll_shmem.h:191);
-    // reduce-scatter ring from MV2_RED_SCAT_RING_ALGO_THRESHOLD (131072, ch3_shmem_coll.c:498)
-    size_t coll_skip_thr = 1024;
-    size_t red_scat_ring_thr = 131072;
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)

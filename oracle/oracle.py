@@ -15,6 +15,31 @@ _PATH = os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 
+class Knobs(ctypes.Structure):
+    """MV2_* selection knobs (oknobs in mv2_oracle.c); default_knobs() = the reference defaults."""
+    _fields_ = [(f, ctypes.c_int) for f in (
+        "coll_skip_thr", "enable_skip_search", "allred_skip_small", "allred_skip_large",
+        "enable_topo", "use_topo_allreduce", "topo_allred_min", "topo_allred_max",
+        "use_topo_reduce", "topo_red_min", "topo_red_max", "tree_degree",
+        "allred_use_ring", "ring_ppn")] + [("ring_thr", ctypes.c_long), ("red_scat_ring_thr", ctypes.c_long)] + [
+        (f, ctypes.c_int) for f in ("smp_use_cma", "inter_k", "use_knomial_reduce", "shmem_intra_reduce_msg",
+                                    "shmem_coll_max_msg", "enable_shmem_allreduce", "enable_shmem_reduce")]
+
+
+# algorithm ids (include/mv2h.h mv2h_plan)
+ALGOS = ["none", "shmem_linear", "pt2pt_rs", "pt2pt_rd", "ring_wrapper", "topo_tree", "two_level_p2p",
+         "binomial", "knomial", "redscat_gather", "rs_ring", "rs_rec_halving", "rs_pairwise", "rs_basic",
+         "reduce_topo"]
+
+
+def default_knobs(**over):
+    k = Knobs()
+    lib().oracle_default_knobs(ctypes.byref(k))
+    for key, v in over.items():
+        setattr(k, key, v)
+    return k
+
+
 def build():
     subprocess.run(["make", "-C", _HERE, "-s"], check=True)
 
@@ -41,6 +66,15 @@ def lib():
         L.oracle_pack_segments.restype = None
         L.oracle_time_reduce_local.argtypes = [vp, vp, l, i, i, i]
         L.oracle_time_reduce_local.restype = ctypes.c_double
+        kp = ctypes.POINTER(Knobs)
+        L.oracle_default_knobs.argtypes = [kp]
+        L.oracle_default_knobs.restype = None
+        L.oracle_allreduce_select.argtypes = [i, l, i, i, i, kp]
+        L.oracle_allreduce_k.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, l, i, i, i, kp]
+        L.oracle_reduce_select.argtypes = [i, l, i, i, kp, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.oracle_reduce.argtypes = [ctypes.POINTER(vp), vp, i, l, i, i, i, i, kp, i]
+        L.oracle_reduce_scatter_select.argtypes = [i, ctypes.POINTER(l), i, kp]
+        L.oracle_reduce_scatter.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(l), vp, i, i, kp, i]
         _lib = L
     return _lib
 
@@ -105,4 +139,61 @@ def pack_segments(src, dst, count, extent, offs, lens, unpack=False):
 
 def unpack_strided(packed, dst, nblocks, blk, stride):
     lib().oracle_unpack_strided(packed.ctypes.data, dst.ctypes.data, nblocks, blk, stride)
+    return dst
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def allreduce_select(n, count, dtype_handle, in_place=False, opkind=0, knobs=None):
+    k = knobs if knobs is not None else default_knobs()
+    return lib().oracle_allreduce_select(n, count, dtype_handle, int(in_place), opkind, ctypes.byref(k))
+
+
+def allreduce_ref(sends, count, dtype_handle, op_handle, in_place=False, knobs=None):
+    """MPI_Allreduce as MVAPICH2 2.3.7 runs it on one node (selection + algorithm), per-rank results."""
+    n = len(sends)
+    k = knobs if knobs is not None else default_knobs()
+    recvs = [np.zeros_like(s) for s in sends]
+    rc = lib().oracle_allreduce_k(_ptrs(sends), _ptrs(recvs), n, count, dtype_handle, op_handle, int(in_place),
+                                  ctypes.byref(k))
+    if rc:
+        raise RuntimeError(f"oracle_allreduce_k rc={rc}")
+    return recvs
+
+
+def reduce_select(n, count, dtype_handle, opkind=0, knobs=None):
+    k = knobs if knobs is not None else default_knobs()
+    kf, r0 = ctypes.c_int(0), ctypes.c_int(0)
+    a = lib().oracle_reduce_select(n, count, dtype_handle, opkind, ctypes.byref(k), ctypes.byref(kf), ctypes.byref(r0))
+    return a, kf.value, r0.value
+
+
+def reduce_ref(sends, count, dtype_handle, op_handle, root, opkind=0, knobs=None, algo=-1):
+    """MPI_Reduce as MVAPICH2 2.3.7 runs it on one node: the root's result."""
+    k = knobs if knobs is not None else default_knobs()
+    out = np.zeros_like(sends[0])
+    rc = lib().oracle_reduce(_ptrs(sends), out.ctypes.data, len(sends), count, dtype_handle, op_handle, root, opkind,
+                             ctypes.byref(k), algo)
+    if rc:
+        raise RuntimeError(f"oracle_reduce rc={rc}")
+    return out
+
+
+def reduce_scatter_select(counts, dtype_handle, knobs=None):
+    k = knobs if knobs is not None else default_knobs()
+    n = len(counts)
+    return lib().oracle_reduce_scatter_select(n, (ctypes.c_long * n)(*counts), dtype_handle, ctypes.byref(k))
+
+
+def reduce_scatter_ref(srcs, counts, dtype_handle, op_handle, knobs=None, algo=-1):
+    """MPI_Reduce_scatter as MVAPICH2 2.3.7 runs it on one node: every rank's block, concatenated."""
+    k = knobs if knobs is not None else default_knobs()
+    n = len(srcs)
+    dst = np.zeros_like(srcs[0])
+    rc = lib().oracle_reduce_scatter(_ptrs(srcs), n, (ctypes.c_long * n)(*counts), dst.ctypes.data, dtype_handle,
+                                     op_handle, ctypes.byref(k), algo)
+    if rc:
+        raise RuntimeError(f"oracle_reduce_scatter rc={rc}")
     return dst

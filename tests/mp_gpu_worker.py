@@ -23,6 +23,68 @@ def inputs(case, rank):
     return rand_typed(case["type"], case["count"], rng, small=case.get("small", False))
 
 
+def big_case(L, case, rank, n):
+    """Full-size BASELINE configs, checked in the worker against closed forms (256 MiB results
+    are not shipped back): returns [number of wrong elements]."""
+    k = case["kind"]
+    F = TYPES["MPI_FLOAT"][0]
+    if k == "big_allreduce":  # configs[2]: osu_allreduce fp32 SUM 256 MiB, OMB-style exact pattern
+        cnt = case["count"]
+        i = np.arange(cnt, dtype=np.int64)
+        x = ((i % 100 + 1) * (rank + 1)).astype(np.float32)
+        sb, rb = m.DeviceBuffer.from_array(x), m.DeviceBuffer(cnt * 4)
+        assert L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, F, OPS["MPI_SUM"], WORLD) == 0
+        got = rb.download(np.float32, count=cnt)
+        want = ((i % 100 + 1) * (n * (n + 1) // 2)).astype(np.float32)
+        return np.array([np.count_nonzero(got != want)])
+    if k == "big_reduce_scatter":  # configs[3]: OMB recvcounts = size/n (+1 for the first size%n)
+        tot = case["count"]
+        counts = [tot // n + (1 if r < tot % n else 0) for r in range(n)]
+        off = sum(counts[:rank])
+        i = np.arange(tot, dtype=np.int64)
+        x = ((i % 100 + 1) * (rank + 1)).astype(np.float32)
+        sb, rb = m.DeviceBuffer.from_array(x), m.DeviceBuffer(counts[rank] * 4)
+        arr = (ctypes.c_int * n)(*counts)
+        assert L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, F, OPS["MPI_SUM"], WORLD) == 0
+        got = rb.download(np.float32, count=counts[rank])
+        j = np.arange(off, off + counts[rank], dtype=np.int64)
+        want = ((j % 100 + 1) * (n * (n + 1) // 2)).astype(np.float32)
+        return np.array([np.count_nonzero(got != want)])
+    if k == "big_allgather":  # configs[3]: MPI_CHAR, `per` bytes from every rank
+        per = case["count"]
+        C = TYPES["MPI_CHAR"][0]
+        x = ((np.arange(per, dtype=np.int64) * 7 + rank) & 0xFF).astype(np.uint8)
+        sb, rb = m.DeviceBuffer.from_array(x), m.DeviceBuffer(per * n)
+        assert L.MPI_Allgather(sb.ptr, per, C, rb.ptr, per, C, WORLD) == 0
+        got = rb.download(np.uint8, count=per * n).reshape(n, per)
+        bad = 0
+        for r in range(n):
+            bad += np.count_nonzero(got[r] != ((np.arange(per, dtype=np.int64) * 7 + r) & 0xFF).astype(np.uint8))
+        return np.array([bad])
+    if k == "big_bcast":  # configs[3]: MPI_CHAR from root 0
+        nbytes = case["count"]
+        C = TYPES["MPI_CHAR"][0]
+        want = ((np.arange(nbytes, dtype=np.int64) * 13 + 5) & 0xFF).astype(np.uint8)
+        b = m.DeviceBuffer.from_array(want if rank == 0 else np.zeros(nbytes, np.uint8))
+        assert L.MPI_Bcast(b.ptr, nbytes, C, 0, WORLD) == 0
+        return np.array([np.count_nonzero(b.download(np.uint8, count=nbytes) != want)])
+    if k == "big_maxloc":  # configs[4]: MAXLOC on MPI_DOUBLE_INT, value floor(U * 1000) (ties), loc = rank
+        cnt = case["count"]
+        dt = np.dtype([("value", "<f8"), ("loc", "<i4"), ("pad", "<i4")])
+        vals = [np.floor(np.random.default_rng(case["seed"] * 100 + r).uniform(0, 1, cnt) * 1000) for r in range(n)]
+        x = np.zeros(cnt, dt)
+        x["value"], x["loc"] = vals[rank], rank
+        D = TYPES["MPI_DOUBLE_INT"][0]
+        sb, rb = m.DeviceBuffer.from_array(x), m.DeviceBuffer(cnt * 16)
+        assert L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, D, OPS["MPI_MAXLOC"], WORLD) == 0
+        got = rb.download(np.uint8, count=cnt * 16).view(dt)
+        v = np.stack(vals)
+        mx = v.max(axis=0)
+        loc = np.argmax(v == mx[None, :], axis=0)  # ties -> the lowest rank
+        return np.array([np.count_nonzero((got["value"] != mx) | (got["loc"] != loc))])
+    raise ValueError(k)
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     out = sys.argv[2]
@@ -125,6 +187,37 @@ def main():
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=counts[rank] * 4)
             L.MPI_Op_free(ctypes.byref(op))
+        elif k == "user_vector_allreduce":
+            # configs[4]: commutative user op on MPI_Type_vector(nb, 4, 8, MPI_FLOAT) operands;
+            # fn(in, io) = 0.5 in + 1.5 io on the type map only; gap bytes must stay untouched
+            nb, cnt = case["nblocks"], count
+            vt = ctypes.c_int()
+            assert L.MPI_Type_vector(nb, 4, 8, TYPES["MPI_FLOAT"][0], ctypes.byref(vt)) == 0
+            assert L.MPI_Type_commit(ctypes.byref(vt)) == 0
+            ext_f = (nb - 1) * 8 + 4
+            elem = (np.arange(nb)[:, None] * 8 + np.arange(4)[None, :]).ravel()
+            FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(ctypes.c_int))
+
+            def uop(inp, io, ln, dt):
+                c = ln[0]
+                idx = (np.arange(c)[:, None] * ext_f + elem[None, :]).ravel()
+                a = np.ctypeslib.as_array((ctypes.c_float * (c * ext_f)).from_address(inp))
+                b = np.ctypeslib.as_array((ctypes.c_float * (c * ext_f)).from_address(io))
+                b[idx] = a[idx] * np.float32(0.5) + b[idx] * np.float32(1.5)
+            cb = FN(uop)
+            op = ctypes.c_int()
+            L.MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), 1, ctypes.byref(op))
+            x = np.random.default_rng(case["seed"] * 1000 + rank).standard_normal(cnt * ext_f).astype(np.float32)
+            sb = m.DeviceBuffer.from_array(x)
+            rb = m.DeviceBuffer.from_array(np.full(cnt * ext_f, -7.0, dtype=np.float32))
+            rc = L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, vt.value, op.value, WORLD)
+            assert rc == 0, (case["id"], rc)
+            res = rb.download(np.uint8, count=cnt * ext_f * 4)
+            L.MPI_Op_free(ctypes.byref(op))
+            L.MPI_Type_free(ctypes.byref(vt))
+        elif k.startswith("big_"):
+            res = big_case(L, case, rank, n)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)
             vt = ctypes.c_int()

@@ -1,9 +1,12 @@
-"""Part (2) parity: the device collectives, one process per rank, several
-ranks sharing the test box's single GPU (peers' arenas mapped through hipIpc
-exactly as across GPUs).  Results are compared bit-exactly with the oracle's
-simulation of the reference's algorithm for the same selection.  The "small"
-geometry forces 3 workgroups x 4 KiB per round, so large cases run dozens of
-rounds and reuse both arena parities within and across calls."""
+"""Part (2) parity: the device collectives, one process per rank.  Each rank
+takes GPU LOCAL_RANK % device_count, so on the 1-GPU test box all ranks share
+one card (peers' arenas mapped through hipIpc exactly as across GPUs) and on
+an 8-GPU node the same tests move every byte over xGMI.  Results are compared
+bit-exactly with the oracle's rank-by-rank simulation of the algorithm
+MVAPICH2 2.3.7 selects for the call (oracle.allreduce_ref / reduce_ref /
+reduce_scatter_ref; user ops: tests/ref_user.py).  The "small" geometry
+forces 3 workgroups x 4 KiB per round, so large cases run dozens of rounds and
+reuse both arena parities within and across calls."""
 import json
 import os
 import subprocess
@@ -15,6 +18,7 @@ import pytest
 
 from mvapich2_amd.consts import DEVICE_UNSUPPORTED, OPS, TYPES
 from oracle import oracle
+from tests import ref_user
 from tests.helpers import as_bytes, assert_bytes_equal, rand_typed
 
 pytestmark = pytest.mark.gpu
@@ -38,7 +42,8 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
-                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="30", MV2AMD_DEVICE="0", **(extra_env or {}))
+                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="30", **(extra_env or {}))
+        env.pop("MV2AMD_DEVICE", None)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), str(spec),
                                        str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
@@ -55,12 +60,18 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
     return lambda cid, r: np.load(out / f"{cid}_r{r}.npy")
 
 
-def expected_allreduce(case, n):
-    sends = [inputs(case, r) for r in range(n)]
-    # IN_PLACE: the ring wrapper runs pt2pt_rs; MPI_Reduce keeps the pt2pt_rs order at every size
-    algo = {"allreduce_inplace": 6, "reduce": 2}.get(case["kind"], -1)
-    return oracle.allreduce([s.copy() for s in sends], case["count"], TYPES[case["type"]][0], OPS[case["op"]],
-                            algo=algo)
+def expected_allreduce(case, n, knobs=None):
+    """MPI_Allreduce as the reference runs it (the nonblocking Iallreduce reduces in the blocking
+    call's order here: iallreduce_osu.c's NBC schedule orders are not restated, fp parity unpinned)"""
+    sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+    return oracle.allreduce_ref(sends, case["count"], TYPES[case["type"]][0], OPS[case["op"]],
+                                in_place=case["kind"] == "allreduce_inplace", knobs=knobs)
+
+
+def expected_reduce(case, n, knobs=None):
+    sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+    return oracle.reduce_ref(sends, case["count"], TYPES[case["type"]][0], OPS[case["op"]], case["root"],
+                             knobs=knobs)
 
 
 BASIC = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_FLOAT"), ("MPI_MIN", "MPI_DOUBLE"),
@@ -70,6 +81,7 @@ BASIC = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_F
 COUNTS = [1, 3, 100, 4099, 70001, 300007]  # one-shot (<=256 KiB) and pipelined sizes, ragged tails
 
 
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "default"), (4, "default"), (3, "small"), (4, "small"),
                                     (7, "small"), (8, "default")])
 def test_collectives_multiprocess(n, geom, tmp_path, golden):
@@ -90,10 +102,19 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
         cases.append({"id": f"ip{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
                       "count": count, "seed": seed})
         seed += 1
-    for count, root in ((5000, n - 1), (70001, 1), (300007, 0)):
-        cases.append({"id": f"rd{seed}", "kind": "reduce", "type": "MPI_DOUBLE", "op": "MPI_SUM", "count": count,
-                      "seed": seed, "root": root})
-        seed += 1
+    # MPI_Reduce: shmem (<= 1 KiB and 2 KiB), knomial (4 KiB, 16 KiB, 64 KiB), redscat_gather
+    # (8 KiB, >= 128 KiB), binomial (n = 2), at several roots; one-shot and pipelined sizes
+    for t, op in (("MPI_FLOAT", "MPI_SUM"), ("MPI_DOUBLE", "MPI_SUM"), ("MPI_FLOAT", "MPI_MAX")):
+        for count, root in ((100, n - 1), (512, 1 % n), (1024, 0), (2048, n - 1), (4096, 1 % n), (16384, 0),
+                            (32768, n // 2), (300007, 1 % n)):
+            if t == "MPI_DOUBLE":
+                count //= 2
+            cases.append({"id": f"rd{seed}", "kind": "reduce", "type": t, "op": op, "count": count,
+                          "seed": seed, "root": root})
+            seed += 1
+    cases.append({"id": f"rd{seed}", "kind": "reduce", "type": "MPI_DOUBLE_INT", "op": "MPI_MAXLOC",
+                  "count": 70001, "seed": seed, "root": n - 1})
+    seed += 1
     cases.append({"id": f"ar{seed}", "kind": "allreduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": 1 << 21,
                   "seed": seed})
     seed += 1
@@ -108,10 +129,13 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
                       "recvcounts": counts, "count": sum(counts), "seed": seed})
         seed += 1
-    # floating point: ring order above 128 KiB total (red_scat_osu.c:1869-1880), linear below
+    # floating point in every reduce-scatter algorithm (red_scat_osu.c:1859-1896): basic (<= 256 B),
+    # recursive halving (<= 16 KiB), pairwise (<= 64 KiB), ring (> 64 KiB)
     for t, op, counts in (("MPI_FLOAT", "MPI_SUM", [70001] * n), ("MPI_DOUBLE", "MPI_SUM", [20000 + r for r in range(n)]),
                           ("MPI_FLOAT", "MPI_MAX", [40000] * n), ("MPI_DOUBLE", "MPI_SUM", [100] * n),
-                          ("MPI_DOUBLE_INT", "MPI_MINLOC", [9000] * n)):
+                          ("MPI_DOUBLE_INT", "MPI_MINLOC", [9000] * n), ("MPI_FLOAT", "MPI_SUM", [4] * n),
+                          ("MPI_FLOAT", "MPI_SUM", [3000 // n + r for r in range(n)]),
+                          ("MPI_DOUBLE", "MPI_MAX", [6000 // n] * n), ("MPI_FLOAT", "MPI_SUM", [24000 // n] * n)):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": t, "op": op,
                       "recvcounts": counts, "count": sum(counts), "seed": seed})
         seed += 1
@@ -156,17 +180,14 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {case['op']} n={n} rank {r}")
         elif k == "reduce":
-            want = expected_allreduce(case, n)
+            want = expected_reduce(case, n)
             root = case["root"]
-            assert_bytes_equal(res(cid, root), want[root], t, case["count"], f"{cid} reduce")
+            assert_bytes_equal(res(cid, root), want, t, case["count"], f"{cid} reduce {t} {case['op']} "
+                               f"count={case['count']} root={root}")
         elif k == "reduce_scatter":
             counts = case["recvcounts"]
-            sends = [inputs(dict(case, count=sum(counts)), r) for r in range(n)]
-            if sum(counts) * TYPES[t][2] >= 131072:
-                full = oracle.reduce_scatter_ring(sends, counts, TYPES[t][0], OPS[case["op"]])
-            else:
-                full = oracle.reduce_linear(sends, sum(counts), TYPES[t][0], OPS[case["op"]])
-            full = as_bytes(full)
+            sends = [as_bytes(inputs(dict(case, count=sum(counts)), r)).copy() for r in range(n)]
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
             ext = TYPES[t][3]
             off = 0
             for r in range(n):
@@ -199,79 +220,29 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
                     assert np.all(got[:, 4:] == -1.0), "gap bytes of a vector type must not be written"
 
 
+def ufn(inp, io):
+    return (inp * 2 + io * 3).astype(np.int32)
+
+
 def user_allreduce_expected(n, count, commute):
-    """Reference order for user ops (allreduce_osu.c): commutative & <= 1 KB ->
-    two-level chain fn(x_i, acc); else recursive doubling with the
-    dst < rank operand swap (:824-845) and the non-pof2 fold (:734-777)."""
-    def fn(inp, io):
-        return (inp * 2 + io * 3).astype(np.int32)
+    """fn(in, io) = 2 in + 3 io in the order the reference takes for a user op (tests/ref_user.py)"""
     xs = [((np.arange(count) + r) % 7).astype(np.int32) for r in range(n)]
-    if commute and count * 4 <= 1024:
-        acc = xs[0].copy()
-        for i in range(1, n):
-            acc = fn(xs[i], acc)
-        return [acc] * n
-    pof2 = 1
-    while pof2 * 2 <= n:
-        pof2 *= 2
-    rem = n - pof2
-    rb = [x.copy() for x in xs]
-    newrank, real = [0] * n, [0] * pof2
-    for r in range(n):
-        if r < 2 * rem:
-            if r % 2 == 0:
-                newrank[r] = -1
-            else:
-                rb[r] = fn(xs[r - 1], rb[r])
-                newrank[r] = r // 2
-        else:
-            newrank[r] = r - rem
-        if newrank[r] >= 0:
-            real[newrank[r]] = r
-    mask = 1
-    while mask < pof2:
-        prev = [rb[real[nr]].copy() for nr in range(pof2)]
-        for nr in range(pof2):
-            r, dst = real[nr], real[nr ^ mask]
-            tmp = prev[nr ^ mask]
-            rb[r] = fn(tmp, rb[r]) if (commute or dst < r) else fn(rb[r], tmp)
-        mask <<= 1
-    for r in range(0, 2 * rem, 2):
-        rb[r] = rb[r + 1]
-    if commute and count * 4 >= (2 << 20) and count >= n:
-        # ring wrapper (allreduce_osu.c:3758-3818): chunk c = fn chain from rank c along the
-        # ring, received partial as inout; the remainder keeps the RD result above
-        cc = count // n
-        for c in range(n):
-            blk = slice(c * cc, (c + 1) * cc)
-            acc = xs[c][blk].copy()
-            for k in range(1, n):
-                acc = fn(xs[(c + k) % n][blk], acc)
-            for r in range(n):
-                rb[r] = rb[r].copy()
-                rb[r][blk] = acc
-    return rb
+    return ref_user.allreduce(xs, ufn, commute, TYPES["MPI_INT"][0], count)
 
 
 def user_reduce_scatter_expected(n, counts, commute):
-    """User-op reduce-scatter orders (mpi_api.cpp user_reduce_scatter): commutative and
-    >= 128 KiB total -> MPIR_Reduce_scatter_ring (red_scat_osu.c:1026-1180, own operand is
-    inout at every hop); otherwise x_0 op x_1 op ... op x_{n-1} right to left."""
-    def fn(inp, io):
-        return (inp * 2 + io * 3).astype(np.int32)
+    """commutative: MPIR_Reduce_scatter_MV2's choice (ref_user.reduce_scatter); non-commutative:
+    the canonical x_0 op (x_1 op (... op x_{n-1})) (mpi_api.cpp user_reduce_scatter)"""
     total = sum(counts)
     xs = [((np.arange(total) + r) % 7).astype(np.int32) for r in range(n)]
+    if commute:
+        return ref_user.reduce_scatter(xs, ufn, TYPES["MPI_INT"][0], counts)
     out, off = [], 0
     for b in range(n):
         blk = slice(off, off + counts[b])
-        if commute and total * 4 >= 131072:
-            acc = xs[(b + 1) % n][blk]
-            for k in range(2, n + 1):
-                acc = fn(acc, xs[(b + k) % n][blk])
-        else:
-            acc = xs[n - 1][blk]
-            for i in range(n - 2, -1, -1):
-                acc = fn(xs[i][blk], acc)
+        acc = xs[n - 1][blk]
+        for i in range(n - 2, -1, -1):
+            acc = ufn(xs[i][blk], acc)
         out.append(acc)
         off += counts[b]
     return out
@@ -279,36 +250,97 @@ def user_reduce_scatter_expected(n, counts, commute):
 
 KNOB_RUNS = [
     # MV2_ALLRED_USE_RING=0 (ch3_shmem_coll.c:2665-2670): >= 2 MiB stays in pt2pt_rs
-    ({"MV2_ALLRED_USE_RING": "0"}, [("MPI_FLOAT", "MPI_SUM", 524291, 2)]),
+    ({"MV2_ALLRED_USE_RING": "0"}, {"allred_use_ring": 0}, [("MPI_FLOAT", "MPI_SUM", 524291)]),
     # MV2_ALLREDUCE_RING_ALGO_THRESHOLD (:3094-3098, K/M suffixes): the ring wrapper from 64 KiB
-    ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "64K"}, [("MPI_FLOAT", "MPI_SUM", 70001, 4),
-                                                    ("MPI_DOUBLE", "MPI_MAX", 10007, 4)]),
-    # ring threshold 0: the small-message shortcut still wins up to 1 KiB (allreduce_osu.c:3155-3160),
-    # everything above takes the ring wrapper (301 elements: padded chunks at n = 2, a remainder)
-    ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "0"}, [("MPI_FLOAT", "MPI_SUM", 10, 1), ("MPI_FLOAT", "MPI_SUM", 301, 4)]),
-    # MV2_COLL_SKIP_TABLE_THRESHOLD=0: no two-level shortcut, small calls take pt2pt_rs / RD
-    ({"MV2_COLL_SKIP_TABLE_THRESHOLD": "0"}, [("MPI_FLOAT", "MPI_SUM", 10, 2), ("MPI_FLOAT", "MPI_SUM", 1, 2)]),
+    ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "64K"}, {"ring_thr": 65536},
+     [("MPI_FLOAT", "MPI_SUM", 70001), ("MPI_DOUBLE", "MPI_MAX", 10007)]),
+    # ring threshold 0: the topology-aware tree still wins up to 2 KiB (allreduce_osu.c:120-133)
+    ({"MV2_ALLREDUCE_RING_ALGO_THRESHOLD": "0"}, {"ring_thr": 0},
+     [("MPI_FLOAT", "MPI_SUM", 10), ("MPI_FLOAT", "MPI_SUM", 301), ("MPI_FLOAT", "MPI_SUM", 601)]),
+    # no topology-aware tree: two-level shmem up to 1 KiB, the tables above
+    ({"MV2_USE_TOPO_AWARE_ALLREDUCE": "0"}, {"use_topo_allreduce": 0},
+     [("MPI_FLOAT", "MPI_SUM", 10), ("MPI_DOUBLE", "MPI_SUM", 200), ("MPI_FLOAT", "MPI_SUM", 400)]),
+    # tree degree 2 (MV2_SHMEM_REDUCE_TREE_DEGREE)
+    ({"MV2_SHMEM_REDUCE_TREE_DEGREE": "2"}, {"tree_degree": 2}, [("MPI_FLOAT", "MPI_SUM", 77)]),
+    # MV2_COLL_SKIP_TABLE_THRESHOLD=0 and no tree: small calls take the tables (pt2pt_rs / RD / two-level)
+    ({"MV2_COLL_SKIP_TABLE_THRESHOLD": "0", "MV2_USE_TOPO_AWARE_ALLREDUCE": "0"},
+     {"coll_skip_thr": 0, "use_topo_allreduce": 0}, [("MPI_FLOAT", "MPI_SUM", 10), ("MPI_FLOAT", "MPI_SUM", 1)]),
 ]
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [2, 3, 5])
 def test_mv2_selection_knobs(n, tmp_path):
     """The reference's MV2_* selection knobs move the algorithm (and so the reduction-order)
-    boundaries; each run is checked bit-exactly against the oracle's algorithm for it."""
+    boundaries; each run is checked bit-exactly against the oracle with the same knobs."""
     seed = 900
-    for i, (env, specs) in enumerate(KNOB_RUNS):
+    for i, (env, kn, specs) in enumerate(KNOB_RUNS):
         cases = []
-        for t, op, count, algo in specs:
-            cases.append({"id": f"kn{seed}", "kind": "allreduce", "type": t, "op": op, "count": count,
-                          "seed": seed, "algo": algo})
+        for t, op, count in specs:
+            cases.append({"id": f"kn{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
+            seed += 1
+            cases.append({"id": f"kr{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
+                          "root": n - 1})
             seed += 1
         d = tmp_path / f"run{i}"
         d.mkdir()
         res = run_workers(n, cases, d, extra_env=env)
+        knobs = oracle.default_knobs(**kn)
         for case in cases:
-            sends = [inputs(case, r) for r in range(n)]
-            want = oracle.allreduce([s.copy() for s in sends], case["count"], TYPES[case["type"]][0],
-                                    OPS[case["op"]], algo=case["algo"])
-            for r in range(n):
-                assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"],
-                                   f"{case['id']} {env} rank {r}")
+            if case["kind"] == "allreduce":
+                want = expected_allreduce(case, n, knobs)
+                for r in range(n):
+                    assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"],
+                                       f"{case['id']} {env} rank {r}")
+            else:
+                want = expected_reduce(case, n, knobs)
+                assert_bytes_equal(res(case["id"], n - 1), want, case["type"], case["count"], f"{case['id']} {env}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_user_op_on_strided_vector_operand(n, tmp_path):
+    """configs[4]: MPI_Allreduce with a commutative user op on MPI_Type_vector(N, 4, 8, MPI_FLOAT)
+    operands (the reference rejects predefined ops on derived types).  The result follows the
+    reference's order for the call and only type-map bytes of recvbuf are written (gap bytes keep
+    their -7.0): MPIR_Localcopy / uop calls touch the type map only."""
+    cases = []
+    for seed, (nb, cnt) in enumerate(((64, 3), (1024, 40), (4096, 33)), start=700):
+        # 4096 x 16 B x 33 elements = 2.1 MiB: the ring wrapper with a remainder
+        cases.append({"id": f"uv{seed}", "kind": "user_vector_allreduce", "nblocks": nb, "count": cnt,
+                      "seed": seed})
+    res = run_workers(n, cases, tmp_path)
+    fn = lambda a, b: (a * np.float32(0.5) + b * np.float32(1.5)).astype(np.float32)
+    for case in cases:
+        nb, cnt = case["nblocks"], case["count"]
+        ext_f = (nb - 1) * 8 + 4
+        elem = (np.arange(nb)[:, None] * 8 + np.arange(4)[None, :]).ravel()
+        idx = (np.arange(cnt)[:, None] * ext_f + elem[None, :]).ravel()
+        packed = []
+        for r in range(n):
+            x = np.random.default_rng(case["seed"] * 1000 + r).standard_normal(cnt * ext_f).astype(np.float32)
+            packed.append(x[idx].reshape(cnt, nb * 4))
+        want = ref_user.allreduce(packed, fn, 1, None, cnt, nbytes=cnt * nb * 16)
+        gap = np.ones(cnt * ext_f, bool)
+        gap[idx] = False
+        for r in range(n):
+            got = res(case["id"], r).view(np.float32)
+            assert np.array_equal(got[idx].view(np.uint32), want[r].ravel().view(np.uint32)), (case["id"], r)
+            assert np.all(got[gap] == -7.0), f"{case['id']} rank {r}: gap bytes of the vector type were written"
+
+
+@pytest.mark.timeout(480)
+@pytest.mark.parametrize("n", [2, 8])
+def test_full_size_baseline_configs(n, tmp_path):
+    """BASELINE configs[2]-[4] at their full sizes: 256 MiB fp32 SUM allreduce, 256 MiB
+    reduce_scatter / allgather / bcast, 16 Mi-record MAXLOC on MPI_DOUBLE_INT; each rank checks
+    its whole result against closed forms."""
+    S = 256 << 20
+    cases = [{"id": "bg1", "kind": "big_allreduce", "count": S // 4, "seed": 1},
+             {"id": "bg2", "kind": "big_reduce_scatter", "count": S // 4, "seed": 2},
+             {"id": "bg3", "kind": "big_allgather", "count": S // n, "seed": 3},
+             {"id": "bg4", "kind": "big_bcast", "count": S, "seed": 4},
+             {"id": "bg5", "kind": "big_maxloc", "count": S // 16, "seed": 5}]
+    res = run_workers(n, cases, tmp_path, timeout=400)
+    for case in cases:
+        for r in range(n):
+            assert int(res(case["id"], r)[0]) == 0, (case["id"], r, int(res(case["id"], r)[0]))

@@ -81,3 +81,55 @@ def test_golden_allred_cases_through_device_tree(golden):
         else:
             got = reduce_n(srcs, c["type"], c["op"], count, 1, -1)
         assert_bytes_equal(got, sol, c["type"], count, c["id"])
+
+
+def reduce_n_prog(srcs, tname, op, count, ps):
+    bufs = [m.DeviceBuffer.from_array(s) for s in srcs]
+    ext = TYPES[tname][3]
+    dst = m.DeviceBuffer(count * ext)
+    arr = (ctypes.c_void_p * len(bufs))(*[b.ptr for b in bufs])
+    rc = m.lib().mv2h_reduce_n_prog(arr, len(bufs), dst.ptr, count, TYPES[tname][0], OPS[op], ctypes.byref(ps), None)
+    assert rc == 0, rc
+    return dst.download(np.uint8, count=count * ext)
+
+
+def progset(coll, n, h, **kw):
+    """the planner's raw program set (mv2h_plan) for one call"""
+    L = m.lib()
+    a, inner, unp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    ps = m.ProgSet()
+    counts = kw.pop("counts", None)
+    cz = (ctypes.c_size_t * n)(*counts) if counts else None
+    m.check(L.mv2h_plan(m.COLL[coll], n, kw.get("rank", 0), kw.get("root", 0), kw.get("count", 0), cz, h, 0, 0,
+                        ctypes.byref(a), ctypes.byref(inner), ctypes.byref(unp), ctypes.byref(ps)), "mv2h_plan")
+    return a.value, ps
+
+
+PROG_SEL = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_MAX", "MPI_FLOAT"), ("MPI_MIN", "MPI_DOUBLE"),
+            ("MPI_MAXLOC", "MPI_DOUBLE_INT"), ("MPI_PROD", "MPI_C_FLOAT_COMPLEX"), ("MPI_SUM", "MPI_C_DOUBLE_COMPLEX"),
+            ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_MINLOC", "MPI_SHORT_INT")]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 7, 8])
+def test_program_evaluator_matches_oracle(n):
+    """The device's program-order evaluator (prog_eval, kernels k_reduce_n / k_oneshot / k_pipe
+    <.., PROG>) on the planner's programs: MPI_Reduce at every algorithm of the selection and
+    root, the topology-aware allreduce tree, vs the oracle's rank-by-rank simulations."""
+    rng = np.random.default_rng(500 + n)
+    for op, t in PROG_SEL:
+        h, oh = TYPES[t][0], OPS[op]
+        size = TYPES[t][2]
+        for nbytes in (400, 1600, 4096, 8192, 16384, 65536, 300000):
+            count = max(1, nbytes // size)
+            srcs = [rand_typed(t, count, rng, small=op == "MPI_PROD") for _ in range(n)]
+            for root in sorted({0, n - 1}):
+                algo, ps = progset("reduce", n, h, count=count, root=root)
+                got = reduce_n_prog(srcs, t, op, count, ps)
+                want = oracle.reduce_ref([s.view(np.uint8).ravel().copy() for s in srcs], count, h, oh, root)
+                assert_bytes_equal(got, want, t, count, f"reduce n={n} {t} {op} count={count} root={root} "
+                                                        f"algo={oracle.ALGOS[algo]}")
+            if nbytes <= 2048:
+                algo, ps = progset("allreduce", n, h, count=count)
+                want = oracle.allreduce_ref([s.view(np.uint8).ravel().copy() for s in srcs], count, h, oh)[0]
+                assert_bytes_equal(reduce_n_prog(srcs, t, op, count, ps), want, t, count,
+                                   f"allreduce n={n} {t} {op} count={count} algo={oracle.ALGOS[algo]}")

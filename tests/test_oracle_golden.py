@@ -56,3 +56,48 @@ def test_oracle_algorithms_agree_on_exact_cases(golden):
                                     c["op_handle"], algo)
             for r in range(c["n"]):
                 assert_bytes_equal(outs[r], sol, c["type"], c["count"], f"{c['id']} algo {algo}")
+
+
+def test_round2_algorithms_reproduce_known_answers(golden):
+    """Every restated algorithm of the one-node selection (topology-aware tree, binomial,
+    knomial, redscat_gather, shmem reduce, reduce-scatter ring / recursive halving / pairwise /
+    basic) reproduces the reference tests' known answers (allred.c, redscat.c)."""
+    cases, arrs = golden
+    seen = set()
+    for c in cases:
+        if c["family"] != "allred":
+            continue
+        ins = arrs[c["id"] + "__in"]
+        sol = arrs[c["id"] + "__sol"]
+        n, count, th, oh, t = c["n"], c["count"], c["type_handle"], c["op_handle"], c["type"]
+        sends = [ins[r].copy() for r in range(n)]
+        # the reference selection (topology-aware tree at these sizes), in place or not
+        for ip in (False, True):
+            outs = oracle.allreduce_ref([s.copy() for s in sends], count, th, oh, in_place=ip)
+            for r in range(n):
+                assert_bytes_equal(outs[r], sol, t, count, f"{c['id']} allreduce_ref rank {r}")
+        # MPI_Reduce in every algorithm and at every root
+        for algo in (1, 7, 8, 9, 14):
+            if algo == 9 and count < 4:
+                continue
+            for root in range(n):
+                out = oracle.reduce_ref([s.copy() for s in sends], count, th, oh, root, algo=algo)
+                assert_bytes_equal(out, sol, t, count, f"{c['id']} reduce algo {algo} root {root}")
+                seen.add(algo)
+        # reduce-scatter of the same operands, equal blocks, every algorithm
+        if count % n == 0 and c["op"] != "MPI_REPLACE":
+            counts = [count // n] * n
+            for algo in (10, 11, 12, 13):
+                full = oracle.reduce_scatter_ref([s.copy() for s in sends], counts, th, oh, algo=algo)
+                assert_bytes_equal(full, sol, t, count, f"{c['id']} reduce_scatter algo {algo}")
+                seen.add(algo)
+    assert seen >= {1, 7, 8, 9, 14, 10, 11, 12, 13}
+    for c in cases:
+        if c["family"] == "redscat":
+            ins = arrs[c["id"] + "__in"]
+            sol = arrs[c["id"] + "__sol"]
+            n = c["n"]
+            for algo in (-1, 10, 11, 12, 13):
+                full = oracle.reduce_scatter_ref([ins[r].copy() for r in range(n)], [c["count"] // n] * n,
+                                                 c["type_handle"], c["op_handle"], algo=algo)
+                assert np.array_equal(full.view(np.int32), sol.view(np.int32)), (c["id"], algo)
