@@ -148,13 +148,16 @@ def bench_n1(args, L):
         m.check(L.MPI_Reduce_local(hx.ctypes.data, hy.ctypes.data, count, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]), "host")
     extra["MPI_FLOAT:MPI_SUM host buffers (PCIe-inclusive)"] = {"GB/s_call": round(3 * S_BYTES * 3 / (time.perf_counter() - t0) / 1e9, 2)}
     del hx, hy
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_reduce_local_r01i.json")
-    if os.path.exists(tfile):
+    # HBM traffic of this kernel from the newest committed PMC pass (rocprofv3 FETCH_SIZE x2 +
+    # WRITE_SIZE in separate passes, tools/pmc_summary.py); the file is named in the line
+    traffic, tsrc = None, None
+    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.startswith("pmc_reduce_local_"))
+    if cands:
+        tsrc = os.path.join("profiles", cands[-1])
         try:
-            traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
+            traffic = json.load(open(os.path.join(ROOT, tsrc))).get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            traffic, tsrc = None, None
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
@@ -163,7 +166,7 @@ def bench_n1(args, L):
                    "count": count, "bytes_per_operand": S_BYTES, "algorithmic_bytes_per_call": alg_bytes,
                    "api": "MPI_Reduce_local via libmpi.so (MPICH ABI)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic, "traffic_source": tsrc,
                      "kernel": "k_reduce_local<R<SUM,F32>,2>", "kernel_ms": round(kern_s * 1e3, 4)},
         "cpu_baseline": cpu_baseline_reduce_local(args.cpu_seconds) if args.cpu_seconds > 0 else None,
         "extra": extra,
@@ -369,6 +372,7 @@ def bench_nranks(args, L, rank, size):
     busbw = 2.0 * f * S_BYTES / step_s / 1e9
     kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
     peak_all = (size - 1) * XGMI_LINK
+    nshare = m.info("nshare")  # ranks sharing one GPU (test rehearsals): no xGMI byte moves then
 
     def line4(t, k, bytes_bus):
         return {"busbw_GBps": round(bytes_bus / t / 1e9, 2), "kernel_busbw_GBps": round(bytes_bus / (k / 1e3) / 1e9, 2),
@@ -396,10 +400,14 @@ def bench_nranks(args, L, rank, size):
                    "count": count, "bytes": S_BYTES, "algorithm": "pipelined direct RS+AG (pushes into peer arenas over xGMI)",
                    "latency_8B_us": round(lat_s * 1e6, 2), "latency_8B_kernel_us": round(lat_k_ms * 1e3, 2),
                    "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing"},
-        "roofline": {"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
-                     "frac": round(kbus / peak_all, 4), "traffic": None,
-                     "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
-                     "kernel_ms": round(kms, 4)},
+        "roofline": ({"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
+                      "frac": round(kbus / peak_all, 4), "traffic": None,
+                      "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
+                      "kernel_ms": round(kms, 4)} if nshare == 1 else
+                     {"bound": "shared-gpu", "achieved": round(kbus, 1), "peak": None, "unit": "GB/s", "frac": None,
+                      "traffic": None, "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)", "kernel_ms": round(kms, 4),
+                      "note": f"{nshare} ranks share one GPU: every 'remote' store lands in the same HBM, no xGMI "
+                              "link is used, so no xGMI roofline fraction applies"}),
         "cpu_baseline": None,
         "extra": extra,
     }

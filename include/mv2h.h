@@ -165,6 +165,8 @@ int mv2h_local_rank(void);
 int mv2h_timing_enable(int on);
 double mv2h_last_kernel_ms(void);
 int mv2h_set_tuning(const char *key, long value);
+/* runtime facts: "nshare" (most ranks sharing one GPU), "device", "cus", "light_release", "oneshot_max" */
+int mv2h_get_info(const char *key, long *value);
 
 #ifdef __cplusplus
 }

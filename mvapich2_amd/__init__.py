@@ -70,6 +70,7 @@ def lib():
         "mv2h_plan": ([c_int, c_int, c_int, c_int, c_sz, ctypes.POINTER(c_sz), c_int, c_int, c_int,
                        ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_vp], c_int),
         "mv2h_knobs_reload": ([], c_int),
+        "mv2h_get_info": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_long)], c_int),
         "mv2h_reduce_n_prog": ([ctypes.POINTER(c_vp), c_int, c_vp, c_sz, c_int, c_int, c_vp, c_vp], c_int),
         "MPI_Init": ([c_vp, c_vp], c_int),
         "MPI_Finalize": ([], c_int),
@@ -225,3 +226,9 @@ def plan(coll, n, rank, dtype_handle, count=0, counts=None, root=0, opkind=0, in
 
 def knobs_reload():
     check(lib().mv2h_knobs_reload(), "mv2h_knobs_reload")
+
+
+def info(key):
+    v = ctypes.c_long()
+    check(lib().mv2h_get_info(key.encode(), ctypes.byref(v)), f"mv2h_get_info({key})")
+    return v.value

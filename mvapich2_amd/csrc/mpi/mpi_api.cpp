@@ -105,6 +105,82 @@ int copy_from_host(void *p, const std::vector<char> &h, size_t bytes) {
     return 0;
 }
 
+// ---- x87 80-bit long double (MPI_LONG_DOUBLE, MPI_C_LONG_DOUBLE_COMPLEX,
+// MPI_LONG_DOUBLE_INT): gfx950 has no 80-bit float, so these builtin ops run
+// on the host, as the reference's own loops do (oputil.h:316-349,
+// opmaxloc.c:65-87), through the same algorithm plans as user ops.  Only
+// these three types take this path; every other builtin type is reduced on
+// the GPU and has no host path.
+int g_ld_op = -1;  // op index of the current x87 call (set under the global critical section)
+
+template <class T>
+inline T x_max(T a, T b) { return (a != a && b != b) ? a : (a != a) ? b : (b != b) ? a : ((b > a) ? b : a); }
+template <class T>
+inline T x_min(T a, T b) { return (a != a && b != b) ? a : (a != a) ? b : (b != b) ? a : ((a > b) ? b : a); }
+
+struct LdInt {
+    long double value;
+    int loc;
+};
+
+void ld_uop(void *in, void *inout, int *len, MPI_Datatype *dt) {
+    const long n = *len;
+    const int op = g_ld_op;
+    if (*dt == MPI_LONG_DOUBLE) {
+        const long double *b = (const long double *)in;
+        long double *a = (long double *)inout;
+        for (long i = 0; i < n; ++i) {
+            switch (op) {
+            case OP_SUM: a[i] = a[i] + b[i]; break;
+            case OP_PROD: a[i] = a[i] * b[i]; break;
+            case OP_MAX: a[i] = x_max(a[i], b[i]); break;
+            case OP_MIN: a[i] = x_min(a[i], b[i]); break;
+            case OP_LAND: a[i] = (a[i] && b[i]); break;
+            case OP_LOR: a[i] = (a[i] || b[i]); break;
+            case OP_LXOR: a[i] = ((a[i] && !b[i]) || (!a[i] && b[i])); break;
+            case OP_REPLACE: a[i] = b[i]; break;
+            default: break;
+            }
+        }
+    } else if (*dt == MPI_C_LONG_DOUBLE_COMPLEX) {
+        const __complex__ long double *b = (const __complex__ long double *)in;
+        __complex__ long double *a = (__complex__ long double *)inout;
+        for (long i = 0; i < n; ++i) {
+            if (op == OP_SUM) a[i] = a[i] + b[i];
+            else if (op == OP_PROD) a[i] = a[i] * b[i];  // Annex G __mulxc3, like the reference's C99 loop
+            else if (op == OP_REPLACE) a[i] = b[i];
+        }
+    } else if (*dt == MPI_LONG_DOUBLE_INT) {
+        const LdInt *b = (const LdInt *)in;
+        LdInt *a = (LdInt *)inout;
+        for (long i = 0; i < n; ++i) {
+            if (op == OP_REPLACE) {
+                memcpy(&a[i].value, &b[i].value, 10);
+                a[i].loc = b[i].loc;
+                continue;
+            }
+            if (op != OP_MAXLOC && op != OP_MINLOC) continue;
+            const long double av = a[i].value, bv = b[i].value;
+            if (av != av && bv != bv) {
+                a[i].loc = std::min(a[i].loc, b[i].loc);
+            } else if (av != av) {
+                a[i].value = bv;
+                a[i].loc = b[i].loc;
+            } else if (bv != bv) {
+            } else if (op == OP_MAXLOC ? av < bv : av > bv) {
+                a[i].value = bv;
+                a[i].loc = b[i].loc;
+            } else if (op == OP_MAXLOC ? av <= bv : av >= bv) {
+                a[i].loc = std::min(a[i].loc, b[i].loc);
+            }
+        }
+    }
+}
+
+bool is_x87(MPI_Datatype dt) {
+    return dt == MPI_LONG_DOUBLE || dt == MPI_C_LONG_DOUBLE_COMPLEX || dt == MPI_LONG_DOUBLE_INT;
+}
+
 int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, UserOp *u) {
     long span = dtype_span(dt, count);
     if (span < 0) return MPI_ERR_TYPE;
@@ -160,7 +236,7 @@ void eval_plan(const ProgSet &ps, std::vector<char> &W, long span, long e_begin,
     }
 }
 
-int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u) {
+int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
     World &w = world();
     const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
     if (span < 0) return MPI_ERR_TYPE;
@@ -170,7 +246,6 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
     int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
     if (rc) return rc;
     if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
-    const int opk = u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM;
     Plan p;
     if (n == 1) {
         dtype_merge_typemap(result.data(), W.data(), dt, count);
@@ -196,7 +271,7 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
 
 // MPI_Reduce with a user op: the root evaluates the plan of
 // MPIR_Reduce_index_tuned_intra_MV2 (binomial / knomial / shmem / ...)
-int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root) {
+int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
     World &w = world();
     const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
     if (span < 0) return MPI_ERR_TYPE;
@@ -210,8 +285,7 @@ int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
     if (n == 1) {
         dtype_merge_typemap(result.data(), W.data(), dt, count);
     } else {
-        if ((rc = plan_reduce(n, me, root, (size_t)count, (int)tsize, (int)extent, &p,
-                              u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM)))
+        if ((rc = plan_reduce(n, me, root, (size_t)count, (int)tsize, (int)extent, &p, opk)))
             return rc;
         eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
     }
@@ -230,7 +304,7 @@ namespace {
 // (MPIR_Reduce_scatter_non_comm_MV2, not restated): the canonical rank order
 // x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
 // associative op, applied as fn(in = x_i, inout = acc).
-int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u) {
+int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
     World &w = world();
     const int n = w.size, me = w.rank;
     const long extent = dtype_extent(dt), tsize = dtype_size(dt);
@@ -251,9 +325,9 @@ int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     if (c == 0) return MPI_SUCCESS;
     const long bspan = dtype_span(dt, c);
     if (copy_to_host(result, recvbuf, bspan)) return MPI_ERR_OTHER;
-    if (u->commute) {
+    if (opk != OPK_USER_NONCOMM) {
         Plan p;
-        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)tsize, (int)extent, &p, OPK_USER_COMM))) return rc;
+        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)tsize, (int)extent, &p, opk))) return rc;
         eval_plan(p.ps, W, span, disp, disp + c, dt, extent, u, result.data());
     } else {
         auto X = [&](int r) { return W.data() + (size_t)r * span + (size_t)disp * extent; };
@@ -437,6 +511,12 @@ int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype
     if (inbuf == MPI_IN_PLACE || inoutbuf == MPI_IN_PLACE) return err_return(MPI_COMM_WORLD, MPI_ERR_BUFFER, fn);
     if (UserOp *u = user_op(op)) return err_return(MPI_COMM_WORLD, user_reduce_local(inbuf, inoutbuf, count, dt, u), fn);
     if (!dtype_is_builtin(dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
+    if (is_x87(dt)) {
+        if (mv2h_op_check(op, dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
+        UserOp x{ld_uop, 1, true};
+        g_ld_op = op_index(op);
+        return err_return(MPI_COMM_WORLD, op_index(op) == OP_NO_OP ? 0 : user_reduce_local(inbuf, inoutbuf, count, dt, &x), fn);
+    }
     return err_return(MPI_COMM_WORLD, mv2h_reduce_local(inbuf, inoutbuf, (size_t)count, dt, op, nullptr), fn);
 }
 int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype dt, MPI_Op op) WEAK(MPI_Reduce_local);
@@ -465,7 +545,13 @@ int PMPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
         }
         return err_return(comm, rc, fn);
     }
-    if (UserOp *u = user_op(op)) return err_return(comm, user_allreduce(sendbuf, recvbuf, count, dt, u), fn);
+    if (UserOp *u = user_op(op))
+        return err_return(comm, user_allreduce(sendbuf, recvbuf, count, dt, u, u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM), fn);
+    if (is_x87(dt) && op_index(op) < OP_REPLACE) {
+        UserOp x{ld_uop, 1, true};
+        g_ld_op = op_index(op);
+        return err_return(comm, user_allreduce(sendbuf, recvbuf, count, dt, &x, OPK_BUILTIN), fn);
+    }
     rc = mv2h_allreduce(sendbuf, recvbuf, (size_t)count, dt, op, nullptr);
     return err_return(comm, rc, fn);
 }
@@ -486,7 +572,13 @@ int PMPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
         }
         return err_return(comm, rc, fn);
     }
-    if (UserOp *u = user_op(op)) return err_return(comm, user_reduce(sendbuf, recvbuf, count, dt, u, root), fn);
+    if (UserOp *u = user_op(op))
+        return err_return(comm, user_reduce(sendbuf, recvbuf, count, dt, u, root, u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM), fn);
+    if (is_x87(dt) && op_index(op) < OP_REPLACE) {
+        UserOp x{ld_uop, 1, true};
+        g_ld_op = op_index(op);
+        return err_return(comm, user_reduce(sendbuf, recvbuf, count, dt, &x, root, OPK_BUILTIN), fn);
+    }
     rc = mv2h_reduce(sendbuf, recvbuf, (size_t)count, dt, op, root, nullptr);
     return err_return(comm, rc, fn);
 }
@@ -508,7 +600,14 @@ int PMPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts
     }
     if (total == 0) return MPI_SUCCESS;
     if (UserOp *u = user_op(op))
-        if (comm != MPI_COMM_SELF) return err_return(comm, user_reduce_scatter(sendbuf, recvbuf, recvcounts, dt, u), fn);
+        if (comm != MPI_COMM_SELF)
+            return err_return(comm, user_reduce_scatter(sendbuf, recvbuf, recvcounts, dt, u,
+                                                        u->commute ? OPK_USER_COMM : OPK_USER_NONCOMM), fn);
+    if (is_x87(dt) && comm != MPI_COMM_SELF && op_index(op) < OP_REPLACE) {
+        UserOp x{ld_uop, 1, true};
+        g_ld_op = op_index(op);
+        return err_return(comm, user_reduce_scatter(sendbuf, recvbuf, recvcounts, dt, &x, OPK_BUILTIN), fn);
+    }
     if (comm == MPI_COMM_SELF) {
         if (sendbuf != MPI_IN_PLACE)
             rc = mv2h_memcpy_dtod(recvbuf, sendbuf, dtype_span(dt, recvcounts[0]));

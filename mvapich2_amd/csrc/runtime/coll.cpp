@@ -431,6 +431,18 @@ int mv2h_set_tuning(const char *key, long value) {
     return 0;
 }
 
+int mv2h_get_info(const char *key, long *value) {
+    World &w = world();
+    if (!key || !value) return E_ARG;
+    if (!strcmp(key, "nshare")) *value = w.nshare;
+    else if (!strcmp(key, "device")) *value = w.device;
+    else if (!strcmp(key, "cus")) *value = w.cus;
+    else if (!strcmp(key, "light_release")) *value = w.light_release;
+    else if (!strcmp(key, "oneshot_max")) *value = (long)w.oneshot_max;
+    else return E_ARG;
+    return 0;
+}
+
 int mv2h_init(void) { return world_init(); }
 int mv2h_finalize(void) { return world_finalize(); }
 int mv2h_rank(void) { return world().rank; }

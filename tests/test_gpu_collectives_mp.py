@@ -55,8 +55,9 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    for r, p in enumerate(procs):
-        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
+    bad = [r for r, p in enumerate(procs) if p.returncode != 0]
+    assert not bad, "ranks " + ", ".join(f"{r} (rc {procs[r].returncode})" for r in bad) + " failed:\n" + \
+        "\n".join(f"--- rank {r}:\n{logs[r][-2000:]}" for r in range(n))
     return lambda cid, r: np.load(out / f"{cid}_r{r}.npy")
 
 
