@@ -90,6 +90,18 @@ struct LaunchCfg {
     Done done{};      // completion word (reduce_local)
 };
 
+// Grid cap for `per_cu` blocks per CU when `nshare` ranks share the GPU.
+// Blocks are dealt round-robin over the 8 XCDs from an XCD that is not fixed
+// (MI355X_MICROARCH.md, Workgroup dispatch), so a grid g puts up to ceil(g/8)
+// blocks on one XCD; with nshare spinning kernels every XCD must hold nshare of
+// those.  The cap is therefore 8 * floor(per_cu * cus_per_xcd / nshare): 256
+// at nshare 1, 48 (not 51) at 5 ranks, where 51-block grids could deadlock.
+inline int xcd_fair_cap(int per_cu, int cus, int nshare) {
+    const int xcds = (cus >= 64 && cus % 8 == 0) ? 8 : 1;
+    const int per_xcd = per_cu * (cus / xcds) / (nshare > 0 ? nshare : 1);
+    return (per_xcd < 1 ? 1 : per_xcd) * xcds;
+}
+
 // Workgroups that are guaranteed co-resident for a kernel (the per-workgroup
 // cross-GPU flags need block b of every rank running together).  The
 // occupancy API can over-report by one block per CU (MI355X_MICROARCH.md,
@@ -98,8 +110,7 @@ inline int resident_grid(const void *kernel, const LaunchCfg &cfg) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kThreads, 0) != hipSuccess || nb < 1) nb = 1;
     nb = nb > 1 ? nb - 1 : 1;
-    int cap = nb * cfg.cus / (cfg.nshare > 0 ? cfg.nshare : 1);
-    return cap < 1 ? 1 : cap;
+    return xcd_fair_cap(nb, cfg.cus, cfg.nshare);
 }
 
 // all return an MPI error class (0 = launched)

@@ -237,7 +237,7 @@ struct PipeGeom {
 // tuning knobs), so block b of every rank handles the same bytes.
 static PipeGeom pipe_geom(size_t maxlen) {
     World &w = world();
-    int cap = std::min(kPipeMaxGrid, std::max(1, w.cus / std::max(1, w.nshare)));
+    int cap = std::min(kPipeMaxGrid, xcd_fair_cap(1, w.cus, w.nshare));  // k_pipe: one block per CU
     cap = std::min(cap, std::max(1, w.pipe_grid));
     const size_t kMinSub = (size_t)16 << 10;
     PipeGeom g{};

@@ -11,6 +11,10 @@ def data_mask(type_name, count):
     """Bytes that carry data (pair padding excluded)."""
     handle, desc, size, ext = TYPES[type_name]
     m = np.ones(count * ext, dtype=bool)
+    if type_name == "MPI_LONG_DOUBLE":  # x87: 10 value bytes in a 16-byte slot
+        m = m.reshape(count, ext)
+        m[:, 10:] = False
+        return m.ravel()
     if size != ext:
         m = m.reshape(count, ext)
         if type_name == "MPI_SHORT_INT":

@@ -126,6 +126,15 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
                                ("allreduce_inplace", "MPI_FLOAT", "MPI_SUM", 524291)):
         cases.append({"id": f"rg{seed}", "kind": kind, "type": t, "op": op, "count": count, "seed": seed})
         seed += 1
+    # x87 long double: reduced on the host in 80-bit (mpi_api.cpp ld_uop) in the reference's order
+    for kind, op, count in (("allreduce", "MPI_SUM", 100), ("allreduce", "MPI_SUM", 70001),
+                            ("allreduce", "MPI_MAX", 1000), ("reduce", "MPI_SUM", 30001)):
+        cases.append({"id": f"x8{seed}", "kind": kind, "type": "MPI_LONG_DOUBLE", "op": op, "count": count,
+                      "seed": seed, "root": n - 1})
+        seed += 1
+    cases.append({"id": f"x8{seed}", "kind": "reduce_scatter", "type": "MPI_LONG_DOUBLE", "op": "MPI_SUM",
+                  "recvcounts": [5000 + r for r in range(n)], "count": sum(5000 + r for r in range(n)), "seed": seed})
+    seed += 1
     for counts in ([1] * n, [1000 + r for r in range(n)], [70001] * n, [65536] * n, [0] + [33] * (n - 1)):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
                       "recvcounts": counts, "count": sum(counts), "seed": seed})

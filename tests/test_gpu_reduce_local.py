@@ -72,7 +72,18 @@ def test_errors_are_mpi_classes():
     assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, TYPES["MPI_INT"][0], OPS["MPI_MAXLOC"]) == 9
     assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, 0x1234, OPS["MPI_SUM"]) == 3    # MPI_ERR_TYPE
     assert L.MPI_Reduce_local(a.ptr, b.ptr, -1, TYPES["MPI_INT"][0], OPS["MPI_SUM"]) == 2
-    assert L.MPI_Reduce_local(a.ptr, b.ptr, 1, TYPES["MPI_LONG_DOUBLE"][0], OPS["MPI_SUM"]) == 3
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 1, TYPES["MPI_LONG_DOUBLE"][0], OPS["MPI_BAND"]) == 9
+
+
+def test_x87_long_double_device_buffers():
+    """MPI_LONG_DOUBLE has no gfx950 representation: device operands are staged through the
+    host and reduced there in 80-bit x87 (mpi_api.cpp ld_uop), not rejected."""
+    L = m.lib()
+    x = (np.arange(100, dtype=np.longdouble) / 3).astype(np.longdouble)
+    y = np.full(100, np.longdouble(1) / 7, dtype=np.longdouble)
+    a, b = m.DeviceBuffer.from_array(x), m.DeviceBuffer.from_array(y)
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 100, TYPES["MPI_LONG_DOUBLE"][0], OPS["MPI_SUM"]) == 0
+    assert np.array_equal(b.download(np.longdouble), x + y)
 
 
 def test_host_buffers_are_reduced_on_the_gpu():
