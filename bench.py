@@ -387,7 +387,9 @@ def bench_nranks(args, L, rank, size):
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
     del sb, rb, rsb
-    if args.rccl:
+    if args.rccl and m.info("nshare") > 1:
+        extra["rccl_comparator"] = {"skipped": "ranks share one GPU: RCCL refuses several ranks on one device"}
+    elif args.rccl:
         try:
             extra["rccl_comparator"] = rccl_comparator(L, world, rank, size, max(5, args.steps // 2))
         except Exception as e:  # comparator only: never fail the bench line on it

@@ -1,7 +1,8 @@
 """Short program for rocprofv3 passes over the device pack / unpack kernels on
 BASELINE configs[4]'s strided operand: MPI_Type_vector(N, 4, 8, MPI_FLOAT)
 with N = 8 Mi blocks (256 MiB strided span, 128 MiB packed), six MPI_Pack and
-six MPI_Unpack calls.  Algorithmic HBM bytes per call = 2 x packed bytes."""
+six MPI_Unpack calls (PMC_MODE=pack or unpack: only those).  Algorithmic HBM
+bytes per call = 2 x packed bytes."""
 import ctypes
 import os
 import sys
@@ -23,10 +24,11 @@ packed = nb * 16
 src = m.DeviceBuffer(span)
 src.upload(np.random.default_rng(1).standard_normal(span // 4).astype(np.float32))
 dst = m.DeviceBuffer(packed)
-for _ in range(6):
+mode = os.environ.get("PMC_MODE", "both")
+for _ in range(6 if mode in ("both", "pack") else 0):
     pos = ctypes.c_int(0)
     m.check(L.MPI_Pack(src.ptr, 1, vt.value, dst.ptr, packed, ctypes.byref(pos), 0x44000000), "MPI_Pack")
-for _ in range(6):
+for _ in range(6 if mode in ("both", "unpack") else 0):
     pos = ctypes.c_int(0)
     m.check(L.MPI_Unpack(dst.ptr, packed, ctypes.byref(pos), src.ptr, 1, vt.value, 0x44000000), "MPI_Unpack")
 L.mv2h_device_synchronize()

@@ -19,8 +19,11 @@ def per_kernel(path, counter, match):
 def main():
     fetch_csv, write_csv, match, out = sys.argv[1:5]
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    last = int(sys.argv[6]) if len(sys.argv) > 6 else 0  # keep only the last N launches (skip init self-tests)
     f = per_kernel(fetch_csv, "FETCH_SIZE", match)
     w = per_kernel(write_csv, "WRITE_SIZE", match)
+    if last:
+        f, w = f[-last:], w[-last:]
     fetch_b = 2.0 * 1024 * sum(f) / len(f)
     write_b = 1024 * sum(w) / len(w)
     res = {"kernel_match": match, "launches_fetch": len(f), "launches_write": len(w),
