@@ -271,12 +271,13 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
         }
     }
     signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
-    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout)) return;
-    // phase B: reduce the n slots (own data straight from sendbuf)
+    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout, a.light != 0)) return;
+    // phase B: reduce the n slots (own data straight from sendbuf; arena slots with
+    // non-temporal loads, which the light acquire relies on)
     auto load = [&](size_t i, v4u (&v)[kMaxRanks]) {
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)
-            v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ((const v4u *)(a.arena_own + (size_t)j * a.slot_bytes))[i];
+            v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ld_nt((const v4u *)(a.arena_own + (size_t)j * a.slot_bytes) + i);
     };
     if constexpr (PROG) {
         // program order: the block of a range that lies in one block is fixed once
@@ -309,7 +310,8 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
             T col[kMaxRanks];
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
-                col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e] : ((const T *)(a.arena_own + (size_t)j * a.slot_bytes))[e];
+                col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e]
+                                                 : ld_nt_elem((const T *)(a.arena_own + (size_t)j * a.slot_bytes) + e);
             if constexpr (PROG) ((T *)a.recv)[e] = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, e)]);
             else ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
         }

@@ -146,7 +146,7 @@ __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) {
             const size_t o = (jb.len[j] & ~(size_t)15) + threadIdx.x;
-            if (o < jb.len[j]) jb.dst[j][o] = jb.src[j][o];
+            if (o < jb.len[j]) jb.dst[j][o] = __builtin_nontemporal_load(jb.src[j] + o);
         }
     }
 }
@@ -191,7 +191,7 @@ __device__ __forceinline__ void blk_copy_multi(const Dsts &d, const char *src, s
     const size_t tb = nbytes & 15;
     if (threadIdx.x < tb) {
         const size_t o = (nv << 4) + threadIdx.x;
-        const char c = src[o];
+        const char c = __builtin_nontemporal_load(src + o);
 #pragma unroll
         for (int k = 0; k < kMaxRanks + 1; ++k)
             if (d.p[k]) d.p[k][o] = c;
@@ -201,7 +201,9 @@ __device__ __forceinline__ void blk_copy_multi(const Dsts &d, const char *src, s
 // Block-wide n-source reduction of nbytes (whole elements) into every
 // non-null destination.  src[j] = rank j's operand for this range; `ebase` =
 // global element index of the first element (reduction-order owner).
-template <class Rd, int U, int ORD>
+// NM: operand columns held in registers (4 when n <= 4: half the load buffers, so
+// the two-column unroll fits without scratch).
+template <class Rd, int U, int ORD, int NM = kMaxRanks>
 __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const (&src)[kMaxRanks], const Dsts &d,
                                            size_t nbytes, size_t ebase) {
     using T = typename Rd::T;
@@ -227,12 +229,12 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
     }
     size_t x = threadIdx.x;
     if (x < nv) {
-        v4u cur[U][kMaxRanks], nxt[U][kMaxRanks];
+        v4u cur[U][NM], nxt[U][NM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t xu = x + (size_t)u * kPipeThreads;
 #pragma unroll
-            for (int j = 0; j < kMaxRanks; ++j)
+            for (int j = 0; j < NM; ++j)
                 cur[u][j] = (j < a.n && xu < nv) ? ld_nt((const v4u *)src[j] + xu) : v4u{0, 0, 0, 0};
         }
         for (;;) {
@@ -243,7 +245,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
                 for (int u = 0; u < U; ++u) {
                     const size_t xu = xn + (size_t)u * kPipeThreads;
 #pragma unroll
-                    for (int j = 0; j < kMaxRanks; ++j)
+                    for (int j = 0; j < NM; ++j)
                         nxt[u][j] = (j < a.n && xu < nv) ? ld_nt((const v4u *)src[j] + xu) : v4u{0, 0, 0, 0};
                 }
             }
@@ -251,9 +253,12 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
             for (int u = 0; u < U; ++u) {
                 const size_t xu = x + (size_t)u * kPipeThreads;
                 if (xu < nv) {
+                    v4u col[kMaxRanks];
+#pragma unroll
+                    for (int j = 0; j < kMaxRanks; ++j) col[j] = j < NM ? cur[u][j < NM ? j : 0] : v4u{0, 0, 0, 0};
                     v4u r;
-                    if constexpr (ORD == 4) r = vreduce_n<Rd, 4>(cur[u], a.n, tpa, ebase + xu * N, fb);
-                    else r = vreduce_n<Rd, ORD>(cur[u], a.n, tp, ebase + xu * N);
+                    if constexpr (ORD == 4) r = vreduce_n<Rd, 4>(col, a.n, tpa, ebase + xu * N, fb);
+                    else r = vreduce_n<Rd, ORD>(col, a.n, tp, ebase + xu * N);
 #pragma unroll
                     for (int k = 0; k < kMaxRanks + 1; ++k)
                         if (d.p[k]) {
@@ -266,7 +271,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int j = 0; j < kMaxRanks; ++j) cur[u][j] = nxt[u][j];
+                for (int j = 0; j < NM; ++j) cur[u][j] = nxt[u][j];
             x = xn;
         }
     }
@@ -275,7 +280,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
         const size_t e = nv * N + threadIdx.x;
         T col[kMaxRanks];
 #pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) col[j] = ((const T *)(j < a.n ? src[j] : src[0]))[e];
+        for (int j = 0; j < kMaxRanks; ++j) col[j] = ld_nt_elem((const T *)(j < a.n ? src[j] : src[0]) + e);
         T r;
         if constexpr (ORD == 4) r = prog_eval<Rd>(col, tpa.ps.p[prog_block(tpa.ps, ebase + e)]);
         else r = tree_reduce<Rd, ORD>(col, a.n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, ebase + e));
@@ -376,9 +381,9 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
     if constexpr (PROG) {
         blk_reduce<Rd, 1, 4>(a, src, d, len, (size_t)((int64_t)e0 + a.eshift));
     } else if (a.n <= 4) {
-        if (a.tp.linear == 2) blk_reduce<Rd, 2, 2>(a, src, d, len, e0);
-        else if (a.tp.linear) blk_reduce<Rd, 2, 1>(a, src, d, len, e0);
-        else blk_reduce<Rd, 2, 0>(a, src, d, len, e0);
+        if (a.tp.linear == 2) blk_reduce<Rd, 2, 2, 4>(a, src, d, len, e0);
+        else if (a.tp.linear) blk_reduce<Rd, 2, 1, 4>(a, src, d, len, e0);
+        else blk_reduce<Rd, 2, 0, 4>(a, src, d, len, e0);
     } else {
         if (a.tp.linear == 2) blk_reduce<Rd, 1, 2>(a, src, d, len, e0);
         else if (a.tp.linear) blk_reduce<Rd, 1, 1>(a, src, d, len, e0);
@@ -404,7 +409,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
             }
             for (int k = 0; k < a.nrounds; ++k) {
                 const uint64_t E = a.epoch0 + 2 * (uint64_t)k;
-                if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout)) return;
+                if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout, a.light != 0)) return;
                 reduce_round<Rd, PROG>(a, k);
                 if (a.mode != PIPE_RS) signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (k + 1 < a.nrounds) {
@@ -412,7 +417,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
                     signal_peers(a.sig_peer, n, me, b, E + 2, a.light);
                 }
                 if (!gathers) continue;
-                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
+                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout, a.light != 0)) return;
                 const size_t rbase = (size_t)k * a.tseg + (size_t)b * a.tsub;
                 gather_slots(a, (a.round0 + (uint64_t)k) & 1, rbase, (size_t)b * a.tsub, -1);
             }
@@ -436,7 +441,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
                 blk_copy_multi(d, a.send + rbase, len);
             }
             signal_peers(a.sig_peer, n, me, b, E, a.light);
-            if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout)) return;
+            if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout, a.light != 0)) return;
             gather_slots(a, par, rbase, soff, -1);
         } else {  // PIPE_BC (send == recv == the buffer, seg_off == recv_off)
             const int root = a.root;
@@ -462,9 +467,9 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
                     blk_copy_multi(d, a.send + a.seg_off[root] + rbase, l);
                 }
                 signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
-                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
+                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout, a.light != 0)) return;
             } else {
-                if (!wait_mask(a.sig_own, 1u << root, b, E, a.err, a.timeout)) return;
+                if (!wait_mask(a.sig_own, 1u << root, b, E, a.err, a.timeout, a.light != 0)) return;
                 const size_t l = rlen(me);
                 if (l) {
                     Dsts d{};
@@ -475,7 +480,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
                     blk_copy_multi(d, pslot(a.rs_peer.p[me], par, root) + soff, l);
                 }
                 signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
-                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout)) return;
+                if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout, a.light != 0)) return;
                 gather_slots(a, par, rbase, soff, -1);
             }
         }

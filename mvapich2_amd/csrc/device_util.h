@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace mv2 {
 
 constexpr int kMaxRanks = 8;        // device collectives: ranks per node
@@ -73,6 +75,23 @@ __device__ __forceinline__ void st_nt(v4u *p, v4u v) { __builtin_nontemporal_sto
 // streamed (read-once) loads: non-temporal.  Measured on MI355X for the 2-read/1-write
 // Reduce_local stream (tools/rl_variants.hip): 6.2-6.3 TB/s vs 5.2-5.3 TB/s with plain loads.
 __device__ __forceinline__ v4u ld_nt(const v4u *p) { return __builtin_nontemporal_load(p); }
+// one element of any kind (complex / pair structs: in the widest aligned words)
+template <class T>
+__device__ __forceinline__ T ld_nt_elem(const T *p) {
+    if constexpr (std::is_arithmetic<T>::value) {
+        return __builtin_nontemporal_load(p);
+    } else {
+        using W = typename std::conditional<sizeof(T) % 8 == 0 && alignof(T) >= 8, uint64_t,
+                  typename std::conditional<sizeof(T) % 4 == 0 && alignof(T) >= 4, uint32_t,
+                  typename std::conditional<sizeof(T) % 2 == 0 && alignof(T) >= 2, uint16_t, uint8_t>::type>::type>::type;
+        W w[sizeof(T) / sizeof(W)];
+#pragma unroll
+        for (size_t i = 0; i < sizeof(T) / sizeof(W); ++i) w[i] = __builtin_nontemporal_load((const W *)p + i);
+        T r;
+        __builtin_memcpy(&r, w, sizeof(T));
+        return r;
+    }
+}
 
 __device__ __forceinline__ void flag_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -104,8 +123,12 @@ __device__ __forceinline__ void signal_peers(const SigTable &sig, int n, int me,
 // `mask` (own slot may be included), then acquire at system scope.  Returns
 // false (and records *err) on timeout.  Call from all threads; the result is
 // block-uniform.
+// light = true: every byte handed off lives in this GPU's uncached arena and is
+// read with non-temporal loads (L1 bypassed, uncached memory not held in L2),
+// so the system-scope acquire (an L1 + L2 invalidate, >= 1.7 us) is skipped;
+// the MPI_Init self-test checks the pairing of light release and light acquire.
 __device__ __forceinline__ bool wait_mask(uint64_t *own_sig, unsigned mask, int blk, uint64_t epoch,
-                                          int *err, uint64_t timeout_ticks) {
+                                          int *err, uint64_t timeout_ticks, bool light = false) {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int j = threadIdx.x;
@@ -123,7 +146,7 @@ __device__ __forceinline__ bool wait_mask(uint64_t *own_sig, unsigned mask, int 
                 __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 s_ok = 0;
             } else {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                if (!light) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 s_ok = 1;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -135,8 +158,8 @@ __device__ __forceinline__ bool wait_mask(uint64_t *own_sig, unsigned mask, int 
 
 // wait on every rank in [0, n)
 __device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, uint64_t epoch,
-                                           int *err, uint64_t timeout_ticks) {
-    return wait_mask(own_sig, (1u << n) - 1u, blk, epoch, err, timeout_ticks);
+                                           int *err, uint64_t timeout_ticks, bool light = false) {
+    return wait_mask(own_sig, (1u << n) - 1u, blk, epoch, err, timeout_ticks, light);
 }
 
 // Arrive at the call's completion word (all threads of the block).  Each
@@ -155,6 +178,12 @@ __device__ __forceinline__ void block_done(const Done &d) {
     if (!d.flag) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (gridDim.x == 1) {
+        // one workgroup (small-message one-shot): no counters, no agent fence; the
+        // system-scope release of the host word writes back this XCD's L2 itself
+        if (threadIdx.x == 0) __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (threadIdx.x == 0) {
         const unsigned nb = gridDim.x, b = blockIdx.x;
         const unsigned i = b % kDoneSub, x = b & 7u;

@@ -12,7 +12,10 @@
 // one-shot push through uncached IPC arenas for small messages, direct
 // reduce-scatter + all-gather over xGMI peer mappings for large ones.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <vector>
@@ -35,6 +38,48 @@ bool log_debug_on() {
 }
 
 static hipStream_t pick_stream(void *s) { return s ? (hipStream_t)s : world().stream; }
+
+// Host-side profile of blocking calls (MV2AMD_HOST_PROFILE=1, printed at
+// MPI_Finalize): time from API entry to the kernel launch (argument checks,
+// plan, staging), inside hipLaunchKernel, and from the launch to the
+// completion word (kernel run + peers' arrival).
+struct HostProf {
+    int on = -1;
+    uint64_t calls = 0, pre_ns = 0, launch_ns = 0, wait_ns = 0;
+    uint64_t t_entry = 0, t_l0 = 0, t_l1 = 0;
+};
+static HostProf g_hp;
+static inline uint64_t now_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+static inline bool hp_on() {
+    if (g_hp.on < 0) {
+        const char *v = getenv("MV2AMD_HOST_PROFILE");
+        g_hp.on = v && atoi(v) > 0;
+    }
+    return g_hp.on;
+}
+static inline void hp_entry() {
+    if (hp_on()) g_hp.t_entry = now_ns();
+}
+static inline void hp_done() {
+    if (!hp_on() || !g_hp.t_entry || !g_hp.t_l1) return;
+    const uint64_t t = now_ns();
+    ++g_hp.calls;
+    g_hp.pre_ns += g_hp.t_l0 - g_hp.t_entry;
+    g_hp.launch_ns += g_hp.t_l1 - g_hp.t_l0;
+    g_hp.wait_ns += t - g_hp.t_l1;
+    g_hp.t_entry = g_hp.t_l0 = g_hp.t_l1 = 0;
+}
+void host_prof_report() {
+    if (!hp_on() || !g_hp.calls) return;
+    const double c = (double)g_hp.calls * 1e3;
+    fprintf(stderr, "[mv2amd rank %d] host profile: %llu calls, entry->launch %.3f us, launch %.3f us, launch->done %.3f us\n",
+            world().rank, (unsigned long long)g_hp.calls, g_hp.pre_ns / c, g_hp.launch_ns / c, g_hp.wait_ns / c);
+}
+
 
 // Completion word for the kernel about to be launched on `st` as the call's
 // last stream operation (only the library's own stream; cleared again by
@@ -112,14 +157,17 @@ static int finish(hipStream_t st, bool timed) {
         __atomic_store_n(w.h_err, 0, __ATOMIC_RELEASE);
         return E_OTHER;
     }
+    hp_done();
     return 0;
 }
 
 static inline void tmark0(hipStream_t st) {
     if (world().timing) hipEventRecord(world().ev0, st);
+    if (hp_on() && g_hp.t_entry && !g_hp.t_l0) g_hp.t_l0 = now_ns();
 }
 static inline void tmark1(hipStream_t st) {
     if (world().timing) hipEventRecord(world().ev1, st);
+    if (hp_on() && g_hp.t_entry) g_hp.t_l1 = now_ns();
 }
 
 // 1 = device memory (hipMalloc / IPC-importable), 0 = anything else
@@ -499,6 +547,7 @@ int mv2h_wait_ticket(unsigned long long ticket) {
 // part (1): MPI_Reduce_local on device buffers (reduce_local.c:36-173)
 // ---------------------------------------------------------------------------
 int mv2h_reduce_local(const void *in, void *inout, size_t count, int dtype, int op, void *stream) {
+    hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
     if (rc) return rc;
@@ -832,6 +881,7 @@ static int allreduce_select(const void *sendbuf, void *recvbuf, size_t count, co
                           tree_rs(n, rest, me, false));
 }
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
     if (rc) return rc;
@@ -842,6 +892,7 @@ int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, 
 }
 
 int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+    hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
     if (rc) return rc;
@@ -900,6 +951,7 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
 
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                         void *stream) {
+    hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
     if (rc) return rc;
@@ -983,6 +1035,7 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
 }
 
 int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
+    hp_entry();
     int rc;
     if ((rc = require_world())) return rc;
     if (bytes == 0) return 0;
@@ -1024,6 +1077,7 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
 }
 
 int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
+    hp_entry();
     int rc;
     if ((rc = require_world())) return rc;
     if (bytes == 0) return 0;

@@ -22,6 +22,7 @@ namespace mv2 {
 // ---------------------------------------------------------------------------
 static Knobs g_knobs;
 static bool g_knobs_ok = false;
+static uint64_t g_knobs_gen = 0;  // bumped by knobs_reload: invalidates cached plans
 
 static bool env_set(const char *name, const char **v) {
     *v = getenv(name);
@@ -110,6 +111,7 @@ void knobs_reload() {
     if (env_set("MV2_SMP_USE_CMA", &v)) k.smp_use_cma = !!atoi(v);
     g_knobs = k;
     g_knobs_ok = true;
+    ++g_knobs_gen;
 }
 
 const Knobs &knobs() {
@@ -522,7 +524,7 @@ static int reduce_helper(const Knobs &K, Plan *p, int n, int root, size_t count,
     return reduce_fill(p, K.use_knomial_reduce == 1 ? ALG_KNOMIAL : ALG_BINOMIAL, n, root, count, k);
 }
 
-int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *p, int opk) {
+static int plan_reduce_build(int n, int me, int root, size_t count, int tsize, int textent, Plan *p, int opk) {
     (void)me;
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
@@ -594,8 +596,8 @@ static int allreduce_fill(Plan *p, int algo, int n, int me, size_t count, int op
     return ok ? 0 : E_INTERN;
 }
 
-int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *p,
-                   int opk) {
+static int plan_allreduce_build(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced,
+                                Plan *p, int opk) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
     const Knobs &K = knobs();
@@ -644,7 +646,7 @@ int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_
         }
         // reduce_p2p (:1616-1684): MPIR_Reduce_MV2 to local rank 0, then the shmem bcast
         Plan r;
-        const int rc = plan_reduce(n, me, 0, count, tsize, textent, &r, opk);
+        const int rc = plan_reduce_build(n, me, 0, count, tsize, textent, &r, opk);
         if (rc) return rc;
         *p = r;
         p->inner = r.algo;
@@ -657,7 +659,8 @@ int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_
 // ---------------------------------------------------------------------------
 // MPI_Reduce_scatter (commutative ops; red_scat_osu.c:1859-1896)
 // ---------------------------------------------------------------------------
-int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *p, int opk) {
+static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int tsize, int textent, Plan *p,
+                                     int opk) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
     if (opk == OPK_USER_NONCOMM) return E_INTERN;  // MPIR_Reduce_scatter_non_comm_MV2: not restated here
@@ -684,7 +687,7 @@ int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int text
     default: {
         // MPIR_Reduce_MV2(total, root 0) then a scatter (:326-413)
         Plan r;
-        const int rc = plan_reduce(n, 0, 0, total, tsize, textent, &r, opk);
+        const int rc = plan_reduce_build(n, 0, 0, total, tsize, textent, &r, opk);
         if (rc) return rc;
         p->ps = r.ps;
         p->inner = r.algo;
@@ -693,6 +696,81 @@ int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int text
         return 0;
     }
     }
+}
+
+// ---------------------------------------------------------------------------
+// plan cache: a plan is a pure function of its arguments and the knobs, and
+// latency-bound loops repeat the same call, so the last plans of this thread
+// are kept (the symbolic run costs 3-6 us per call on the host).
+// ---------------------------------------------------------------------------
+namespace {
+struct PlanKey {
+    int32_t coll, n, me, root, tsize, textent, in_place, forced, opk, pad;
+    uint64_t count, gen;
+    uint64_t counts[kMaxRanks];
+};
+constexpr int kPlanCache = 16;
+struct PlanCache {
+    PlanKey key[kPlanCache];
+    Plan plan[kPlanCache];
+    int used = 0, next = 0;
+};
+thread_local PlanCache t_cache;
+
+PlanKey make_key(int coll, int n, int me, int root, size_t count, const size_t *counts, int tsize, int textent,
+                 bool in_place, int forced, int opk) {
+    PlanKey k;
+    memset(&k, 0, sizeof(k));  // padding included: keys are compared bytewise
+    k.coll = coll;
+    k.n = n;
+    k.me = me;
+    k.root = root;
+    k.tsize = tsize;
+    k.textent = textent;
+    k.in_place = in_place;
+    k.forced = forced;
+    k.opk = opk;
+    k.count = count;
+    knobs();
+    k.gen = g_knobs_gen;
+    if (counts)
+        for (int j = 0; j < n && j < kMaxRanks; ++j) k.counts[j] = counts[j];
+    return k;
+}
+
+template <class F>
+int cached(const PlanKey &k, Plan *p, F build) {
+    PlanCache &c = t_cache;
+    for (int i = 0; i < c.used; ++i)
+        if (!memcmp(&c.key[i], &k, sizeof(k))) {
+            *p = c.plan[i];
+            return 0;
+        }
+    const int rc = build();
+    if (rc) return rc;
+    const int i = c.next;
+    c.key[i] = k;
+    c.plan[i] = *p;
+    c.next = (c.next + 1) % kPlanCache;
+    if (c.used < kPlanCache) ++c.used;
+    return 0;
+}
+}  // namespace
+
+int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *p, int opk) {
+    return cached(make_key(0, n, me, 0, count, nullptr, tsize, textent, in_place, forced, opk), p,
+                  [&] { return plan_allreduce_build(n, me, count, tsize, textent, in_place, forced, p, opk); });
+}
+
+int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *p, int opk) {
+    return cached(make_key(1, n, me, root, count, nullptr, tsize, textent, false, 0, opk), p,
+                  [&] { return plan_reduce_build(n, me, root, count, tsize, textent, p, opk); });
+}
+
+int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *p, int opk) {
+    if (n > kMaxRanks) return plan_reduce_scatter_build(n, me, counts, tsize, textent, p, opk);
+    return cached(make_key(2, n, me, 0, 0, counts, tsize, textent, false, 0, opk), p,
+                  [&] { return plan_reduce_scatter_build(n, me, counts, tsize, textent, p, opk); });
 }
 
 }  // namespace mv2

@@ -329,6 +329,7 @@ int world_finalize() {
     World &w = g_world;
     if (!w.inited || w.finalized) return 0;
     if (w.stream) hipStreamSynchronize(w.stream);
+    host_prof_report();
     if (w.size > 1 && w.shm) {
         host_barrier();
         for (int j = 0; j < kMaxRanks; ++j) {

@@ -144,5 +144,6 @@ void host_barrier();
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
+void host_prof_report();  // coll.cpp: MV2AMD_HOST_PROFILE summary
 
 }  // namespace mv2
