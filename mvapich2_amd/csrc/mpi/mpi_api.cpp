@@ -19,6 +19,7 @@
 
 #include "../../../include/mpi.h"
 #include "../../../include/mv2h.h"
+#include "../../../include/mpir_op.h"
 #include "../common.h"
 #include "../runtime/log.h"
 #include "../runtime/orders.h"
@@ -501,6 +502,19 @@ int PMPI_Op_commutative(MPI_Op op, int *commute) {
 int MPI_Op_commutative(MPI_Op op, int *commute) WEAK(MPI_Op_commutative);
 
 // ---------------------------------------------------------------- reductions
+// A builtin op on `count` elements of a builtin type (device or host buffers;
+// x87 types on the host): the MPI error class, no error handler.
+static int builtin_reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype dt, MPI_Op op) {
+    if (!dtype_is_builtin(dt)) return MPI_ERR_OP;
+    if (is_x87(dt)) {
+        if (mv2h_op_check(op, dt)) return MPI_ERR_OP;
+        UserOp x{ld_uop, 1, true};
+        g_ld_op = op_index(op);
+        return op_index(op) == OP_NO_OP ? 0 : user_reduce_local(inbuf, inoutbuf, count, dt, &x);
+    }
+    return mv2h_reduce_local(inbuf, inoutbuf, (size_t)count, dt, op, nullptr);
+}
+
 int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype dt, MPI_Op op) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPI_Reduce_local";
@@ -510,16 +524,78 @@ int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype
     if (count == 0) return MPI_SUCCESS;
     if (inbuf == MPI_IN_PLACE || inoutbuf == MPI_IN_PLACE) return err_return(MPI_COMM_WORLD, MPI_ERR_BUFFER, fn);
     if (UserOp *u = user_op(op)) return err_return(MPI_COMM_WORLD, user_reduce_local(inbuf, inoutbuf, count, dt, u), fn);
-    if (!dtype_is_builtin(dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
-    if (is_x87(dt)) {
-        if (mv2h_op_check(op, dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
-        UserOp x{ld_uop, 1, true};
-        g_ld_op = op_index(op);
-        return err_return(MPI_COMM_WORLD, op_index(op) == OP_NO_OP ? 0 : user_reduce_local(inbuf, inoutbuf, count, dt, &x), fn);
-    }
-    return err_return(MPI_COMM_WORLD, mv2h_reduce_local(inbuf, inoutbuf, (size_t)count, dt, op, nullptr), fn);
+    return err_return(MPI_COMM_WORLD, builtin_reduce_local(inbuf, inoutbuf, count, dt, op), fn);
 }
 int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype dt, MPI_Op op) WEAK(MPI_Reduce_local);
+
+// ---------------------------------------------------------------------------
+// The predefined ops as MPI_User_function entry points (include/mpir_op.h):
+// MPIR_Op_table (allreduce.c:95-100) indexed by MPIR_OP_HDL_TO_FN
+// (mpiimpl.h:4031), and the per-op type checks (MPIR_Op_check_dtype_table).
+// Unlike the reference's host loops (opsum.c:26-90 ...) they take device
+// buffers: one HBM-streaming kernel, synchronous like any MPI_User_function;
+// host buffers are staged as for MPI_Reduce_local.  A type the op does not
+// accept leaves inoutvec untouched and sets the error MPIR_Op_errno returns
+// (the reference keeps it in the thread-private op_errno, opsum.c:82-86).
+// ---------------------------------------------------------------------------
+static thread_local int t_op_errno = MPI_SUCCESS;
+
+static void op_entry(MPI_Op op, void *invec, void *inoutvec, int *len, MPI_Datatype *type) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (!len || !type || *len < 0) {
+        t_op_errno = MPI_ERR_ARG;
+        return;
+    }
+    if (*len == 0) return;
+    if (!dtype_valid(*type)) {
+        t_op_errno = MPI_ERR_TYPE;
+        return;
+    }
+    if (mv2h_op_check(op, *type)) {
+        t_op_errno = MPI_ERR_OP;
+        return;
+    }
+    const int rc = builtin_reduce_local(invec, inoutvec, *len, *type, op);
+    if (rc) t_op_errno = rc;
+}
+
+#define MV2_OP_FN(NAME, HANDLE)                                                               \
+    void NAME(void *invec, void *inoutvec, int *len, MPI_Datatype *type) {                     \
+        op_entry(HANDLE, invec, inoutvec, len, type);                                          \
+    }                                                                                          \
+    int NAME##_check_dtype(MPI_Datatype type) {                                                \
+        return !dtype_valid(type) ? MPI_ERR_TYPE : (mv2h_op_check(HANDLE, type) ? MPI_ERR_OP : MPI_SUCCESS); \
+    }
+MV2_OP_FN(MPIR_MAXF, MPI_MAX)
+MV2_OP_FN(MPIR_MINF, MPI_MIN)
+MV2_OP_FN(MPIR_SUM, MPI_SUM)
+MV2_OP_FN(MPIR_PROD, MPI_PROD)
+MV2_OP_FN(MPIR_LAND, MPI_LAND)
+MV2_OP_FN(MPIR_BAND, MPI_BAND)
+MV2_OP_FN(MPIR_LOR, MPI_LOR)
+MV2_OP_FN(MPIR_BOR, MPI_BOR)
+MV2_OP_FN(MPIR_LXOR, MPI_LXOR)
+MV2_OP_FN(MPIR_BXOR, MPI_BXOR)
+MV2_OP_FN(MPIR_MINLOC, MPI_MINLOC)
+MV2_OP_FN(MPIR_MAXLOC, MPI_MAXLOC)
+MV2_OP_FN(MPIR_REPLACE, MPI_REPLACE)
+MV2_OP_FN(MPIR_NO_OP, MPI_NO_OP)
+#undef MV2_OP_FN
+
+// order of the predefined op handles' low nibble (mpi.h: MPI_MAX = ...01 .. MPI_NO_OP = ...0e)
+MPI_User_function *MPIR_Op_table[] = {MPIR_MAXF, MPIR_MINF, MPIR_SUM,  MPIR_PROD,   MPIR_LAND,   MPIR_BAND,    MPIR_LOR,
+                                      MPIR_BOR,  MPIR_LXOR, MPIR_BXOR, MPIR_MINLOC, MPIR_MAXLOC, MPIR_REPLACE, MPIR_NO_OP};
+MPIR_Op_check_dtype_fn *MPIR_Op_check_dtype_table[] = {
+    MPIR_MAXF_check_dtype, MPIR_MINF_check_dtype,   MPIR_SUM_check_dtype,    MPIR_PROD_check_dtype,
+    MPIR_LAND_check_dtype, MPIR_BAND_check_dtype,   MPIR_LOR_check_dtype,    MPIR_BOR_check_dtype,
+    MPIR_LXOR_check_dtype, MPIR_BXOR_check_dtype,   MPIR_MINLOC_check_dtype, MPIR_MAXLOC_check_dtype,
+    MPIR_REPLACE_check_dtype, MPIR_NO_OP_check_dtype};
+
+int MPIR_Op_errno(void) {
+    const int e = t_op_errno;
+    t_op_errno = MPI_SUCCESS;
+    return e;
+}
 
 static int coll_checks(MPI_Comm comm, int count, MPI_Datatype dt, MPI_Op op) {
     if (!g_initialized || g_finalized) return MPI_ERR_OTHER;

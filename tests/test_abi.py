@@ -74,3 +74,28 @@ def test_op_legality_matches_oracle():
         for t, (h, *_r) in TYPES.items():
             assert (L.mv2h_op_check(oh, h) == 0) == (oracle.op_check(oh, h) == 0), (op, t)
     assert L.mv2h_op_check(OPS["MPI_SUM"], 0x12345) == 3  # unknown type -> MPI_ERR_TYPE
+
+
+def test_op_table_header_symbols_are_exported():
+    """include/mpir_op.h: the predefined ops as MPI_User_function entry points
+    (MPIR_Op_table, allreduce.c:95-107) — every declared name and both tables."""
+    txt = open(os.path.join(ROOT, "include", "mpir_op.h")).read()
+    names = set(re.findall(r"^\s*(?:void|int)\s+(MPIR_\w+)\(", txt, flags=re.M))
+    assert len(names) == 29
+    syms = exported()
+    missing = sorted(n for n in names | {"MPIR_Op_table", "MPIR_Op_check_dtype_table"} if n not in syms)
+    assert not missing, missing
+
+
+def test_op_table_check_dtype_matches_legality():
+    """MPIR_OP_HDL_TO_DTYPE_FN(op)(type) == MPI_SUCCESS exactly where the op accepts the type
+    (host-side tables only: no GPU call)."""
+    L = m.lib()
+    table = (ctypes.c_void_p * 14).in_dll(L, "MPIR_Op_check_dtype_table")
+    CHK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int)
+    for op, oh in OPS.items():
+        fn = CHK(table[(oh & 0xF) - 1])
+        for t, (h, *_r) in TYPES.items():
+            want = 0 if L.mv2h_op_check(oh, h) == 0 else 9  # MPI_ERR_OP
+            assert fn(h) == want, (op, t)
+        assert fn(0x1234) == 3  # not a datatype: MPI_ERR_TYPE

@@ -137,3 +137,32 @@ def test_full_size_256MiB(tname, op):
     with np.errstate(over="ignore"):
         want = (x + y) if op == "MPI_SUM" else np.maximum(x, y)
     assert np.array_equal(got, want)
+
+
+def test_op_table_entries_on_device_buffers():
+    """include/mpir_op.h: MPIR_OP_HDL_TO_FN(op)(in, inout, &len, &type) on device buffers gives
+    MPI_Reduce_local's bits (MPIR_Op_table, allreduce.c:95-100); a type the op rejects leaves
+    inoutvec untouched and MPIR_Op_errno() returns MPI_ERR_OP (opsum.c:82-86)."""
+    import ctypes
+    L = m.lib()
+    table = (ctypes.c_void_p * 14).in_dll(L, "MPIR_Op_table")
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+    rng = np.random.default_rng(4031)
+    count = 3001
+    for op, t in PAIRS:
+        x = rand_typed(t, count, rng, small=op == "MPI_PROD")
+        y = rand_typed(t, count, rng, small=op == "MPI_PROD")
+        want = y.copy()
+        assert oracle.reduce_local(x, want, count, TYPES[t][0], OPS[op]) == 0
+        a, b = m.DeviceBuffer.from_array(x), m.DeviceBuffer.from_array(y)
+        n, ty = ctypes.c_int(count), ctypes.c_int(TYPES[t][0])
+        UF(table[(OPS[op] & 0xF) - 1])(a.ptr, b.ptr, ctypes.byref(n), ctypes.byref(ty))
+        assert L.MPIR_Op_errno() == 0, (op, t)
+        assert_bytes_equal(b.download(np.uint8), as_bytes(want), t, count, f"MPIR_Op_table {op}")
+    a, b = m.DeviceBuffer.from_array(np.ones(16, np.float32)), m.DeviceBuffer.from_array(np.full(16, 5, np.float32))
+    n, ty = ctypes.c_int(16), ctypes.c_int(TYPES["MPI_FLOAT"][0])
+    UF(table[(OPS["MPI_BXOR"] & 0xF) - 1])(a.ptr, b.ptr, ctypes.byref(n), ctypes.byref(ty))
+    assert L.MPIR_Op_errno() == 9
+    assert L.MPIR_Op_errno() == 0
+    assert np.all(b.download(np.float32) == 5)
