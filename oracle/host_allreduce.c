@@ -7,15 +7,19 @@
  * cpu_baseline leg runs it on the GPU box's host cores; the product never
  * links or calls it.
  *
- * What is restated (single node, generic tuning table,
- * allreduce_tuning.c:2734-2750, allreduce_osu.c:3146-3375):
- *   nbytes <  1 KiB: two-level shared memory — every rank copies its operand
- *                    into its shmem slot, the leader reduces the slots in rank
- *                    order (reduce_shmem, allreduce_osu.c:1482-1614: recv = x0;
- *                    uop(slot_i, recv) for i = 1..L-1), then the shmem bcast
- *                    (bcast_osu.c:1356: leader writes one slot, the others copy
- *                    it out).
- *   nbytes >= 1 KiB: MPIR_Allreduce_pt2pt_rs_MV2 (:633-1054): non-pof2 fold,
+ * What is restated (single node, MVAPICH2's default selection for one node,
+ * MPIR_Allreduce_index_tuned_intra_MV2 allreduce_osu.c:3015-3420 with the skip
+ * macros :118-188; the same choice as runtime/orders.cpp plan_allreduce):
+ *   nbytes <= 2 KiB: the topology-aware shm tree (…_topo_aware_hierarchical_MV2
+ *                    :2272 -> mv2_shm_tree_reduce, ch3_shmem_coll.c:4272-4359):
+ *                    every rank copies its operand into its shmem slot, group
+ *                    leaders (rank % 4 == 0) reduce their members' slots in
+ *                    order, local rank 0 reduces the leaders' slots, then the
+ *                    shmem bcast (bcast_osu.c:1356: rank 0 writes one slot, the
+ *                    others copy it out).  MV2_USE_TOPO_AWARE_ALLREDUCE=0 gives
+ *                    the flat two-level reduce_shmem (:1482-1614) up to 1 KiB.
+ *   nbytes >= 2 MiB: the flat ring wrapper (:3758-3818 -> pt2pt_ring :3824-4025).
+ *   otherwise:       MPIR_Allreduce_pt2pt_rs_MV2 (:633-1054): non-pof2 fold,
  *                    recursive-halving reduce-scatter, recursive-doubling
  *                    allgather, non-pof2 post-step; recursive doubling when
  *                    count < pof2 (:802).
@@ -148,6 +152,34 @@ static void allreduce_two_level(const char *send, char *recv, long count) {
     }
 }
 
+/* topology-aware shm tree, one topology level, degree 4 (see the header) */
+static void allreduce_topo_tree(const char *send, char *recv, long count) {
+    const size_t bytes = (size_t)count * 4;
+    const int deg = 4;
+    unsigned long g = ++gen_slot;
+    memcpy(slot_of(ME), send, bytes);
+    if (ME % deg == 0) {
+        for (int i = ME + 1; i < ME + deg && i < N; i++) {
+            spin_until(&C->slot_flag[i].v, g);
+            oracle_reduce_local(slot_of(i), slot_of(ME), count, H_FLOAT, OP_SUM);
+        }
+    }
+    if (ME != 0) {
+        atomic_store_explicit(&C->slot_flag[ME].v, g, memory_order_release);
+        spin_until(&C->bc_flag.v, g);
+        memcpy(recv, slot_of(0), bytes);
+        atomic_store_explicit(&C->bc_done[ME].v, g, memory_order_release);
+    } else {
+        for (int i = deg; i < N; i += deg) {
+            spin_until(&C->slot_flag[i].v, g);
+            oracle_reduce_local(slot_of(i), slot_of(0), count, H_FLOAT, OP_SUM);
+        }
+        memcpy(recv, slot_of(0), bytes);
+        atomic_store_explicit(&C->bc_flag.v, g, memory_order_release);
+        for (int i = 1; i < N; i++) spin_until(&C->bc_done[i].v, g);
+    }
+}
+
 /* MPIR_Allreduce_pt2pt_rs_MV2 allreduce_osu.c:633-1054 on this rank.  The
  * receive buffer of every rank is its shared region recv_of(rank). */
 static void allreduce_rs(const char *send, long count) {
@@ -266,11 +298,14 @@ static void allreduce_ring(long count) {
     }
 }
 
-/* single-node selection (MPIR_Allreduce_index_tuned_intra_MV2 allreduce_osu.c:3144-3160):
- * <= 1024 B two-level, >= 2 MiB the ring wrapper (:163-170; power-of-two sizes divide
- * evenly over the ranks, so no pt2pt_rs remainder), pt2pt_rs between */
+/* single-node selection (see the header): <= 2 KiB the topology-aware tree (or, with
+ * MV2_USE_TOPO_AWARE_ALLREDUCE=0, two-level up to 1 KiB), >= 2 MiB the ring wrapper
+ * (:163-170; power-of-two sizes divide evenly over the ranks, so no pt2pt_rs remainder),
+ * pt2pt_rs between */
+static int TOPO = 1;
 static void allreduce(const char *send, char *recv_private, long count) {
-    if ((size_t)count * 4 <= 1024) allreduce_two_level(send, recv_private, count);
+    if (TOPO && (size_t)count * 4 <= 2048) allreduce_topo_tree(send, recv_private, count);
+    else if (!TOPO && (size_t)count * 4 <= 1024) allreduce_two_level(send, recv_private, count);
     else if ((size_t)count * 4 >= (2u << 20) && N > 1 && count % N == 0) allreduce_ring(count);
     else allreduce_rs(send, count);
 }
@@ -306,6 +341,8 @@ int main(int argc, char **argv) {
     double tcap = 3.0;
     int first_core = 0;
     int c;
+    const char *topo = getenv("MV2_USE_TOPO_AWARE_ALLREDUCE");
+    if (topo) TOPO = atoi(topo) != 0;
     while ((c = getopt(argc, argv, "n:m:i:I:cT:p:")) != -1) {
         switch (c) {
         case 'n': N = atoi(optarg); break;
@@ -369,7 +406,8 @@ int main(int argc, char **argv) {
                 if (ME == 0) C->bad[MAXR - 1] = 0;
                 int bad = 0;
                 if (validate) {
-                    const float *res = (sz <= 1024) ? recvp : (const float *)recv_of(ME);
+                    const int priv = TOPO ? sz <= 2048 : sz <= 1024;  /* shmem paths write recv_private */
+                    const float *res = priv ? recvp : (const float *)recv_of(ME);
                     const float tot = (float)(N * (N + 1) / 2);
                     for (long i = 0; i < count; i++)
                         if (res[i] != (float)((i % 100) + 1) * tot) { bad = 1; break; }
