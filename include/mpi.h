@@ -173,7 +173,91 @@ typedef void(MPI_User_function)(void *, void *, int *, MPI_Datatype *);
 #define MPI_ERR_UNSUPPORTED_OPERATION 44
 #define MPI_ERR_LASTCODE 0x3fffffff
 
+
+/* ---- MPI_T tool information interface (MPICH encodings, mpi.h.in:605-700, :874-892) ---- */
+typedef struct MPIR_T_enum_s *MPI_T_enum;
+typedef struct MPIR_T_cvar_handle_s *MPI_T_cvar_handle;
+typedef struct MPIR_T_pvar_handle_s *MPI_T_pvar_handle;
+typedef struct MPIR_T_pvar_session_s *MPI_T_pvar_session;
+extern struct MPIR_T_pvar_handle_s *const MPI_T_PVAR_ALL_HANDLES;
+#define MPI_T_ENUM_NULL ((MPI_T_enum)0)
+#define MPI_T_CVAR_HANDLE_NULL ((MPI_T_cvar_handle)0)
+#define MPI_T_PVAR_HANDLE_NULL ((MPI_T_pvar_handle)0)
+#define MPI_T_PVAR_SESSION_NULL ((MPI_T_pvar_session)0)
+enum MPIR_T_verbosity_t {
+    MPI_T_VERBOSITY_USER_BASIC = 221, MPI_T_VERBOSITY_USER_DETAIL, MPI_T_VERBOSITY_USER_ALL,
+    MPI_T_VERBOSITY_TUNER_BASIC, MPI_T_VERBOSITY_TUNER_DETAIL, MPI_T_VERBOSITY_TUNER_ALL,
+    MPI_T_VERBOSITY_MPIDEV_BASIC, MPI_T_VERBOSITY_MPIDEV_DETAIL, MPI_T_VERBOSITY_MPIDEV_ALL
+};
+enum MPIR_T_bind_t {
+    MPI_T_BIND_NO_OBJECT = 9700, MPI_T_BIND_MPI_COMM, MPI_T_BIND_MPI_DATATYPE, MPI_T_BIND_MPI_ERRHANDLER,
+    MPI_T_BIND_MPI_FILE, MPI_T_BIND_MPI_GROUP, MPI_T_BIND_MPI_OP, MPI_T_BIND_MPI_REQUEST, MPI_T_BIND_MPI_WIN,
+    MPI_T_BIND_MPI_MESSAGE, MPI_T_BIND_MPI_INFO
+};
+enum MPIR_T_scope_t {
+    MPI_T_SCOPE_CONSTANT = 60438, MPI_T_SCOPE_READONLY, MPI_T_SCOPE_LOCAL, MPI_T_SCOPE_GROUP,
+    MPI_T_SCOPE_GROUP_EQ, MPI_T_SCOPE_ALL, MPI_T_SCOPE_ALL_EQ
+};
+enum MPIR_T_pvar_class_t {
+    MPI_T_PVAR_CLASS_STATE = 240, MPI_T_PVAR_CLASS_LEVEL, MPI_T_PVAR_CLASS_SIZE, MPI_T_PVAR_CLASS_PERCENTAGE,
+    MPI_T_PVAR_CLASS_HIGHWATERMARK, MPI_T_PVAR_CLASS_LOWWATERMARK, MPI_T_PVAR_CLASS_COUNTER,
+    MPI_T_PVAR_CLASS_AGGREGATE, MPI_T_PVAR_CLASS_TIMER, MPI_T_PVAR_CLASS_GENERIC
+};
+#define MPI_T_ERR_MEMORY 59
+#define MPI_T_ERR_NOT_INITIALIZED 60
+#define MPI_T_ERR_CANNOT_INIT 61
+#define MPI_T_ERR_INVALID_INDEX 62
+#define MPI_T_ERR_INVALID_ITEM 63
+#define MPI_T_ERR_INVALID_HANDLE 64
+#define MPI_T_ERR_OUT_OF_HANDLES 65
+#define MPI_T_ERR_OUT_OF_SESSIONS 66
+#define MPI_T_ERR_INVALID_SESSION 67
+#define MPI_T_ERR_CVAR_SET_NOT_NOW 68
+#define MPI_T_ERR_CVAR_SET_NEVER 69
+#define MPI_T_ERR_PVAR_NO_STARTSTOP 70
+#define MPI_T_ERR_PVAR_NO_WRITE 71
+#define MPI_T_ERR_PVAR_NO_ATOMIC 72
+#define MPI_T_ERR_INVALID_NAME 73
+#define MPI_T_ERR_INVALID 74
+
 /* ---- environment ---- */
+int MPI_T_init_thread(int required, int *provided);
+int MPI_T_finalize(void);
+int MPI_T_enum_get_info(MPI_T_enum enumtype, int *num, char *name, int *name_len);
+int MPI_T_enum_get_item(MPI_T_enum enumtype, int indx, int *value, char *name, int *name_len);
+int MPI_T_cvar_get_num(int *num_cvar);
+int MPI_T_cvar_get_info(int cvar_index, char *name, int *name_len, int *verbosity, MPI_Datatype *datatype,
+                        MPI_T_enum *enumtype, char *desc, int *desc_len, int *binding, int *scope);
+int MPI_T_cvar_get_index(const char *name, int *cvar_index);
+int MPI_T_cvar_handle_alloc(int cvar_index, void *obj_handle, MPI_T_cvar_handle *handle, int *count);
+int MPI_T_cvar_handle_free(MPI_T_cvar_handle *handle);
+int MPI_T_cvar_read(MPI_T_cvar_handle handle, void *buf);
+int MPI_T_cvar_write(MPI_T_cvar_handle handle, const void *buf);
+int MPI_T_pvar_get_num(int *num_pvar);
+int MPI_T_pvar_get_info(int pvar_index, char *name, int *name_len, int *verbosity, int *var_class,
+                        MPI_Datatype *datatype, MPI_T_enum *enumtype, char *desc, int *desc_len, int *binding,
+                        int *readonly, int *continuous, int *atomic);
+int MPI_T_pvar_get_index(const char *name, int var_class, int *pvar_index);
+int MPI_T_pvar_session_create(MPI_T_pvar_session *session);
+int MPI_T_pvar_session_free(MPI_T_pvar_session *session);
+int MPI_T_pvar_handle_alloc(MPI_T_pvar_session session, int pvar_index, void *obj_handle, MPI_T_pvar_handle *handle,
+                            int *count);
+int MPI_T_pvar_handle_free(MPI_T_pvar_session session, MPI_T_pvar_handle *handle);
+int MPI_T_pvar_start(MPI_T_pvar_session session, MPI_T_pvar_handle handle);
+int MPI_T_pvar_stop(MPI_T_pvar_session session, MPI_T_pvar_handle handle);
+int MPI_T_pvar_read(MPI_T_pvar_session session, MPI_T_pvar_handle handle, void *buf);
+int MPI_T_pvar_write(MPI_T_pvar_session session, MPI_T_pvar_handle handle, const void *buf);
+int MPI_T_pvar_reset(MPI_T_pvar_session session, MPI_T_pvar_handle handle);
+int MPI_T_pvar_readreset(MPI_T_pvar_session session, MPI_T_pvar_handle handle, void *buf);
+int MPI_T_category_get_num(int *num_cat);
+int MPI_T_category_get_info(int cat_index, char *name, int *name_len, char *desc, int *desc_len, int *num_cvars,
+                            int *num_pvars, int *num_categories);
+int MPI_T_category_get_index(const char *name, int *cat_index);
+int MPI_T_category_get_cvars(int cat_index, int len, int indices[]);
+int MPI_T_category_get_pvars(int cat_index, int len, int indices[]);
+int MPI_T_category_get_categories(int cat_index, int len, int indices[]);
+int MPI_T_category_changed(int *stamp);
+
 int MPI_Init(int *argc, char ***argv);
 int MPI_Init_thread(int *argc, char ***argv, int required, int *provided);
 int MPI_Finalize(void);
@@ -373,6 +457,42 @@ int PMPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbu
 int PMPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
                 MPI_Datatype datatype, MPI_Comm comm);
 int PMPI_Pack_size(int incount, MPI_Datatype datatype, MPI_Comm comm, int *size);
+int PMPI_T_init_thread(int required, int *provided);
+int PMPI_T_finalize(void);
+int PMPI_T_enum_get_info(MPI_T_enum enumtype, int *num, char *name, int *name_len);
+int PMPI_T_enum_get_item(MPI_T_enum enumtype, int indx, int *value, char *name, int *name_len);
+int PMPI_T_cvar_get_num(int *num_cvar);
+int PMPI_T_cvar_get_info(int cvar_index, char *name, int *name_len, int *verbosity, MPI_Datatype *datatype,
+                        MPI_T_enum *enumtype, char *desc, int *desc_len, int *binding, int *scope);
+int PMPI_T_cvar_get_index(const char *name, int *cvar_index);
+int PMPI_T_cvar_handle_alloc(int cvar_index, void *obj_handle, MPI_T_cvar_handle *handle, int *count);
+int PMPI_T_cvar_handle_free(MPI_T_cvar_handle *handle);
+int PMPI_T_cvar_read(MPI_T_cvar_handle handle, void *buf);
+int PMPI_T_cvar_write(MPI_T_cvar_handle handle, const void *buf);
+int PMPI_T_pvar_get_num(int *num_pvar);
+int PMPI_T_pvar_get_info(int pvar_index, char *name, int *name_len, int *verbosity, int *var_class,
+                        MPI_Datatype *datatype, MPI_T_enum *enumtype, char *desc, int *desc_len, int *binding,
+                        int *readonly, int *continuous, int *atomic);
+int PMPI_T_pvar_get_index(const char *name, int var_class, int *pvar_index);
+int PMPI_T_pvar_session_create(MPI_T_pvar_session *session);
+int PMPI_T_pvar_session_free(MPI_T_pvar_session *session);
+int PMPI_T_pvar_handle_alloc(MPI_T_pvar_session session, int pvar_index, void *obj_handle, MPI_T_pvar_handle *handle,
+                            int *count);
+int PMPI_T_pvar_handle_free(MPI_T_pvar_session session, MPI_T_pvar_handle *handle);
+int PMPI_T_pvar_start(MPI_T_pvar_session session, MPI_T_pvar_handle handle);
+int PMPI_T_pvar_stop(MPI_T_pvar_session session, MPI_T_pvar_handle handle);
+int PMPI_T_pvar_read(MPI_T_pvar_session session, MPI_T_pvar_handle handle, void *buf);
+int PMPI_T_pvar_write(MPI_T_pvar_session session, MPI_T_pvar_handle handle, const void *buf);
+int PMPI_T_pvar_reset(MPI_T_pvar_session session, MPI_T_pvar_handle handle);
+int PMPI_T_pvar_readreset(MPI_T_pvar_session session, MPI_T_pvar_handle handle, void *buf);
+int PMPI_T_category_get_num(int *num_cat);
+int PMPI_T_category_get_info(int cat_index, char *name, int *name_len, char *desc, int *desc_len, int *num_cvars,
+                            int *num_pvars, int *num_categories);
+int PMPI_T_category_get_index(const char *name, int *cat_index);
+int PMPI_T_category_get_cvars(int cat_index, int len, int indices[]);
+int PMPI_T_category_get_pvars(int cat_index, int len, int indices[]);
+int PMPI_T_category_get_categories(int cat_index, int len, int indices[]);
+int PMPI_T_category_changed(int *stamp);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@
 #include "../common.h"
 #include "../runtime/log.h"
 #include "../runtime/orders.h"
+#include "../runtime/pvars.h"
 #include "../runtime/world.h"
 #include "datatype.h"
 
@@ -237,7 +238,7 @@ void eval_plan(const ProgSet &ps, std::vector<char> &W, long span, long e_begin,
     }
 }
 
-int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
+int user_allreduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
     World &w = world();
     const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
     if (span < 0) return MPI_ERR_TYPE;
@@ -252,7 +253,7 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
         dtype_merge_typemap(result.data(), W.data(), dt, count);
     } else if ((rc = plan_allreduce(n, me, (size_t)count, (int)tsize, (int)extent, in_place, 0, &p, opk))) {
         return rc;
-    } else if (p.algo != ALG_RING) {
+    } else if (pvar_note(PV_COLL_ALLREDUCE, p, in_place, (size_t)count, n), p.algo != ALG_RING) {
         eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
     } else {
         // ring wrapper (allreduce_osu.c:3758-3818): ring over (count/n)*n elements unless
@@ -270,9 +271,17 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
     return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
 
+// one MPI_T-counted call (runtime/pvars.h)
+int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
+    pvar_begin();
+    const int rc = user_allreduce_body(sendbuf, recvbuf, count, dt, u, opk);
+    pvar_end(rc == MPI_SUCCESS);
+    return rc;
+}
+
 // MPI_Reduce with a user op: the root evaluates the plan of
 // MPIR_Reduce_index_tuned_intra_MV2 (binomial / knomial / shmem / ...)
-int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
+int user_reduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
     World &w = world();
     const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
     if (span < 0) return MPI_ERR_TYPE;
@@ -280,17 +289,25 @@ int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
     const bool in_place = sendbuf == MPI_IN_PLACE;
     std::vector<char> W, result;
     int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
-    if (rc || me != root) return rc;
-    if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
+    if (rc) return rc;
     Plan p;
-    if (n == 1) {
-        dtype_merge_typemap(result.data(), W.data(), dt, count);
-    } else {
-        if ((rc = plan_reduce(n, me, root, (size_t)count, (int)tsize, (int)extent, &p, opk)))
-            return rc;
-        eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
+    if (n > 1) {
+        if ((rc = plan_reduce(n, me, root, (size_t)count, (int)tsize, (int)extent, &p, opk))) return rc;
+        pvar_note(PV_COLL_REDUCE, p, in_place, (size_t)count, n);  // every rank runs the algorithm
     }
+    if (me != root) return MPI_SUCCESS;
+    if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
+    if (n == 1) dtype_merge_typemap(result.data(), W.data(), dt, count);
+    else eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
     return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+// one MPI_T-counted call (runtime/pvars.h)
+int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
+    pvar_begin();
+    const int rc = user_reduce_body(sendbuf, recvbuf, count, dt, u, root, opk);
+    pvar_end(rc == MPI_SUCCESS);
+    return rc;
 }
 
 }  // namespace
@@ -305,7 +322,7 @@ namespace {
 // (MPIR_Reduce_scatter_non_comm_MV2, not restated): the canonical rank order
 // x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
 // associative op, applied as fn(in = x_i, inout = acc).
-int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
+int user_reduce_scatter_body(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
     World &w = world();
     const int n = w.size, me = w.rank;
     const long extent = dtype_extent(dt), tsize = dtype_size(dt);
@@ -322,13 +339,18 @@ int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     std::vector<char> W, result;
     int rc = gather_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, span, W);
     if (rc) return rc;
+    Plan p;
+    if (opk != OPK_USER_NONCOMM) {
+        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)tsize, (int)extent, &p, opk))) return rc;
+        pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
+    } else if (n > 1) {
+        pvar_note_id(PV_RS_NON_COMM);
+    }
     const int c = counts[me];
     if (c == 0) return MPI_SUCCESS;
     const long bspan = dtype_span(dt, c);
     if (copy_to_host(result, recvbuf, bspan)) return MPI_ERR_OTHER;
     if (opk != OPK_USER_NONCOMM) {
-        Plan p;
-        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)tsize, (int)extent, &p, opk))) return rc;
         eval_plan(p.ps, W, span, disp, disp + c, dt, extent, u, result.data());
     } else {
         auto X = [&](int r) { return W.data() + (size_t)r * span + (size_t)disp * extent; };
@@ -339,6 +361,14 @@ int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
         dtype_merge_typemap(result.data(), acc.data(), dt, c);
     }
     return copy_from_host(recvbuf, result, bspan) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+// one MPI_T-counted call (runtime/pvars.h)
+int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
+    pvar_begin();
+    const int rc = user_reduce_scatter_body(sendbuf, recvbuf, counts, dt, u, opk);
+    pvar_end(rc == MPI_SUCCESS);
+    return rc;
 }
 
 }  // namespace

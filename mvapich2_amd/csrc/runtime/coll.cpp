@@ -23,6 +23,7 @@
 #include "../../../include/mv2h.h"
 #include "log.h"
 #include "orders.h"
+#include "pvars.h"
 #include "world.h"
 
 namespace mv2 {
@@ -890,6 +891,7 @@ static int allreduce_select(const void *sendbuf, void *recvbuf, size_t count, co
     int rc = plan_allreduce(n, me, count, dt->size, dt->extent, in_place, 0, &p);
     if (rc) return rc;
     log_plan("allreduce", p, count);
+    pvar_note(PV_COLL_ALLREDUCE, p, in_place, count, n);
     if (p.algo != ALG_RING) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tree_from_plan(p, n, count, me));
     if (count < (size_t)n) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tree_rs(n, count, me, false));
     const size_t main = (count / n) * n, rest = count - main, off = main * (size_t)dt->extent;
@@ -899,7 +901,7 @@ static int allreduce_select(const void *sendbuf, void *recvbuf, size_t count, co
     return allreduce_impl(in_place ? sendbuf : (const char *)sendbuf + off, (char *)recvbuf + off, rest, dt, oi, st,
                           tree_rs(n, rest, me, false));
 }
-int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
@@ -909,8 +911,14 @@ int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, 
     if ((rc = require_world())) return rc;
     return allreduce_select(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
 }
+int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    pvar_begin();
+    const int rc = allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream);
+    pvar_end(rc == 0);
+    return rc;
+}
 
-int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
     hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
@@ -929,6 +937,7 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
     Plan p;
     if ((rc = plan_reduce(w.size, w.rank, root, count, dt->size, dt->extent, &p))) return rc;
     log_plan("reduce", p, count);
+    pvar_note(PV_COLL_REDUCE, p, in_place, count, w.size);
     const TreeParams tp = tree_from_plan(p, w.size, count, w.rank);
     // small messages, REPLACE / NO_OP, one rank: every rank computes the root's result
     // (one-shot); non-roots discard theirs
@@ -967,8 +976,14 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
     if (is_root) stage_out(s, st);
     return finish(st, w.timing);
 }
+int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+    pvar_begin();
+    const int rc = reduce_entry(sendbuf, recvbuf, count, dtype, op, root, stream);
+    pvar_end(rc == 0);
+    return rc;
+}
 
-int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
+static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                         void *stream) {
     hp_entry();
     const DtypeInfo *dt = nullptr;
@@ -1039,6 +1054,7 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     Plan p;
     if ((rc = plan_reduce_scatter(n, w.rank, recvcounts, dt->size, dt->extent, &p))) return rc;
     log_plan("reduce_scatter", p, total);
+    pvar_note(PV_COLL_REDUCE_SCATTER, p, false, total, n);
     TreeParams tp = tree_base(n);
     if (p.algo == ALG_RS_RING) {
         tp.linear = 2;  // rotated sources, specialised chain (coll/pipe.h reduce_round)
@@ -1051,6 +1067,13 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
     if (!direct && mycnt) enq_copy(recvbuf, dst, mycnt * ext, st);
     return finish(st, w.timing);
+}
+int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
+                        void *stream) {
+    pvar_begin();
+    const int rc = reduce_scatter_entry(sendbuf, recvbuf, recvcounts, dtype, op, stream);
+    pvar_end(rc == 0);
+    return rc;
 }
 
 int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {

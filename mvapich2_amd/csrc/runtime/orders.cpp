@@ -515,6 +515,7 @@ static int reduce_helper(const Knobs &K, Plan *p, int n, int root, size_t count,
                          const ReduceEntry *e) {
     const long stride = (long)count * textent;
     const int k = reduce_k(K, e);
+    p->via |= VIA_TWO_LEVEL_HELPER;
     if (stride <= K.shmem_intra_reduce_msg && K.enable_shmem_reduce) {
         // MPIR_Reduce_shmem_MV2 at local root 0 (then sent to the root), or the intra knomial
         // wrapper at 0 from the shmem slot size on (:2125-2133)
@@ -583,7 +584,10 @@ static const AllreduceEntry kAr16 = {
 
 // pt2pt_rs falls back to recursive doubling for user ops and count < pof2 (:802)
 static int allreduce_fill(Plan *p, int algo, int n, int me, size_t count, int opk = OPK_BUILTIN) {
-    if (algo == ALG_PT2PT_RS && (opk != OPK_BUILTIN || count < (size_t)pof2_of(n))) algo = ALG_PT2PT_RD;
+    if (algo == ALG_PT2PT_RS && (opk != OPK_BUILTIN || count < (size_t)pof2_of(n))) {
+        algo = ALG_PT2PT_RD;
+        p->via |= VIA_RS_ENTRY;
+    }
     p->algo = algo;
     bool ok = false;
     switch (algo) {
@@ -693,6 +697,7 @@ static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int ts
         p->inner = r.algo;
         p->k = r.k;
         p->unpinned = r.unpinned;
+        p->via = r.via;
         return 0;
     }
     }

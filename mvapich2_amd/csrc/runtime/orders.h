@@ -73,11 +73,20 @@ struct Knobs {
 const Knobs &knobs();  // parsed from the environment on first use
 void knobs_reload();   // re-read the environment (tests)
 
+// Plan::via: how the reference reached the algorithm (for the MPI_T counters
+// of its call chain, runtime/pvars.cpp)
+enum : int {
+    VIA_RS_ENTRY = 1,          // recursive doubling run inside MPIR_Allreduce_pt2pt_rs_MV2 (:802)
+    VIA_TWO_LEVEL_HELPER = 2,  // reduce through MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2030)
+};
+
 struct Plan {
     int algo;    // Algo
     int inner;   // ALG_TWO_LEVEL_P2P / ALG_RS_BASIC: the MPIR_Reduce_MV2 algorithm inside
     int k;       // knomial factor / shm tree degree
     int unpinned;// 1: the reference result depends on message arrival (knomial Waitany)
+    int via;     // VIA_* bits
+    int pad;
     ProgSet ps;  // order of every element of this rank's result (global element index)
 };
 

@@ -85,6 +85,14 @@ def big_case(L, case, rank, n):
     raise ValueError(k)
 
 
+_COMM = ctypes.c_void_p(0xC0FFEE0)  # stands for MVAPICH2's MPID_Comm * (opaque to the plugin)
+
+
+def collops_comm(L, rank, n):
+    assert L.MV2AMD_Comm_attach(_COMM, rank, n) == 0
+    return _COMM
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     out = sys.argv[2]
@@ -111,7 +119,14 @@ def main():
             rb = m.DeviceBuffer(count * ext)
             rb.upload(np.full(count * ext, 0xA5, dtype=np.uint8))
             op = OPS[case["op"]]
-            if k == "allreduce":
+            if case.get("via") == "collops":  # include/mv2amd_collops.h (MPID_Collops entries)
+                comm, err = collops_comm(L, rank, n), ctypes.c_int(0)
+                if k == "allreduce":
+                    rc = L.MV2AMD_Allreduce(sb.ptr, rb.ptr, count, h, op, comm, ctypes.byref(err))
+                else:
+                    rc = L.MV2AMD_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], comm, ctypes.byref(err))
+                assert err.value == 0
+            elif k == "allreduce":
                 rc = L.MPI_Allreduce(sb.ptr, rb.ptr, count, h, op, WORLD)
             elif k == "allreduce_inplace":
                 rc = L.MPI_Allreduce(ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF), sb.ptr, count, h, op, WORLD)
@@ -125,26 +140,75 @@ def main():
                 rc = L.MPI_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * ext)
+        elif k == "mpit_counts":  # MPI_T: start every counter, run the calls, read the counters
+            prov = ctypes.c_int()
+            assert L.MPI_T_init_thread(3, ctypes.byref(prov)) == 0
+            sess, npv = ctypes.c_void_p(), ctypes.c_int()
+            assert L.MPI_T_pvar_session_create(ctypes.byref(sess)) == 0
+            assert L.MPI_T_pvar_get_num(ctypes.byref(npv)) == 0
+            names, handles = [], []
+            for i in range(npv.value):
+                nm, nl, cls = ctypes.create_string_buffer(128), ctypes.c_int(128), ctypes.c_int()
+                assert L.MPI_T_pvar_get_info(i, nm, ctypes.byref(nl), None, ctypes.byref(cls), None, None, None, None,
+                                             None, None, None, None) == 0
+                if cls.value != 246:  # counters only
+                    continue
+                hd, cnt = ctypes.c_void_p(), ctypes.c_int()
+                assert L.MPI_T_pvar_handle_alloc(sess, i, None, ctypes.byref(hd), ctypes.byref(cnt)) == 0
+                names.append(nm.value.decode())
+                handles.append(hd)
+            assert L.MPI_T_pvar_start(sess, ctypes.c_void_p.in_dll(L, "MPI_T_PVAR_ALL_HANDLES")) == 0
+            for call in case["calls"]:
+                cnt, tt = call["count"], TYPES[call["type"]][0]
+                e = TYPES[call["type"]][3]
+                sb, rb = m.DeviceBuffer(max(16, cnt * e * n)), m.DeviceBuffer(max(16, cnt * e * n))
+                if call["coll"] == "allreduce":
+                    src = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF) if call.get("in_place") else sb.ptr
+                    rc = L.MPI_Allreduce(src, rb.ptr, cnt, tt, OPS["MPI_SUM"], WORLD)
+                elif call["coll"] == "reduce":
+                    rc = L.MPI_Reduce(sb.ptr, rb.ptr, cnt, tt, OPS["MPI_SUM"], call["root"], WORLD)
+                else:
+                    rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, (ctypes.c_int * n)(*([cnt] * n)), tt, OPS["MPI_SUM"],
+                                              WORLD)
+                assert rc == 0, (call, rc)
+            assert L.MPI_T_pvar_stop(sess, ctypes.c_void_p.in_dll(L, "MPI_T_PVAR_ALL_HANDLES")) == 0
+            vals = {}
+            for nm, hd in zip(names, handles):
+                v = ctypes.c_ulonglong()
+                assert L.MPI_T_pvar_read(sess, hd, ctypes.byref(v)) == 0
+                vals[nm] = v.value
+            assert L.MPI_T_pvar_session_free(ctypes.byref(sess)) == 0
+            assert L.MPI_T_finalize() == 0
+            res = np.frombuffer(json.dumps(vals).encode(), dtype=np.uint8)
         elif k == "reduce_scatter":
             counts = case["recvcounts"]
             x = inputs(dict(case, count=sum(counts)), rank)
             sb = m.DeviceBuffer.from_array(x)
             rb = m.DeviceBuffer(max(1, counts[rank]) * ext)
             arr = (ctypes.c_int * n)(*counts)
-            rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, h, OPS[case["op"]], WORLD)
+            if case.get("via") == "collops":
+                rc = L.MV2AMD_Reduce_scatter(sb.ptr, rb.ptr, arr, h, OPS[case["op"]], collops_comm(L, rank, n), None)
+            else:
+                rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, h, OPS[case["op"]], WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=counts[rank] * ext)
         elif k == "allgather":
             x = inputs(case, rank)
             sb = m.DeviceBuffer.from_array(x)
             rb = m.DeviceBuffer(count * ext * n)
-            rc = L.MPI_Allgather(sb.ptr, count, h, rb.ptr, count, h, WORLD)
+            if case.get("via") == "collops":
+                rc = L.MV2AMD_Allgather(sb.ptr, count, h, rb.ptr, count, h, collops_comm(L, rank, n), None)
+            else:
+                rc = L.MPI_Allgather(sb.ptr, count, h, rb.ptr, count, h, WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * ext * n)
         elif k == "bcast":
             x = inputs(case, rank)
             b = m.DeviceBuffer.from_array(x)
-            rc = L.MPI_Bcast(b.ptr, count, h, case["root"], WORLD)
+            if case.get("via") == "collops":
+                rc = L.MV2AMD_Bcast(b.ptr, count, h, case["root"], collops_comm(L, rank, n), None)
+            else:
+                rc = L.MPI_Bcast(b.ptr, count, h, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
             res = b.download(np.uint8, count=count * ext)
         elif k == "user_allreduce":

@@ -99,3 +99,24 @@ def test_op_table_check_dtype_matches_legality():
             want = 0 if L.mv2h_op_check(oh, h) == 0 else 9  # MPI_ERR_OP
             assert fn(h) == want, (op, t)
         assert fn(0x1234) == 3  # not a datatype: MPI_ERR_TYPE
+
+
+def test_collops_plugin_symbols_and_attach_without_world():
+    """include/mv2amd_collops.h (MPID_Collops members, mpiimpl.h:1999-2033): every entry is
+    exported; a communicator that is not the node world is refused with MPI_ERR_COMM and every
+    entry then returns MPI_ERR_COMM before touching data (the caller falls back)."""
+    txt = open(os.path.join(ROOT, "include", "mv2amd_collops.h")).read()
+    names = set(re.findall(r"^\s*int\s+(MV2AMD_\w+)\(", txt, flags=re.M))
+    assert len(names) == 10
+    syms = exported()
+    assert not sorted(n for n in names if n not in syms)
+    L = m.lib()
+    fake = ctypes.c_void_p(0x1000)
+    assert L.MV2AMD_Comm_attach(fake, 0, 99) == 5  # MPI_ERR_COMM: not this world's size
+    err = ctypes.c_int(0)
+    assert L.MV2AMD_Allreduce(None, None, 4, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], fake, ctypes.byref(err)) == 5
+    assert L.MV2AMD_Barrier(fake, ctypes.byref(err)) == 5
+    assert err.value == 0
+    ops = (ctypes.c_void_p * 7)()
+    assert L.MV2AMD_Collops_get(ops) == 0
+    assert all(ops)

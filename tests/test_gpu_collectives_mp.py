@@ -135,6 +135,21 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
     cases.append({"id": f"x8{seed}", "kind": "reduce_scatter", "type": "MPI_LONG_DOUBLE", "op": "MPI_SUM",
                   "recvcounts": [5000 + r for r in range(n)], "count": sum(5000 + r for r in range(n)), "seed": seed})
     seed += 1
+    # the same calls through the coll-function-table plugin (include/mv2amd_collops.h)
+    for kind, t, op, count in (("allreduce", "MPI_FLOAT", "MPI_SUM", 301), ("allreduce", "MPI_DOUBLE", "MPI_SUM", 300007),
+                               ("reduce", "MPI_FLOAT", "MPI_SUM", 70001)):
+        cases.append({"id": f"co{seed}", "kind": kind, "type": t, "op": op, "count": count, "seed": seed,
+                      "root": n - 1, "via": "collops"})
+        seed += 1
+    cases.append({"id": f"co{seed}", "kind": "reduce_scatter", "type": "MPI_FLOAT", "op": "MPI_SUM", "via": "collops",
+                  "recvcounts": [9000 + r for r in range(n)], "count": sum(9000 + r for r in range(n)), "seed": seed})
+    seed += 1
+    cases.append({"id": f"co{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": 100003,
+                  "seed": seed, "via": "collops"})
+    seed += 1
+    cases.append({"id": f"co{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": 70001,
+                  "seed": seed, "root": 1 % n, "via": "collops"})
+    seed += 1
     for counts in ([1] * n, [1000 + r for r in range(n)], [70001] * n, [65536] * n, [0] + [33] * (n - 1)):
         cases.append({"id": f"rs{seed}", "kind": "reduce_scatter", "type": "MPI_INT", "op": "MPI_SUM",
                       "recvcounts": counts, "count": sum(counts), "seed": seed})
@@ -354,3 +369,32 @@ def test_full_size_baseline_configs(n, tmp_path):
     for case in cases:
         for r in range(n):
             assert int(res(case["id"], r)[0]) == 0, (case["id"], r, int(res(case["id"], r)[0]))
+
+
+def test_mpit_counters_follow_the_selection(tmp_path):
+    """MPI_T (mpi/mpit.cpp): a started counter handle counts the calls of the algorithms the
+    reference's call chain runs for each call (its MPIR_T_PVAR_COUNTER_INC sites), 4 ranks:
+      allreduce 8 B          topo-aware tree                     allreduce_osu.c:2279
+      allreduce 4000 B       pt2pt_rs (16ppn table)              :640
+      allreduce 524291 fp32  ring wrapper, ring body, pt2pt_rs on the 3-element remainder  :3762, :3899, :640
+      allreduce 2 MiB IN_PLACE  ring wrapper, in-place body falls back to pt2pt_rs (:4095) :3762, :640
+      reduce 400 B           two-level helper + MPIR_Reduce_shmem_MV2 (+ shmem coll call)  reduce_osu.c:2039, :1187
+      reduce 4 KiB           knomial (CMA 16ppn table inter entry)                         :1672
+      reduce_scatter 4x100 int   recursive halving                                         red_scat_osu.c:456
+      reduce_scatter 4x70001 int ring                                                      :1039"""
+    n = 4
+    calls = [{"coll": "allreduce", "type": "MPI_FLOAT", "count": 2}, {"coll": "allreduce", "type": "MPI_FLOAT", "count": 1000},
+             {"coll": "allreduce", "type": "MPI_FLOAT", "count": 524291},
+             {"coll": "allreduce", "type": "MPI_FLOAT", "count": 524288, "in_place": True},
+             {"coll": "reduce", "type": "MPI_FLOAT", "count": 100, "root": 1},
+             {"coll": "reduce", "type": "MPI_FLOAT", "count": 1024, "root": 2},
+             {"coll": "reduce_scatter", "type": "MPI_INT", "count": 100},
+             {"coll": "reduce_scatter", "type": "MPI_INT", "count": 70001}]
+    res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path)
+    want = {"mv2_coll_allreduce_topo_aware_hierarchical": 1, "mv2_coll_allreduce_shm_rs": 3,
+            "mv2_coll_allreduce_pt2pt_ring_wrapper": 2, "mv2_coll_allreduce_pt2pt_ring": 1,
+            "mv2_coll_reduce_two_level_helper": 1, "mv2_coll_reduce_shmem": 1, "mv2_num_shmem_coll_calls": 1,
+            "mv2_coll_reduce_knomial": 1, "mv2_coll_reduce_scatter_rec_halving": 1, "mv2_coll_reduce_scatter_ring": 1}
+    for r in range(n):
+        got = json.loads(res("mpit", r).tobytes().decode())
+        assert {k: v for k, v in got.items() if v} == want, (r, got)
