@@ -85,6 +85,7 @@ def big_case(L, case, rank, n):
     raise ValueError(k)
 
 
+P = ctypes.c_void_p  # the plugin entries have no ctypes prototypes: pass pointers as pointers
 _COMM = ctypes.c_void_p(0xC0FFEE0)  # stands for MVAPICH2's MPID_Comm * (opaque to the plugin)
 
 
@@ -122,9 +123,9 @@ def main():
             if case.get("via") == "collops":  # include/mv2amd_collops.h (MPID_Collops entries)
                 comm, err = collops_comm(L, rank, n), ctypes.c_int(0)
                 if k == "allreduce":
-                    rc = L.MV2AMD_Allreduce(sb.ptr, rb.ptr, count, h, op, comm, ctypes.byref(err))
+                    rc = L.MV2AMD_Allreduce(P(sb.ptr), P(rb.ptr), count, h, op, comm, ctypes.byref(err))
                 else:
-                    rc = L.MV2AMD_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], comm, ctypes.byref(err))
+                    rc = L.MV2AMD_Reduce(P(sb.ptr), P(rb.ptr), count, h, op, case["root"], comm, ctypes.byref(err))
                 assert err.value == 0
             elif k == "allreduce":
                 rc = L.MPI_Allreduce(sb.ptr, rb.ptr, count, h, op, WORLD)
@@ -187,7 +188,7 @@ def main():
             rb = m.DeviceBuffer(max(1, counts[rank]) * ext)
             arr = (ctypes.c_int * n)(*counts)
             if case.get("via") == "collops":
-                rc = L.MV2AMD_Reduce_scatter(sb.ptr, rb.ptr, arr, h, OPS[case["op"]], collops_comm(L, rank, n), None)
+                rc = L.MV2AMD_Reduce_scatter(P(sb.ptr), P(rb.ptr), arr, h, OPS[case["op"]], collops_comm(L, rank, n), None)
             else:
                 rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, h, OPS[case["op"]], WORLD)
             assert rc == 0, (case["id"], rc)
@@ -197,7 +198,7 @@ def main():
             sb = m.DeviceBuffer.from_array(x)
             rb = m.DeviceBuffer(count * ext * n)
             if case.get("via") == "collops":
-                rc = L.MV2AMD_Allgather(sb.ptr, count, h, rb.ptr, count, h, collops_comm(L, rank, n), None)
+                rc = L.MV2AMD_Allgather(P(sb.ptr), count, h, P(rb.ptr), count, h, collops_comm(L, rank, n), None)
             else:
                 rc = L.MPI_Allgather(sb.ptr, count, h, rb.ptr, count, h, WORLD)
             assert rc == 0, (case["id"], rc)
@@ -206,7 +207,7 @@ def main():
             x = inputs(case, rank)
             b = m.DeviceBuffer.from_array(x)
             if case.get("via") == "collops":
-                rc = L.MV2AMD_Bcast(b.ptr, count, h, case["root"], collops_comm(L, rank, n), None)
+                rc = L.MV2AMD_Bcast(P(b.ptr), count, h, case["root"], collops_comm(L, rank, n), None)
             else:
                 rc = L.MPI_Bcast(b.ptr, count, h, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
