@@ -149,6 +149,19 @@ enum mv2h_coll {
  * *unpinned = 1 when the reference's own result depends on message arrival. */
 int mv2h_plan(int coll, int n, int rank, int root, size_t count, const size_t *counts, int dtype, int opkind,
               int in_place, int *algo, int *inner, int *unpinned, mv2h_progset *ps);
+/* Nonblocking initiation: between mv2h_nbc_begin(kind) and mv2h_nbc_end() on this thread
+ * the reducing collectives take the reference's nonblocking selection (MPIR_Iallreduce_MV2,
+ * MPIR_Ireduce_MV2, MPIR_Ireduce_scatter_MV2, MPICH MPIR_Ireduce_scatter_block_intra) and
+ * its reduction order instead of the blocking one. */
+enum mv2h_nbc {
+    MV2H_NBC_NONE = 0,
+    MV2H_NBC_IALLREDUCE = 1,
+    MV2H_NBC_IREDUCE = 2,
+    MV2H_NBC_IREDUCE_SCATTER = 3,
+    MV2H_NBC_IREDUCE_SCATTER_BLOCK = 4
+};
+int mv2h_nbc_begin(int kind);
+int mv2h_nbc_end(void);
 int mv2h_knobs_reload(void);
 /* dst = reduce(srcs[0..nsrc-1]) by the programs of *ps (single GPU; order tests) */
 int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t count, int dtype, int op,

@@ -70,6 +70,8 @@ def lib():
         "mv2h_plan": ([c_int, c_int, c_int, c_int, c_sz, ctypes.POINTER(c_sz), c_int, c_int, c_int,
                        ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_vp], c_int),
         "mv2h_knobs_reload": ([], c_int),
+        "mv2h_nbc_begin": ([c_int], c_int),
+        "mv2h_nbc_end": ([], c_int),
         "mv2h_get_info": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_long)], c_int),
         "mv2h_reduce_n_prog": ([ctypes.POINTER(c_vp), c_int, c_vp, c_sz, c_int, c_int, c_vp, c_vp], c_int),
         "MPI_Init": ([c_vp, c_vp], c_int),
@@ -222,6 +224,25 @@ def plan(coll, n, rank, dtype_handle, count=0, counts=None, root=0, opkind=0, in
                       ctypes.byref(inner), ctypes.byref(unp), ctypes.byref(ps)), "mv2h_plan")
     progs = [([(p.dst[i], p.src[i]) for i in range(p.nsteps)], p.res) for p in ps.p[:ps.nprog]]
     return algo.value, inner.value, unp.value, progs, ps.blk
+
+
+NBC = {"iallreduce": 1, "ireduce": 2, "ireduce_scatter": 3, "reduce_scatter_block": 4}
+
+
+class nbc:
+    """Context: plan() / the reducing collectives take the nonblocking selection `kind`
+    (or MPI_Reduce_scatter_block's) on this thread (mv2h_nbc_begin / mv2h_nbc_end)."""
+
+    def __init__(self, kind):
+        self.kind = NBC[kind]
+
+    def __enter__(self):
+        check(lib().mv2h_nbc_begin(self.kind), "mv2h_nbc_begin")
+        return self
+
+    def __exit__(self, *exc):
+        lib().mv2h_nbc_end()
+        return False
 
 
 def knobs_reload():

@@ -128,7 +128,12 @@ int MV2AMD_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcoun
     if (int rc = check_reduce(dt, op, &ext)) return rc;
     if (recvcount < 0) return MPI_ERR_COUNT;
     std::vector<size_t> counts((size_t)mv2h_size(), (size_t)recvcount);
-    return fail(mv2h_reduce_scatter(sendbuf, recvbuf, counts.data(), dt, op, nullptr), errflag);
+    // MPIR_Reduce_scatter_block_MV2 runs MPICH's reduce_scatter_block selection (see
+    // PMPI_Reduce_scatter_block, mpi_api.cpp)
+    mv2h_nbc_begin(MV2H_NBC_IREDUCE_SCATTER_BLOCK);
+    const int rc = mv2h_reduce_scatter(sendbuf, recvbuf, counts.data(), dt, op, nullptr);
+    mv2h_nbc_end();
+    return fail(rc, errflag);
 }
 
 int MV2AMD_Collops_get(MV2AMD_Collops *ops) {

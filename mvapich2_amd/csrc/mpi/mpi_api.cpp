@@ -727,9 +727,18 @@ int MPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[
 
 int PMPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
                               MPI_Comm comm) {
+    // MVAPICH2's MPIR_Reduce_scatter_block_MV2 never sizes the message (nbytes stays 0,
+    // red_scat_block_osu.c:320-372), so the default table's first entry runs: MPICH's
+    // MPIR_Reduce_scatter_block (red_scat_block.c:305, :515: recursive halving below
+    // MPIR_CVAR_REDSCAT_COMMUTATIVE_LONG_MSG_SIZE, pairwise from it) — the same
+    // selection as MPI_Ireduce_scatter_block's schedule
     const int n = comm == MPI_COMM_SELF ? 1 : world().size;
     std::vector<int> counts(n, recvcount);
-    return PMPI_Reduce_scatter(sendbuf, recvbuf, counts.data(), dt, op, comm);
+    const bool set = nbc_kind() == NBC_NONE;
+    if (set) nbc_set(NBC_IREDUCE_SCATTER_BLOCK);
+    const int rc = PMPI_Reduce_scatter(sendbuf, recvbuf, counts.data(), dt, op, comm);
+    if (set) nbc_set(NBC_NONE);
+    return rc;
 }
 int MPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
                              MPI_Comm comm) WEAK(MPI_Reduce_scatter_block);
@@ -916,10 +925,12 @@ int req_test(MReq &r, int *flag, MPI_Status *st) {
 // nonblocking collective = the blocking implementation initiated with
 // deferred completion (the kernel is enqueued, the ticket waits later)
 template <class F>
-int start_coll(MPI_Request *request, const char *fn, F &&call) {
+int start_coll(MPI_Request *request, const char *fn, F &&call, int nbc = MV2H_NBC_NONE) {
     if (!request) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, fn);
     mv2h_defer_begin();
+    mv2h_nbc_begin(nbc);  // the nonblocking selection and reduction order (runtime/orders.h)
     const int rc = call();
+    mv2h_nbc_end();
     unsigned long long t = 0;
     mv2h_defer_end(&t);
     if (rc) return rc;  // already passed through the error handler
@@ -1020,7 +1031,9 @@ extern "C" {
 int PMPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm,
                     MPI_Request *request) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
-    return start_coll(request, "MPI_Iallreduce", [&] { return PMPI_Allreduce(sendbuf, recvbuf, count, dt, op, comm); });
+    return start_coll(
+        request, "MPI_Iallreduce", [&] { return PMPI_Allreduce(sendbuf, recvbuf, count, dt, op, comm); },
+        MV2H_NBC_IALLREDUCE);
 }
 int MPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm,
                    MPI_Request *request) WEAK(MPI_Iallreduce);
@@ -1028,7 +1041,9 @@ int MPI_Iallreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
 int PMPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm,
                  MPI_Request *request) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
-    return start_coll(request, "MPI_Ireduce", [&] { return PMPI_Reduce(sendbuf, recvbuf, count, dt, op, root, comm); });
+    return start_coll(
+        request, "MPI_Ireduce", [&] { return PMPI_Reduce(sendbuf, recvbuf, count, dt, op, root, comm); },
+        MV2H_NBC_IREDUCE);
 }
 int MPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm,
                 MPI_Request *request) WEAK(MPI_Ireduce);
@@ -1036,8 +1051,9 @@ int MPI_Ireduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
 int PMPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
                          MPI_Comm comm, MPI_Request *request) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
-    return start_coll(request, "MPI_Ireduce_scatter",
-                      [&] { return PMPI_Reduce_scatter(sendbuf, recvbuf, recvcounts, dt, op, comm); });
+    return start_coll(
+        request, "MPI_Ireduce_scatter", [&] { return PMPI_Reduce_scatter(sendbuf, recvbuf, recvcounts, dt, op, comm); },
+        MV2H_NBC_IREDUCE_SCATTER);
 }
 int MPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
                         MPI_Comm comm, MPI_Request *request) WEAK(MPI_Ireduce_scatter);
@@ -1045,8 +1061,10 @@ int MPI_Ireduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts
 int PMPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
                                MPI_Comm comm, MPI_Request *request) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
-    return start_coll(request, "MPI_Ireduce_scatter_block",
-                      [&] { return PMPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, dt, op, comm); });
+    return start_coll(
+        request, "MPI_Ireduce_scatter_block",
+        [&] { return PMPI_Reduce_scatter_block(sendbuf, recvbuf, recvcount, dt, op, comm); },
+        MV2H_NBC_IREDUCE_SCATTER_BLOCK);
 }
 int MPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype dt, MPI_Op op,
                               MPI_Comm comm, MPI_Request *request) WEAK(MPI_Ireduce_scatter_block);

@@ -674,6 +674,16 @@ int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t coun
     return finish(st, world().timing);
 }
 
+int mv2h_nbc_begin(int kind) {
+    if (kind < MV2H_NBC_NONE || kind > MV2H_NBC_IREDUCE_SCATTER_BLOCK) return E_ARG;
+    nbc_set(kind);
+    return 0;
+}
+int mv2h_nbc_end(void) {
+    nbc_set(NBC_NONE);
+    return 0;
+}
+
 int mv2h_knobs_reload(void) {
     knobs_reload();
     return 0;

@@ -109,6 +109,12 @@ void knobs_reload() {
     if (env_set("MV2_TOPO_AWARE_REDUCE_NODE_THRESHOLD", &v)) k.topo_red_nodes = atoi(v);
     // CMA selects the reduce tables (reduce_tuning.c:1578-1629; ibv_param.c:716)
     if (env_set("MV2_SMP_USE_CMA", &v)) k.smp_use_cma = !!atoi(v);
+    k.reduce_short_msg = 2048;
+    k.redscat_comm_long = 524288;
+    if (env_set("MPIR_CVAR_REDUCE_SHORT_MSG_SIZE", &v) || env_set("MPICH_REDUCE_SHORT_MSG_SIZE", &v))
+        k.reduce_short_msg = atoi(v);
+    if (env_set("MPIR_CVAR_REDSCAT_COMMUTATIVE_LONG_MSG_SIZE", &v) || env_set("MPICH_REDSCAT_COMMUTATIVE_LONG_MSG_SIZE", &v))
+        k.redscat_comm_long = atoi(v);
     g_knobs = k;
     g_knobs_ok = true;
     ++g_knobs_gen;
@@ -704,6 +710,59 @@ static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int ts
 }
 
 // ---------------------------------------------------------------------------
+// Nonblocking collectives (one node, <= 8 ranks: the first row of each default
+// nonblocking table, i.e. the unlisted-architecture "RI" tables)
+// ---------------------------------------------------------------------------
+static thread_local int t_nbc = NBC_NONE;
+void nbc_set(int kind) { t_nbc = kind; }
+int nbc_kind() { return t_nbc; }
+
+// MPIR_Iallreduce_intra_MV2 (iallreduce_osu.c:186-261) -> iallreduce_tuning.c:184-190:
+// MPIR_Iallreduce_naive (iallreduce.c:109-139) = MPIR_Ireduce_intra to rank 0
+// (ireduce.c:700-731: redscat_gather for builtin ops above
+// MPIR_CVAR_REDUCE_SHORT_MSG_SIZE with count >= pof2, else binomial) + MPIR_Ibcast:
+// every rank ends with rank 0's result.  The schedules reduce like the blocking
+// algorithms (ireduce.c:219-224 binomial; :408-439, :524 redscat_gather).
+static int plan_iallreduce_build(int n, int me, size_t count, int tsize, Plan *p, int opk) {
+    (void)me;
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    const long nbytes = (long)count * tsize;
+    if (nbytes > knobs().reduce_short_msg && opk == OPK_BUILTIN && count >= (size_t)pof2_of(n))
+        return reduce_fill(p, ALG_REDSCAT_GATHER, n, 0, count, 0);
+    return reduce_fill(p, ALG_BINOMIAL, n, 0, count, 0, opk == OPK_USER_NONCOMM);
+}
+
+// MPIR_Ireduce_intra_MV2 (ireduce_osu.c:115-) -> ireduce_tuning.c default first row:
+// MPIR_Ireduce_binomial (its tune helper only diverts redscat_gather, ireduce_osu.c:97-105)
+static int plan_ireduce_build(int n, int root, size_t count, Plan *p, int opk) {
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    return reduce_fill(p, ALG_BINOMIAL, n, root, count, 0, opk == OPK_USER_NONCOMM);
+}
+
+// MPI_Ireduce_scatter: MPIR_Ireduce_scatter_MV2 -> ired_scat_tuning.c default first row:
+// MPIR_Ireduce_scatter_pairwise for commutative ops (ired_scat_osu.c:187-190; the
+// schedule reduces like the blocking Pair_Wise, ired_scat.c:404-440).
+// MPI_Ireduce_scatter_block: MPICH's MPIR_Ireduce_scatter_block_intra
+// (ired_scat_block.c:882-920): recursive halving below
+// MPIR_CVAR_REDSCAT_COMMUTATIVE_LONG_MSG_SIZE, pairwise from it (the schedules
+// reduce like the blocking Rec_Halving / Pair_Wise, ired_scat_block.c:150-215).
+static int plan_ireduce_scatter_build(int n, int me, const size_t *counts, int tsize, bool block, Plan *p, int opk) {
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    if (opk == OPK_USER_NONCOMM) return E_INTERN;  // noncomm / rec_dbl schedules: not restated
+    size_t total = 0;
+    for (int j = 0; j < n; ++j) total += counts[j];
+    const long nbytes = (long)total * tsize;
+    p->algo = (block && nbytes < knobs().redscat_comm_long) ? ALG_RS_REC_HALVING : ALG_RS_PAIRWISE;
+    Sym s;
+    if (p->algo == ALG_RS_PAIRWISE) return single_expr(s, rs_pairwise_expr(s, n, me), p->ps) ? 0 : E_INTERN;
+    const int e = rs_rec_halving_expr(s, n, me);
+    return (e >= 0 && single_expr(s, e, p->ps)) ? 0 : E_INTERN;
+}
+
+// ---------------------------------------------------------------------------
 // plan cache: a plan is a pure function of its arguments and the knobs, and
 // latency-bound loops repeat the same call, so the last plans of this thread
 // are kept (the symbolic run costs 3-6 us per call on the host).
@@ -763,17 +822,28 @@ int cached(const PlanKey &k, Plan *p, F build) {
 }  // namespace
 
 int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *p, int opk) {
+    if (t_nbc == NBC_IALLREDUCE && !forced)
+        return cached(make_key(3, n, me, 0, count, nullptr, tsize, textent, in_place, 0, opk), p,
+                      [&] { return plan_iallreduce_build(n, me, count, tsize, p, opk); });
     return cached(make_key(0, n, me, 0, count, nullptr, tsize, textent, in_place, forced, opk), p,
                   [&] { return plan_allreduce_build(n, me, count, tsize, textent, in_place, forced, p, opk); });
 }
 
 int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *p, int opk) {
+    if (t_nbc == NBC_IREDUCE)
+        return cached(make_key(4, n, me, root, count, nullptr, tsize, textent, false, 0, opk), p,
+                      [&] { return plan_ireduce_build(n, root, count, p, opk); });
     return cached(make_key(1, n, me, root, count, nullptr, tsize, textent, false, 0, opk), p,
                   [&] { return plan_reduce_build(n, me, root, count, tsize, textent, p, opk); });
 }
 
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *p, int opk) {
     if (n > kMaxRanks) return plan_reduce_scatter_build(n, me, counts, tsize, textent, p, opk);
+    if (t_nbc == NBC_IREDUCE_SCATTER || t_nbc == NBC_IREDUCE_SCATTER_BLOCK) {
+        const bool block = t_nbc == NBC_IREDUCE_SCATTER_BLOCK;
+        return cached(make_key(block ? 6 : 5, n, me, 0, 0, counts, tsize, textent, false, 0, opk), p,
+                      [&] { return plan_ireduce_scatter_build(n, me, counts, tsize, block, p, opk); });
+    }
     return cached(make_key(2, n, me, 0, 0, counts, tsize, textent, false, 0, opk), p,
                   [&] { return plan_reduce_scatter_build(n, me, counts, tsize, textent, p, opk); });
 }

@@ -68,6 +68,10 @@ struct Knobs {
     int32_t shmem_coll_max_msg;         // MV2_SHMEM_COLL_MAX_MSG_SIZE (32 KiB)
     int32_t shmem_intra_reduce_msg;     // MV2_INTRA_SHMEM_REDUCE_MSG (2048)
     int64_t red_scat_ring_thr;          // MV2_RED_SCAT_RING_ALGO_THRESHOLD (131072, user_val_to_bytes)
+    // MPICH cvars of the nonblocking schedules (MPIR_CVAR_*, also MPICH_* env names)
+    int32_t reduce_short_msg;           // MPIR_CVAR_REDUCE_SHORT_MSG_SIZE (2048, reduce.c:28-31)
+    int32_t pad1;
+    int64_t redscat_comm_long;          // MPIR_CVAR_REDSCAT_COMMUTATIVE_LONG_MSG_SIZE (524288, red_scat.c)
 };
 
 const Knobs &knobs();  // parsed from the environment on first use
@@ -106,6 +110,22 @@ int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, P
 // counts[n] per-rank block counts; elements are indexed over the whole operand
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *out,
                         int opk = OPK_BUILTIN);
+
+// Nonblocking collectives.  While a nonblocking call is being initiated
+// (nbc_set(kind) on this thread), plan_allreduce / plan_reduce /
+// plan_reduce_scatter restate the nonblocking selection instead of the
+// blocking one: MVAPICH2 installs MPIR_Iallreduce_MV2 / MPIR_Ireduce_MV2 /
+// MPIR_Ireduce_scatter_MV2 (ch3i_comm.c:38-43, enabled by default,
+// ch3_shmem_coll.c:432-441) and MPICH's MPIR_Ireduce_scatter_block_intra.
+enum NbcKind : int {
+    NBC_NONE = 0,
+    NBC_IALLREDUCE = 1,
+    NBC_IREDUCE = 2,
+    NBC_IREDUCE_SCATTER = 3,
+    NBC_IREDUCE_SCATTER_BLOCK = 4,  // also the blocking MPI_Reduce_scatter_block (same MPICH selection)
+};
+void nbc_set(int kind);
+int nbc_kind();
 
 const char *algo_name(int algo);
 

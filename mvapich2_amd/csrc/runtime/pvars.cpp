@@ -130,13 +130,15 @@ void pvar_begin() {
 }
 
 void pvar_note_id(int id) {
-    if (t_rec.depth != 1 || t_rec.noted) return;
+    if (t_rec.depth != 1 || t_rec.noted || nbc_kind() != NBC_NONE) return;
     t_rec.noted = true;
     push(id);
 }
 
 void pvar_note(int coll, const Plan &p, bool in_place, size_t count, int n) {
-    if (t_rec.depth != 1 || t_rec.noted || p.algo == ALG_NONE) return;
+    // nonblocking initiations run the MPI_I* schedules, whose mv2_coll_i* counters are not
+    // among these variables
+    if (t_rec.depth != 1 || t_rec.noted || p.algo == ALG_NONE || nbc_kind() != NBC_NONE) return;
     t_rec.noted = true;
     switch (coll) {
     case PV_COLL_ALLREDUCE:

@@ -75,6 +75,8 @@ def lib():
         L.oracle_reduce.argtypes = [ctypes.POINTER(vp), vp, i, l, i, i, i, i, kp, i]
         L.oracle_reduce_scatter_select.argtypes = [i, ctypes.POINTER(l), i, kp]
         L.oracle_reduce_scatter.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(l), vp, i, i, kp, i]
+        L.oracle_iallreduce_select.argtypes = [i, l, i, i, l]
+        L.oracle_reduce_scatter_block_select.argtypes = [i, l, i, l]
         _lib = L
     return _lib
 
@@ -197,3 +199,24 @@ def reduce_scatter_ref(srcs, counts, dtype_handle, op_handle, knobs=None, algo=-
     if rc:
         raise RuntimeError(f"oracle_reduce_scatter rc={rc}")
     return dst
+
+
+def iallreduce_select(n, count, dtype_handle, opkind=0, short_msg=2048):
+    """MPI_Iallreduce on one node: naive = Ireduce to rank 0 (binomial or redscat_gather) + Ibcast"""
+    return lib().oracle_iallreduce_select(n, count, dtype_handle, opkind, short_msg)
+
+
+def iallreduce_ref(sends, count, dtype_handle, op_handle, opkind=0, short_msg=2048):
+    """every rank's MPI_Iallreduce result: rank 0's Ireduce result"""
+    a = iallreduce_select(len(sends), count, dtype_handle, opkind, short_msg)
+    r0 = reduce_ref(sends, count, dtype_handle, op_handle, 0, opkind=opkind, algo=a)
+    return [r0.copy() for _ in sends]
+
+
+def ireduce_ref(sends, count, dtype_handle, op_handle, root, opkind=0):
+    """MPI_Ireduce on one node: MPIR_Ireduce_binomial"""
+    return reduce_ref(sends, count, dtype_handle, op_handle, root, opkind=opkind, algo=ALGOS.index("binomial"))
+
+
+def reduce_scatter_block_select(n, recvcount, dtype_handle, long_msg=524288):
+    return lib().oracle_reduce_scatter_block_select(n, recvcount, dtype_handle, long_msg)

@@ -109,7 +109,7 @@ def main():
         h, ext = TYPES[t][0], TYPES[t][3]
         count = case.get("count", 0)
         res = None
-        if k in ("allreduce", "allreduce_inplace", "reduce", "iallreduce"):
+        if k in ("allreduce", "allreduce_inplace", "reduce", "iallreduce", "ireduce"):
             if "golden" in case:
                 if golden is None:
                     golden = np.load(os.path.join(ROOT, "tests", "golden", "golden.npz"), allow_pickle=False)
@@ -135,6 +135,11 @@ def main():
             elif k == "iallreduce":  # nonblocking: initiate, then MPI_Wait (completion word)
                 req = ctypes.c_int()
                 rc = L.MPI_Iallreduce(sb.ptr, rb.ptr, count, h, op, WORLD, ctypes.byref(req))
+                if rc == 0:
+                    rc = L.MPI_Wait(ctypes.byref(req), None)
+            elif k == "ireduce":
+                req = ctypes.c_int()
+                rc = L.MPI_Ireduce(sb.ptr, rb.ptr, count, h, op, case["root"], WORLD, ctypes.byref(req))
                 if rc == 0:
                     rc = L.MPI_Wait(ctypes.byref(req), None)
             else:
@@ -189,6 +194,17 @@ def main():
             arr = (ctypes.c_int * n)(*counts)
             if case.get("via") == "collops":
                 rc = L.MV2AMD_Reduce_scatter(P(sb.ptr), P(rb.ptr), arr, h, OPS[case["op"]], collops_comm(L, rank, n), None)
+            elif case.get("via") in ("block", "iblock", "inb"):
+                req = ctypes.c_int()
+                if case["via"] == "block":
+                    rc = L.MPI_Reduce_scatter_block(P(sb.ptr), P(rb.ptr), counts[0], h, OPS[case["op"]], WORLD)
+                elif case["via"] == "iblock":
+                    rc = L.MPI_Ireduce_scatter_block(P(sb.ptr), P(rb.ptr), counts[0], h, OPS[case["op"]], WORLD,
+                                                     ctypes.byref(req))
+                else:
+                    rc = L.MPI_Ireduce_scatter(P(sb.ptr), P(rb.ptr), arr, h, OPS[case["op"]], WORLD, ctypes.byref(req))
+                if rc == 0 and case["via"] != "block":
+                    rc = L.MPI_Wait(ctypes.byref(req), None)
             else:
                 rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, h, OPS[case["op"]], WORLD)
             assert rc == 0, (case["id"], rc)

@@ -62,15 +62,19 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
 
 
 def expected_allreduce(case, n, knobs=None):
-    """MPI_Allreduce as the reference runs it (the nonblocking Iallreduce reduces in the blocking
-    call's order here: iallreduce_osu.c's NBC schedule orders are not restated, fp parity unpinned)"""
+    """MPI_Allreduce as the reference runs it; MPI_Iallreduce: its own schedule (naive = Ireduce
+    to rank 0 + Ibcast, iallreduce_tuning.c:184-190)"""
     sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+    if case["kind"] == "iallreduce":
+        return oracle.iallreduce_ref(sends, case["count"], TYPES[case["type"]][0], OPS[case["op"]])
     return oracle.allreduce_ref(sends, case["count"], TYPES[case["type"]][0], OPS[case["op"]],
                                 in_place=case["kind"] == "allreduce_inplace", knobs=knobs)
 
 
 def expected_reduce(case, n, knobs=None):
     sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+    if case["kind"] == "ireduce":  # MPIR_Ireduce_binomial (ireduce_tuning.c default)
+        return oracle.ireduce_ref(sends, case["count"], TYPES[case["type"]][0], OPS[case["op"]], case["root"])
     return oracle.reduce_ref(sends, case["count"], TYPES[case["type"]][0], OPS[case["op"]], case["root"],
                              knobs=knobs)
 
@@ -99,6 +103,15 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
         for count in (5, 70001):
             cases.append({"id": f"ia{seed}", "kind": "iallreduce", "type": t, "op": op, "count": count, "seed": seed})
             seed += 1
+    # nonblocking reduce and the block reduce-scatters: their own selections (fp, order-sensitive)
+    for count, root in ((100, n - 1), (5000, 0), (300007, 1 % n)):
+        cases.append({"id": f"ir{seed}", "kind": "ireduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
+    for via, per in (("block", 100), ("block", 70001), ("iblock", 1000), ("iblock", 140000), ("inb", 3000)):
+        cases.append({"id": f"rb{seed}", "kind": "reduce_scatter", "type": "MPI_FLOAT", "op": "MPI_SUM", "via": via,
+                      "recvcounts": [per] * n, "count": per * n, "seed": seed})
+        seed += 1
     for count in (10, 70001, 300007):
         cases.append({"id": f"ip{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
                       "count": count, "seed": seed})
@@ -204,7 +217,7 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             want = expected_allreduce(case, n)
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {case['op']} n={n} rank {r}")
-        elif k == "reduce":
+        elif k in ("reduce", "ireduce"):
             want = expected_reduce(case, n)
             root = case["root"]
             assert_bytes_equal(res(cid, root), want, t, case["count"], f"{cid} reduce {t} {case['op']} "
@@ -212,7 +225,12 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
         elif k == "reduce_scatter":
             counts = case["recvcounts"]
             sends = [as_bytes(inputs(dict(case, count=sum(counts)), r)).copy() for r in range(n)]
-            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
+            algo = -1
+            if case.get("via") in ("block", "iblock"):  # MPICH reduce_scatter_block selection
+                algo = oracle.reduce_scatter_block_select(n, counts[0], TYPES[t][0])
+            elif case.get("via") == "inb":                # MPIR_Ireduce_scatter_pairwise
+                algo = oracle.ALGOS.index("rs_pairwise")
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]], algo=algo)
             ext = TYPES[t][3]
             off = 0
             for r in range(n):

@@ -306,3 +306,44 @@ def test_user_op_plans_match_reference_restatement(commute):
                     got = eval_progs_fn(xs, progs, blk, off, off + counts[r], fn)
                     assert np.array_equal(got, want[r]), (n, counts, r)
                     off += counts[r]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 7, 8])
+def test_nonblocking_plans_match_reference(n):
+    """MPI_Iallreduce / MPI_Ireduce / MPI_Ireduce_scatter(_block) and the blocking
+    MPI_Reduce_scatter_block take their own selections (oracle.iallreduce_select and
+    friends, citing iallreduce_tuning.c / ireduce_tuning.c / ired_scat_tuning.c /
+    red_scat_block.c); every rank of an Iallreduce gets rank 0's Ireduce result."""
+    rng = np.random.default_rng(4000 + n)
+    t, op = "MPI_FLOAT", "MPI_SUM"
+    h, _, size, ext = TYPES[t]
+    for count in (1, 3, 100, 512, 513, 1000, 5000, 70001):
+        xs = [wide(t, count, rng) for _ in range(n)]
+        with m.nbc("iallreduce"):
+            want = oracle.iallreduce_ref([x.copy() for x in xs], count, h, OPS[op])
+            for r in range(n):
+                algo, _, _, progs, blk = m.plan("allreduce", n, r, h, count=count)
+                assert algo == oracle.iallreduce_select(n, count, h)
+                got = eval_progs(xs, progs, blk, 0, count, ext, h, OPS[op])
+                assert_bytes_equal(got, want[r], t, count, f"iallreduce n={n} count={count} rank {r}")
+        with m.nbc("ireduce"):
+            root = n - 1
+            algo, _, _, progs, blk = m.plan("reduce", n, root, h, count=count, root=root)
+            assert oracle.ALGOS[algo] == "binomial"
+            got = eval_progs(xs, progs, blk, 0, count, ext, h, OPS[op])
+            want = oracle.ireduce_ref([x.copy() for x in xs], count, h, OPS[op], root)
+            assert_bytes_equal(got, want, t, count, f"ireduce n={n} count={count}")
+    for per in (1, 10, 1000, 40000):
+        counts = [per] * n
+        xs = [wide(t, per * n, rng) for _ in range(n)]
+        for kind, algo_want in (("ireduce_scatter", oracle.ALGOS.index("rs_pairwise")),
+                                ("reduce_scatter_block", oracle.reduce_scatter_block_select(n, per, h))):
+            want = oracle.reduce_scatter_ref([x.copy() for x in xs], counts, h, OPS[op], algo=algo_want)
+            with m.nbc(kind):
+                for r in range(n):
+                    algo, _, _, progs, blk = m.plan("reduce_scatter", n, r, h, counts=counts)
+                    assert algo == algo_want, (kind, n, per)
+                    got = eval_progs(xs, progs, blk, r * per, (r + 1) * per, ext, h, OPS[op])
+                    assert_bytes_equal(got, want[r * per * ext:(r + 1) * per * ext], t, per, f"{kind} n={n} rank {r}")
+    # outside the context the blocking selections come back
+    assert oracle.ALGOS[m.plan("allreduce", n, 0, h, count=2)[0]] in ("topo_tree", "shmem_linear")
