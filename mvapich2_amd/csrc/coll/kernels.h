@@ -48,14 +48,19 @@ enum PipeMode : int {
 };
 
 // Arena layout per rank and region (RS region, AG region):
-//   [parity 0..1][source rank 0..kMaxRanks-1][kPipeSlot bytes]
+//   [parity 0..1][source rank 0..kMaxRanks-1][kPipeSlotStride bytes]
 // Round k of a call uses parity (round0 + k) & 1; block b moves the bytes
-// [k*tseg + b*tsub, +tsub) of every segment, stored at slot offset b*tsub.
+// [k*tseg + b*tsub, +tsub) of every segment, stored at slot offset
+// b*tsub + (segment offset mod 16): a segment that starts off a 16-byte
+// boundary (ring chunks of n = 3, 5, 6 ...) keeps its misalignment in the
+// slot, so every copy and reduction pairs addresses of equal alignment
+// (scalar head, 16-byte body, scalar tail).  The stride leaves room for it.
 constexpr int kPipeThreads = 512;                // 8 waves per workgroup
 constexpr int kPipeMaxGrid = 256;                // one workgroup per CU
 constexpr size_t kPipeMaxSub = (size_t)64 << 10;
-constexpr size_t kPipeSlot = (size_t)kPipeMaxGrid * kPipeMaxSub;  // 16 MiB
-constexpr size_t kPipeRegion = 2 * (size_t)kMaxRanks * kPipeSlot;
+constexpr size_t kPipeSlot = (size_t)kPipeMaxGrid * kPipeMaxSub;  // 16 MiB of data
+constexpr size_t kPipeSlotStride = kPipeSlot + 256;
+constexpr size_t kPipeRegion = 2 * (size_t)kMaxRanks * kPipeSlotStride;
 
 struct PipeArgs {
     int mode, n, me, root;

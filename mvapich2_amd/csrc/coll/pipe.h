@@ -53,7 +53,7 @@ struct Jobs {
 };
 
 __device__ __forceinline__ char *pslot(char *region, uint64_t par, int src) {
-    return region + ((size_t)par * kMaxRanks + (size_t)src) * kPipeSlot;
+    return region + ((size_t)par * kMaxRanks + (size_t)src) * kPipeSlotStride;
 }
 
 // The copy / reduce loops below are software-pipelined: the loads of the next
@@ -83,6 +83,12 @@ __device__ __forceinline__ void job_addr(const JobTable &t, size_t f, const v4u 
 // LocalDst: destinations are this GPU's own buffers -> plain stores (the HBM
 // write path the Reduce_local sweep measured fastest); arena destinations on
 // peers keep non-temporal stores.
+// head bytes of a range before its first 16-byte boundary (src and dst share the alignment)
+__device__ __forceinline__ size_t head_bytes(const char *p, size_t len) {
+    const size_t h = (16 - ((uintptr_t)p & 15)) & 15;
+    return h < len ? h : len;
+}
+
 template <bool LocalDst>
 __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
     constexpr int U = 4;
@@ -92,10 +98,11 @@ __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
         size_t acc = 0;
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) {
+            const size_t h = jb.len[j] ? head_bytes(jb.src[j], jb.len[j]) : 0;
             t.pre[j] = acc;
-            t.src[j] = jb.src[j];
-            t.dst[j] = jb.dst[j];
-            acc += jb.len[j] >> 4;
+            t.src[j] = jb.src[j] + h;
+            t.dst[j] = jb.dst[j] + h;
+            acc += (jb.len[j] - h) >> 4;
         }
         t.pre[kMaxRanks] = acc;
     }
@@ -142,18 +149,37 @@ __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
             f = fn;
         }
     }
-    if (threadIdx.x < 16) {
+    if (threadIdx.x < 32) {  // lanes 0-15: the head, 16-31: the tail of every job
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) {
-            const size_t o = (jb.len[j] & ~(size_t)15) + threadIdx.x;
-            if (o < jb.len[j]) jb.dst[j][o] = __builtin_nontemporal_load(jb.src[j] + o);
+            if (!jb.len[j]) continue;
+            const size_t h = head_bytes(jb.src[j], jb.len[j]);
+            const size_t body = (jb.len[j] - h) & ~(size_t)15;
+            const size_t o = threadIdx.x < 16 ? threadIdx.x : h + body + (threadIdx.x - 16);
+            if (threadIdx.x < 16 ? o < h : o < jb.len[j])
+                jb.dst[j][o] = __builtin_nontemporal_load(jb.src[j] + o);
         }
     }
 }
 
 // Block-wide copy of nbytes from one source to every non-null destination.
-__device__ __forceinline__ void blk_copy_multi(const Dsts &d, const char *src, size_t nbytes) {
+// src and every destination share the same alignment mod 16: a scalar head up to the
+// first 16-byte boundary, then the 16-byte body, then the tail.
+__device__ __forceinline__ void blk_copy_multi(const Dsts &dd, const char *src0, size_t nbytes0) {
     constexpr int U = 4;
+    const size_t h = head_bytes(src0, nbytes0);
+    if (threadIdx.x < h) {
+        const char c = __builtin_nontemporal_load(src0 + threadIdx.x);
+#pragma unroll
+        for (int k = 0; k < kMaxRanks + 1; ++k)
+            if (dd.p[k]) dd.p[k][threadIdx.x] = c;
+    }
+    Dsts d = dd;
+#pragma unroll
+    for (int k = 0; k < kMaxRanks + 1; ++k)
+        if (d.p[k]) d.p[k] += h;
+    const char *src = src0 + h;
+    const size_t nbytes = nbytes0 - h;
     const size_t nv = nbytes >> 4;
     const v4u *s = (const v4u *)src;
     size_t x = threadIdx.x;
@@ -290,6 +316,30 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
     }
 }
 
+// Scalar reduction of the first nbytes (< 16, whole elements) of a range whose start is not
+// 16-byte aligned, in the call's order; ebase = global index of the first element.
+template <class Rd, bool PROG>
+__device__ __forceinline__ void blk_reduce_head(const PipeArgs &a, const char *const (&src)[kMaxRanks], const Dsts &d,
+                                                size_t nbytes, size_t ebase) {
+    using T = typename Rd::T;
+    const size_t cnt = nbytes / sizeof(T);
+    if (threadIdx.x >= cnt) return;
+    const size_t e = threadIdx.x;
+    T col[kMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) col[j] = ld_nt_elem((const T *)(j < a.n ? src[j] : src[0]) + e);
+    T r;
+    if constexpr (PROG) {
+        r = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, ebase + e)]);
+    } else {
+        const TreeParams &tp = a.tp;
+        r = tree_reduce<Rd>(col, a.n, tp.linear, tp.pof2, tp.rem, elem_owner<Rd>(tp, ebase + e));
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxRanks + 1; ++k)
+        if (d.p[k]) ((T *)d.p[k])[e] = r;
+}
+
 __device__ __forceinline__ size_t range_len(const PipeArgs &a, int j, size_t rbase) {
     return rbase < a.seg_len[j] ? (a.seg_len[j] - rbase < a.tsub ? a.seg_len[j] - rbase : a.tsub) : 0;
 }
@@ -300,7 +350,7 @@ __device__ __forceinline__ void gather_slots(const PipeArgs &a, uint64_t par, si
 #pragma unroll
     for (int j = 0; j < kMaxRanks; ++j) {
         if (j < a.n && j != a.me && j != skip) {
-            jb.src[j] = pslot(a.ag_peer.p[a.me], par, j) + soff;
+            jb.src[j] = pslot(a.ag_peer.p[a.me], par, j) + soff + (a.seg_off[j] & 15);
             jb.dst[j] = a.recv + a.recv_off[j] + rbase;
             jb.len[j] = range_len(a, j, rbase);
         }
@@ -319,7 +369,7 @@ __device__ __forceinline__ void scatter_round(const PipeArgs &a, int k) {
     for (int j = 0; j < kMaxRanks; ++j) {
         if (j < a.n && j != a.me) {
             jb.src[j] = a.send + a.seg_off[j] + rbase;
-            jb.dst[j] = pslot(a.rs_peer.p[j], par, a.me) + soff;
+            jb.dst[j] = pslot(a.rs_peer.p[j], par, a.me) + soff + (a.seg_off[j] & 15);
             jb.len[j] = range_len(a, j, rbase);
         }
     }
@@ -340,6 +390,7 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
     const int me = a.me;
     const size_t len = range_len(a, me, rbase);
     if (!len) return;
+    const size_t mis = a.seg_off[me] & 15;  // segment misalignment, kept in the slots
     const char *src[kMaxRanks];
     if (a.tp.linear == 2) {
         // ring order: source k is rank me+1+k (mod n), so the chain ends with my own operand
@@ -347,7 +398,7 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
         for (int k = 0; k < kMaxRanks; ++k) {
             int j = me + 1 + k;
             while (j >= a.n) j -= a.n;
-            src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+            src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff + mis;
         }
     } else if (a.tp.linear == 3) {
         // flat ring allreduce (MPIR_Allreduce_pt2pt_ring_MV2 allreduce_osu.c:3925-3958): segment
@@ -357,37 +408,53 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
         for (int k = 0; k < kMaxRanks; ++k) {
             int j = me + k;
             while (j >= a.n) j -= a.n;
-            src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+            src[k] = (k >= a.n || j == me) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff + mis;
         }
     } else {
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)
-            src[j] = (j == me || j >= a.n) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff;
+            src[j] = (j == me || j >= a.n) ? a.send + a.seg_off[me] + rbase : pslot(a.rs_peer.p[me], par, j) + soff + mis;
     }
     Dsts d{};
     if (a.mode == PIPE_AR) {
         d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)
-            if (j < a.n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
+            if (j < a.n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff + mis;
     } else if (a.mode == PIPE_RS || me == a.root) {
         d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
     } else {
-        d.p[0] = pslot(a.ag_peer.p[a.root], par, me) + soff;
+        d.p[0] = pslot(a.ag_peer.p[a.root], par, me) + soff + mis;
     }
+    size_t e0 = (a.seg_off[me] + rbase) / (size_t)a.esize;
+    size_t body = len;
+    if (mis) {
+        // scalar head up to the first 16-byte boundary (whole elements: extents are powers of two
+        // <= 16, so the misalignment is a multiple of the extent), then the aligned body
+        const size_t h = (16 - mis) < len ? (16 - mis) : len;
+        blk_reduce_head<Rd, PROG>(a, src, d, h, (size_t)((int64_t)e0 + (PROG ? a.eshift : 0)));
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) src[j] += h;
+#pragma unroll
+        for (int k = 0; k < kMaxRanks + 1; ++k)
+            if (d.p[k]) d.p[k] += h;
+        e0 += h / (size_t)a.esize;
+        body = len - h;
+        if (!body) return;
+    }
+    const size_t len_body = body;
     // fewer sources -> more columns per thread, so >= 4 loads stay in flight
     // one specialised loop per (unroll, order); the order is uniform over the call
-    const size_t e0 = (a.seg_off[me] + rbase) / (size_t)a.esize;
     if constexpr (PROG) {
-        blk_reduce<Rd, 1, 4>(a, src, d, len, (size_t)((int64_t)e0 + a.eshift));
+        blk_reduce<Rd, 1, 4>(a, src, d, len_body, (size_t)((int64_t)e0 + a.eshift));
     } else if (a.n <= 4) {
-        if (a.tp.linear == 2) blk_reduce<Rd, 2, 2, 4>(a, src, d, len, e0);
-        else if (a.tp.linear) blk_reduce<Rd, 2, 1, 4>(a, src, d, len, e0);
-        else blk_reduce<Rd, 2, 0, 4>(a, src, d, len, e0);
+        if (a.tp.linear == 2) blk_reduce<Rd, 2, 2, 4>(a, src, d, len_body, e0);
+        else if (a.tp.linear) blk_reduce<Rd, 2, 1, 4>(a, src, d, len_body, e0);
+        else blk_reduce<Rd, 2, 0, 4>(a, src, d, len_body, e0);
     } else {
-        if (a.tp.linear == 2) blk_reduce<Rd, 1, 2>(a, src, d, len, e0);
-        else if (a.tp.linear) blk_reduce<Rd, 1, 1>(a, src, d, len, e0);
-        else blk_reduce<Rd, 1, 0>(a, src, d, len, e0);
+        if (a.tp.linear == 2) blk_reduce<Rd, 1, 2>(a, src, d, len_body, e0);
+        else if (a.tp.linear) blk_reduce<Rd, 1, 1>(a, src, d, len_body, e0);
+        else blk_reduce<Rd, 1, 0>(a, src, d, len_body, e0);
     }
 }
 
@@ -436,7 +503,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
                 Dsts d{};
 #pragma unroll
                 for (int j = 0; j < kMaxRanks; ++j)
-                    if (j < n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
+                    if (j < n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff + (a.seg_off[me] & 15);
                 if (a.send != a.recv + a.recv_off[me]) d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
                 blk_copy_multi(d, a.send + rbase, len);
             }

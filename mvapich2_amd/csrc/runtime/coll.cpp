@@ -62,7 +62,9 @@ static inline bool hp_on() {
     }
     return g_hp.on;
 }
+static bool g_call_start = true;  // tmark0: record ev0 at the first launch of this API call
 static inline void hp_entry() {
+    g_call_start = true;
     if (hp_on()) g_hp.t_entry = now_ns();
 }
 static inline void hp_done() {
@@ -169,8 +171,11 @@ static int finish(hipStream_t st, bool timed) {
     return 0;
 }
 
+// kernel-time events bracket the call's first launch to its last (calls made of several
+// launches: ring main part + remainder, staged copies)
 static inline void tmark0(hipStream_t st) {
-    if (world().timing) hipEventRecord(world().ev0, st);
+    if (world().timing && g_call_start) hipEventRecord(world().ev0, st);
+    g_call_start = false;
     if (hp_on() && g_hp.t_entry && !g_hp.t_l0) g_hp.t_l0 = now_ns();
 }
 static inline void tmark1(hipStream_t st) {
@@ -847,11 +852,12 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     a.recv = s.recv;
     a.esize = dt->extent;
     if (ring) {
-        // segment j = ring chunk j; chunks that are not 16-byte multiples go through
-        // padded copies of the operand and the result
+        // segment j = ring chunk j.  Chunks that are not 16-byte multiples keep their
+        // misalignment through the arena slots (coll/pipe.h: scalar head, aligned body);
+        // only operands whose base is not 16-byte aligned go through padded copies
         tp.linear = 3;
         const size_t cb = (count / n) * (size_t)dt->extent;
-        if (cb % 16 == 0) {
+        if (cb % 16 == 0 || ((uintptr_t)s.send % 16 == 0 && (uintptr_t)s.recv % 16 == 0)) {
             for (int j = 0; j < n; ++j) {
                 a.seg_off[j] = a.recv_off[j] = (size_t)j * cb;
                 a.seg_len[j] = cb;
@@ -1026,10 +1032,12 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     PipeArgs a{};
     a.mode = PIPE_RS;
     a.esize = (int)ext;
-    // operand: the caller's buffer when it is aligned device memory with aligned
-    // segments (and not IN_PLACE: the result overwrites the operand's head);
-    // otherwise a staged copy with every segment padded to 16 bytes
-    if (!in_place && natural && is_device(send) && (uintptr_t)send % 16 == 0) {
+    // operand: the caller's buffer when it is aligned device memory (and not IN_PLACE:
+    // the result overwrites the operand's head) — segments off 16-byte boundaries keep
+    // their misalignment through the kernel; otherwise a staged copy with every segment
+    // padded to 16 bytes
+    (void)natural;
+    if (!in_place && is_device(send) && (uintptr_t)send % 16 == 0) {
         a.send = (const char *)send;
         size_t o = 0;
         for (int j = 0; j < n; ++j) {
@@ -1051,14 +1059,19 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
         }
         a.send = t;
     }
-    const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0;
+    // the result must share my segment's misalignment: the caller's buffer when it does,
+    // else a scratch block at that misalignment, copied out after the kernel
+    const size_t mis = a.seg_off[w.rank] & 15;
+    const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == mis;
     char *dst = (char *)recvbuf;
-    if (!direct && mycnt) {
-        dst = (char *)get_scratch(1, mycnt * ext);
-        if (!dst) return E_NO_MEM;
-    }
-    a.recv = dst;
     a.recv_off[w.rank] = 0;
+    if (!direct && mycnt) {
+        char *t = (char *)get_scratch(1, mycnt * ext + 16);
+        if (!t) return E_NO_MEM;
+        dst = t + mis;
+    }
+    a.recv = dst - (direct ? 0 : mis);
+    a.recv_off[w.rank] = direct ? 0 : mis;
     // MPIR_Reduce_scatter_MV2's one-node choice (orders.cpp plan_reduce_scatter): ring,
     // recursive halving, pairwise or reduce + scatter, each in its own order
     Plan p;
@@ -1096,8 +1109,11 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
     const int n = w.size;
     const int me = w.rank;
     const bool in_place = sendbuf == (const void *)-1;
-    const size_t pitch = (bytes + 15) & ~(size_t)15;
-    const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0 && pitch == bytes;
+    // direct: rank j's block lands at recvbuf + j*bytes even when that is off a 16-byte
+    // boundary (coll/pipe.h keeps each block's misalignment through the slots); the
+    // contribution must then share its block's misalignment
+    const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0;
+    const size_t pitch = direct ? bytes : (bytes + 15) & ~(size_t)15;
     char *dst = direct ? (char *)recvbuf : (char *)get_scratch(1, pitch * n);
     if (!dst) return E_NO_MEM;
     const char *src = in_place ? (const char *)recvbuf + (size_t)me * bytes : (const char *)sendbuf;
@@ -1105,11 +1121,12 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
         if (!in_place) hipMemcpyAsync(recvbuf, src, bytes, hipMemcpyDefault, st);
         return finish(st, false);
     }
-    if (!(direct && in_place) && !(is_device(src) && (uintptr_t)src % 16 == 0)) {
-        char *t = (char *)get_scratch(0, bytes);
+    const size_t mis = ((size_t)me * pitch) & 15;
+    if (!(direct && in_place) && !(is_device(src) && (uintptr_t)src % 16 == mis)) {
+        char *t = (char *)get_scratch(0, bytes + 16);
         if (!t) return E_NO_MEM;
-        hipMemcpyAsync(t, src, bytes, hipMemcpyDefault, st);
-        src = t;
+        hipMemcpyAsync(t + mis, src, bytes, hipMemcpyDefault, st);
+        src = t + mis;
     }
     PipeArgs a{};
     a.mode = PIPE_AG;
@@ -1118,7 +1135,7 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
     a.esize = 1;
     for (int j = 0; j < n; ++j) {
         a.seg_len[j] = bytes;
-        a.recv_off[j] = (size_t)j * pitch;
+        a.recv_off[j] = a.seg_off[j] = (size_t)j * pitch;  // seg_off: the block's misalignment
     }
     if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
     if (!direct) {
