@@ -35,6 +35,7 @@ METRIC = "osu_allreduce busbw GB/s fp32 SUM 256MB at 1/2/4/8 MI355X; 8B latency 
 HBM_PEAK = 8000.0        # GB/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK = 153.0        # GB/s per link per direction (task statement)
 S_BYTES = 256 * 1024 * 1024
+WORLD = 0x44000000        # MPI_COMM_WORLD (MPICH ABI)
 
 
 def cpu_info():
@@ -129,6 +130,33 @@ def reduce_local_run(L, type_name, op_name, nbytes, steps, warmup):
     return t / steps, float(np.mean(kms)) / 1e3, count, got
 
 
+def pack_run(L, steps):
+    """configs[4]'s strided operand, device MPI_Pack / MPI_Unpack (replicas: per-GPU work).
+    Algorithmic bytes = 2 x packed; the HBM floor of this layout is the whole
+    strided span plus the packed bytes (1.5 x, profiles/pmc_pack_vector_r02e.json)."""
+    nb = 8 << 20
+    vt = ctypes.c_int()
+    m.check(L.MPI_Type_vector(nb, 4, 8, TYPES["MPI_FLOAT"][0], ctypes.byref(vt)), "MPI_Type_vector")
+    m.check(L.MPI_Type_commit(ctypes.byref(vt)), "MPI_Type_commit")
+    span, packed = ((nb - 1) * 8 + 4) * 4, nb * 16
+    src, dst = m.DeviceBuffer(span), m.DeviceBuffer(packed)
+    src.upload(np.random.default_rng(7).standard_normal(span // 4).astype(np.float32))
+    out = {}
+    for name, fn in (("pack", lambda pos: L.MPI_Pack(src.ptr, 1, vt.value, dst.ptr, packed, ctypes.byref(pos), WORLD)),
+                     ("unpack", lambda pos: L.MPI_Unpack(dst.ptr, packed, ctypes.byref(pos), src.ptr, 1, vt.value, WORLD))):
+        m.check(fn(ctypes.c_int(0)), name)
+        L.mv2h_device_synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m.check(fn(ctypes.c_int(0)), name)
+        L.mv2h_device_synchronize()
+        t = (time.perf_counter() - t0) / steps
+        out[name] = {"GB/s_algorithmic": round(2 * packed / t / 1e9, 1), "GB/s_hbm_floor": round((span + packed) / t / 1e9, 1),
+                     "ms": round(t * 1e3, 4)}
+    m.check(L.MPI_Type_free(ctypes.byref(vt)), "MPI_Type_free")
+    return out
+
+
 def bench_n1(args, L):
     step_s, kern_s, count, _ = reduce_local_run(L, "MPI_FLOAT", "MPI_SUM", S_BYTES, args.steps, args.warmup)
     alg_bytes = 3 * count * 4
@@ -148,6 +176,7 @@ def bench_n1(args, L):
         m.check(L.MPI_Reduce_local(hx.ctypes.data, hy.ctypes.data, count, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]), "host")
     extra["MPI_FLOAT:MPI_SUM host buffers (PCIe-inclusive)"] = {"GB/s_call": round(3 * S_BYTES * 3 / (time.perf_counter() - t0) / 1e9, 2)}
     del hx, hy
+    extra["MPI_Pack/Unpack MPI_Type_vector(8Mi,4,8,MPI_FLOAT)"] = pack_run(L, max(3, args.steps // 2))
     # HBM traffic of this kernel from the newest committed PMC pass (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py); the file is named in the line
     traffic, tsrc = None, None

@@ -33,6 +33,10 @@ struct Derived {
     long size = 0, lb = 0, extent = 0, true_lb = 0, true_extent = 0;
     long align = 1;         // alignsize (mpid_type_struct.c:42-124)
     std::vector<Seg> segs;  // one element, sorted by construction order, merged
+    // layout summary, computed once (pack calls then cost O(1) host work): one element is
+    // reg_n blocks of reg_blk bytes at reg_stride from offset 0
+    bool summarised = false, reg = false;
+    long reg_n = 0, reg_blk = 0, reg_stride = 0;
 };
 
 std::vector<Derived> g_types;
@@ -156,26 +160,45 @@ int make_type(const std::vector<long> &block_offsets, int blocklen, MPI_Datatype
     return make_struct(blocks, out);
 }
 
-// regular layout of `count` elements: nblocks x blk bytes at constant stride
-bool regular(const Derived *d, long extent, int count, long &nblocks, long &blk, long &stride) {
+void summarise(Derived *d) {
+    if (d->summarised) return;
+    d->summarised = true;
     const auto &s = d->segs;
-    if (s.empty()) return false;
-    blk = s[0].len;
-    stride = s.size() > 1 ? s[1].off - s[0].off : extent;
-    if (s[0].off != 0) return false;
+    d->reg = false;
+    if (s.empty() || s[0].off != 0) return;
+    const long blk = s[0].len, stride = s.size() > 1 ? s[1].off - s[0].off : d->extent;
     for (size_t i = 0; i < s.size(); ++i)
-        if (s[i].len != blk || s[i].off != (long)i * stride) return false;
-    if (count > 1 && (long)s.size() * stride != extent) return false;
-    nblocks = (long)s.size() * count;
+        if (s[i].len != blk || s[i].off != (long)i * stride) return;
+    d->reg = stride >= blk;
+    d->reg_n = (long)s.size();
+    d->reg_blk = blk;
+    d->reg_stride = stride;
+}
+
+// regular layout of `count` elements: nblocks x blk bytes at constant stride
+bool regular(Derived *d, long extent, int count, long &nblocks, long &blk, long &stride) {
+    summarise(d);
+    if (!d->reg) return false;
+    blk = d->reg_blk;
+    stride = d->reg_n > 1 ? d->reg_stride : extent;
+    if (count > 1 && d->reg_n * stride != extent) return false;
+    nblocks = d->reg_n * count;
     return stride >= blk;
 }
 
 int pack_impl(const char *in, int count, MPI_Datatype dt, char *out, bool unpack) {
-    std::vector<Seg> segs;
+    // a derived type's segments are used in place (no per-call copy of a large type map)
+    std::vector<Seg> bsegs;
     long ext = 0, size = 0;
-    if (!type_segs(dt, segs, ext, size)) return MPI_ERR_TYPE;
-    const bool din = mv2h_is_device_ptr(in), dout = mv2h_is_device_ptr(out);
     Derived *d = derived(dt);
+    if (d) {
+        ext = d->extent;
+        size = d->size;
+    } else if (!type_segs(dt, bsegs, ext, size)) {
+        return MPI_ERR_TYPE;
+    }
+    const std::vector<Seg> &segs = d ? d->segs : bsegs;
+    const bool din = mv2h_is_device_ptr(in), dout = mv2h_is_device_ptr(out);
     if (!din && !dout) {
         // host <-> host: reference semantics, host copies
         long pos = 0;

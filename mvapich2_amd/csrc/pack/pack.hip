@@ -24,19 +24,32 @@
 
 namespace mv2 {
 
+// kPackU units per thread, all loads issued before the stores (one tile per workgroup,
+// full grid: the Reduce_local shape); both sides streamed with non-temporal accesses
+constexpr int kPackU = 4;
 template <typename G>
 __global__ __launch_bounds__(kThreads) void k_pack_units(const char *__restrict__ src, char *__restrict__ dst,
                                                          size_t nrows, uint32_t upr, size_t stride_units,
                                                          int unpack) {
     const size_t total = nrows * upr;
-    const size_t step = (size_t)gridDim.x * kThreads;
+    const size_t base = (size_t)blockIdx.x * kThreads * kPackU + threadIdx.x;
     const G *s = (const G *)src;
     G *d = (G *)dst;
-    for (size_t u = (size_t)blockIdx.x * kThreads + threadIdx.x; u < total; u += step) {
-        const size_t i = u / upr, j = u - i * upr;
-        if (!unpack) d[u] = s[i * stride_units + j];
-        else d[i * stride_units + j] = s[u];
+    G v[kPackU];
+    size_t at[kPackU];
+#pragma unroll
+    for (int k = 0; k < kPackU; ++k) {
+        const size_t u = base + (size_t)k * kThreads;
+        if (u < total) {
+            const size_t i = upr == 1 ? u : u / upr, j = u - i * upr;
+            const size_t strided = i * stride_units + j;
+            at[k] = unpack ? strided : u;
+            v[k] = __builtin_nontemporal_load(s + (unpack ? u : strided));
+        }
     }
+#pragma unroll
+    for (int k = 0; k < kPackU; ++k)
+        if (base + (size_t)k * kThreads < total) __builtin_nontemporal_store(v[k], d + at[k]);
 }
 
 // LDS-staged pack of narrow rows: rows [r0, r0+R) per workgroup.
@@ -230,8 +243,9 @@ int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
     while (g > 1 && ((blk % g) || (stride % g) || (a % g))) g >>= 1;
     const size_t upr = blk / g;
     const size_t total = nblocks * upr;
-    size_t grid = (total + kThreads - 1) / kThreads;
-    if (grid > 4096) grid = 4096;
+    const size_t tile = (size_t)kThreads * kPackU;
+    const size_t grid = (total + tile - 1) / tile;
+    if (grid > 0x7fffffffu) return E_ARG;
     const size_t su = stride / g;
     switch (g) {
     case 16: hipLaunchKernelGGL(k_pack_units<v4u>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
