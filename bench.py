@@ -343,6 +343,32 @@ def bench_nranks(args, L, rank, size):
     ml = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, nrec, DINT, MAXLOC, world)  # noqa: E731
     ml_s, ml_k = _timed(L, world, ml, ks, 2)
 
+    # configs[4]: a commutative user op on MPI_Type_vector(N, 4, 8, MPI_FLOAT) operands (the
+    # reference rejects predefined ops on derived types); the op runs on the host in the
+    # selected algorithm's order (recursive doubling for user ops), as in the reference
+    nbv = 1 << 20
+    vt = ctypes.c_int()
+    m.check(L.MPI_Type_vector(nbv, 4, 8, F32, ctypes.byref(vt)), "MPI_Type_vector")
+    m.check(L.MPI_Type_commit(ctypes.byref(vt)), "MPI_Type_commit")
+    vspan = ((nbv - 1) * 8 + 4) * 4
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+
+    def _vsum(inp, io, ln, dt):  # io += in on the type map of ln[0] vector elements
+        for e in range(ln[0]):
+            a = np.ctypeslib.as_array((ctypes.c_float * (vspan // 4)).from_address(inp + e * vspan))
+            b = np.ctypeslib.as_array((ctypes.c_float * (vspan // 4)).from_address(io + e * vspan))
+            bv = np.lib.stride_tricks.as_strided(b, (nbv, 4), (32, 4))
+            av = np.lib.stride_tricks.as_strided(a, (nbv, 4), (32, 4))
+            bv += av
+    ufn = UF(_vsum)
+    uop = ctypes.c_int()
+    m.check(L.MPI_Op_create(ctypes.cast(ufn, ctypes.c_void_p), 1, ctypes.byref(uop)), "MPI_Op_create")
+    uv = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, 1, vt.value, uop.value, world)  # noqa: E731
+    uv_s, _ = _timed(L, world, uv, 2, 1)
+    L.MPI_Op_free(ctypes.byref(uop))
+    L.MPI_Type_free(ctypes.byref(vt))
+
     # 8-byte latency (OSU: small-message iterations, skip 100)
     s8 = m.DeviceBuffer(8)
     r8 = m.DeviceBuffer(8)
@@ -391,12 +417,13 @@ def bench_nranks(args, L, rank, size):
 
     # max over ranks through the library itself (device allreduce MAX)
     vals = np.array([step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat / args.lat_iters,
-                     float(np.median(lat_k)), 0.0 if (ok and lat_ok) else 1.0, p2p_s], dtype=np.float64)
+                     float(np.median(lat_k)), 0.0 if (ok and lat_ok) else 1.0, p2p_s, uv_s], dtype=np.float64)
     dm = m.DeviceBuffer(vals.nbytes)
     dm.upload(vals)
     dr = m.DeviceBuffer(vals.nbytes)
     m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, len(vals), F64, MAX, world), "max")
-    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad, p2p_s) = dr.download(np.float64)
+    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad, p2p_s,
+     uv_s) = dr.download(np.float64)
     f = (size - 1) / size
     busbw = 2.0 * f * S_BYTES / step_s / 1e9
     kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
@@ -412,6 +439,10 @@ def bench_nranks(args, L, rank, size):
         "allgather_char": line4(ag_s, ag_k, f * S_BYTES),
         "bcast_char": line4(bc_s, bc_k, S_BYTES),
         "allreduce_maxloc_double_int": line4(ml_s, ml_k, 2.0 * f * nrec * 12),
+        "allreduce_user_op_vector": {"payload_busbw_GBps": round(2.0 * f * nbv * 16 / uv_s / 1e9, 2),
+                                     "ms": round(uv_s * 1e3, 3),
+                                     "what": "configs[4]: commutative user op (host callback) on MPI_Type_vector(1Mi,4,8,"
+                                             "MPI_FLOAT), 16 MiB payload, recursive-doubling order"},
         "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
