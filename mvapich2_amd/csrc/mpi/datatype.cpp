@@ -286,7 +286,26 @@ long dtype_extent(MPI_Datatype dt) {
     Derived *d = derived(dt);
     return d ? d->extent : -1;
 }
+template <size_t B>
+static void copy_blocks(char *dst, const char *src, long nblocks, long stride) {
+    for (long i = 0; i < nblocks; ++i) memcpy(dst + i * stride, src + i * stride, B);
+}
+
 void dtype_merge_typemap(char *dst, const char *src, MPI_Datatype dt, long count) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (Derived *d = derived(dt)) {
+        // regular layouts (vectors): fixed-size block copies, no per-block call
+        long nb = 0, blk = 0, stride = 0;
+        if (count > 0 && regular(d, d->extent, (int)count, nb, blk, stride)) {
+            switch (blk) {
+            case 4: copy_blocks<4>(dst, src, nb, stride); return;
+            case 8: copy_blocks<8>(dst, src, nb, stride); return;
+            case 16: copy_blocks<16>(dst, src, nb, stride); return;
+            case 32: copy_blocks<32>(dst, src, nb, stride); return;
+            default: break;
+            }
+        }
+    }
     std::vector<Seg> segs;
     long extent = 0, size = 0;
     if (!type_segs(dt, segs, extent, size)) return;

@@ -95,13 +95,54 @@ bool is_dev(const void *p) { return p && p != MPI_IN_PLACE && mv2h_is_device_ptr
 
 // ---- user-op path: user functions are host callbacks (the reference also
 // calls them on host copies of device buffers, reduce_local.c:54-164) ----
-int copy_to_host(std::vector<char> &h, const void *p, size_t bytes) {
+// Host staging of the host-side paths (user ops, x87): pinned buffers kept per
+// slot and grown on demand, so a call pays neither page faults nor a zero
+// fill, and the device copies run as DMA from pinned memory.  These paths run
+// under the global critical section; each concurrent use takes its own slot.
+enum HostSlot { HS_OPERANDS, HS_RESULT, HS_MINE, HS_IN, HS_INOUT, HS_COUNT };
+class HostBuf {
+  public:
+    explicit HostBuf(int slot) : slot_(slot) {}
+    void resize(size_t n) {
+        static char *buf[HS_COUNT];
+        static size_t cap[HS_COUNT];
+        static bool pinned[HS_COUNT];
+        if (n > cap[slot_]) {
+            if (buf[slot_]) {
+                if (pinned[slot_]) (void)hipHostFree(buf[slot_]);
+                else free(buf[slot_]);
+            }
+            const size_t want = std::max(n, 2 * cap[slot_]);
+            void *q = nullptr;
+            pinned[slot_] = hipHostMalloc(&q, want, hipHostMallocDefault) == hipSuccess;
+            if (!pinned[slot_]) {
+                (void)hipGetLastError();
+                q = malloc(want);  // no GPU (host-buffer x87 calls): plain memory
+            }
+            buf[slot_] = (char *)q;
+            cap[slot_] = q ? want : 0;
+        }
+        p_ = buf[slot_];
+        n_ = n;
+    }
+    char *data() { return p_; }
+    const char *data() const { return p_; }
+    size_t size() const { return n_; }
+
+  private:
+    int slot_;
+    char *p_ = nullptr;
+    size_t n_ = 0;
+};
+
+int copy_to_host(HostBuf &h, const void *p, size_t bytes) {
     h.resize(bytes ? bytes : 1);
+    if (!h.data()) return MPI_ERR_NO_MEM;
     if (is_dev(p)) return mv2h_memcpy_dtoh(h.data(), p, bytes);
     memcpy(h.data(), p, bytes);
     return 0;
 }
-int copy_from_host(void *p, const std::vector<char> &h, size_t bytes) {
+int copy_from_host(void *p, const HostBuf &h, size_t bytes) {
     if (is_dev(p)) return mv2h_memcpy_htod(p, h.data(), bytes);
     memcpy(p, h.data(), bytes);
     return 0;
@@ -186,7 +227,7 @@ bool is_x87(MPI_Datatype dt) {
 int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, UserOp *u) {
     long span = dtype_span(dt, count);
     if (span < 0) return MPI_ERR_TYPE;
-    std::vector<char> hin, hio;
+    HostBuf hin(HS_IN), hio(HS_INOUT);
     int rc = copy_to_host(hin, in, span);
     if (!rc) rc = copy_to_host(hio, inout, span);
     if (rc) return MPI_ERR_OTHER;
@@ -203,12 +244,13 @@ int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, U
 // (its own user-op path also runs on host copies of device buffers).  Only
 // the type-map bytes of the result are written back (MPIR_Localcopy /
 // Segment_unpack semantics): gap bytes of a strided recvbuf stay untouched.
-int gather_operands(const void *src, long span, std::vector<char> &all) {
+int gather_operands(const void *src, long span, HostBuf &all) {
     World &w = world();
     const int n = w.size;
-    std::vector<char> mine;
+    HostBuf mine(HS_MINE);
     if (copy_to_host(mine, src, span)) return MPI_ERR_OTHER;
-    all.assign((size_t)span * n + 1, 0);
+    all.resize((size_t)span * n + 1);
+    if (!all.data()) return MPI_ERR_NO_MEM;
     if (n > 1) return mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
     memcpy(all.data(), mine.data(), span);
     return MPI_SUCCESS;
@@ -217,7 +259,7 @@ int gather_operands(const void *src, long span, std::vector<char> &all) {
 // Run ps over elements [e_begin, e_end) of the n operands in W (span bytes
 // each, element e at e*extent); merge the type-map bytes of the result into
 // out, whose element 0 is element e_begin.
-void eval_plan(const ProgSet &ps, std::vector<char> &W, long span, long e_begin, long e_end, MPI_Datatype dt,
+void eval_plan(const ProgSet &ps, HostBuf &W, long span, long e_begin, long e_end, MPI_Datatype dt,
                long extent, UserOp *u, char *out) {
     long e = e_begin;
     while (e < e_end) {
@@ -244,7 +286,7 @@ int user_allreduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datat
     if (span < 0) return MPI_ERR_TYPE;
     const int n = w.size, me = w.rank;
     const bool in_place = sendbuf == MPI_IN_PLACE;
-    std::vector<char> W, result;
+    HostBuf W(HS_OPERANDS), result(HS_RESULT);
     int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
     if (rc) return rc;
     if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
@@ -287,7 +329,7 @@ int user_reduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datatype
     if (span < 0) return MPI_ERR_TYPE;
     const int n = w.size, me = w.rank;
     const bool in_place = sendbuf == MPI_IN_PLACE;
-    std::vector<char> W, result;
+    HostBuf W(HS_OPERANDS), result(HS_RESULT);
     int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
     if (rc) return rc;
     Plan p;
@@ -336,7 +378,7 @@ int user_reduce_scatter_body(const void *sendbuf, void *recvbuf, const int *coun
     }
     const long span = dtype_span(dt, (int)total);
     if (span < 0) return MPI_ERR_TYPE;
-    std::vector<char> W, result;
+    HostBuf W(HS_OPERANDS), result(HS_RESULT);
     int rc = gather_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, span, W);
     if (rc) return rc;
     Plan p;
