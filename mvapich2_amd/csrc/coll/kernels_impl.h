@@ -183,8 +183,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_n(PeerTable src, int n, cha
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * kThreads;
             if (i < nvec)
-                st_nt((v4u *)dst + i, tp.linear == 4 ? vreduce_n<Rd, 4>(v[u], n, tp, i * N)
-                                                     : vreduce_n<Rd>(v[u], n, tp, i * N));
+                ((v4u *)dst)[i] = tp.linear == 4 ? vreduce_n<Rd, 4>(v[u], n, tp, i * N) : vreduce_n<Rd>(v[u], n, tp, i * N);
         }
     }
     if (blockIdx.x == 0) {

@@ -25,12 +25,17 @@
 namespace mv2 {
 
 // kPackU units per thread, all loads issued before the stores (one tile per workgroup,
-// full grid: the Reduce_local shape); both sides streamed with non-temporal accesses
-constexpr int kPackU = 4;
+// full grid: the Reduce_local shape); non-temporal loads, plain stores.  Shape from the
+// tools/pack_variants.hip sweep on the configs[4] vector (profiles/r02y_pack_variants.txt):
+// plain stores let L2 merge the half-line writes of an unpack into whole lines' byte masks
+// (0.122 -> 0.074 ms), and two units per thread beat four (pack 0.0645 -> 0.060 ms).
+constexpr int kPackU = 2;
+constexpr int kPackThreads = 512;
 template <typename G>
-__global__ __launch_bounds__(kThreads) void k_pack_units(const char *__restrict__ src, char *__restrict__ dst,
-                                                         size_t nrows, uint32_t upr, size_t stride_units,
-                                                         int unpack) {
+__global__ __launch_bounds__(kPackThreads) void k_pack_units(const char *__restrict__ src, char *__restrict__ dst,
+                                                             size_t nrows, uint32_t upr, size_t stride_units,
+                                                             int unpack) {
+    constexpr int kThreads = kPackThreads;
     const size_t total = nrows * upr;
     const size_t base = (size_t)blockIdx.x * kThreads * kPackU + threadIdx.x;
     const G *s = (const G *)src;
@@ -49,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void k_pack_units(const char *__restrict_
     }
 #pragma unroll
     for (int k = 0; k < kPackU; ++k)
-        if (base + (size_t)k * kThreads < total) __builtin_nontemporal_store(v[k], d + at[k]);
+        if (base + (size_t)k * kThreads < total) d[at[k]] = v[k];
 }
 
 // LDS-staged pack of narrow rows: rows [r0, r0+R) per workgroup.
@@ -85,7 +90,7 @@ __global__ __launch_bounds__(kThreads) void k_pack_lds(const char *__restrict__ 
                 const uint32_t row = b / blk, col = b - row * blk;
                 u.b[k] = lds[lead + row * stride + col];
             }
-            st_nt((v4u *)o + c, u.v);
+            ((v4u *)o)[c] = u.v;
         }
         done = nch * 16;
     }
@@ -243,10 +248,11 @@ int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
     while (g > 1 && ((blk % g) || (stride % g) || (a % g))) g >>= 1;
     const size_t upr = blk / g;
     const size_t total = nblocks * upr;
-    const size_t tile = (size_t)kThreads * kPackU;
+    const size_t tile = (size_t)kPackThreads * kPackU;
     const size_t grid = (total + tile - 1) / tile;
     if (grid > 0x7fffffffu) return E_ARG;
     const size_t su = stride / g;
+    constexpr int kThreads = kPackThreads;
     switch (g) {
     case 16: hipLaunchKernelGGL(k_pack_units<v4u>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
     case 8: hipLaunchKernelGGL(k_pack_units<uint64_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
