@@ -446,6 +446,11 @@ def bench_nranks(args, L, rank, size):
         "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
+    tiling = {"grid": m.info("pipe_grid"), "bytes_per_workgroup_round": m.info("pipe_sub"),
+              "autotuned_at_init": bool(m.info("pipe_tuned")),
+              "candidates_max_over_ranks_us": [
+                  {"grid": m.info(f"tune_grid_{k}"), "sub": m.info(f"tune_sub_{k}"), "us": m.info(f"tune_us_{k}")}
+                  for k in range(m.info("tune_n"))]}
     del sb, rb, rsb
     if args.rccl and m.info("nshare") > 1:
         extra["rccl_comparator"] = {"skipped": "ranks share one GPU: RCCL refuses several ranks on one device"}
@@ -461,7 +466,8 @@ def bench_nranks(args, L, rank, size):
         "config": {"workload": "configs[2]: osu_allreduce -d rocm fp32 SUM 256 MiB, 1 rank per GPU over xGMI",
                    "count": count, "bytes": S_BYTES, "algorithm": "pipelined direct RS+AG (pushes into peer arenas over xGMI)",
                    "latency_8B_us": round(lat_s * 1e6, 2), "latency_8B_kernel_us": round(lat_k_ms * 1e3, 2),
-                   "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing"},
+                   "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing",
+                   "pipe_tiling": tiling},
         "roofline": ({"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
                       "frac": round(kbus / peak_all, 4), "traffic": None,
                       "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",

@@ -178,7 +178,9 @@ int mv2h_local_rank(void);
 int mv2h_timing_enable(int on);
 double mv2h_last_kernel_ms(void);
 int mv2h_set_tuning(const char *key, long value);
-/* runtime facts: "nshare" (most ranks sharing one GPU), "device", "cus", "light_release", "oneshot_max" */
+/* runtime facts: "nshare" (most ranks sharing one GPU), "device", "cus", "light_release", "oneshot_max",
+ * "pipe_grid" / "pipe_sub" (pipelined kernels' tiling), "pipe_tuned" (1: chosen by the MPI_Init
+ * autotune), "tune_n" and per candidate k "tune_grid_<k>", "tune_sub_<k>", "tune_us_<k>" (max over ranks) */
 int mv2h_get_info(const char *key, long *value);
 
 #ifdef __cplusplus

@@ -57,8 +57,8 @@ enum PipeMode : int {
 // (scalar head, 16-byte body, scalar tail).  The stride leaves room for it.
 constexpr int kPipeThreads = 512;                // 8 waves per workgroup
 constexpr int kPipeMaxGrid = 256;                // one workgroup per CU
-constexpr size_t kPipeMaxSub = (size_t)64 << 10;
-constexpr size_t kPipeSlot = (size_t)kPipeMaxGrid * kPipeMaxSub;  // 16 MiB of data
+constexpr size_t kPipeMaxSub = (size_t)128 << 10;
+constexpr size_t kPipeSlot = (size_t)kPipeMaxGrid * kPipeMaxSub;  // 32 MiB of data
 constexpr size_t kPipeSlotStride = kPipeSlot + 256;
 constexpr size_t kPipeRegion = 2 * (size_t)kMaxRanks * kPipeSlotStride;
 

@@ -18,6 +18,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "../../../include/mv2h.h"
@@ -305,7 +306,9 @@ static PipeGeom pipe_geom(size_t maxlen) {
     g.grid = (int)std::min<size_t>((size_t)cap, std::max<size_t>(1, (maxlen + kMinSub - 1) / kMinSub));
     size_t tsub = (maxlen + g.grid - 1) / g.grid;
     tsub = (tsub + 4095) & ~(size_t)4095;
-    g.tsub = std::min(tsub, std::min(kPipeMaxSub, std::max<size_t>(4096, w.pipe_sub)));
+    // a round's slot (grid x tsub) must fit the kPipeSlot bytes of an arena slot
+    const size_t sub_cap = std::min(kPipeSlot / (size_t)g.grid, std::max<size_t>(4096, w.pipe_sub));
+    g.tsub = std::min(tsub, sub_cap & ~(size_t)4095);
     g.tseg = (size_t)g.grid * g.tsub;
     g.nrounds = (int)((maxlen + g.tseg - 1) / g.tseg);
     return g;
@@ -429,6 +432,86 @@ int coll_selftest() {
     return verdict;
 }
 
+// Init-time choice of the pipelined kernels' tiling (workgroups x bytes per workgroup per
+// round) on this node's links.  The link rate of a peer store stream and the cost of a
+// round's flag exchange are properties of the machine, not of the message, so MPI_Init times
+// the headline operation — a 256 MiB fp32 SUM MPI_Allreduce, which takes the ring-wrapper
+// order — under a few tilings on every rank, takes each candidate's maximum over ranks through
+// the host control segment, and every rank adopts the same minimum (kernels pair workgroup b
+// of every rank, so the grid must agree).  The tiling never changes a result: the reduction
+// order is fixed per element by the plan.  Runs with one rank per GPU (xGMI) unless
+// MV2AMD_PIPE_AUTOTUNE=0, or on a shared GPU with MV2AMD_PIPE_AUTOTUNE=1; an explicit
+// MV2AMD_PIPE_GRID / MV2AMD_PIPE_SUB disables it.
+int pipe_autotune() {
+    World &w = world();
+    const char *ev = getenv("MV2AMD_PIPE_AUTOTUNE");
+    const long mode = ev && *ev ? atol(ev) : -1;
+    if (mode == 0 || (mode < 0 && w.nshare > 1) || w.size < 2 || getenv("MV2AMD_PIPE_GRID") ||
+        getenv("MV2AMD_PIPE_SUB"))
+        return 0;
+    const char *eb = getenv("MV2AMD_PIPE_AUTOTUNE_BYTES");
+    const size_t count = (size_t)(eb && atol(eb) > 0 ? atol(eb) : 256L << 20) / 4;
+    const int MPI_FLOAT_H = 0x4c00040a, MPI_SUM_H = 0x58000003;
+    void *sb = nullptr, *rb = nullptr;
+    if (hipMalloc(&sb, count * 4) != hipSuccess || hipMalloc(&rb, count * 4) != hipSuccess) {
+        if (sb) hipFree(sb);
+        MV2_DEBUG("pipe autotune skipped: no device memory for the probe buffers");
+        return 0;
+    }
+    hipMemset(sb, 0, count * 4);
+    hipDeviceSynchronize();
+    static const int kGrid[] = {256, 256, 256, 128, 128, 64};
+    static const size_t kSub[] = {128 << 10, 64 << 10, 32 << 10, 256 << 10, 128 << 10, 512 << 10};
+    const int g0 = w.pipe_grid;
+    const size_t s0 = w.pipe_sub;
+    int nc = 0;
+    int rc = 0;
+    for (int c = 0; c < (int)(sizeof(kGrid) / sizeof(kGrid[0])) && nc < kTuneMax; ++c) {
+        w.pipe_grid = kGrid[c];
+        w.pipe_sub = kSub[c];
+        const PipeGeom g = pipe_geom((count * 4 + w.size - 1) / w.size);
+        bool dup = false;  // the grid cap of a shared GPU can fold candidates together
+        for (int k = 0; k < nc; ++k) dup |= w.tune_grid[k] == g.grid && w.tune_sub[k] == g.tsub;
+        if (dup) continue;
+        w.tune_grid[nc] = g.grid;
+        w.tune_sub[nc] = g.tsub;
+        double best = 1e30;
+        for (int it = 0; it < 4 && !rc; ++it) {  // the first call warms the tiling up
+            host_barrier();
+            const auto t0 = std::chrono::steady_clock::now();
+            rc = mv2h_allreduce(sb, rb, count, MPI_FLOAT_H, MPI_SUM_H, nullptr);
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            if (it) best = std::min(best, us);
+        }
+        if (rc) break;
+        w.shm->r[w.rank].tune_us[nc] = best;
+        ++nc;
+    }
+    hipFree(sb);
+    hipFree(rb);
+    host_barrier();  // every rank's timings are in the control segment
+    w.pipe_grid = g0;
+    w.pipe_sub = s0;
+    if (rc) {
+        MV2_ERR("pipe autotune: probe allreduce failed");
+        return rc;
+    }
+    int pick = 0;
+    for (int k = 0; k < nc; ++k) {
+        double m = 0;
+        for (int j = 0; j < w.size; ++j) m = std::max(m, w.shm->r[j].tune_us[k]);
+        w.tune_us[k] = m;
+        if (m < w.tune_us[pick]) pick = k;
+    }
+    host_barrier();  // every rank has read every timing
+    w.tune_n = nc;
+    w.pipe_grid = w.tune_grid[pick];
+    w.pipe_sub = w.tune_sub[pick];
+    w.pipe_tuned = 1;
+    MV2_DEBUG("pipe autotune: grid %d sub %zu (%.1f us of %d candidates)", w.pipe_grid, w.pipe_sub, w.tune_us[pick], nc);
+    return 0;
+}
+
 }  // namespace mv2
 
 using namespace mv2;
@@ -500,7 +583,19 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "cus")) *value = w.cus;
     else if (!strcmp(key, "light_release")) *value = w.light_release;
     else if (!strcmp(key, "oneshot_max")) *value = (long)w.oneshot_max;
-    else return E_ARG;
+    else if (!strcmp(key, "pipe_grid")) *value = w.pipe_grid;
+    else if (!strcmp(key, "pipe_sub")) *value = (long)w.pipe_sub;
+    else if (!strcmp(key, "pipe_tuned")) *value = w.pipe_tuned;
+    else if (!strcmp(key, "tune_n")) *value = w.tune_n;
+    else if (!strncmp(key, "tune_", 5) && strlen(key) > 7 && key[strlen(key) - 2] == '_') {
+        // tune_grid_<k> / tune_sub_<k> / tune_us_<k>: candidate k of pipe_autotune
+        const int k = key[strlen(key) - 1] - '0';
+        if (k < 0 || k >= w.tune_n) return E_ARG;
+        if (!strncmp(key, "tune_grid_", 10)) *value = w.tune_grid[k];
+        else if (!strncmp(key, "tune_sub_", 9)) *value = (long)w.tune_sub[k];
+        else if (!strncmp(key, "tune_us_", 8)) *value = (long)(w.tune_us[k] + 0.5);
+        else return E_ARG;
+    } else return E_ARG;
     return 0;
 }
 

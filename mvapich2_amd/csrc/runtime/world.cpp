@@ -315,7 +315,8 @@ int world_init() {
     }
     w.inited = true;
     if (w.size > 1 && w.size <= kMaxRanks && !control_only && env_long("MV2AMD_SELFTEST", 1) != 0) {
-        const int rc = coll_selftest();
+        int rc = coll_selftest();
+        if (!rc) rc = pipe_autotune();
         if (rc) {
             w.inited = false;
             return rc;

@@ -52,6 +52,8 @@ struct alignas(64) P2PChan {
     P2PRec rec[kP2PSlots];
 };
 
+constexpr int kTuneMax = 8;  // pipe_autotune candidates
+
 struct alignas(64) ShmRank {
     std::atomic<uint64_t> arrive;  // host barrier generation
     char pad0[56];
@@ -67,6 +69,7 @@ struct alignas(64) ShmRank {
     hipIpcMemHandle_t pipe_ag_handle;
     hipIpcMemHandle_t p2p_handle;
     int selftest_ok;  // coll_selftest verdict of this rank (agreed through host_barrier)
+    double tune_us[kTuneMax];  // pipe_autotune: this rank's time per candidate tiling
     Knobs knobs;      // MV2_* selection knobs as this rank parsed them (must agree)
 };
 
@@ -118,6 +121,11 @@ struct World {
     int pipe_grid = kPipeMaxGrid;                 // pipelined collectives: workgroups (<= kPipeMaxGrid)
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
+    int pipe_tuned = 0;                           // 1: pipe_grid / pipe_sub chosen by pipe_autotune
+    int tune_n = 0;                               // candidates timed by pipe_autotune
+    int tune_grid[kTuneMax] = {};
+    size_t tune_sub[kTuneMax] = {};
+    double tune_us[kTuneMax] = {};                // max over ranks per candidate
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
@@ -144,6 +152,7 @@ void host_barrier();
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
+int pipe_autotune();  // coll.cpp: init-time choice of the pipelined kernels' tiling
 void host_prof_report();  // coll.cpp: MV2AMD_HOST_PROFILE summary
 
 }  // namespace mv2

@@ -146,6 +146,9 @@ def main():
                 rc = L.MPI_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * ext)
+        elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)
+            keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n"]
+            res = np.array([m.info(key) for key in keys], dtype=np.int64)
         elif k == "mpit_counts":  # MPI_T: start every counter, run the calls, read the counters
             prov = ctypes.c_int()
             assert L.MPI_T_init_thread(3, ctypes.byref(prov)) == 0

@@ -9,7 +9,8 @@ import numpy as np
 from oracle import oracle
 
 PIPE_MAX_GRID = 256
-PIPE_MAX_SUB = 64 << 10
+PIPE_MAX_SUB = 128 << 10
+PIPE_SLOT = PIPE_MAX_GRID * PIPE_MAX_SUB  # bytes of one arena slot (kPipeSlot)
 PIPE_MIN_SUB = 16 << 10
 
 
@@ -19,7 +20,7 @@ def pipe_geom(maxlen, cus=256, nshare=1, pipe_grid=PIPE_MAX_GRID, pipe_sub=PIPE_
     g = min(cap, max(1, -(-maxlen // PIPE_MIN_SUB)))
     tsub = -(-maxlen // g)
     tsub = (tsub + 4095) & ~4095
-    tsub = min(tsub, min(PIPE_MAX_SUB, max(4096, pipe_sub)))
+    tsub = min(tsub, min(PIPE_SLOT // g, max(4096, pipe_sub)) & ~4095)
     tseg = g * tsub
     return g, tsub, tseg, -(-maxlen // tseg)
 

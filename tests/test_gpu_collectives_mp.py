@@ -416,3 +416,25 @@ def test_mpit_counters_follow_the_selection(tmp_path):
     for r in range(n):
         got = json.loads(res("mpit", r).tobytes().decode())
         assert {k: v for k, v in got.items() if v} == want, (r, got)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_pipe_autotune_agrees_and_keeps_results(n, tmp_path):
+    """MPI_Init's tiling autotune (coll.cpp pipe_autotune), forced on the shared GPU with a
+    16 MiB probe: every rank adopts the same grid and bytes per workgroup (workgroup b of every
+    rank pairs with workgroup b), and the calls after it stay bit-exact with the oracle (the
+    tiling never changes the reduction order)."""
+    cases = [{"id": "ti", "kind": "tiling_info"}]
+    for seed, (t, op, count) in enumerate((("MPI_FLOAT", "MPI_SUM", 1 << 21), ("MPI_DOUBLE", "MPI_SUM", 300007),
+                                           ("MPI_FLOAT", "MPI_SUM", 70001)), start=600):
+        cases.append({"id": f"at{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
+    res = run_workers(n, cases, tmp_path, extra_env={"MV2AMD_PIPE_AUTOTUNE": "1",
+                                                     "MV2AMD_PIPE_AUTOTUNE_BYTES": str(16 << 20)})
+    infos = [res("ti", r).view(np.int64) for r in range(n)]
+    assert infos[0][0] == 1 and infos[0][3] >= 1, infos[0]
+    for r in range(1, n):
+        assert np.array_equal(infos[r], infos[0]), (r, infos[r], infos[0])
+    for case in cases[1:]:
+        want = expected_allreduce(case, n)
+        for r in range(n):
+            assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"], f"{case['id']} rank {r}")

@@ -28,8 +28,12 @@ def inputs(t, count, rank, seed):
 
 
 def test_geometry_matches_runtime_rules():
-    # 256 MiB fp32 on 8 ranks: 32 MiB segments, 256 workgroups x 64 KiB, 2 rounds
-    assert pm.pipe_geom(32 << 20) == (256, 64 << 10, 16 << 20, 2)
+    # 256 MiB fp32 on 8 ranks: 32 MiB segments, 256 workgroups x 128 KiB, one round (default tiling)
+    assert pm.pipe_geom(32 << 20) == (256, 128 << 10, 32 << 20, 1)
+    # 256 MiB on 2 ranks: 128 MiB segments, 4 rounds; a tuned 128 x 256 KiB tiling keeps the slot size
+    assert pm.pipe_geom(128 << 20) == (256, 128 << 10, 32 << 20, 4)
+    assert pm.pipe_geom(128 << 20, pipe_grid=128, pipe_sub=256 << 10) == (128, 256 << 10, 32 << 20, 4)
+    assert pm.pipe_geom(128 << 20, pipe_grid=256, pipe_sub=512 << 10)[1] == 128 << 10
     # 1 MiB segment: 64 workgroups x 16 KiB, one round
     assert pm.pipe_geom(1 << 20) == (64, 16 << 10, 1 << 20, 1)
     # tests sharing one GPU between 4 ranks: grid capped at cus / 4
