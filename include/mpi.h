@@ -314,6 +314,25 @@ int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]);
 int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]);
 int MPI_Request_free(MPI_Request *request);
 
+/* ---- stream-ordered collectives (extension, not in MVAPICH2 2.3.7): the blocking calls'
+ * algorithms launched on a HIP stream (`stream` is a hipStream_t) behind every collective
+ * issued before, returning without waiting (mv2h.h *_enqueue).  Device buffers, predefined
+ * ops and contiguous predefined types only; MPIX_Enqueue_check reports a peer timeout of a
+ * stream-ordered call after its stream has been synchronised.  MPICH 4's MPIX_*_enqueue
+ * take the stream from a stream communicator; here it is an argument of COMM_WORLD calls. */
+int MPIX_Allreduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                           MPI_Op op, MPI_Comm comm, void *stream);
+int MPIX_Reduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                        MPI_Op op, int root, MPI_Comm comm, void *stream);
+int MPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int recvcounts[],
+                                MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, void *stream);
+int MPIX_Allgather_enqueue(const void *sendbuf, int sendcount, MPI_Datatype sendtype,
+                           void *recvbuf, int recvcount, MPI_Datatype recvtype, MPI_Comm comm,
+                           void *stream);
+int MPIX_Bcast_enqueue(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm,
+                       void *stream);
+int MPIX_Enqueue_check(MPI_Comm comm);
+
 /* ---- point-to-point on device or host buffers, COMM_WORLD of one node (MPI-3.1 3.2-3.7) ---- */
 int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
 int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
@@ -405,6 +424,18 @@ int PMPI_Ireduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount
                               MPI_Request *request);
 int PMPI_Iallgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf,
                    int recvcount, MPI_Datatype recvtype, MPI_Comm comm, MPI_Request *request);
+int PMPIX_Allreduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                            MPI_Op op, MPI_Comm comm, void *stream);
+int PMPIX_Reduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                         MPI_Op op, int root, MPI_Comm comm, void *stream);
+int PMPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int recvcounts[],
+                                 MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, void *stream);
+int PMPIX_Allgather_enqueue(const void *sendbuf, int sendcount, MPI_Datatype sendtype,
+                            void *recvbuf, int recvcount, MPI_Datatype recvtype, MPI_Comm comm,
+                            void *stream);
+int PMPIX_Bcast_enqueue(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm,
+                        void *stream);
+int PMPIX_Enqueue_check(MPI_Comm comm);
 int PMPI_Ibcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm,
                MPI_Request *request);
 int PMPI_Ibarrier(MPI_Comm comm, MPI_Request *request);

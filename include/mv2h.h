@@ -5,8 +5,9 @@
  * void*, NULL = the library's internal stream).
  *
  * Every entry point is synchronous with respect to the caller (MPI blocking
- * semantics): on return the result is complete in device memory.  Return
- * value is MPI_SUCCESS (0) or an MPI error class.
+ * semantics): on return the result is complete in device memory — except the
+ * stream-ordered *_enqueue calls, which complete in the order of their stream.
+ * Return value is MPI_SUCCESS (0) or an MPI error class.
  *
  * Reference interfaces each entry point replaces (MVAPICH2 2.3.7):
  *   mv2h_reduce_local   MPIR_Reduce_local_impl        src/mpi/coll/reduce_local.c:36-173
@@ -72,6 +73,25 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
 int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes_per_rank, void *stream);
 int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream);
 int mv2h_barrier(void);
+
+/* ---- stream-ordered collectives (SURVEY §8(f) rank 3 "stream-ordered variants") ----
+ * Same selection, reduction orders and kernels as the calls above, launched on `stream`
+ * (a hipStream_t, required) after every collective this process issued before on any
+ * stream, and returning without waiting: work queued behind them on `stream` sees the
+ * result.  Device buffers and predefined ops only (E_ARG otherwise).  Buffers must stay
+ * valid until the stream reaches the call.  A peer that never arrives makes the kernel
+ * give up after MV2AMD_TIMEOUT_S and raise the error that mv2h_enqueue_check (or the next
+ * blocking call) returns once the stream has been synchronised. */
+int mv2h_allreduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op,
+                           void *stream);
+int mv2h_reduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op,
+                        int root, void *stream);
+int mv2h_reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const size_t *recvcounts,
+                                int dtype, int op, void *stream);
+int mv2h_allgather_enqueue(const void *sendbuf, void *recvbuf, size_t bytes_per_rank, void *stream);
+int mv2h_bcast_enqueue(void *buffer, size_t bytes, int root, void *stream);
+int mv2h_copy_enqueue(void *dst, const void *src, size_t bytes, void *stream);
+int mv2h_enqueue_check(void);
 
 /* ---- nonblocking collectives (MPI_Iallreduce family, reference iallreduce_osu.c) ----
  * Between mv2h_defer_begin() and mv2h_defer_end(&ticket) the device collectives above

@@ -129,6 +129,13 @@ def lib():
         "MPI_Irecv": ([c_vp, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)], c_int),
         "MPI_Sendrecv": ([c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "MPI_Get_count": ([c_vp, c_int, ctypes.POINTER(c_int)], c_int),
+        # stream-ordered collectives (extension; the last argument is a hipStream_t)
+        "MPIX_Allreduce_enqueue": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "MPIX_Reduce_enqueue": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "MPIX_Reduce_scatter_enqueue": ([c_vp, c_vp, ctypes.POINTER(c_int), c_int, c_int, c_int, c_vp], c_int),
+        "MPIX_Allgather_enqueue": ([c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp], c_int),
+        "MPIX_Bcast_enqueue": ([c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "MPIX_Enqueue_check": ([c_int], c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

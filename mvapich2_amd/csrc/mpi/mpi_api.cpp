@@ -869,6 +869,126 @@ int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm
 }
 int MPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm) WEAK(MPI_Bcast);
 
+// ---------------------------------------------------------------------------
+// Stream-ordered collectives (extension; mv2h.h *_enqueue): argument checks of the blocking
+// calls, then the same algorithms launched on the caller's HIP stream without waiting.
+// Calls the host would have to finish after the kernel — user ops, x87 types, derived
+// types, host buffers — are refused with MPI_ERR_ARG / MPI_ERR_TYPE instead of blocking.
+// ---------------------------------------------------------------------------
+static int enqueue_arg_checks(MPI_Datatype dt, MPI_Op op, void *stream) {
+    if (!stream) return MPI_ERR_ARG;
+    if (user_op(op)) return MPI_ERR_ARG;
+    if (is_x87(dt) || !dtype_is_contiguous(dt)) return MPI_ERR_TYPE;
+    return MPI_SUCCESS;
+}
+
+int PMPIX_Allreduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm,
+                            void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPIX_Allreduce_enqueue";
+    int rc = coll_checks(comm, count, dt, op);
+    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
+    if (rc) return err_return(comm, rc, fn);
+    if (count == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) {  // a stream-ordered copy
+        if (sendbuf == MPI_IN_PLACE || sendbuf == recvbuf) return MPI_SUCCESS;
+        if (!is_dev(sendbuf) || !is_dev(recvbuf)) return err_return(comm, MPI_ERR_ARG, fn);
+        return err_return(comm, mv2h_copy_enqueue(recvbuf, sendbuf, (size_t)dtype_span(dt, count), stream), fn);
+    }
+    return err_return(comm, mv2h_allreduce_enqueue(sendbuf, recvbuf, (size_t)count, dt, op, stream), fn);
+}
+int MPIX_Allreduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm,
+                           void *stream) WEAK(MPIX_Allreduce_enqueue);
+
+int PMPIX_Reduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root,
+                         MPI_Comm comm, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPIX_Reduce_enqueue";
+    int rc = coll_checks(comm, count, dt, op);
+    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
+    if (rc) return err_return(comm, rc, fn);
+    const int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (count == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) return PMPIX_Allreduce_enqueue(sendbuf, recvbuf, count, dt, op, comm, stream);
+    return err_return(comm, mv2h_reduce_enqueue(sendbuf, recvbuf, (size_t)count, dt, op, root, stream), fn);
+}
+int MPIX_Reduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root,
+                        MPI_Comm comm, void *stream) WEAK(MPIX_Reduce_enqueue);
+
+int PMPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
+                                 MPI_Comm comm, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPIX_Reduce_scatter_enqueue";
+    int rc = coll_checks(comm, 0, dt, op);
+    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
+    if (rc) return err_return(comm, rc, fn);
+    if (!recvcounts) return err_return(comm, MPI_ERR_ARG, fn);
+    const int n = comm == MPI_COMM_SELF ? 1 : world().size;
+    std::vector<size_t> rc_sz(n);
+    size_t total = 0;
+    for (int j = 0; j < n; ++j) {
+        if (recvcounts[j] < 0) return err_return(comm, MPI_ERR_COUNT, fn);
+        rc_sz[j] = (size_t)recvcounts[j];
+        total += rc_sz[j];
+    }
+    if (total == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) return PMPIX_Allreduce_enqueue(sendbuf, recvbuf, recvcounts[0], dt, op, comm, stream);
+    return err_return(comm, mv2h_reduce_scatter_enqueue(sendbuf, recvbuf, rc_sz.data(), dt, op, stream), fn);
+}
+int MPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype dt, MPI_Op op,
+                                MPI_Comm comm, void *stream) WEAK(MPIX_Reduce_scatter_enqueue);
+
+int PMPIX_Allgather_enqueue(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                            MPI_Datatype recvtype, MPI_Comm comm, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPIX_Allgather_enqueue";
+    if (!g_initialized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
+    if (!stream) return err_return(comm, MPI_ERR_ARG, fn);
+    if (recvcount < 0 || (sendbuf != MPI_IN_PLACE && sendcount < 0)) return err_return(comm, MPI_ERR_COUNT, fn);
+    if (!dtype_valid(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_valid(sendtype)))
+        return err_return(comm, MPI_ERR_TYPE, fn);
+    if (!dtype_is_contiguous(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_is_contiguous(sendtype)))
+        return err_return(comm, MPI_ERR_TYPE, fn);
+    const size_t rbytes = (size_t)dtype_span(recvtype, recvcount);
+    if (sendbuf != MPI_IN_PLACE && (size_t)dtype_span(sendtype, sendcount) != rbytes)
+        return err_return(comm, MPI_ERR_TRUNCATE, fn);
+    if (rbytes == 0) return MPI_SUCCESS;
+    if (comm == MPI_COMM_SELF) {
+        if (sendbuf == MPI_IN_PLACE || sendbuf == recvbuf) return MPI_SUCCESS;
+        if (!is_dev(sendbuf) || !is_dev(recvbuf)) return err_return(comm, MPI_ERR_ARG, fn);
+        return err_return(comm, mv2h_copy_enqueue(recvbuf, sendbuf, rbytes, stream), fn);
+    }
+    return err_return(comm, mv2h_allgather_enqueue(sendbuf, recvbuf, rbytes, stream), fn);
+}
+int MPIX_Allgather_enqueue(const void *sendbuf, int sendcount, MPI_Datatype sendtype, void *recvbuf, int recvcount,
+                           MPI_Datatype recvtype, MPI_Comm comm, void *stream) WEAK(MPIX_Allgather_enqueue);
+
+int PMPIX_Bcast_enqueue(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    const char *fn = "MPIX_Bcast_enqueue";
+    if (!g_initialized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
+    if (!stream) return err_return(comm, MPI_ERR_ARG, fn);
+    if (count < 0) return err_return(comm, MPI_ERR_COUNT, fn);
+    if (!dtype_valid(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
+    if (!dtype_is_contiguous(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
+    const int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (count == 0 || size == 1) return MPI_SUCCESS;
+    return err_return(comm, mv2h_bcast_enqueue(buffer, (size_t)dtype_span(dt, count), root, stream), fn);
+}
+int MPIX_Bcast_enqueue(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm, void *stream)
+    WEAK(MPIX_Bcast_enqueue);
+
+int PMPIX_Enqueue_check(MPI_Comm comm) {
+    std::lock_guard<std::recursive_mutex> lk(g_cs);
+    if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPIX_Enqueue_check");
+    return err_return(comm, mv2h_enqueue_check(), "MPIX_Enqueue_check");
+}
+int MPIX_Enqueue_check(MPI_Comm comm) WEAK(MPIX_Enqueue_check);
+
 }  // extern "C"
 
 // ---------------------------------------------------------------- requests

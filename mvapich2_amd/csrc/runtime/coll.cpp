@@ -39,7 +39,34 @@ bool log_debug_on() {
     return on == 1;
 }
 
-static hipStream_t pick_stream(void *s) { return s ? (hipStream_t)s : world().stream; }
+// The stream of a call.  Every collective kernel of this process shares the arenas, flag
+// epochs and slot parities, which the host hands out in call order, so the kernels must also
+// run in call order whatever stream each call names.  One event carries the order: a call on
+// a caller's stream records it on that stream when it ends (stream_tail — the caller may
+// destroy the stream afterwards, so the library never touches it again), a call on the
+// library's own stream records it lazily when the next call names another stream; a call on
+// a stream other than the previous one first waits for it.  Calls that stay on one stream
+// pay nothing for the order.  (A caller's stream handle reused after hipStreamDestroy is
+// safe: the destroy drains the stream's queue first.)
+static hipStream_t pick_stream(void *s) {
+    World &w = world();
+    hipStream_t st = s ? (hipStream_t)s : w.stream;
+    if (w.last_st && st != w.last_st) {
+        if (!w.sw_ev) hipEventCreateWithFlags(&w.sw_ev, hipEventDisableTiming);
+        if (w.sw_ev) {
+            if (w.last_st == w.stream && st != w.stream) hipEventRecord(w.sw_ev, w.stream);
+            hipStreamWaitEvent(st, w.sw_ev, 0);
+        }
+    }
+    w.last_st = st;
+    return st;
+}
+static void stream_tail(hipStream_t st) {
+    World &w = world();
+    if (st == w.stream) return;
+    if (!w.sw_ev) hipEventCreateWithFlags(&w.sw_ev, hipEventDisableTiming);
+    if (w.sw_ev) hipEventRecord(w.sw_ev, st);
+}
 
 // Host-side profile of blocking calls (MV2AMD_HOST_PROFILE=1, printed at
 // MPI_Finalize): time from API entry to the kernel launch (argument checks,
@@ -90,7 +117,7 @@ void host_prof_report() {
 // any copy enqueued after it, see enq_copy).
 static Done arm_done(hipStream_t st) {
     World &w = world();
-    if (w.sync_mode != 0 || !w.done_flag || st != w.stream) return Done{nullptr, nullptr, 0};
+    if (w.sync_mode != 0 || !w.done_flag || st != w.stream || w.enqueue) return Done{nullptr, nullptr, 0};
     w.pending = ++w.done_seq;
     return Done{w.done_ctr, w.done_flag, w.pending};
 }
@@ -143,6 +170,8 @@ static int finish(hipStream_t st, bool timed) {
     hipError_t e;
     const uint64_t want = w.pending;
     w.pending = 0;
+    stream_tail(st);
+    if (w.enqueue) return 0;  // stream-ordered: the caller's stream carries the completion
     if (w.defer && want) {  // nonblocking initiation: the ticket waits later
         w.deferred = want;
         return 0;
@@ -1304,5 +1333,84 @@ int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent, 
     if (rc) return rc;
     return finish(st, world().timing);
 }
+
+// ---------------------------------------------------------------------------
+// Stream-ordered collectives (§8(f) rank 3, "stream-ordered variants"): the same selection,
+// orders and kernels as the blocking calls, launched on the caller's HIP stream after every
+// collective this process issued before (pick_stream), returning without waiting.  Kernels
+// queued behind it on that stream see the result; the host never blocks, so compute and
+// communication overlap without MPI_Wait.  Device buffers only (a host buffer would need a
+// host copy after the kernel) and builtin ops (user ops and x87 run on the host).
+// ---------------------------------------------------------------------------
+struct EnqueueScope {
+    EnqueueScope() { world().enqueue = true; }
+    ~EnqueueScope() { world().enqueue = false; }
+};
+static int enqueue_checks(const void *send, const void *recv, void *stream) {
+    if (!stream) return E_ARG;
+    if (!is_device(recv) || (send && send != (const void *)-1 && !is_device(send))) {
+        MV2_ERR("stream-ordered collectives take device buffers only");
+        return E_ARG;
+    }
+    return 0;
+}
+
+int mv2h_allreduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    int rc = count ? enqueue_checks(sendbuf, recvbuf, stream) : 0;
+    if (rc || !count) return rc;
+    EnqueueScope q;
+    return mv2h_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+}
+
+int mv2h_reduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+    if (!count) return 0;
+    const World &w = world();
+    // recvbuf is significant at the root only
+    int rc = enqueue_checks(sendbuf, w.rank == root ? recvbuf : (sendbuf == (const void *)-1 ? nullptr : sendbuf),
+                            stream);
+    if (rc) return rc;
+    EnqueueScope q;
+    return mv2h_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
+}
+
+int mv2h_reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
+                                void *stream) {
+    const World &w = world();
+    if (!recvcounts) return E_ARG;
+    int rc = enqueue_checks(sendbuf, recvcounts[w.rank] ? recvbuf : (sendbuf == (const void *)-1 ? nullptr : sendbuf),
+                            stream);
+    if (rc) return rc;
+    EnqueueScope q;
+    return mv2h_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
+}
+
+int mv2h_allgather_enqueue(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
+    int rc = bytes ? enqueue_checks(sendbuf, recvbuf, stream) : 0;
+    if (rc || !bytes) return rc;
+    EnqueueScope q;
+    return mv2h_allgather(sendbuf, recvbuf, bytes, stream);
+}
+
+int mv2h_bcast_enqueue(void *buffer, size_t bytes, int root, void *stream) {
+    int rc = bytes ? enqueue_checks(nullptr, buffer, stream) : 0;
+    if (rc || !bytes) return rc;
+    EnqueueScope q;
+    return mv2h_bcast(buffer, bytes, root, stream);
+}
+
+// device-to-device copy in the same stream order (COMM_SELF forms of the calls above)
+int mv2h_copy_enqueue(void *dst, const void *src, size_t bytes, void *stream) {
+    int rc = bytes ? enqueue_checks(src, dst, stream) : 0;
+    if (rc || !bytes) return rc;
+    if ((rc = ensure_init_for_device())) return rc;
+    hipStream_t st = pick_stream(stream);
+    rc = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : E_INTERN;
+    stream_tail(st);
+    return rc;
+}
+
+// errors of stream-ordered calls (a peer that never arrived) surface once their stream has
+// been synchronised: the kernels set the host error word instead of hanging
+int mv2h_enqueue_check(void) { return check_err_word(); }
 
 }  // extern "C"

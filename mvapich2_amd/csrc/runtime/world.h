@@ -133,6 +133,9 @@ struct World {
     uint64_t done_seq = 0;          // last sequence number armed
     uint64_t pending = 0;           // seq the current call waits for (0: stream sync)
     bool defer = false;             // nonblocking initiation: finish() leaves the wait to a ticket
+    bool enqueue = false;           // stream-ordered call (mv2h_*_enqueue): launch on the caller's stream, no wait
+    hipStream_t last_st = nullptr;  // stream of the last library launch (cross-stream ordering, pick_stream)
+    hipEvent_t sw_ev = nullptr;     // recorded on last_st when a call switches streams
     uint64_t deferred = 0;          // ticket of the last deferred call (0: completed at initiation)
 
     // timing (bench)

@@ -23,6 +23,53 @@ def inputs(case, rank):
     return rand_typed(case["type"], case["count"], rng, small=case.get("small", False))
 
 
+def enqueue_seq(L, case, rank, n):
+    """On a HIP stream of its own: y = Allreduce(x); z = Allreduce(y) (reads the previous call's
+    result in stream order); Bcast(xb) from root 1 % n; Reduce_scatter(x); Allgather(first `per`
+    elements of x); then a blocking MPI_Allreduce(x) -> w on the library's stream (must run after
+    the queued calls); then Reduce(x, MAX) to root 0 on the stream again.  One host sync at the
+    end; the stream is destroyed and one more blocking MPI_Allreduce(x) -> w2 follows.
+    Returns the concatenated bytes y | z | xb | w | rs | ag | r | w2."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+    F, SUM, MAX = TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], OPS["MPI_MAX"]
+    c = case["count"]
+    x = inputs(case, rank)
+    counts = case["recvcounts"]
+    per = case["per"]
+    sb = m.DeviceBuffer.from_array(x)
+    y, z, w, r = (m.DeviceBuffer(c * 4) for _ in range(4))
+    xb = m.DeviceBuffer.from_array(x)
+    rs, ag = m.DeviceBuffer(max(1, counts[rank]) * 4), m.DeviceBuffer(per * n * 4)
+    for b in (y, z, w, r):
+        b.upload(np.zeros(c, dtype=np.float32))
+    rcs = (ctypes.c_int * n)(*counts)
+    s = st.value
+    P = ctypes.c_void_p
+    assert L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), c, F, SUM, WORLD, P(s)) == 0
+    assert L.MPIX_Allreduce_enqueue(P(y.ptr), P(z.ptr), c, F, SUM, WORLD, P(s)) == 0
+    assert L.MPIX_Bcast_enqueue(P(xb.ptr), c, F, 1 % n, WORLD, P(s)) == 0
+    assert L.MPIX_Reduce_scatter_enqueue(P(sb.ptr), P(rs.ptr), rcs, F, SUM, WORLD, P(s)) == 0
+    assert L.MPIX_Allgather_enqueue(P(sb.ptr), per, F, P(ag.ptr), per, F, WORLD, P(s)) == 0
+    assert L.MPI_Allreduce(sb.ptr, w.ptr, c, F, SUM, WORLD) == 0
+    assert L.MPIX_Reduce_enqueue(P(sb.ptr), P(r.ptr), c, F, MAX, 0, WORLD, P(s)) == 0
+    # refused: host buffers and user ops cannot be stream-ordered
+    hx = np.zeros(4, dtype=np.float32)
+    assert L.MPIX_Allreduce_enqueue(P(hx.ctypes.data), P(y.ptr), 4, F, SUM, WORLD, P(s)) != 0
+    assert L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), 4, F, SUM, WORLD, None) != 0
+    assert hip.hipStreamSynchronize(st) == 0
+    assert L.MPIX_Enqueue_check(WORLD) == 0
+    out = [b.download(np.uint8, count=nb) for b, nb in ((y, c * 4), (z, c * 4), (xb, c * 4), (w, c * 4),
+                                                       (rs, counts[rank] * 4), (ag, per * n * 4), (r, c * 4))]
+    hip.hipStreamDestroy(st)
+    # a blocking call after the caller destroyed its stream: the library keeps no handle to it
+    w2 = m.DeviceBuffer(c * 4)
+    assert L.MPI_Allreduce(sb.ptr, w2.ptr, c, F, SUM, WORLD) == 0
+    out.append(w2.download(np.uint8, count=c * 4))
+    return np.concatenate(out)
+
+
 def big_case(L, case, rank, n):
     """Full-size BASELINE configs, checked in the worker against closed forms (256 MiB results
     are not shipped back): returns [number of wrong elements]."""
@@ -146,6 +193,8 @@ def main():
                 rc = L.MPI_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * ext)
+        elif k == "enqueue_seq":  # stream-ordered collectives (MPIX_*_enqueue) mixed with a blocking call
+            res = enqueue_seq(L, case, rank, n)
         elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)
             keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n"]
             res = np.array([m.info(key) for key in keys], dtype=np.int64)

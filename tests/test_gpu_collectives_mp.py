@@ -438,3 +438,45 @@ def test_pipe_autotune_agrees_and_keeps_results(n, tmp_path):
         want = expected_allreduce(case, n)
         for r in range(n):
             assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"], f"{case['id']} rank {r}")
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_stream_ordered_collectives(n, tmp_path):
+    """MPIX_*_enqueue (mv2h.h stream-ordered collectives): a chain of calls on one HIP stream,
+    the second reading the first's result in stream order, a blocking MPI_Allreduce between them
+    (ordered after the queued calls), one host synchronisation at the end; every result is
+    bit-exact with the oracle's simulation of the algorithm the blocking call would take."""
+    cases = []
+    for seed, c in ((501, 1000), (502, (1 << 20) + 5)):
+        counts = [c // n + (1 if r < c % n else 0) for r in range(n)]
+        cases.append({"id": f"eq{seed}", "kind": "enqueue_seq", "type": "MPI_FLOAT", "count": c, "seed": seed,
+                      "recvcounts": counts, "per": c // n})
+    res = run_workers(n, cases, tmp_path)
+    F, SUM, MAX = TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], OPS["MPI_MAX"]
+    for case in cases:
+        c, counts, per = case["count"], case["recvcounts"], case["per"]
+        xs = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+        y = oracle.allreduce_ref(xs, c, F, SUM)
+        z = oracle.allreduce_ref([y[r].copy() for r in range(n)], c, F, SUM)
+        rs_full = oracle.reduce_scatter_ref([x.copy() for x in xs], counts, F, SUM)
+        ag = np.concatenate([x[:per * 4] for x in xs])
+        red = oracle.reduce_ref([x.copy() for x in xs], c, F, MAX, 0)
+        for r in range(n):
+            got = res(case["id"], r)
+            o = 0
+            parts = {}
+            for name, nb in (("y", c * 4), ("z", c * 4), ("xb", c * 4), ("w", c * 4), ("rs", counts[r] * 4),
+                             ("ag", per * n * 4), ("r", c * 4), ("w2", c * 4)):
+                parts[name] = got[o:o + nb]
+                o += nb
+            tag = f"{case['id']} rank {r}"
+            assert_bytes_equal(parts["y"], y[r], "MPI_FLOAT", c, tag + " y")
+            assert_bytes_equal(parts["z"], z[r], "MPI_FLOAT", c, tag + " z")
+            assert np.array_equal(parts["xb"], xs[1 % n]), tag + " bcast"
+            assert_bytes_equal(parts["w"], y[r], "MPI_FLOAT", c, tag + " blocking w")
+            assert_bytes_equal(parts["w2"], y[r], "MPI_FLOAT", c, tag + " blocking w2 after hipStreamDestroy")
+            off = sum(counts[:r]) * 4
+            assert_bytes_equal(parts["rs"], rs_full[off:off + counts[r] * 4], "MPI_FLOAT", counts[r], tag + " rs")
+            assert np.array_equal(parts["ag"], ag), tag + " allgather"
+            if r == 0:
+                assert_bytes_equal(parts["r"], red, "MPI_FLOAT", c, tag + " reduce")
