@@ -84,6 +84,28 @@ def big_case(L, case, rank, n):
         got = rb.download(np.float32, count=cnt)
         want = ((i % 100 + 1) * (n * (n + 1) // 2)).astype(np.float32)
         return np.array([np.count_nonzero(got != want)])
+    if k in ("big_allreduce_rand", "big_reduce_scatter_rand"):
+        # random N(0,1) fp32 at the full size, bit-exact against the oracle's simulation of the
+        # algorithm the reference selects (every rank regenerates all ranks' inputs from seeds)
+        from oracle import oracle
+        cnt = case["count"]
+        xs = [np.random.default_rng(case["seed"] * 1000 + r).standard_normal(cnt, dtype=np.float32) for r in range(n)]
+        sb = m.DeviceBuffer.from_array(xs[rank])
+        if k == "big_allreduce_rand":
+            rb = m.DeviceBuffer(cnt * 4)
+            assert L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, F, OPS["MPI_SUM"], WORLD) == 0
+            got = rb.download(np.uint32, count=cnt)
+            want = oracle.allreduce_ref([x.view(np.uint8) for x in xs], cnt, F, OPS["MPI_SUM"])[rank].view(np.uint32)
+        else:
+            counts = [cnt // n + (1 if r < cnt % n else 0) for r in range(n)]
+            off = sum(counts[:rank])
+            rb = m.DeviceBuffer(counts[rank] * 4)
+            arr = (ctypes.c_int * n)(*counts)
+            assert L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, F, OPS["MPI_SUM"], WORLD) == 0
+            got = rb.download(np.uint32, count=counts[rank])
+            full = oracle.reduce_scatter_ref([x.view(np.uint8) for x in xs], counts, F, OPS["MPI_SUM"]).view(np.uint32)
+            want = full[off:off + counts[rank]]
+        return np.array([np.count_nonzero(got != want)])
     if k == "big_reduce_scatter":  # configs[3]: OMB recvcounts = size/n (+1 for the first size%n)
         tot = case["count"]
         counts = [tot // n + (1 if r < tot % n else 0) for r in range(n)]

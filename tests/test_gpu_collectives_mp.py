@@ -376,13 +376,17 @@ def test_user_op_on_strided_vector_operand(n, tmp_path):
 def test_full_size_baseline_configs(n, tmp_path):
     """BASELINE configs[2]-[4] at their full sizes: 256 MiB fp32 SUM allreduce, 256 MiB
     reduce_scatter / allgather / bcast, 16 Mi-record MAXLOC on MPI_DOUBLE_INT; each rank checks
-    its whole result against closed forms."""
+    its whole result against closed forms — and random N(0,1) fp32 allreduce / reduce_scatter at
+    256 MiB bit-exact against the oracle's simulation of the reference's algorithm (ring wrapper
+    and reduce-scatter ring)."""
     S = 256 << 20
     cases = [{"id": "bg1", "kind": "big_allreduce", "count": S // 4, "seed": 1},
              {"id": "bg2", "kind": "big_reduce_scatter", "count": S // 4, "seed": 2},
              {"id": "bg3", "kind": "big_allgather", "count": S // n, "seed": 3},
              {"id": "bg4", "kind": "big_bcast", "count": S, "seed": 4},
-             {"id": "bg5", "kind": "big_maxloc", "count": S // 16, "seed": 5}]
+             {"id": "bg5", "kind": "big_maxloc", "count": S // 16, "seed": 5},
+             {"id": "bg6", "kind": "big_allreduce_rand", "count": S // 4, "seed": 6},
+             {"id": "bg7", "kind": "big_reduce_scatter_rand", "count": S // 4, "seed": 7}]
     res = run_workers(n, cases, tmp_path, timeout=400)
     for case in cases:
         for r in range(n):
