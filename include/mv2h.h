@@ -81,7 +81,9 @@ int mv2h_barrier(void);
  * result.  Device buffers and predefined ops only (E_ARG otherwise).  Buffers must stay
  * valid until the stream reaches the call.  A peer that never arrives makes the kernel
  * give up after MV2AMD_TIMEOUT_S and raise the error that mv2h_enqueue_check (or the next
- * blocking call) returns once the stream has been synchronised. */
+ * blocking call) returns once the stream has been synchronised.  A stream that is being
+ * captured into a HIP graph is refused (E_UNSUPPORTED): a replay would reuse the captured
+ * call's flag epochs. */
 int mv2h_allreduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op,
                            void *stream);
 int mv2h_reduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op,

@@ -1,16 +1,16 @@
 // coll.cpp — the mv2h_* C-ABI (include/mv2h.h): op layer entry points and
 // host orchestration of the device collectives.
 //
-// Algorithm / order selection restates the reference's single-node choice
-// (MPIR_Allreduce_index_tuned_intra_MV2, allreduce_osu.c:3144-3160): nbytes <=
-// 1024 (mv2_coll_skip_table_threshold, coll_shmem.h:191) -> two-level
-// reduce_shmem order (LINEAR); nbytes >= 2 MiB -> the flat ring wrapper
-// (allreduce_osu.c:163-170, :3758-3818: ring order over count/n chunks, the
-// remainder and every IN_PLACE call through pt2pt_rs); otherwise pt2pt_rs
-// order (BUTTERFLY; recursive-doubling owner when count < pof2,
-// allreduce_osu.c:802).  The data path is MI355X-native:
-// one-shot push through uncached IPC arenas for small messages, direct
-// reduce-scatter + all-gather over xGMI peer mappings for large ones.
+// Every reducing call first takes the reference's one-node algorithm choice
+// (orders.cpp plan_allreduce / plan_reduce / plan_reduce_scatter, restating
+// MPIR_Allreduce_index_tuned_intra_MV2 allreduce_osu.c:3015-3420,
+// MPIR_Reduce_index_tuned_intra_MV2 reduce_osu.c:2391-2660 and
+// MPIR_Reduce_scatter_MV2 red_scat_osu.c:1859-1896) and then runs that
+// algorithm's operand order on the device (specialised LINEAR / ring /
+// butterfly evaluators, or per-element programs).  The data path is
+// MI355X-native: one-shot push through uncached IPC arenas for small messages,
+// pipelined direct reduce-scatter + all-gather pushed into peers' arenas over
+// xGMI for large ones (coll/pipe.h), tiled by the MPI_Init autotune.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1348,6 +1348,13 @@ struct EnqueueScope {
 };
 static int enqueue_checks(const void *send, const void *recv, void *stream) {
     if (!stream) return E_ARG;
+    // a kernel captured into a graph would replay this call's flag epochs and slot parities,
+    // which the host hands out once per call: refuse capture instead of hanging a replay
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        MV2_ERR("stream-ordered collectives cannot be captured into a HIP graph");
+        return E_UNSUPPORTED;
+    }
     if (!is_device(recv) || (send && send != (const void *)-1 && !is_device(send))) {
         MV2_ERR("stream-ordered collectives take device buffers only");
         return E_ARG;

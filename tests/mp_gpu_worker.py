@@ -58,6 +58,16 @@ def enqueue_seq(L, case, rank, n):
     hx = np.zeros(4, dtype=np.float32)
     assert L.MPIX_Allreduce_enqueue(P(hx.ctypes.data), P(y.ptr), 4, F, SUM, WORLD, P(s)) != 0
     assert L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), 4, F, SUM, WORLD, None) != 0
+    # refused: a stream being captured into a HIP graph (a replay would reuse the call's epochs)
+    cap, graph = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(cap)) == 0
+    assert hip.hipStreamBeginCapture(cap, 2) == 0  # hipStreamCaptureModeRelaxed
+    rc_cap = L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), c, F, SUM, WORLD, cap)
+    assert hip.hipStreamEndCapture(cap, ctypes.byref(graph)) == 0
+    if graph.value:
+        hip.hipGraphDestroy(graph)
+    hip.hipStreamDestroy(cap)
+    assert rc_cap != 0
     assert hip.hipStreamSynchronize(st) == 0
     assert L.MPIX_Enqueue_check(WORLD) == 0
     out = [b.download(np.uint8, count=nb) for b, nb in ((y, c * 4), (z, c * 4), (xb, c * 4), (w, c * 4),
