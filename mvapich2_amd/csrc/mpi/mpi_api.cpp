@@ -76,7 +76,7 @@ int err_return(MPI_Comm comm, int code, const char *fn) {
     const int ci = comm_index(comm);
     const MPI_Errhandler eh = ci >= 0 ? g_eh[ci] : MPI_ERRORS_ARE_FATAL;
     if (eh == MPI_ERRORS_ARE_FATAL) {
-        fprintf(stderr, "[mv2amd rank %d] Fatal error in %s: %s\n", world().rank, fn, err_name(code));
+        fprintf(stderr, "[mv2amd rank %d] Fatal error in %s: %s\n", mv2h_rank(), fn, err_name(code));
         fflush(stderr);
         abort();
     }
@@ -315,6 +315,10 @@ int user_allreduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datat
 
 // one MPI_T-counted call (runtime/pvars.h)
 int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
+    if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
+        fprintf(stderr, "[mv2amd] user ops and long double types are not supported across nodes\n");
+        return MPI_ERR_UNSUPPORTED_OPERATION;
+    }
     pvar_begin();
     const int rc = user_allreduce_body(sendbuf, recvbuf, count, dt, u, opk);
     pvar_end(rc == MPI_SUCCESS);
@@ -346,6 +350,10 @@ int user_reduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datatype
 
 // one MPI_T-counted call (runtime/pvars.h)
 int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
+    if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
+        fprintf(stderr, "[mv2amd] user ops and long double types are not supported across nodes\n");
+        return MPI_ERR_UNSUPPORTED_OPERATION;
+    }
     pvar_begin();
     const int rc = user_reduce_body(sendbuf, recvbuf, count, dt, u, root, opk);
     pvar_end(rc == MPI_SUCCESS);
@@ -407,6 +415,10 @@ int user_reduce_scatter_body(const void *sendbuf, void *recvbuf, const int *coun
 
 // one MPI_T-counted call (runtime/pvars.h)
 int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
+    if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
+        fprintf(stderr, "[mv2amd] user ops and long double types are not supported across nodes\n");
+        return MPI_ERR_UNSUPPORTED_OPERATION;
+    }
     pvar_begin();
     const int rc = user_reduce_scatter_body(sendbuf, recvbuf, counts, dt, u, opk);
     pvar_end(rc == MPI_SUCCESS);
@@ -458,7 +470,7 @@ int PMPI_Finalized(int *flag) {
 int MPI_Finalized(int *flag) WEAK(MPI_Finalized);
 
 int PMPI_Abort(MPI_Comm, int errorcode) {
-    fprintf(stderr, "[mv2amd rank %d] MPI_Abort(%d)\n", world().rank, errorcode);
+    fprintf(stderr, "[mv2amd rank %d] MPI_Abort(%d)\n", mv2h_rank(), errorcode);
     fflush(stderr);
     _exit(errorcode ? errorcode : 1);
 }
@@ -519,7 +531,7 @@ int MPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler *eh) WEAK(MPI_Comm_get
 int PMPI_Comm_rank(MPI_Comm comm, int *rank) {
     const int ci = comm_index(comm);
     if (ci < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPI_Comm_rank");
-    *rank = ci == 0 ? world().rank : 0;
+    *rank = ci == 0 ? mv2h_rank() : 0;
     return MPI_SUCCESS;
 }
 int MPI_Comm_rank(MPI_Comm comm, int *rank) WEAK(MPI_Comm_rank);
@@ -527,7 +539,7 @@ int MPI_Comm_rank(MPI_Comm comm, int *rank) WEAK(MPI_Comm_rank);
 int PMPI_Comm_size(MPI_Comm comm, int *size) {
     const int ci = comm_index(comm);
     if (ci < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPI_Comm_size");
-    *size = ci == 0 ? world().size : 1;
+    *size = ci == 0 ? mv2h_size() : 1;
     return MPI_SUCCESS;
 }
 int MPI_Comm_size(MPI_Comm comm, int *size) WEAK(MPI_Comm_size);
@@ -536,7 +548,7 @@ int PMPI_Barrier(MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const int ci = comm_index(comm);
     if (ci < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, "MPI_Barrier");
-    if (ci == 0) host_barrier();
+    if (ci == 0 && mv2h_barrier()) return err_return(comm, MPI_ERR_OTHER, "MPI_Barrier");
     return MPI_SUCCESS;
 }
 int MPI_Barrier(MPI_Comm comm) WEAK(MPI_Barrier);
@@ -710,7 +722,7 @@ int PMPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
     const char *fn = "MPI_Reduce";
     int rc = coll_checks(comm, count, dt, op);
     if (rc) return err_return(comm, rc, fn);
-    int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
     if (count == 0) return MPI_SUCCESS;
     if (comm == MPI_COMM_SELF) {
@@ -738,7 +750,7 @@ int PMPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts
     const char *fn = "MPI_Reduce_scatter";
     int rc = coll_checks(comm, 0, dt, op);
     if (rc) return err_return(comm, rc, fn);
-    const int n = comm == MPI_COMM_SELF ? 1 : world().size;
+    const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     std::vector<size_t> rc_sz(n);
     size_t total = 0;
     for (int j = 0; j < n; ++j) {
@@ -774,7 +786,7 @@ int PMPI_Reduce_scatter_block(const void *sendbuf, void *recvbuf, int recvcount,
     // MPIR_Reduce_scatter_block (red_scat_block.c:305, :515: recursive halving below
     // MPIR_CVAR_REDSCAT_COMMUTATIVE_LONG_MSG_SIZE, pairwise from it) — the same
     // selection as MPI_Ireduce_scatter_block's schedule
-    const int n = comm == MPI_COMM_SELF ? 1 : world().size;
+    const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     std::vector<int> counts(n, recvcount);
     const bool set = nbc_kind() == NBC_NONE;
     if (set) nbc_set(NBC_IREDUCE_SCATTER_BLOCK);
@@ -797,7 +809,7 @@ static int allgather_derived(const void *sendbuf, int sendcount, MPI_Datatype se
     const long psize = rsize * recvcount;
     if (sendbuf != MPI_IN_PLACE && dtype_size(sendtype) * sendcount != psize) return MPI_ERR_TRUNCATE;
     if (psize == 0) return MPI_SUCCESS;
-    const int n = comm == MPI_COMM_SELF ? 1 : world().size, me = comm == MPI_COMM_SELF ? 0 : world().rank;
+    const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size(), me = comm == MPI_COMM_SELF ? 0 : mv2h_rank();
     void *mine = nullptr, *all = nullptr;
     if (mv2h_malloc(&mine, (size_t)psize)) return MPI_ERR_NO_MEM;
     if (mv2h_malloc(&all, (size_t)psize * n)) {
@@ -849,7 +861,7 @@ int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm
     if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
     if (count < 0) return err_return(comm, MPI_ERR_COUNT, fn);
     if (!dtype_valid(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
-    const int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    const int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
     if (count == 0 || size == 1) return MPI_SUCCESS;
     if (dtype_is_contiguous(dt)) return err_return(comm, mv2h_bcast(buffer, (size_t)dtype_span(dt, count), root, nullptr), fn);
@@ -860,10 +872,10 @@ int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm
     void *packed = nullptr;
     if (mv2h_malloc(&packed, (size_t)psize)) return err_return(comm, MPI_ERR_NO_MEM, fn);
     int pos = 0, rc = MPI_SUCCESS;
-    if (world().rank == root) rc = PMPI_Pack(buffer, count, dt, packed, psize, &pos, comm);
+    if (mv2h_rank() == root) rc = PMPI_Pack(buffer, count, dt, packed, psize, &pos, comm);
     if (!rc) rc = mv2h_bcast(packed, (size_t)psize, root, nullptr);
     pos = 0;
-    if (!rc && world().rank != root) rc = PMPI_Unpack(packed, psize, &pos, buffer, count, dt, comm);
+    if (!rc && mv2h_rank() != root) rc = PMPI_Unpack(packed, psize, &pos, buffer, count, dt, comm);
     mv2h_free(packed);
     return err_return(comm, rc, fn);
 }
@@ -907,7 +919,7 @@ int PMPIX_Reduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Data
     int rc = coll_checks(comm, count, dt, op);
     if (!rc) rc = enqueue_arg_checks(dt, op, stream);
     if (rc) return err_return(comm, rc, fn);
-    const int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    const int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
     if (count == 0) return MPI_SUCCESS;
     if (comm == MPI_COMM_SELF) return PMPIX_Allreduce_enqueue(sendbuf, recvbuf, count, dt, op, comm, stream);
@@ -924,7 +936,7 @@ int PMPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int r
     if (!rc) rc = enqueue_arg_checks(dt, op, stream);
     if (rc) return err_return(comm, rc, fn);
     if (!recvcounts) return err_return(comm, MPI_ERR_ARG, fn);
-    const int n = comm == MPI_COMM_SELF ? 1 : world().size;
+    const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     std::vector<size_t> rc_sz(n);
     size_t total = 0;
     for (int j = 0; j < n; ++j) {
@@ -974,7 +986,7 @@ int PMPIX_Bcast_enqueue(void *buffer, int count, MPI_Datatype dt, int root, MPI_
     if (count < 0) return err_return(comm, MPI_ERR_COUNT, fn);
     if (!dtype_valid(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
     if (!dtype_is_contiguous(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
-    const int size = comm == MPI_COMM_SELF ? 1 : world().size;
+    const int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
     if (count == 0 || size == 1) return MPI_SUCCESS;
     return err_return(comm, mv2h_bcast_enqueue(buffer, (size_t)dtype_span(dt, count), root, stream), fn);
@@ -1105,6 +1117,10 @@ int start_coll(MPI_Request *request, const char *fn, F &&call, int nbc = MV2H_NB
 
 int p2p_checks(MPI_Comm comm, int count, MPI_Datatype dt, int tag, bool recv) {
     if (!g_initialized) return MPI_ERR_OTHER;
+    if (world().nnodes > 1) {  // device channels connect the ranks of one node
+        fprintf(stderr, "[mv2amd] point-to-point is not supported across nodes\n");
+        return MPI_ERR_UNSUPPORTED_OPERATION;
+    }
     if (comm != MPI_COMM_WORLD) return comm_index(comm) < 0 ? MPI_ERR_COMM : MPI_ERR_UNSUPPORTED_OPERATION;
     if (count < 0) return MPI_ERR_COUNT;
     if (!dtype_valid(dt)) return MPI_ERR_TYPE;

@@ -26,6 +26,7 @@
 #include "orders.h"
 #include "pvars.h"
 #include "world.h"
+#include "internode.h"
 
 namespace mv2 {
 
@@ -388,6 +389,12 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
 
 }  // namespace mv2
 
+// the node-level allreduce (defined with the C-ABI below): MPI_Init's self-test and tiling
+// probe run on this node's world, before any inter-node link exists
+extern "C" {
+static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
+}
+
 namespace mv2 {
 
 // Init-time check of the cross-GPU publish protocol on this node's topology.
@@ -428,7 +435,7 @@ int coll_selftest() {
             const size_t c = sizes[call];
             hipMemset(rb, 0, bytes);
             hipDeviceSynchronize();
-            if (mv2h_allreduce(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr) != 0) {
+            if (::allreduce_entry(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr)  /* this node */ != 0) {
                 ok = 0;
                 break;
             }
@@ -508,7 +515,7 @@ int pipe_autotune() {
         for (int it = 0; it < 4 && !rc; ++it) {  // the first call warms the tiling up
             host_barrier();
             const auto t0 = std::chrono::steady_clock::now();
-            rc = mv2h_allreduce(sb, rb, count, MPI_FLOAT_H, MPI_SUM_H, nullptr);
+            rc = ::allreduce_entry(sb, rb, count, MPI_FLOAT_H, MPI_SUM_H, nullptr);  // this node
             const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
             if (it) best = std::min(best, us);
         }
@@ -612,6 +619,8 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "cus")) *value = w.cus;
     else if (!strcmp(key, "light_release")) *value = w.light_release;
     else if (!strcmp(key, "oneshot_max")) *value = (long)w.oneshot_max;
+    else if (!strcmp(key, "nnodes")) *value = w.nnodes;
+    else if (!strcmp(key, "node")) *value = w.node;
     else if (!strcmp(key, "pipe_grid")) *value = w.pipe_grid;
     else if (!strcmp(key, "pipe_sub")) *value = (long)w.pipe_sub;
     else if (!strcmp(key, "pipe_tuned")) *value = w.pipe_tuned;
@@ -630,14 +639,11 @@ int mv2h_get_info(const char *key, long *value) {
 
 int mv2h_init(void) { return world_init(); }
 int mv2h_finalize(void) { return world_finalize(); }
-int mv2h_rank(void) { return world().rank; }
-int mv2h_size(void) { return world().size; }
+int mv2h_rank(void) { return world().grank; }
+int mv2h_size(void) { return world().gsize; }
 int mv2h_local_rank(void) { return world().local_rank; }
 
-int mv2h_barrier(void) {
-    host_barrier();
-    return 0;
-}
+int mv2h_barrier(void) { return global_barrier(); }
 
 int mv2h_defer_begin(void) {
     World &w = world();
@@ -1051,7 +1057,15 @@ static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int
     if ((rc = require_world())) return rc;
     return allreduce_select(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
 }
+static int mn_allreduce(const void *, void *, size_t, int, int, void *);
+static int mn_reduce(const void *, void *, size_t, int, int, int, void *);
+static int mn_unsupported(const char *what);
+
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    if (world().nnodes > 1) {
+        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        return mn_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+    }
     pvar_begin();
     const int rc = allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream);
     pvar_end(rc == 0);
@@ -1117,6 +1131,10 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
     return finish(st, w.timing);
 }
 int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+    if (world().nnodes > 1) {
+        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        return mn_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
+    }
     pvar_begin();
     const int rc = reduce_entry(sendbuf, recvbuf, count, dtype, op, root, stream);
     pvar_end(rc == 0);
@@ -1217,13 +1235,14 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
 }
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                         void *stream) {
+    if (world().nnodes > 1) return mn_unsupported("MPI_Reduce_scatter");
     pvar_begin();
     const int rc = reduce_scatter_entry(sendbuf, recvbuf, recvcounts, dtype, op, stream);
     pvar_end(rc == 0);
     return rc;
 }
 
-int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
+static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
     hp_entry();
     int rc;
     if ((rc = require_world())) return rc;
@@ -1269,7 +1288,7 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
     return finish(st, w.timing);
 }
 
-int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
+static int bcast_node(void *buffer, size_t bytes, int root, void *stream) {
     hp_entry();
     int rc;
     if ((rc = require_world())) return rc;
@@ -1295,6 +1314,248 @@ int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
     if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
     if (!direct && w.rank != root) enq_copy(buffer, buf, bytes, st);
     return finish(st, w.timing);
+}
+
+// ---------------------------------------------------------------------------
+// Several nodes: MVAPICH2's two-level structure, node step on the
+// device kernels above (this process's world is its node), inter-node step between the
+// node leaders (local rank 0) over internode.cpp's links with host staging; every
+// reduction stays a device kernel (mv2h_reduce_local: the reference's uop(tmp, recv)).
+//   Allreduce = MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1687): node reduction
+//     (the node's own allreduce: the degree-4 tree up to 2 KiB / shmem LINEAR, the
+//     reference's intra step of its topology-aware and skip-small paths, :2272, :118-160),
+//     recursive doubling among the leaders (MPIR_Allreduce_pt2pt_rd_MV2 :360-630, the
+//     inter step of both paths, :2215-2262), node broadcast.
+//   Bcast = node broadcast at the root's node, binomial over the leaders, node broadcast.
+//   Reduce = node reduce to the leader, binomial reduce over the leaders to the root's node
+//     (MPIR_Reduce_binomial_MV2 reduce_osu.c:425, commutative form), leader -> root.
+//   Allgather = node allgather into the node's section, ring over the leaders, node bcast.
+// ---------------------------------------------------------------------------
+namespace {
+struct MnBufs {
+    char *h0 = nullptr, *h1 = nullptr;  // pinned host staging
+    size_t hcap = 0;
+    char *d0 = nullptr, *d1 = nullptr;  // device: leader partial / received operand
+    size_t dcap = 0;
+};
+MnBufs g_mn;
+
+int mn_reserve(size_t bytes) {
+    if (bytes > g_mn.hcap) {
+        if (g_mn.h0) hipHostFree(g_mn.h0);
+        if (g_mn.h1) hipHostFree(g_mn.h1);
+        g_mn.h0 = g_mn.h1 = nullptr;
+        g_mn.hcap = 0;
+        if (hipHostMalloc((void **)&g_mn.h0, bytes, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&g_mn.h1, bytes, hipHostMallocDefault) != hipSuccess)
+            return E_NO_MEM;
+        g_mn.hcap = bytes;
+    }
+    if (bytes > g_mn.dcap) {
+        hipDeviceSynchronize();
+        if (g_mn.d0) hipFree(g_mn.d0);
+        if (g_mn.d1) hipFree(g_mn.d1);
+        g_mn.d0 = g_mn.d1 = nullptr;
+        g_mn.dcap = 0;
+        if (hipMalloc((void **)&g_mn.d0, bytes) != hipSuccess || hipMalloc((void **)&g_mn.d1, bytes) != hipSuccess)
+            return E_NO_MEM;
+        g_mn.dcap = bytes;
+    }
+    return 0;
+}
+
+int mn_d2h(void *h, const void *d, size_t b) { return hipMemcpy(h, d, b, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN; }
+int mn_h2d(void *d, const void *h, size_t b) { return hipMemcpy(d, h, b, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN; }
+
+// leaders: recursive doubling on `acc` (device, `count` elements), allreduce_osu.c:455-600 with
+// the nodes as ranks; every step's uop(tmp, recv) is one device Reduce_local
+int leader_rd(char *acc, size_t count, int dtype, int op, size_t bytes) {
+    World &w = world();
+    const int n = w.nnodes, rank = w.node;
+    int pof2 = 1;
+    while (pof2 * 2 <= n) pof2 *= 2;
+    const int rem = n - pof2;
+    int rc = 0, newrank;
+    if (rank < 2 * rem) {
+        if (rank % 2 == 0) {
+            if ((rc = mn_d2h(g_mn.h0, acc, bytes)) || (rc = net_send(rank + 1, g_mn.h0, bytes))) return rc;
+            newrank = -1;
+        } else {
+            if ((rc = net_recv(rank - 1, g_mn.h1, bytes)) || (rc = mn_h2d(g_mn.d1, g_mn.h1, bytes)) ||
+                (rc = mv2h_reduce_local(g_mn.d1, acc, count, dtype, op, nullptr)))
+                return rc;
+            newrank = rank / 2;
+        }
+    } else {
+        newrank = rank - rem;
+    }
+    if (newrank != -1) {
+        for (int mask = 1; mask < pof2; mask <<= 1) {
+            const int newdst = newrank ^ mask;
+            const int dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+            if ((rc = mn_d2h(g_mn.h0, acc, bytes)) || (rc = net_sendrecv(dst, g_mn.h0, bytes, g_mn.h1, bytes)) ||
+                (rc = mn_h2d(g_mn.d1, g_mn.h1, bytes)) ||
+                (rc = mv2h_reduce_local(g_mn.d1, acc, count, dtype, op, nullptr)))  // builtin ops commute
+                return rc;
+        }
+    }
+    if (rank < 2 * rem) {
+        if (rank % 2) {
+            if ((rc = mn_d2h(g_mn.h0, acc, bytes)) || (rc = net_send(rank - 1, g_mn.h0, bytes))) return rc;
+        } else {
+            if ((rc = net_recv(rank + 1, g_mn.h1, bytes)) || (rc = mn_h2d(acc, g_mn.h1, bytes))) return rc;
+        }
+    }
+    return 0;
+}
+
+// leaders: binomial broadcast of the host buffer h from node `root` (MPIR_Bcast_binomial order)
+int leader_bcast(char *h, size_t bytes, int root) {
+    World &w = world();
+    const int n = w.nnodes, rel = (w.node - root + n) % n;
+    int mask = 1, rc = 0;
+    while (mask < n) {
+        if (rel & mask) {
+            if ((rc = net_recv((w.node - mask + n) % n, h, bytes))) return rc;
+            break;
+        }
+        mask <<= 1;
+    }
+    for (mask >>= 1; mask > 0; mask >>= 1)
+        if (rel + mask < n && (rc = net_send((w.node + mask) % n, h, bytes))) return rc;
+    return 0;
+}
+}  // namespace
+
+static int mn_require_device_reduction(int dtype, int op) {
+    const DtypeInfo *dt = nullptr;
+    int rc = check_op_dtype(op, dtype, &dt);
+    if (rc) return rc;
+    return kind_supported(dt);
+}
+
+static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    World &w = world();
+    int rc = mn_require_device_reduction(dtype, op);
+    if (rc || count == 0) return rc;
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const size_t bytes = count * (size_t)dt->extent;
+    // node step: every rank of the node holds the node's partial
+    if ((rc = allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream))) return rc;
+    if (w.rank == 0) {
+        if ((rc = mn_reserve(bytes))) return rc;
+        if ((rc = mn_h2d(g_mn.d0, recvbuf, bytes)) || (rc = leader_rd(g_mn.d0, count, dtype, op, bytes)) ||
+            (rc = mn_d2h(recvbuf, g_mn.d0, bytes)))
+            return rc;
+    }
+    return bcast_node(recvbuf, bytes, 0, stream);  // MPIR_Shmem_Bcast_MV2 from the leader
+}
+
+static int mn_bcast(void *buffer, size_t bytes, int root, void *stream) {
+    World &w = world();
+    if (root < 0 || root >= w.gsize) return E_ROOT;
+    if (bytes == 0) return 0;
+    const int rnode = root / w.size, rlocal = root % w.size;
+    int rc = 0;
+    if (w.node == rnode && rlocal != 0 && (rc = bcast_node(buffer, bytes, rlocal, stream))) return rc;
+    if (w.rank == 0) {
+        if ((rc = mn_reserve(bytes))) return rc;
+        if (w.node == rnode && (rc = mn_d2h(g_mn.h0, buffer, bytes))) return rc;
+        if ((rc = leader_bcast(g_mn.h0, bytes, rnode))) return rc;
+        if (w.node != rnode && (rc = mn_h2d(buffer, g_mn.h0, bytes))) return rc;
+    }
+    if (w.node != rnode || rlocal == 0) rc = bcast_node(buffer, bytes, 0, stream);
+    return rc;
+}
+
+static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+    World &w = world();
+    if (root < 0 || root >= w.gsize) return E_ROOT;
+    int rc = mn_require_device_reduction(dtype, op);
+    if (rc || count == 0) return rc;
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const size_t bytes = count * (size_t)dt->extent;
+    const int rnode = root / w.size, rlocal = root % w.size;
+    const bool me_root = w.grank == root;
+    const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;  // IN_PLACE: at the root only
+    if ((rc = mn_reserve(bytes))) return rc;
+    // node step: the leader's partial lands in g_mn.d0 (a non-root's recvbuf is not significant)
+    if ((rc = reduce_entry(src, w.rank == 0 ? g_mn.d0 : nullptr, count, dtype, op, 0, stream))) return rc;
+    if (w.rank == 0) {
+        // binomial over the leaders to the root's node, commutative form (reduce_osu.c:425-681)
+        const int n = w.nnodes, rel = (w.node - rnode + n) % n;
+        for (int mask = 1; mask < n; mask <<= 1) {
+            if (rel & mask) {
+                const int dst = ((rel & ~mask) + rnode) % n;
+                if ((rc = mn_d2h(g_mn.h0, g_mn.d0, bytes)) || (rc = net_send(dst, g_mn.h0, bytes))) return rc;
+                break;
+            }
+            if ((rel | mask) < n) {
+                const int srcn = ((rel | mask) + rnode) % n;
+                if ((rc = net_recv(srcn, g_mn.h1, bytes)) || (rc = mn_h2d(g_mn.d1, g_mn.h1, bytes)) ||
+                    (rc = mv2h_reduce_local(g_mn.d1, g_mn.d0, count, dtype, op, nullptr)))
+                    return rc;
+            }
+        }
+    }
+    if (w.node != rnode) return 0;
+    if (rlocal == 0) return me_root ? mn_d2h(recvbuf, g_mn.d0, bytes) : 0;
+    // the root is not the leader: the node's device point-to-point channel carries the result
+    unsigned long long req = 0;
+    if (w.rank == 0) {
+        if ((rc = mv2h_isend(g_mn.d0, bytes, rlocal, 0x7d01, &req))) return rc;
+        return mv2h_p2p_wait(req, nullptr, nullptr, nullptr);
+    }
+    if (me_root) {
+        if ((rc = mv2h_irecv(recvbuf, bytes, 0, 0x7d01, &req))) return rc;
+        return mv2h_p2p_wait(req, nullptr, nullptr, nullptr);
+    }
+    return 0;
+}
+
+static int mn_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
+    World &w = world();
+    if (bytes == 0) return 0;
+    const size_t sect = bytes * (size_t)w.size, total = sect * (size_t)w.nnodes;
+    char *mine = (char *)recvbuf + (size_t)w.node * sect;
+    const bool in_place = sendbuf == (const void *)-1;
+    int rc = allgather_node(in_place ? (const void *)(mine + (size_t)w.rank * bytes) : sendbuf, mine, bytes, stream);
+    if (rc) return rc;
+    if (w.rank == 0) {
+        if ((rc = mn_reserve(total))) return rc;
+        if ((rc = mn_d2h(g_mn.h0 + (size_t)w.node * sect, mine, sect))) return rc;
+        // ring over the leaders: step k passes node (node - k)'s section to the right
+        const int n = w.nnodes, right = (w.node + 1) % n, left = (w.node - 1 + n) % n;
+        for (int k = 0; k < n - 1; ++k) {
+            const int so = (w.node - k + n) % n, ro = (w.node - k - 1 + n) % n;
+            if ((rc = net_sendrecv(right, g_mn.h0 + (size_t)so * sect, sect, nullptr, 0)) ||
+                (rc = net_sendrecv(left, nullptr, 0, g_mn.h0 + (size_t)ro * sect, sect)))
+                return rc;
+        }
+        if ((rc = mn_h2d(recvbuf, g_mn.h0, total))) return rc;
+    }
+    return bcast_node(recvbuf, total, 0, stream);
+}
+
+static int mn_unsupported(const char *what) {
+    MV2_ERR("%s is not supported across nodes (two-level: Allreduce, Reduce, Bcast, Allgather, Barrier)", what);
+    return E_UNSUPPORTED;
+}
+
+int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
+    if (world().nnodes > 1) {
+        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        return mn_allgather(sendbuf, recvbuf, bytes, stream);
+    }
+    return allgather_node(sendbuf, recvbuf, bytes, stream);
+}
+
+int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
+    if (world().nnodes > 1) {
+        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        return mn_bcast(buffer, bytes, root, stream);
+    }
+    return bcast_node(buffer, bytes, root, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,296 @@
+// internode.cpp — leader transport between nodes (internode.h).
+//
+// The reference's two-level collectives run their inter-node step on leader_comm, the
+// communicator of the nodes' local rank 0 (create_2level_comm.c:1843), over its network
+// channel.  Here the leaders keep one TCP stream per pair of nodes:
+//   rendezvous: the leader of node 0 listens on MV2AMD_BOOT_ADDR:MV2AMD_BOOT_PORT (default
+//               MASTER_ADDR : MASTER_PORT + 1); every other leader opens its own listener,
+//               connects, and sends {node, listener port}; node 0 answers with every
+//               leader's address and port (the boot connections stay as the links to node 0);
+//   mesh:       leader i connects to leaders 1 .. i-1 and accepts leaders i+1 .. n-1.
+// Every exchange is a fixed-size message both sides know in advance (the schedules of the
+// collectives are deterministic), so there is no framing; sendrecv interleaves both
+// directions with poll() so two leaders exchanging large buffers never block each other.
+#include "internode.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+#include "../common.h"
+#include "log.h"
+#include "world.h"
+
+namespace mv2 {
+
+namespace {
+
+struct Hello {
+    int32_t magic;
+    int32_t node;
+    int32_t port;  // the sender's mesh listener
+    int32_t nnodes;
+};
+struct Entry {
+    char ip[64];
+    int32_t port;
+};
+constexpr int32_t kMagic = 0x6d76326e;  // "mv2n"
+
+struct Net {
+    std::vector<int> fd;  // fd[node] (-1: self / not connected)
+    int listen_fd = -1;
+    bool up = false;
+};
+Net g_net;
+
+double now_s() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+double timeout_s() {
+    const char *v = getenv("MV2AMD_TIMEOUT_S");
+    const long t = v && *v ? atol(v) : 120;
+    return t > 0 ? (double)t : 120.0;
+}
+
+void tune(int fd) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    int buf = 8 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
+}
+
+int open_listener(const char *addr, int port, int *bound_port) {
+    const int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) return -1;
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)port);
+    sa.sin_addr.s_addr = addr ? inet_addr(addr) : htonl(INADDR_ANY);
+    if (bind(fd, (sockaddr *)&sa, sizeof(sa)) != 0 || listen(fd, 64) != 0) {
+        close(fd);
+        return -1;
+    }
+    socklen_t len = sizeof(sa);
+    getsockname(fd, (sockaddr *)&sa, &len);
+    if (bound_port) *bound_port = ntohs(sa.sin_port);
+    return fd;
+}
+
+int connect_retry(const char *host, int port) {
+    const double t_end = now_s() + timeout_s();
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    char ps[16];
+    snprintf(ps, sizeof(ps), "%d", port);
+    if (getaddrinfo(host, ps, &hints, &res) != 0 || !res) return -1;
+    int fd = -1;
+    while (now_s() < t_end) {
+        fd = socket(AF_INET, SOCK_STREAM, 0);
+        if (fd < 0) break;
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+        close(fd);
+        fd = -1;
+        usleep(20000);  // the peer's listener is not up yet
+    }
+    freeaddrinfo(res);
+    if (fd >= 0) tune(fd);
+    return fd;
+}
+
+int accept_timed(int lfd) {
+    pollfd p{lfd, POLLIN, 0};
+    const int ms = (int)(timeout_s() * 1000.0);
+    if (poll(&p, 1, ms) <= 0) return -1;
+    const int fd = accept(lfd, nullptr, nullptr);
+    if (fd >= 0) tune(fd);
+    return fd;
+}
+
+// full-duplex transfer on one socket: send sn bytes and receive rn bytes, interleaved
+int xfer(int fd, const char *sb, size_t sn, char *rb, size_t rn) {
+    size_t so = 0, ro = 0;
+    const int ms = (int)(timeout_s() * 1000.0);
+    while (so < sn || ro < rn) {
+        pollfd p{fd, (short)((so < sn ? POLLOUT : 0) | (ro < rn ? POLLIN : 0)), 0};
+        const int r = poll(&p, 1, ms);
+        if (r <= 0) {
+            if (r < 0 && errno == EINTR) continue;
+            MV2_ERR("inter-node transfer timed out (MV2AMD_TIMEOUT_S)");
+            return E_OTHER;
+        }
+        if (p.revents & (POLLERR | POLLHUP | POLLNVAL) && !(p.revents & POLLIN)) {
+            MV2_ERR("inter-node connection lost");
+            return E_OTHER;
+        }
+        if ((p.revents & POLLIN) && ro < rn) {
+            const ssize_t k = recv(fd, rb + ro, rn - ro, 0);
+            if (k == 0) {
+                MV2_ERR("inter-node connection closed by the peer");
+                return E_OTHER;
+            }
+            if (k < 0 && errno != EINTR && errno != EAGAIN) return E_OTHER;
+            if (k > 0) ro += (size_t)k;
+        }
+        if ((p.revents & POLLOUT) && so < sn) {
+            const ssize_t k = send(fd, sb + so, sn - so, MSG_NOSIGNAL | MSG_DONTWAIT);
+            if (k < 0 && errno != EINTR && errno != EAGAIN && errno != EWOULDBLOCK) return E_OTHER;
+            if (k > 0) so += (size_t)k;
+        }
+    }
+    return 0;
+}
+
+int link_fd(int peer) {
+    if (peer < 0 || peer >= (int)g_net.fd.size() || g_net.fd[peer] < 0) {
+        MV2_ERR("no inter-node link to node %d", peer);
+        return -1;
+    }
+    return g_net.fd[peer];
+}
+
+}  // namespace
+
+int net_send(int peer, const void *buf, size_t bytes) {
+    const int fd = link_fd(peer);
+    return fd < 0 ? E_INTERN : xfer(fd, (const char *)buf, bytes, nullptr, 0);
+}
+int net_recv(int peer, void *buf, size_t bytes) {
+    const int fd = link_fd(peer);
+    return fd < 0 ? E_INTERN : xfer(fd, nullptr, 0, (char *)buf, bytes);
+}
+int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes) {
+    const int fd = link_fd(peer);
+    return fd < 0 ? E_INTERN : xfer(fd, (const char *)sbuf, sbytes, (char *)rbuf, rbytes);
+}
+
+int net_init() {
+    World &w = world();
+    const int nn = w.nnodes, me = w.node;
+    g_net.fd.assign((size_t)nn, -1);
+    const char *ba = getenv("MV2AMD_BOOT_ADDR");
+    const char *ma = getenv("MASTER_ADDR");
+    const std::string host = ba && *ba ? ba : (ma && *ma ? ma : "127.0.0.1");
+    const char *bp = getenv("MV2AMD_BOOT_PORT");
+    const char *mp = getenv("MASTER_PORT");
+    const int port = bp && *bp ? atoi(bp) : (mp && *mp ? atoi(mp) + 1 : 0);
+    if (port <= 0) {
+        MV2_ERR("multi-node job: set MV2AMD_BOOT_PORT (or MASTER_PORT) for the leaders' rendezvous");
+        return E_OTHER;
+    }
+    std::vector<Entry> table((size_t)nn);
+    if (me == 0) {
+        int bound = 0;
+        g_net.listen_fd = open_listener(nullptr, port, &bound);
+        if (g_net.listen_fd < 0) {
+            MV2_ERR("leader rendezvous: cannot listen on port %d", port);
+            return E_OTHER;
+        }
+        for (int k = 1; k < nn; ++k) {
+            const int fd = accept_timed(g_net.listen_fd);
+            Hello h{};
+            if (fd < 0 || xfer(fd, nullptr, 0, (char *)&h, sizeof(h)) || h.magic != kMagic || h.node <= 0 ||
+                h.node >= nn || h.nnodes != nn || g_net.fd[h.node] >= 0) {
+                MV2_ERR("leader rendezvous: bad or missing hello (%d of %d leaders)", k - 1, nn - 1);
+                if (fd >= 0) close(fd);
+                return E_OTHER;
+            }
+            sockaddr_in sa{};
+            socklen_t len = sizeof(sa);
+            getpeername(fd, (sockaddr *)&sa, &len);
+            inet_ntop(AF_INET, &sa.sin_addr, table[h.node].ip, sizeof(table[h.node].ip));
+            table[h.node].port = h.port;
+            g_net.fd[h.node] = fd;
+        }
+        for (int j = 1; j < nn; ++j)
+            if (xfer(g_net.fd[j], (const char *)table.data(), table.size() * sizeof(Entry), nullptr, 0)) return E_OTHER;
+    } else {
+        int myport = 0;
+        g_net.listen_fd = open_listener(nullptr, 0, &myport);
+        if (g_net.listen_fd < 0) return E_OTHER;
+        const int fd = connect_retry(host.c_str(), port);
+        if (fd < 0) {
+            MV2_ERR("leader of node %d: cannot reach the rendezvous %s:%d", me, host.c_str(), port);
+            return E_OTHER;
+        }
+        Hello h{kMagic, me, myport, nn};
+        if (xfer(fd, (const char *)&h, sizeof(h), nullptr, 0) ||
+            xfer(fd, nullptr, 0, (char *)table.data(), table.size() * sizeof(Entry))) {
+            close(fd);
+            return E_OTHER;
+        }
+        g_net.fd[0] = fd;
+        // mesh among nodes 1..nn-1: connect down, accept up
+        for (int j = 1; j < me; ++j) {
+            const int c = connect_retry(table[j].ip, table[j].port);
+            Hello hj{kMagic, me, myport, nn};
+            if (c < 0 || xfer(c, (const char *)&hj, sizeof(hj), nullptr, 0)) {
+                MV2_ERR("leader of node %d: cannot connect to node %d", me, j);
+                return E_OTHER;
+            }
+            g_net.fd[j] = c;
+        }
+        for (int k = me + 1; k < nn; ++k) {
+            const int c = accept_timed(g_net.listen_fd);
+            Hello hk{};
+            if (c < 0 || xfer(c, nullptr, 0, (char *)&hk, sizeof(hk)) || hk.magic != kMagic || hk.node <= me ||
+                hk.node >= nn || g_net.fd[hk.node] >= 0) {
+                MV2_ERR("leader of node %d: bad or missing mesh connection", me);
+                if (c >= 0) close(c);
+                return E_OTHER;
+            }
+            g_net.fd[hk.node] = c;
+        }
+    }
+    g_net.up = true;
+    MV2_DEBUG("inter-node mesh up: node %d of %d", me, nn);
+    return net_barrier();
+}
+
+// dissemination barrier over the leaders (log2(nnodes) rounds of one-byte tokens)
+int net_barrier() {
+    World &w = world();
+    const int nn = w.nnodes, me = w.node;
+    if (nn <= 1) return 0;
+    for (int d = 1; d < nn; d <<= 1) {
+        const int to = (me + d) % nn, from = (me - d + nn) % nn;
+        char t = 1, r = 0;
+        int rc = net_send(to, &t, 1);  // one byte never blocks in the socket buffer
+        if (!rc) rc = net_recv(from, &r, 1);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+void net_finalize() {
+    for (int &fd : g_net.fd)
+        if (fd >= 0) {
+            close(fd);
+            fd = -1;
+        }
+    if (g_net.listen_fd >= 0) close(g_net.listen_fd);
+    g_net.listen_fd = -1;
+    g_net.up = false;
+}
+
+}  // namespace mv2

@@ -1,0 +1,18 @@
+// internode.h — leader transport between nodes (the inter-node step of
+// MVAPICH2's two-level collectives, create_2level_comm.c:1843 leader_comm).  One TCP stream
+// per pair of node leaders (local rank 0 of each node); every other rank talks to its node
+// only (IPC arenas, runtime/world.cpp).  Host staging; the reductions stay on the GPU.
+#pragma once
+#include <stddef.h>
+
+namespace mv2 {
+
+int net_init();      // leaders: bootstrap + full mesh (rank 0's leader serves the rendezvous)
+void net_finalize();
+int net_barrier();   // leaders only
+// blocking exchanges with the leader of node `peer` (both sides issue the matching call)
+int net_send(int peer, const void *buf, size_t bytes);
+int net_recv(int peer, void *buf, size_t bytes);
+int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes);
+
+}  // namespace mv2

@@ -4,6 +4,7 @@
 // init + CUDA IPC region setup: reference init.c:186-300,
 // ch3_shmem_coll.c:1365-1455, ibv_cuda_ipc.c:400.)
 #include "world.h"
+#include "internode.h"
 
 #include <fcntl.h>
 #include <sched.h>
@@ -175,9 +176,23 @@ int world_init() {
         MV2_ERR("invalid rank/size from environment: rank=%d size=%d", w.rank, w.size);
         return E_OTHER;
     }
+    w.grank = w.rank;
+    w.gsize = w.size;
     if (lsize != w.size) {
-        MV2_ERR("multi-node launch (local size %d != world size %d) is not supported yet", lsize, w.size);
-        return E_UNSUPPORTED;
+        // several nodes: this process's world below is its node (rank = local rank); the
+        // leaders (local rank 0) add the inter-node links (internode.cpp).  Ranks must be
+        // numbered node-major with the same count per node (the reference's is_blocked /
+        // is_uniform communicators, create_2level_comm.c)
+        if (lsize < 1 || w.size % lsize != 0 || w.local_rank < 0 || w.local_rank >= lsize ||
+            w.rank != (w.rank / lsize) * lsize + w.local_rank) {
+            MV2_ERR("multi-node launch needs node-major ranks and the same ranks per node "
+                    "(rank %d, local rank %d, local size %d, size %d)", w.rank, w.local_rank, lsize, w.size);
+            return E_UNSUPPORTED;
+        }
+        w.nnodes = w.size / lsize;
+        w.node = w.rank / lsize;
+        w.rank = w.local_rank;
+        w.size = lsize;
     }
     if (w.size > kShmMaxRanks) {
         MV2_ERR("world size %d exceeds %d", w.size, kShmMaxRanks);
@@ -194,7 +209,7 @@ int world_init() {
     }
 
     if (w.size > 1) {
-        w.shm_name = "/mv2amd." + job_key();
+        w.shm_name = "/mv2amd." + job_key() + (w.nnodes > 1 ? ".n" + std::to_string(w.node) : std::string());
         int fd = shm_open(w.shm_name.c_str(), O_CREAT | O_RDWR, 0600);
         if (fd < 0) {
             MV2_ERR("shm_open(%s) failed", w.shm_name.c_str());
@@ -235,6 +250,10 @@ int world_init() {
                 if (w.shm->r[j].pci_bus == w.shm->r[i].pci_bus && w.shm->r[j].pci_device == w.shm->r[i].pci_device) ++c;
             if (c > w.nshare) w.nshare = c;
         }
+        // emulated nodes on one GPU (tests, mv2run --nodes --share-gpu): the GPU is shared with
+        // the other nodes' ranks too, which this node's segment cannot see
+        const long ns = env_long("MV2AMD_NSHARE", 0);
+        if (ns > w.nshare) w.nshare = (int)ns;
 
         if (w.size <= kMaxRanks && !control_only) {
             // signal page + one-shot arena, IPC-exported
@@ -322,8 +341,28 @@ int world_init() {
             return rc;
         }
     }
-    MV2_DEBUG("init rank %d/%d local %d device %d nshare %d", w.rank, w.size, w.local_rank, w.device, w.nshare);
+    if (w.nnodes > 1) {
+        if (w.rank == 0) {
+            const int rc = net_init();
+            if (rc) {
+                w.inited = false;
+                return rc;
+            }
+        }
+        host_barrier();  // the node's leader is linked to every other node
+    }
+    MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d)", w.grank, w.gsize, w.rank, w.device,
+              w.nshare, w.node, w.nnodes);
     return 0;
+}
+
+int global_barrier() {
+    World &w = world();
+    host_barrier();
+    int rc = 0;
+    if (w.nnodes > 1 && w.rank == 0) rc = net_barrier();
+    host_barrier();
+    return rc;
 }
 
 int world_finalize() {
@@ -331,6 +370,10 @@ int world_finalize() {
     if (!w.inited || w.finalized) return 0;
     if (w.stream) hipStreamSynchronize(w.stream);
     host_prof_report();
+    if (w.nnodes > 1) {
+        global_barrier();
+        if (w.rank == 0) net_finalize();
+    }
     if (w.size > 1 && w.shm) {
         host_barrier();
         for (int j = 0; j < kMaxRanks; ++j) {

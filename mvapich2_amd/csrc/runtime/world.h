@@ -85,7 +85,10 @@ struct ShmSeg {
 struct World {
     bool inited = false;
     bool finalized = false;
-    int rank = 0, size = 1, local_rank = 0, device = 0;
+    int rank = 0, size = 1, local_rank = 0, device = 0;  // this node's world (rank = local rank)
+    // the job: global rank / size; nodes of `size` ranks each, ranks numbered node-major
+    // (rank = node * size + local rank); nnodes > 1 adds the leader transport (internode.cpp)
+    int grank = 0, gsize = 1, node = 0, nnodes = 1;
     int nshare = 1;  // max over ranks of the ranks sharing one GPU (test setups); same on all ranks
     int cus = 256;   // compute units of this GPU
     hipStream_t stream = nullptr;
@@ -152,6 +155,7 @@ World &world();
 int world_init();
 int world_finalize();
 void host_barrier();
+int global_barrier();  // node barrier, leaders' barrier across nodes, node barrier
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol

@@ -50,13 +50,60 @@ def test_shm_barrier(size, env_style):
     assert not os.path.exists("/dev/shm/mv2amd." + jobid)  # rank 0 unlinked the segment
 
 
-def test_multinode_launch_is_rejected():
+def _mn_worker(rank, size, ppn, jobid, port, counter, iters, q):
+    try:
+        os.environ.update(MV2AMD_CONTROL_PLANE_ONLY="1", MV2AMD_JOBID=jobid, RANK=str(rank), WORLD_SIZE=str(size),
+                          LOCAL_RANK=str(rank % ppn), LOCAL_WORLD_SIZE=str(ppn), MV2AMD_BOOT_ADDR="127.0.0.1",
+                          MV2AMD_BOOT_PORT=str(port), MV2AMD_TIMEOUT_S="60")
+        import mvapich2_amd as m
+        L = m.lib()
+        assert L.mv2h_init() == 0
+        assert L.mv2h_rank() == rank and L.mv2h_size() == size and L.mv2h_local_rank() == rank % ppn
+        assert m.info("nnodes") == size // ppn and m.info("node") == rank // ppn
+        for k in range(iters):
+            with counter.get_lock():
+                counter.value += 1
+            assert L.mv2h_barrier() == 0
+            assert counter.value >= size * (k + 1), (rank, k, counter.value)
+        assert L.mv2h_finalize() == 0
+        q.put((rank, "ok"))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("size,ppn", [(4, 2), (6, 2), (3, 1), (8, 4)])
+def test_multinode_bootstrap_and_global_barrier(size, ppn):
+    """Several nodes emulated on one host: every node gets its own
+    control segment, the node leaders rendezvous at MV2AMD_BOOT_ADDR:PORT and link over TCP
+    (runtime/internode.cpp); MPI_Barrier = node barrier + leaders' dissemination barrier + node
+    barrier, so no rank passes barrier k before every rank of every node has reached it."""
+    import socket
+    ctx = mp.get_context("fork")
+    counter = ctx.Value("i", 0)
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    jobid = "n" + uuid.uuid4().hex[:12]
+    procs = [ctx.Process(target=_mn_worker, args=(r, size, ppn, jobid, port, counter, 50, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
+    assert counter.value == 50 * size
+
+
+def test_multinode_needs_node_major_ranks():
     ctx = mp.get_context("fork")
     q = ctx.Queue()
 
     def w(q):
-        os.environ.update(MV2AMD_CONTROL_PLANE_ONLY="1", RANK="0", WORLD_SIZE="4", LOCAL_WORLD_SIZE="2",
-                          MV2AMD_JOBID="t" + uuid.uuid4().hex[:8])
+        # rank 1 claiming local rank 0 of 2: not numbered node-major
+        os.environ.update(MV2AMD_CONTROL_PLANE_ONLY="1", RANK="1", WORLD_SIZE="4", LOCAL_RANK="0",
+                          LOCAL_WORLD_SIZE="2", MV2AMD_JOBID="t" + uuid.uuid4().hex[:8])
         import mvapich2_amd as m
         q.put(m.lib().mv2h_init())
 

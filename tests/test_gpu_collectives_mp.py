@@ -33,16 +33,27 @@ def inputs(case, rank):
 GEOMS = {"default": {}, "small": {"MV2AMD_PIPE_GRID": "3", "MV2AMD_PIPE_SUB": "4096"}}
 
 
-def run_workers(n, cases, tmp_path, timeout=100, extra_env=None):
+def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None):
+    """n ranks of tests/mp_gpu_worker.py; ppn < n emulates n / ppn nodes (node-major ranks,
+    leaders linked over 127.0.0.1, runtime/internode.cpp)"""
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"cases": cases}))
     out = tmp_path / "out"
     out.mkdir()
     jobid = "g" + uuid.uuid4().hex[:12]
+    ppn = ppn or n
+    boot = {}
+    if ppn < n:
+        import socket
+        so = socket.socket()
+        so.bind(("127.0.0.1", 0))
+        boot = {"MV2AMD_BOOT_ADDR": "127.0.0.1", "MV2AMD_BOOT_PORT": str(so.getsockname()[1]),
+                "MV2AMD_NSHARE": str(n)}  # every emulated node's ranks share the one GPU
+        so.close()
     procs = []
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
-                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="30", **(extra_env or {}))
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r % ppn), LOCAL_WORLD_SIZE=str(ppn),
+                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="30", **boot, **(extra_env or {}))
         env.pop("MV2AMD_DEVICE", None)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), str(spec),
                                        str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))

@@ -1,0 +1,109 @@
+"""Several nodes, emulated on the GPU box: n ranks split node-major into
+n / ppn nodes, each with its own control segment and IPC world, the node leaders linked over
+TCP (runtime/internode.cpp).  Results are checked bit-exactly against a restatement of
+MVAPICH2's two-level structure built from the oracle: node step = the oracle's one-node
+algorithm for the node's ranks, inter-node step = recursive doubling (allreduce, the inter step
+of MPIR_Allreduce_two_level_MV2 / topo-aware hierarchical, allreduce_osu.c:360-630, :2215) or
+binomial reduce (reduce_osu.c:425) over the node leaders, every uop an oracle op-loop call."""
+import numpy as np
+import pytest
+
+from mvapich2_amd.consts import OPS, TYPES
+from oracle import oracle
+from tests.helpers import as_bytes, assert_bytes_equal
+from tests.test_gpu_collectives_mp import inputs, run_workers
+
+pytestmark = pytest.mark.gpu
+
+
+def uop(tmp, acc, count, t, op):
+    """uop(tmp, recv) of the reference: recv = tmp (+) recv, the C op loop"""
+    out = acc.copy()
+    assert oracle.reduce_local(tmp, out, count, TYPES[t][0], OPS[op]) == 0
+    return out
+
+
+def rd_leaders(parts, count, t, op):
+    """MPIR_Allreduce_pt2pt_rd_MV2 over the leaders (allreduce_osu.c:455-600), commutative form"""
+    n = len(parts)
+    acc = [p.copy() for p in parts]
+    pof2 = 1
+    while pof2 * 2 <= n:
+        pof2 *= 2
+    rem = n - pof2
+    for r in range(1, 2 * rem, 2):
+        acc[r] = uop(acc[r - 1], acc[r], count, t, op)
+    newrank = {r: (r // 2 if r < 2 * rem else r - rem) for r in range(n) if not (r < 2 * rem and r % 2 == 0)}
+    mask = 1
+    while mask < pof2:
+        snap = [a.copy() for a in acc]
+        for r, nr in newrank.items():
+            nd = nr ^ mask
+            dst = nd * 2 + 1 if nd < rem else nd + rem
+            acc[r] = uop(snap[dst], acc[r], count, t, op)
+        mask <<= 1
+    for r in range(0, 2 * rem, 2):
+        acc[r] = acc[r + 1].copy()
+    return acc
+
+
+def binomial_leaders(parts, count, t, op, root):
+    """MPIR_Reduce_binomial_MV2 over the leaders to node `root`, commutative form"""
+    n = len(parts)
+    acc = {rel: parts[(rel + root) % n].copy() for rel in range(n)}
+    mask = 1
+    while mask < n:
+        for rel in range(0, n, 2 * mask):
+            if rel | mask < n:
+                acc[rel] = uop(acc[rel | mask], acc[rel], count, t, op)
+        mask <<= 1
+    return acc[0]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 2), (3, 1), (8, 4)])
+def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
+    nodes = n // ppn
+    cases, seed = [], 300
+    for t, op, count in (("MPI_FLOAT", "MPI_SUM", 10), ("MPI_FLOAT", "MPI_SUM", 300), ("MPI_DOUBLE", "MPI_MAX", 200),
+                         ("MPI_FLOAT", "MPI_SUM", 70001), ("MPI_INT", "MPI_SUM", 100003),
+                         ("MPI_DOUBLE_INT", "MPI_MAXLOC", 5000), ("MPI_UNSIGNED_CHAR", "MPI_BXOR", 4099)):
+        cases.append({"id": f"ma{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
+        seed += 1
+    for t, op, count, root in (("MPI_FLOAT", "MPI_SUM", 1000, n - 1), ("MPI_INT", "MPI_SUM", 70001, 1 % n),
+                               ("MPI_DOUBLE", "MPI_MIN", 300, 0)):
+        cases.append({"id": f"mr{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "root": root})
+        seed += 1
+    for count, root in ((70001, n - 1), (1000, 1 % n), (5, 0)):
+        cases.append({"id": f"mb{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
+    for count in (1000, 100003):
+        cases.append({"id": f"mg{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": count,
+                      "seed": seed})
+        seed += 1
+    res = run_workers(n, cases, tmp_path, ppn=ppn)
+    for case in cases:
+        k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
+        sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+        if k == "allreduce":
+            parts = [oracle.allreduce_ref(sends[j * ppn:(j + 1) * ppn], count, TYPES[t][0], OPS[case["op"]])[0]
+                     for j in range(nodes)]
+            want = rd_leaders(parts, count, t, case["op"])
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r // ppn], t, count, f"{cid} {t} {case['op']} rank {r}")
+        elif k == "reduce":
+            rnode = case["root"] // ppn
+            parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0],
+                                       OPS[case["op"]], 0) for j in range(nodes)]
+            want = binomial_leaders(parts, count, t, case["op"], rnode)
+            assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
+        elif k == "bcast":
+            want = as_bytes(inputs(case, case["root"]))
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        elif k == "allgather":
+            want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
