@@ -16,6 +16,18 @@ struct TreeParams {
     ProgSet ps;      // linear == 4
 };
 
+// Sequence numbers of the graph lane (coll.cpp, HIP graph capture): a captured kernel cannot
+// carry host-assigned flag epochs and slot parities, because every replay would reuse them, so
+// graph-lane kernels read their base here when they start and the last workgroup to finish
+// advances it for the next call (uncached device memory; one block per process).
+struct DevSeq {
+    uint64_t epoch;   // last flag epoch used
+    uint64_t round;   // pipeline rounds issued (slot parity)
+    uint64_t os;      // one-shot calls issued (arena half)
+    uint32_t arrive;  // workgroups of the running kernel that have finished
+    uint32_t pad[9];
+};
+
 struct OneShotArgs {
     const char *send;
     char *recv;
@@ -31,6 +43,10 @@ struct OneShotArgs {
     uint64_t timeout;
     int light;    // 1: signal without the L2 writeback (peers read only uncached arena data)
     Done done;
+    // graph lane (HIP graph capture): epoch and arena half come from the device sequence
+    // block at run time (arena_peer / arena_own then point at half 0; `half` = bytes per half)
+    DevSeq *dseq;
+    size_t half;
 };
 
 // ---------------------------------------------------------------------------
@@ -84,6 +100,7 @@ struct PipeArgs {
     int *err;
     uint64_t timeout;
     Done done;
+    DevSeq *dseq;                   // graph lane: epoch0 / round0 read from here at run time
 };
 
 struct LaunchCfg {

@@ -244,8 +244,35 @@ struct LReduceN {
 // No exit barrier: the arena half used alternates per call (parity), and a
 // peer can only reach call i+2 after every rank finished call i.
 // ============================================================================
+// Graph lane (DevSeq, kernels.h): every workgroup reads the call's base when it starts; the
+// last workgroup to finish advances it, after all of them have read it.
+struct SeqBase {
+    uint64_t epoch, round, os;
+};
+__device__ __forceinline__ SeqBase dseq_read(DevSeq *d) {
+    __shared__ uint64_t s_q[3];
+    if (threadIdx.x == 0) {
+        s_q[0] = __hip_atomic_load(&d->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_q[1] = __hip_atomic_load(&d->round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_q[2] = __hip_atomic_load(&d->os, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return SeqBase{s_q[0], s_q[1], s_q[2]};
+}
+__device__ __forceinline__ void dseq_advance(DevSeq *d, uint64_t de, uint64_t dr, uint64_t dos) {
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&d->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x) {
+        __hip_atomic_store(&d->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (de) __hip_atomic_fetch_add(&d->epoch, de, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dr) __hip_atomic_fetch_add(&d->round, dr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dos) __hip_atomic_fetch_add(&d->os, dos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+}
+
 template <class Rd, bool PROG>
-__device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
+__device__ __forceinline__ void oneshot_body(const OneShotArgs &a, uint64_t epoch, size_t poff) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const int blk = blockIdx.x, G = gridDim.x;
@@ -258,7 +285,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
         const v4u x = send[i];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)
-            if (j < a.n && j != a.me) ((v4u *)(a.arena_peer.p[j] + (size_t)a.me * a.slot_bytes))[i] = x;
+            if (j < a.n && j != a.me) ((v4u *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes))[i] = x;
     }
     const size_t tail0 = a.nvec * N;
     if (blk == 0) {
@@ -266,17 +293,18 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
             const T x = ((const T *)a.send)[e];
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
-                if (j < a.n && j != a.me) ((T *)(a.arena_peer.p[j] + (size_t)a.me * a.slot_bytes))[e] = x;
+                if (j < a.n && j != a.me) ((T *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes))[e] = x;
         }
     }
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
-    if (!wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout, a.light != 0)) return;
+    signal_peers(a.sig_peer, a.n, a.me, blk, epoch, a.light != 0);
+    if (!wait_peers(a.sig_own, a.n, blk, epoch, a.err, a.timeout, a.light != 0)) return;
+    const char *arena_own = a.arena_own + poff;
     // phase B: reduce the n slots (own data straight from sendbuf; arena slots with
     // non-temporal loads, which the light acquire relies on)
     auto load = [&](size_t i, v4u (&v)[kMaxRanks]) {
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)
-            v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ld_nt((const v4u *)(a.arena_own + (size_t)j * a.slot_bytes) + i);
+            v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ld_nt((const v4u *)(arena_own + (size_t)j * a.slot_bytes) + i);
     };
     if constexpr (PROG) {
         // program order: the block of a range that lies in one block is fixed once
@@ -310,7 +338,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
                 col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e]
-                                                 : ld_nt_elem((const T *)(a.arena_own + (size_t)j * a.slot_bytes) + e);
+                                                 : ld_nt_elem((const T *)(arena_own + (size_t)j * a.slot_bytes) + e);
             if constexpr (PROG) ((T *)a.recv)[e] = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, e)]);
             else ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
         }
@@ -319,7 +347,15 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a) {
 
 template <class Rd, bool PROG>
 __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
-    oneshot_body<Rd, PROG>(a);
+    uint64_t epoch = a.epoch;
+    size_t poff = 0;
+    if (a.dseq) {  // graph lane: this replay's epoch and arena half
+        const SeqBase q = dseq_read(a.dseq);
+        epoch = q.epoch + 1;
+        poff = (q.os & 1) * a.half;
+    }
+    oneshot_body<Rd, PROG>(a, epoch, poff);
+    if (a.dseq) dseq_advance(a.dseq, 1, 0, 1);
     block_done(a.done);
 }
 

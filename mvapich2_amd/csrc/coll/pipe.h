@@ -360,8 +360,8 @@ __device__ __forceinline__ void gather_slots(const PipeArgs &a, uint64_t par, si
 
 // P1 of round k: my part of every other segment -> its owner's RS slot [par][me]
 // (all n-1 links at once)
-__device__ __forceinline__ void scatter_round(const PipeArgs &a, int k) {
-    const uint64_t par = (a.round0 + (uint64_t)k) & 1;
+__device__ __forceinline__ void scatter_round(const PipeArgs &a, uint64_t round0, int k) {
+    const uint64_t par = (round0 + (uint64_t)k) & 1;
     const size_t rbase = (size_t)k * a.tseg + (size_t)blockIdx.x * a.tsub;
     const size_t soff = (size_t)blockIdx.x * a.tsub;
     Jobs jb{};
@@ -383,8 +383,8 @@ __device__ __forceinline__ void scatter_round(const PipeArgs &a, int k) {
 // that its register demand never lowers the occupancy of the hot ring /
 // butterfly kernel.
 template <class Rd, bool PROG>
-__device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
-    const uint64_t par = (a.round0 + (uint64_t)k) & 1;
+__device__ __forceinline__ void reduce_round(const PipeArgs &a, uint64_t round0, int k) {
+    const uint64_t par = (round0 + (uint64_t)k) & 1;
     const size_t rbase = (size_t)k * a.tseg + (size_t)blockIdx.x * a.tsub;
     const size_t soff = (size_t)blockIdx.x * a.tsub;
     const int me = a.me;
@@ -459,7 +459,7 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, int k) {
 }
 
 template <class Rd, bool PROG = false>
-__device__ __forceinline__ void pipe_body(const PipeArgs &a) {
+__device__ __forceinline__ void pipe_body(const PipeArgs &a, uint64_t epoch0, uint64_t round0) {
     const int b = blockIdx.x;
     const int n = a.n, me = a.me;
     const unsigned all = (1u << n) - 1u;
@@ -471,29 +471,29 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
             //   P1(0) E(0) | wait E(k); P2(k); E(k)+1; P1(k+1); E(k+1); wait E(k)+1; P3(k) |
             const bool gathers = a.mode == PIPE_AR || (a.mode == PIPE_RED && me == a.root);
             if (a.nrounds > 0) {
-                scatter_round(a, 0);
-                signal_peers(a.sig_peer, n, me, b, a.epoch0, a.light);
+                scatter_round(a, round0, 0);
+                signal_peers(a.sig_peer, n, me, b, epoch0, a.light);
             }
             for (int k = 0; k < a.nrounds; ++k) {
-                const uint64_t E = a.epoch0 + 2 * (uint64_t)k;
+                const uint64_t E = epoch0 + 2 * (uint64_t)k;
                 if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout, a.light != 0)) return;
-                reduce_round<Rd, PROG>(a, k);
+                reduce_round<Rd, PROG>(a, round0, k);
                 if (a.mode != PIPE_RS) signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (k + 1 < a.nrounds) {
-                    scatter_round(a, k + 1);
+                    scatter_round(a, round0, k + 1);
                     signal_peers(a.sig_peer, n, me, b, E + 2, a.light);
                 }
                 if (!gathers) continue;
                 if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout, a.light != 0)) return;
                 const size_t rbase = (size_t)k * a.tseg + (size_t)b * a.tsub;
-                gather_slots(a, (a.round0 + (uint64_t)k) & 1, rbase, (size_t)b * a.tsub, -1);
+                gather_slots(a, (round0 + (uint64_t)k) & 1, rbase, (size_t)b * a.tsub, -1);
             }
         }
         return;
     }
     for (int k = 0; k < a.nrounds; ++k) {
-        const uint64_t par = (a.round0 + (uint64_t)k) & 1;
-        const uint64_t E = a.epoch0 + 2 * (uint64_t)k;
+        const uint64_t par = (round0 + (uint64_t)k) & 1;
+        const uint64_t E = epoch0 + 2 * (uint64_t)k;
         const size_t rbase = (size_t)k * a.tseg + (size_t)b * a.tsub;  // segment-relative
         const size_t soff = (size_t)b * a.tsub;                        // slot-relative
         auto rlen = [&](int j) -> size_t { return range_len(a, j, rbase); };
@@ -556,7 +556,14 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a) {
 
 template <class Rd, bool PROG = false>
 __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
-    pipe_body<Rd, PROG>(a);
+    uint64_t epoch0 = a.epoch0, round0 = a.round0;
+    if (a.dseq) {  // graph lane: this replay's base, read before any workgroup can advance it
+        const SeqBase q = dseq_read(a.dseq);
+        epoch0 = q.epoch + 1;
+        round0 = q.round;
+    }
+    pipe_body<Rd, PROG>(a, epoch0, round0);
+    if (a.dseq) dseq_advance(a.dseq, 2 * (uint64_t)a.nrounds, (uint64_t)a.nrounds, 0);
     block_done(a.done);
 }
 

@@ -52,6 +52,7 @@ bool log_debug_on() {
 static hipStream_t pick_stream(void *s) {
     World &w = world();
     hipStream_t st = s ? (hipStream_t)s : w.stream;
+    if (w.graph) return st;  // graph lane: disjoint arenas and epochs, ordered by the graph itself
     if (w.last_st && st != w.last_st) {
         if (!w.sw_ev) hipEventCreateWithFlags(&w.sw_ev, hipEventDisableTiming);
         if (w.sw_ev) {
@@ -64,7 +65,7 @@ static hipStream_t pick_stream(void *s) {
 }
 static void stream_tail(hipStream_t st) {
     World &w = world();
-    if (st == w.stream) return;
+    if (st == w.stream || w.graph) return;
     if (!w.sw_ev) hipEventCreateWithFlags(&w.sw_ev, hipEventDisableTiming);
     if (w.sw_ev) hipEventRecord(w.sw_ev, st);
 }
@@ -364,17 +365,25 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
     for (int j = 0; j < a.n; ++j) maxlen = std::max(maxlen, a.seg_len[j]);
     if (maxlen == 0) return 0;  // every rank sees the same geometry
     const PipeGeom g = pipe_geom(maxlen);
-    a.rs_peer = w.peer_rs;
-    a.ag_peer = w.peer_ag;
-    a.sig_peer = w.peer_sig;
-    a.sig_own = w.sig;
     a.tsub = g.tsub;
     a.tseg = g.tseg;
     a.nrounds = g.nrounds;
-    a.round0 = w.round;
-    w.round += (uint64_t)g.nrounds;
-    a.epoch0 = w.epoch + 1;
-    w.epoch += 2 * (uint64_t)g.nrounds;
+    if (w.graph) {  // graph lane: own arenas and flags; epochs and parities from the device
+        a.rs_peer = w.g_peer_rs;
+        a.ag_peer = w.g_peer_ag;
+        a.sig_peer = w.g_peer_sig;
+        a.sig_own = w.g_sig;
+        a.dseq = w.dseq;
+    } else {
+        a.rs_peer = w.peer_rs;
+        a.ag_peer = w.peer_ag;
+        a.sig_peer = w.peer_sig;
+        a.sig_own = w.sig;
+        a.round0 = w.round;
+        w.round += (uint64_t)g.nrounds;
+        a.epoch0 = w.epoch + 1;
+        w.epoch += 2 * (uint64_t)g.nrounds;
+    }
     a.err = w.h_err;
     a.timeout = w.timeout_ticks;
     a.light = w.light_release;
@@ -881,6 +890,22 @@ struct Staged {
     size_t bytes;
 };
 
+// Device staging space of a call.  A captured call (graph lane) cannot use the shared scratch
+// buffers — a graph keeps their addresses for every replay while later calls regrow or reuse
+// them — so it takes a private piece of a pool that lives until MPI_Finalize.
+static void *call_scratch(int idx, size_t bytes) {
+    World &w = world();
+    if (!w.graph) return get_scratch(idx, bytes);
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (!w.g_pool || w.g_pool_used + need > w.g_pool_bytes) {
+        MV2_ERR("graph lane: staging pool exhausted (%zu bytes)", w.g_pool_bytes);
+        return nullptr;
+    }
+    void *p = w.g_pool + w.g_pool_used;
+    w.g_pool_used += need;
+    return p;
+}
+
 static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, bool in_place, hipStream_t st,
                     Staged &s) {
     s.copy_back = false;
@@ -890,7 +915,7 @@ static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, 
     if (recv_ok) {
         s.recv = (char *)recv;
     } else {
-        s.recv = (char *)get_scratch(1, rbytes);
+        s.recv = (char *)call_scratch(1, rbytes);
         if (!s.recv) return E_NO_MEM;
         s.copy_back = true;
         if (in_place) hipMemcpyAsync(s.recv, recv, rbytes, hipMemcpyDefault, st);
@@ -902,7 +927,7 @@ static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, 
         if (send_ok) {
             s.send = (const char *)send;
         } else {
-            char *t = (char *)get_scratch(0, sbytes);
+            char *t = (char *)call_scratch(0, sbytes);
             if (!t) return E_NO_MEM;
             hipMemcpyAsync(t, send, sbytes, hipMemcpyDefault, st);
             s.send = t;
@@ -948,19 +973,27 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.send = s.send;
         a.recv = s.recv;
         const size_t half = (size_t)kMaxRanks * w.slot_bytes;
-        const size_t par = (w.os_calls++ & 1) * half;
-        const uint64_t epoch = ++w.epoch;
-        for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j] + par;
-        a.arena_own = w.arena + par;
-        a.sig_peer = w.peer_sig;
-        a.sig_own = w.sig;
+        if (w.graph) {  // graph lane: the kernel picks the half and the epoch from the device
+            for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.g_peer_arena[j];
+            a.arena_own = w.g_arena;
+            a.sig_peer = w.g_peer_sig;
+            a.sig_own = w.g_sig;
+            a.dseq = w.dseq;
+            a.half = half;
+        } else {
+            const size_t par = (w.os_calls++ & 1) * half;
+            for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j] + par;
+            a.arena_own = w.arena + par;
+            a.sig_peer = w.peer_sig;
+            a.sig_own = w.sig;
+            a.epoch = ++w.epoch;
+        }
         a.count = count;
         a.nvec = nvec;
         a.slot_bytes = w.slot_bytes;
         a.n = n;
         a.me = w.rank;
         a.tp = tp;
-        a.epoch = epoch;
         a.err = w.h_err;
         a.timeout = w.timeout_ticks;
         a.light = w.light_release;
@@ -994,7 +1027,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
             }
         } else {
             const size_t pcb = (cb + 15) & ~(size_t)15;
-            char *ps = (char *)get_scratch(3, pcb * n), *pr = (char *)get_scratch(4, pcb * n);
+            char *ps = (char *)call_scratch(3, pcb * n), *pr = (char *)call_scratch(4, pcb * n);
             if (!ps || !pr) return E_NO_MEM;
             if (hipMemcpy2DAsync(ps, pcb, s.send, cb, cb, n, hipMemcpyDeviceToDevice, st) != hipSuccess)
                 return E_INTERN;
@@ -1604,17 +1637,34 @@ int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent, 
 // host copy after the kernel) and builtin ops (user ops and x87 run on the host).
 // ---------------------------------------------------------------------------
 struct EnqueueScope {
-    EnqueueScope() { world().enqueue = true; }
-    ~EnqueueScope() { world().enqueue = false; }
+    explicit EnqueueScope(bool graph = false) {
+        world().enqueue = true;
+        world().graph = graph;
+    }
+    ~EnqueueScope() {
+        world().enqueue = false;
+        world().graph = false;
+    }
 };
-static int enqueue_checks(const void *send, const void *recv, void *stream) {
-    if (!stream) return E_ARG;
-    // a kernel captured into a graph would replay this call's flag epochs and slot parities,
-    // which the host hands out once per call: refuse capture instead of hanging a replay
+static bool capturing(void *stream) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
-        MV2_ERR("stream-ordered collectives cannot be captured into a HIP graph");
-        return E_UNSUPPORTED;
+    return stream && hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+static int enqueue_checks(const void *send, const void *recv, void *stream, bool graph_ok = false) {
+    if (!stream) return E_ARG;
+    // host-managed epochs and parities would be replayed by a graph: a captured call must take
+    // the graph lane (allreduce on 16-byte-aligned device buffers), anything else is refused
+    if (capturing(stream)) {
+        const World &w = world();
+        if (!graph_ok || !w.graph_lane || w.size < 2 || w.nnodes > 1) {
+            MV2_ERR("only MPI_Allreduce on one node can be captured into a HIP graph (graph lane %s)",
+                    w.graph_lane ? "on" : "off");
+            return E_UNSUPPORTED;
+        }
+        if ((uintptr_t)recv % 16 || (send && send != (const void *)-1 && (uintptr_t)send % 16)) {
+            MV2_ERR("a captured allreduce needs 16-byte-aligned buffers (no staging inside a graph)");
+            return E_ARG;
+        }
     }
     if (!is_device(recv) || (send && send != (const void *)-1 && !is_device(send))) {
         MV2_ERR("stream-ordered collectives take device buffers only");
@@ -1624,9 +1674,11 @@ static int enqueue_checks(const void *send, const void *recv, void *stream) {
 }
 
 int mv2h_allreduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
-    int rc = count ? enqueue_checks(sendbuf, recvbuf, stream) : 0;
+    int rc = count ? enqueue_checks(sendbuf, recvbuf, stream, true) : 0;
     if (rc || !count) return rc;
-    EnqueueScope q;
+    const bool graph = capturing(stream);
+    if (graph && op_index(op) >= OP_REPLACE) return E_OP;
+    EnqueueScope q(graph);
     return mv2h_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
 }
 

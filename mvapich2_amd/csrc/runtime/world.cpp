@@ -279,6 +279,32 @@ int world_init() {
                         kPipeRegion >> 20);
                 return E_NO_MEM;
             }
+            // graph lane (MV2AMD_GRAPH_LANE=0 leaves it out): the same layout again, for
+            // collectives captured into HIP graphs, whose sequence numbers live on the device
+            w.graph_lane = env_long("MV2AMD_GRAPH_LANE", 1) != 0;
+            if (w.graph_lane &&
+                (hipExtMallocWithFlags((void **)&w.g_sig, sig_bytes, hipDeviceMallocUncached) != hipSuccess ||
+                 hipExtMallocWithFlags((void **)&w.g_arena, arena_bytes, hipDeviceMallocUncached) != hipSuccess ||
+                 hipExtMallocWithFlags((void **)&w.g_rs, kPipeRegion, hipDeviceMallocUncached) != hipSuccess ||
+                 hipExtMallocWithFlags((void **)&w.g_ag, kPipeRegion, hipDeviceMallocUncached) != hipSuccess ||
+                 hipExtMallocWithFlags((void **)&w.dseq, sizeof(DevSeq), hipDeviceMallocUncached) != hipSuccess)) {
+                MV2_ERR("graph lane: device allocation failed");
+                return E_NO_MEM;
+            }
+            if (w.graph_lane) {
+                w.g_pool_bytes = (size_t)env_long("MV2AMD_GRAPH_POOL", 4L << 20);
+                if (hipMalloc((void **)&w.g_pool, w.g_pool_bytes) != hipSuccess) return E_NO_MEM;
+                hipMemset(w.g_sig, 0, sig_bytes);
+                hipMemset(w.dseq, 0, sizeof(DevSeq));
+                if (hipIpcGetMemHandle(&me.g_sig_handle, w.g_sig) != hipSuccess ||
+                    hipIpcGetMemHandle(&me.g_arena_handle, w.g_arena) != hipSuccess ||
+                    hipIpcGetMemHandle(&me.g_rs_handle, w.g_rs) != hipSuccess ||
+                    hipIpcGetMemHandle(&me.g_ag_handle, w.g_ag) != hipSuccess) {
+                    MV2_ERR("hipIpcGetMemHandle failed for the graph lane");
+                    return E_OTHER;
+                }
+            }
+            me.graph_lane = w.graph_lane ? 1 : 0;
             hipDeviceSynchronize();
             if (hipIpcGetMemHandle(&me.sig_handle, w.sig) != hipSuccess ||
                 hipIpcGetMemHandle(&me.arena_handle, w.arena) != hipSuccess ||
@@ -298,7 +324,29 @@ int world_init() {
                     w.peer_rs.p[j] = w.pipe_rs;
                     w.peer_ag.p[j] = w.pipe_ag;
                     w.peer_p2p[j] = w.p2p;
+                    w.g_peer_sig.p[j] = w.g_sig;
+                    w.g_peer_arena[j] = w.g_arena;
+                    w.g_peer_rs.p[j] = w.g_rs;
+                    w.g_peer_ag.p[j] = w.g_ag;
                     continue;
+                }
+                if (w.shm->r[j].graph_lane != (w.graph_lane ? 1 : 0)) {
+                    MV2_ERR("MV2AMD_GRAPH_LANE differs between ranks");
+                    return E_OTHER;
+                }
+                if (w.graph_lane) {
+                    void *q[4] = {};
+                    if (hipIpcOpenMemHandle(&q[0], w.shm->r[j].g_sig_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                        hipIpcOpenMemHandle(&q[1], w.shm->r[j].g_arena_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                        hipIpcOpenMemHandle(&q[2], w.shm->r[j].g_rs_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                        hipIpcOpenMemHandle(&q[3], w.shm->r[j].g_ag_handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                        MV2_ERR("hipIpcOpenMemHandle failed for rank %d's graph lane", j);
+                        return E_OTHER;
+                    }
+                    w.g_peer_sig.p[j] = (uint64_t *)q[0];
+                    w.g_peer_arena[j] = (char *)q[1];
+                    w.g_peer_rs.p[j] = (char *)q[2];
+                    w.g_peer_ag.p[j] = (char *)q[3];
                 }
                 if (w.shm->r[j].slot_bytes != w.slot_bytes) {
                     MV2_ERR("MV2AMD_ONESHOT_MAX differs between ranks");
@@ -383,6 +431,12 @@ int world_finalize() {
                 if (w.peer_rs.p[j]) hipIpcCloseMemHandle(w.peer_rs.p[j]);
                 if (w.peer_ag.p[j]) hipIpcCloseMemHandle(w.peer_ag.p[j]);
                 if (w.peer_p2p[j]) hipIpcCloseMemHandle(w.peer_p2p[j]);
+                if (w.graph_lane) {
+                    if (w.g_peer_sig.p[j]) hipIpcCloseMemHandle(w.g_peer_sig.p[j]);
+                    if (w.g_peer_arena[j]) hipIpcCloseMemHandle(w.g_peer_arena[j]);
+                    if (w.g_peer_rs.p[j]) hipIpcCloseMemHandle(w.g_peer_rs.p[j]);
+                    if (w.g_peer_ag.p[j]) hipIpcCloseMemHandle(w.g_peer_ag.p[j]);
+                }
             }
         }
         host_barrier();  // nobody maps our pages any more
@@ -397,6 +451,8 @@ int world_finalize() {
     if (w.pipe_rs) hipFree(w.pipe_rs);
     if (w.pipe_ag) hipFree(w.pipe_ag);
     if (w.p2p) hipFree(w.p2p);
+    for (void *p : {(void *)w.g_sig, (void *)w.g_arena, (void *)w.g_rs, (void *)w.g_ag, (void *)w.dseq, (void *)w.g_pool})
+        if (p) hipFree(p);
     w.finalized = true;
     return 0;
 }

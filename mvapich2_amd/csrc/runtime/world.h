@@ -68,6 +68,8 @@ struct alignas(64) ShmRank {
     hipIpcMemHandle_t pipe_rs_handle;
     hipIpcMemHandle_t pipe_ag_handle;
     hipIpcMemHandle_t p2p_handle;
+    hipIpcMemHandle_t g_sig_handle, g_arena_handle, g_rs_handle, g_ag_handle;  // graph lane
+    int graph_lane;   // 1: this rank allocated the graph lane
     int selftest_ok;  // coll_selftest verdict of this rank (agreed through host_barrier)
     double tune_us[kTuneMax];  // pipe_autotune: this rank's time per candidate tiling
     Knobs knobs;      // MV2_* selection knobs as this rank parsed them (must agree)
@@ -108,6 +110,20 @@ struct World {
     uint64_t epoch = 0;       // last flag epoch used (identical on every rank)
     uint64_t round = 0;       // pipeline rounds issued (slot parity)
     uint64_t os_calls = 0;    // one-shot calls issued (arena parity)
+
+    // graph lane (HIP graph capture of stream-ordered allreduce, coll.cpp): its own signal page,
+    // one-shot arena and pipeline arenas, with the sequence numbers kept on the device (DevSeq)
+    bool graph_lane = false;
+    bool graph = false;  // the current call is being captured into a graph
+    uint64_t *g_sig = nullptr;
+    SigTable g_peer_sig{};
+    char *g_arena = nullptr;
+    char *g_peer_arena[kMaxRanks] = {};
+    char *g_rs = nullptr, *g_ag = nullptr;
+    PeerTableW g_peer_rs{}, g_peer_ag{};
+    DevSeq *dseq = nullptr;
+    char *g_pool = nullptr;        // staging pieces of captured calls (never reused)
+    size_t g_pool_bytes = 0, g_pool_used = 0;
 
     // point-to-point (runtime/p2p.cpp)
     char *p2p = nullptr;                  // my P2P arena: [src][slot] chunks

@@ -58,11 +58,11 @@ def enqueue_seq(L, case, rank, n):
     hx = np.zeros(4, dtype=np.float32)
     assert L.MPIX_Allreduce_enqueue(P(hx.ctypes.data), P(y.ptr), 4, F, SUM, WORLD, P(s)) != 0
     assert L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), 4, F, SUM, WORLD, None) != 0
-    # refused: a stream being captured into a HIP graph (a replay would reuse the call's epochs)
+    # refused: a collective other than Allreduce on a stream being captured into a HIP graph
     cap, graph = ctypes.c_void_p(), ctypes.c_void_p()
     assert hip.hipStreamCreate(ctypes.byref(cap)) == 0
     assert hip.hipStreamBeginCapture(cap, 2) == 0  # hipStreamCaptureModeRelaxed
-    rc_cap = L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), c, F, SUM, WORLD, cap)
+    rc_cap = L.MPIX_Bcast_enqueue(P(xb.ptr), c, F, 0, WORLD, cap)  # only Allreduce takes the graph lane
     assert hip.hipStreamEndCapture(cap, ctypes.byref(graph)) == 0
     if graph.value:
         hip.hipGraphDestroy(graph)
@@ -77,6 +77,49 @@ def enqueue_seq(L, case, rank, n):
     w2 = m.DeviceBuffer(c * 4)
     assert L.MPI_Allreduce(sb.ptr, w2.ptr, c, F, SUM, WORLD) == 0
     out.append(w2.download(np.uint8, count=c * 4))
+    return np.concatenate(out)
+
+
+def graph_allreduce(L, case, rank, n):
+    """HIP graph capture (graph lane): MPIX_Allreduce_enqueue captured on a stream for each count,
+    the graphs instantiated once and replayed `reps` times in an interleaved order with new
+    operands each time and a blocking MPI_Allreduce between replays (the host lane); returns
+    every replay's result and every blocking result, concatenated."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    F, SUM = TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]
+    P = ctypes.c_void_p
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+    counts, reps = case["counts"], case["reps"]
+    bufs, execs = [], []
+    for c in counts:
+        sb, rb = m.DeviceBuffer(c * 4), m.DeviceBuffer(c * 4)
+        graph, ex = ctypes.c_void_p(), ctypes.c_void_p()
+        assert hip.hipStreamBeginCapture(st, 2) == 0  # hipStreamCaptureModeRelaxed
+        rc = L.MPIX_Allreduce_enqueue(P(sb.ptr), P(rb.ptr), c, F, SUM, WORLD, st)
+        assert hip.hipStreamEndCapture(st, ctypes.byref(graph)) == 0
+        assert rc == 0, rc
+        assert hip.hipGraphInstantiate(ctypes.byref(ex), graph, None, None, 0) == 0
+        bufs.append((sb, rb, graph))
+        execs.append(ex)
+    out = []
+    hb_s, hb_r = m.DeviceBuffer(4096 * 4), m.DeviceBuffer(4096 * 4)
+    for k in range(reps):
+        for g, c in enumerate(counts):
+            sb, rb, _ = bufs[g]
+            sb.upload(np.random.default_rng(case["seed"] * 100000 + k * 1000 + g * 10 + rank).standard_normal(c).astype(np.float32))
+            assert hip.hipGraphLaunch(execs[g], st) == 0
+            assert hip.hipStreamSynchronize(st) == 0
+            out.append(rb.download(np.uint8, count=c * 4))
+        # the host lane between replays
+        hb_s.upload(np.random.default_rng(case["seed"] * 7 + k * 13 + rank).standard_normal(4096).astype(np.float32))
+        assert L.MPI_Allreduce(hb_s.ptr, hb_r.ptr, 4096, F, SUM, WORLD) == 0
+        out.append(hb_r.download(np.uint8, count=4096 * 4))
+    assert L.MPIX_Enqueue_check(WORLD) == 0
+    for g, ex in enumerate(execs):
+        hip.hipGraphExecDestroy(ex)
+        hip.hipGraphDestroy(bufs[g][2])
+    hip.hipStreamDestroy(st)
     return np.concatenate(out)
 
 
@@ -225,6 +268,8 @@ def main():
                 rc = L.MPI_Reduce(sb.ptr, rb.ptr, count, h, op, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * ext)
+        elif k == "graph_allreduce":  # HIP graph capture of MPIX_Allreduce_enqueue (graph lane)
+            res = graph_allreduce(L, case, rank, n)
         elif k == "enqueue_seq":  # stream-ordered collectives (MPIX_*_enqueue) mixed with a blocking call
             res = enqueue_seq(L, case, rank, n)
         elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)
