@@ -275,7 +275,26 @@ static TreeParams tree_rs(int n, size_t count, int me, bool force_rd) {
     return tp;
 }
 
+// A program set whose every program is acc = ((x0 . x1) . x2) ... (the degree-4 tree over one
+// group of <= 4 ranks, and any other algorithm that reduces to it) runs on the specialised
+// LINEAR evaluator instead of the program kernel: same operands in the same order.
+static bool progs_are_linear(const ProgSet &ps, int n) {
+    if (ps.nprog < 1) return false;
+    for (int k = 0; k < ps.nprog; ++k) {
+        const Prog &q = ps.p[k];
+        if (q.nsteps != n - 1 || q.res != 0) return false;
+        for (int s = 0; s < n - 1; ++s)
+            if (q.dst[s] != 0 || q.src[s] != s + 1) return false;
+    }
+    return true;
+}
+
 static TreeParams tree_from_plan(const Plan &p, int n, size_t count, int me) {
+    if (p.algo != ALG_PT2PT_RS && p.algo != ALG_PT2PT_RD && p.algo != ALG_SHMEM_LINEAR && progs_are_linear(p.ps, n)) {
+        TreeParams tp = tree_base(n);
+        tp.linear = 1;
+        return tp;
+    }
     switch (p.algo) {
     case ALG_PT2PT_RS: return tree_rs(n, count, me, false);
     case ALG_PT2PT_RD: return tree_rs(n, count, me, true);
