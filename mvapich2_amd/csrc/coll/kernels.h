@@ -9,7 +9,8 @@
 namespace mv2 {
 
 struct TreeParams {
-    int linear;      // 1: LINEAR, 0: BUTTERFLY, 2: RS ring, 3: AR ring (rotated), 4: PROGRAM (ps)
+    int linear;      // 1: LINEAR, 0: BUTTERFLY, 2: RS ring, 3: AR ring (rotated), 4: PROGRAM (ps),
+                     // 5: GROUPED (one-shot kernel only; group size in pof2)
     int pof2, rem, lg;
     int owner_fixed; // >= 0: fixed owner newrank; -1: reduce-scatter block owner
     size_t rs_blk;   // elements per reduce-scatter block (count / pof2)

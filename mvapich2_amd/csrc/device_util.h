@@ -223,6 +223,7 @@ __device__ __forceinline__ v4u vapply(v4u a, v4u b) {
 // LINEAR   : ((v0 . v1) . v2) ...                (two-level reduce_shmem order; linear == 3 is
 //                                                  the flat ring allreduce on rotated sources)
 // RING     : v_{n-1} . (... (v2 . (v1 . v0)))    (linear == 2; reduce-scatter ring, rotated sources)
+// GROUPED  : (g_0 . g_d) . g_2d ..., g_k = LINEAR over ranks k .. k+d-1 (linear == 5, d in pof2)
 // BUTTERFLY: non-pof2 fold w[i] = v[2i+1] . v[2i] for i < rem, then levels
 //            m = 1, 2, 4 pairing (j, j+m); the left operand is the subtree
 //            containing `owner` (recursive halving / doubling order).
@@ -240,6 +241,30 @@ __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[
 #pragma unroll
         for (int i = 1; i < kMaxRanks; ++i)
             if (i < n) acc = Rd::apply(v[i], acc);
+        return acc;
+    }
+    if (linear == 5) {
+        // GROUPED (one-shot only; `pof2` carries the group size d): the two-level degree-d shm
+        // tree, mv2_shm_tree_reduce ch3_shmem_coll.c:4302-4340 — the leader of each group of d
+        // reduces its members in order, rank 0 then reduces the other leaders in order
+        const int d = pof2;
+        T acc = v[0], grp = v[0];
+        bool first = true;
+#pragma unroll
+        for (int i = 1; i < kMaxRanks; ++i) {
+            if (i < n) {
+                if (i % d == 0) {
+                    if (!first) acc = Rd::apply(acc, grp);
+                    grp = v[i];
+                    first = false;
+                } else if (first) {
+                    acc = Rd::apply(acc, v[i]);
+                } else {
+                    grp = Rd::apply(grp, v[i]);
+                }
+            }
+        }
+        if (!first) acc = Rd::apply(acc, grp);
         return acc;
     }
     if (linear) {

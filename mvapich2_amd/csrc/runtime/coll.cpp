@@ -289,6 +289,25 @@ static bool progs_are_linear(const ProgSet &ps, int n) {
     return true;
 }
 
+// The two-level degree-d tree (d < n) as a program: each group leader g reduces g+1 .. g+d-1,
+// then rank 0 reduces the leaders d, 2d, ... in order.  Returns d when `ps` is that program.
+static int progs_grouped(const ProgSet &ps, int n) {
+    if (ps.nprog != 1) return 0;
+    const Prog &q = ps.p[0];
+    for (int d = 2; d < n; ++d) {
+        uint8_t dst[kMaxRanks], src[kMaxRanks];
+        int k = 0;
+        for (int g = 0; g < n; g += d)
+            for (int m = g + 1; m < g + d && m < n; ++m) dst[k] = (uint8_t)g, src[k++] = (uint8_t)m;
+        for (int g = d; g < n; g += d) dst[k] = 0, src[k++] = (uint8_t)g;
+        if (k != q.nsteps || q.res != 0) continue;
+        bool same = true;
+        for (int s = 0; s < k && same; ++s) same = q.dst[s] == dst[s] && q.src[s] == src[s];
+        if (same) return d;
+    }
+    return 0;
+}
+
 static TreeParams tree_from_plan(const Plan &p, int n, size_t count, int me) {
     if (p.algo != ALG_PT2PT_RS && p.algo != ALG_PT2PT_RD && p.algo != ALG_SHMEM_LINEAR && progs_are_linear(p.ps, n)) {
         TreeParams tp = tree_base(n);
@@ -988,6 +1007,14 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     const size_t nvec = bytes / 16;
     const int gcap = grid_cap();
     if (!ring && bytes <= w.oneshot_max && bytes <= w.slot_bytes) {
+        // the degree-d tree (the default small-message order at 6-8 ranks) on its own evaluator
+        if (tp.linear == 4) {
+            const int d = progs_grouped(tp.ps, n);
+            if (d) {
+                tp.linear = 5;
+                tp.pof2 = d;
+            }
+        }
         OneShotArgs a{};
         a.send = s.send;
         a.recv = s.recv;
