@@ -1607,8 +1607,7 @@ static int mn_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *
         const int n = w.nnodes, right = (w.node + 1) % n, left = (w.node - 1 + n) % n;
         for (int k = 0; k < n - 1; ++k) {
             const int so = (w.node - k + n) % n, ro = (w.node - k - 1 + n) % n;
-            if ((rc = net_sendrecv(right, g_mn.h0 + (size_t)so * sect, sect, nullptr, 0)) ||
-                (rc = net_sendrecv(left, nullptr, 0, g_mn.h0 + (size_t)ro * sect, sect)))
+            if ((rc = net_shift(right, g_mn.h0 + (size_t)so * sect, sect, left, g_mn.h0 + (size_t)ro * sect, sect)))
                 return rc;
         }
         if ((rc = mn_h2d(recvbuf, g_mn.h0, total))) return rc;

@@ -161,6 +161,43 @@ int xfer(int fd, const char *sb, size_t sn, char *rb, size_t rn) {
     return 0;
 }
 
+// send sn bytes on fd_out while receiving rn bytes on fd_in (a ring step: different peers),
+// interleaved so that neither side's socket buffers can fill up and stall the ring
+int xfer2(int fd_out, const char *sb, size_t sn, int fd_in, char *rb, size_t rn) {
+    size_t so = 0, ro = 0;
+    const int ms = (int)(timeout_s() * 1000.0);
+    while (so < sn || ro < rn) {
+        pollfd p[2] = {{fd_out, (short)(so < sn ? POLLOUT : 0), 0}, {fd_in, (short)(ro < rn ? POLLIN : 0), 0}};
+        const int r = poll(p, 2, ms);
+        if (r <= 0) {
+            if (r < 0 && errno == EINTR) continue;
+            MV2_ERR("inter-node transfer timed out (MV2AMD_TIMEOUT_S)");
+            return E_OTHER;
+        }
+        if ((p[1].revents & POLLIN) && ro < rn) {
+            const ssize_t k = recv(fd_in, rb + ro, rn - ro, 0);
+            if (k == 0) {
+                MV2_ERR("inter-node connection closed by the peer");
+                return E_OTHER;
+            }
+            if (k < 0 && errno != EINTR && errno != EAGAIN) return E_OTHER;
+            if (k > 0) ro += (size_t)k;
+        } else if (p[1].revents & (POLLERR | POLLHUP | POLLNVAL)) {
+            MV2_ERR("inter-node connection lost");
+            return E_OTHER;
+        }
+        if ((p[0].revents & POLLOUT) && so < sn) {
+            const ssize_t k = send(fd_out, sb + so, sn - so, MSG_NOSIGNAL | MSG_DONTWAIT);
+            if (k < 0 && errno != EINTR && errno != EAGAIN && errno != EWOULDBLOCK) return E_OTHER;
+            if (k > 0) so += (size_t)k;
+        } else if (p[0].revents & (POLLERR | POLLHUP | POLLNVAL)) {
+            MV2_ERR("inter-node connection lost");
+            return E_OTHER;
+        }
+    }
+    return 0;
+}
+
 int link_fd(int peer) {
     if (peer < 0 || peer >= (int)g_net.fd.size() || g_net.fd[peer] < 0) {
         MV2_ERR("no inter-node link to node %d", peer);
@@ -182,6 +219,12 @@ int net_recv(int peer, void *buf, size_t bytes) {
 int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes) {
     const int fd = link_fd(peer);
     return fd < 0 ? E_INTERN : xfer(fd, (const char *)sbuf, sbytes, (char *)rbuf, rbytes);
+}
+
+int net_shift(int to, const void *sbuf, size_t sbytes, int from, void *rbuf, size_t rbytes) {
+    if (to == from) return net_sendrecv(to, sbuf, sbytes, rbuf, rbytes);
+    const int fo = link_fd(to), fi = link_fd(from);
+    return fo < 0 || fi < 0 ? E_INTERN : xfer2(fo, (const char *)sbuf, sbytes, fi, (char *)rbuf, rbytes);
 }
 
 int net_init() {

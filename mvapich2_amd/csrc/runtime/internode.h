@@ -14,5 +14,7 @@ int net_barrier();   // leaders only
 int net_send(int peer, const void *buf, size_t bytes);
 int net_recv(int peer, void *buf, size_t bytes);
 int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes);
+// one ring step: send to `to` while receiving from `from`, both directions in flight together
+int net_shift(int to, const void *sbuf, size_t sbytes, int from, void *rbuf, size_t rbytes);
 
 }  // namespace mv2
