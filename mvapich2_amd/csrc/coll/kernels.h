@@ -147,8 +147,8 @@ int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg
 // data-movement pipeline modes (AG / BC)
 int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg);
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride,
-                        int unpack, hipStream_t stream);
+                        int unpack, hipStream_t stream, Done done = Done{});
 int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
-                     const int64_t *lens, int nseg, int unpack, hipStream_t stream);
+                     const int64_t *lens, int nseg, int unpack, hipStream_t stream, Done done = Done{});
 
 }  // namespace mv2

@@ -34,7 +34,7 @@ constexpr int kPackThreads = 512;
 template <typename G>
 __global__ __launch_bounds__(kPackThreads) void k_pack_units(const char *__restrict__ src, char *__restrict__ dst,
                                                              size_t nrows, uint32_t upr, size_t stride_units,
-                                                             int unpack) {
+                                                             int unpack, Done done) {
     constexpr int kThreads = kPackThreads;
     const size_t total = nrows * upr;
     const size_t base = (size_t)blockIdx.x * kThreads * kPackU + threadIdx.x;
@@ -55,16 +55,14 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_units(const char *__restr
 #pragma unroll
     for (int k = 0; k < kPackU; ++k)
         if (base + (size_t)k * kThreads < total) d[at[k]] = v[k];
+    block_done(done);  // completion word of a blocking MPI_Pack / MPI_Unpack
 }
 
 // LDS-staged pack of narrow rows: rows [r0, r0+R) per workgroup.
 constexpr int kLdsSpan = 32768;  // bytes of strided span staged per workgroup
-__global__ __launch_bounds__(kThreads) void k_pack_lds(const char *__restrict__ src, char *__restrict__ dst,
-                                                       size_t nrows, uint32_t blk, uint32_t stride,
-                                                       uint32_t rows_per_wg) {
+__device__ __forceinline__ void pack_lds_rows(const char *__restrict__ src, char *__restrict__ dst, size_t nrows,
+                                              uint32_t blk, uint32_t stride, uint32_t rows_per_wg, size_t r0) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    const size_t r0 = (size_t)blockIdx.x * rows_per_wg;
-    if (r0 >= nrows) return;
     const size_t r1 = r0 + rows_per_wg < nrows ? r0 + rows_per_wg : nrows;
     // strided span [r0*stride, (r1-1)*stride + blk) loaded with 16B vectors from a 16B-aligned base
     const uintptr_t sb = (uintptr_t)src + r0 * stride;
@@ -99,6 +97,13 @@ __global__ __launch_bounds__(kThreads) void k_pack_lds(const char *__restrict__ 
         o[b] = lds[lead + row * stride + col];
     }
 }
+__global__ __launch_bounds__(kThreads) void k_pack_lds(const char *__restrict__ src, char *__restrict__ dst,
+                                                       size_t nrows, uint32_t blk, uint32_t stride,
+                                                       uint32_t rows_per_wg, Done done) {
+    const size_t r0 = (size_t)blockIdx.x * rows_per_wg;
+    if (r0 < nrows) pack_lds_rows(src, dst, nrows, blk, stride, rows_per_wg, r0);
+    block_done(done);
+}
 
 // ---------------------------------------------------------------------------
 // Any flattened layout (pair types, indexed types, vectors with count > 1,
@@ -127,20 +132,9 @@ __device__ __forceinline__ uint64_t udiv(uint64_t a, uint64_t b) {
 }
 
 template <typename G>
-__global__ __launch_bounds__(kThreads) void k_pack_runs(const G *__restrict__ src, G *__restrict__ dst,
-                                                        uint64_t count, uint64_t ext, uint64_t upe,
-                                                        const PackRun *__restrict__ runs, int nrun,
-                                                        int unpack) {
-    __shared__ PackRun lr[kRunLds];
-    const bool staged = nrun <= kRunLds;
-    if (staged) {
-        for (int k = threadIdx.x; k < nrun; k += kThreads) lr[k] = runs[k];
-        __syncthreads();
-    }
-    const uint64_t total = count * upe;
-    const uint64_t step = (uint64_t)gridDim.x * kThreads;
-    uint64_t u = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (u >= total) return;
+__device__ __forceinline__ void pack_runs_units(const G *__restrict__ src, G *__restrict__ dst, uint64_t ext,
+                                                uint64_t upe, uint64_t total, uint64_t step, uint64_t u,
+                                                const PackRun *rt, int nrun, int unpack) {
     // (element, unit-in-element) advanced incrementally: no per-unit 64-bit division
     uint64_t e = udiv(u, upe), q = u - e * upe;
     const uint64_t se = udiv(step, upe), sq = step - se * upe;
@@ -148,11 +142,10 @@ __global__ __launch_bounds__(kThreads) void k_pack_runs(const G *__restrict__ sr
         int lo = 0, hi = nrun;  // largest k with pp[k] <= q
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            const uint64_t p = staged ? lr[mid].pp : runs[mid].pp;
-            if (p <= q) lo = mid;
+            if (rt[mid].pp <= q) lo = mid;
             else hi = mid;
         }
-        const PackRun r = staged ? lr[lo] : runs[lo];
+        const PackRun r = rt[lo];
         const uint64_t w = q - r.pp;
         const uint64_t i = r.nrep > 1 ? udiv(w, r.blk) : 0;
         const int64_t su = (int64_t)(e * ext) + r.off + (int64_t)i * r.stride + (int64_t)(w - i * r.blk);
@@ -167,8 +160,26 @@ __global__ __launch_bounds__(kThreads) void k_pack_runs(const G *__restrict__ sr
     }
 }
 
+template <typename G>
+__global__ __launch_bounds__(kThreads) void k_pack_runs(const G *__restrict__ src, G *__restrict__ dst,
+                                                        uint64_t count, uint64_t ext, uint64_t upe,
+                                                        const PackRun *__restrict__ runs, int nrun,
+                                                        int unpack, Done done) {
+    __shared__ PackRun lr[kRunLds];
+    const bool staged = nrun <= kRunLds;
+    if (staged) {
+        for (int k = threadIdx.x; k < nrun; k += kThreads) lr[k] = runs[k];
+        __syncthreads();
+    }
+    const uint64_t total = count * upe;
+    const uint64_t step = (uint64_t)gridDim.x * kThreads;
+    uint64_t u = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (u < total) pack_runs_units(src, dst, ext, upe, total, step, u, staged ? lr : runs, nrun, unpack);
+    block_done(done);  // completion word of a blocking call (every thread of the block arrives)
+}
+
 int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
-                     const int64_t *lens, int nseg, int unpack, hipStream_t stream) {
+                     const int64_t *lens, int nseg, int unpack, hipStream_t stream, Done done) {
     if (count == 0 || nseg <= 0) return 0;
     if (!offs || !lens) return E_ARG;
     uint64_t acc = (uint64_t)extent | (uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst;
@@ -221,7 +232,7 @@ int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, co
     if (grid > 4096) grid = 4096;
 #define MV2_RUNS(G)                                                                                          \
     hipLaunchKernelGGL(k_pack_runs<G>, dim3(grid), dim3(kThreads), 0, stream, (const G *)src, (G *)dst,     \
-                       (uint64_t)count, ext_u, upe, d_tab, nrun, unpack)
+                       (uint64_t)count, ext_u, upe, d_tab, nrun, unpack, done)
     switch (g) {
     case 16: MV2_RUNS(v4u); break;
     case 8: MV2_RUNS(uint64_t); break;
@@ -234,13 +245,13 @@ int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, co
 }
 
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride, int unpack,
-                        hipStream_t stream) {
+                        hipStream_t stream, Done done) {
     if (nblocks == 0 || blk == 0) return 0;
     if (!unpack && blk < 16 && stride <= 64 && stride >= blk) {
         const uint32_t rows = (uint32_t)((kLdsSpan - 32) / stride);
         const size_t g = (nblocks + rows - 1) / rows;
         hipLaunchKernelGGL(k_pack_lds, dim3(g), dim3(kThreads), kLdsSpan, stream, (const char *)src, (char *)dst,
-                           nblocks, (uint32_t)blk, (uint32_t)stride, rows);
+                           nblocks, (uint32_t)blk, (uint32_t)stride, rows, done);
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
     size_t g = 16;
@@ -254,11 +265,11 @@ int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
     const size_t su = stride / g;
     constexpr int kThreads = kPackThreads;
     switch (g) {
-    case 16: hipLaunchKernelGGL(k_pack_units<v4u>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
-    case 8: hipLaunchKernelGGL(k_pack_units<uint64_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
-    case 4: hipLaunchKernelGGL(k_pack_units<uint32_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
-    case 2: hipLaunchKernelGGL(k_pack_units<uint16_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
-    default: hipLaunchKernelGGL(k_pack_units<uint8_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack); break;
+    case 16: hipLaunchKernelGGL(k_pack_units<v4u>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack, done); break;
+    case 8: hipLaunchKernelGGL(k_pack_units<uint64_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack, done); break;
+    case 4: hipLaunchKernelGGL(k_pack_units<uint32_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack, done); break;
+    case 2: hipLaunchKernelGGL(k_pack_units<uint16_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack, done); break;
+    default: hipLaunchKernelGGL(k_pack_units<uint8_t>, dim3(grid), dim3(kThreads), 0, stream, (const char *)src, (char *)dst, nblocks, (uint32_t)upr, su, unpack, done); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
 }

@@ -1644,7 +1644,7 @@ int mv2h_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, si
     if ((rc = ensure_init_for_device())) return rc;
     hipStream_t st = pick_stream(stream);
     tmark0(st);
-    rc = launch_pack_strided(src, dst, nblocks, blk, stride, 0, st);
+    rc = launch_pack_strided(src, dst, nblocks, blk, stride, 0, st, arm_done(st));
     tmark1(st);
     if (rc) return rc;
     return finish(st, world().timing);
@@ -1655,7 +1655,7 @@ int mv2h_unpack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
     if ((rc = ensure_init_for_device())) return rc;
     hipStream_t st = pick_stream(stream);
     tmark0(st);
-    rc = launch_pack_strided(src, dst, nblocks, blk, stride, 1, st);
+    rc = launch_pack_strided(src, dst, nblocks, blk, stride, 1, st, arm_done(st));
     tmark1(st);
     if (rc) return rc;
     return finish(st, world().timing);
@@ -1667,7 +1667,7 @@ int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent, 
     if ((rc = ensure_init_for_device())) return rc;
     hipStream_t st = pick_stream(stream);
     tmark0(st);
-    rc = launch_pack_runs(src, dst, count, extent, offs, lens, nseg, unpack ? 1 : 0, st);
+    rc = launch_pack_runs(src, dst, count, extent, offs, lens, nseg, unpack ? 1 : 0, st, arm_done(st));
     tmark1(st);
     if (rc) return rc;
     return finish(st, world().timing);
