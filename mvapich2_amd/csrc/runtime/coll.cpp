@@ -1139,6 +1139,7 @@ static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int
 static int mn_allreduce(const void *, void *, size_t, int, int, void *);
 static int mn_reduce(const void *, void *, size_t, int, int, int, void *);
 static int mn_unsupported(const char *what);
+static int mn_reduce_scatter(const void *, void *, const size_t *, int, int, void *);
 
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     if (world().nnodes > 1) {
@@ -1314,7 +1315,10 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
 }
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                         void *stream) {
-    if (world().nnodes > 1) return mn_unsupported("MPI_Reduce_scatter");
+    if (world().nnodes > 1) {
+        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        return mn_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
+    }
     pvar_begin();
     const int rc = reduce_scatter_entry(sendbuf, recvbuf, recvcounts, dtype, op, stream);
     pvar_end(rc == 0);
@@ -1615,8 +1619,35 @@ static int mn_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *
     return bcast_node(recvbuf, total, 0, stream);
 }
 
+// Reduce_scatter across nodes: the two-level allreduce of the whole operand, then this rank's
+// block.  The reference runs its flat reduce-scatter algorithms over all ranks here (red_scat_osu.c
+// :1859-1896), whose fp order is not restated across nodes; integer, logical, bitwise and LOC
+// results are exact.
+static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
+                             void *stream) {
+    World &w = world();
+    int rc = mn_require_device_reduction(dtype, op);
+    if (rc) return rc;
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    size_t total = 0, off = 0;
+    for (int j = 0; j < w.gsize; ++j) {
+        if (j == w.grank) off = total;
+        total += recvcounts[j];
+    }
+    if (total == 0) return 0;
+    const size_t ext = (size_t)dt->extent;
+    char *tmp = nullptr;
+    if (hipMalloc((void **)&tmp, total * ext) != hipSuccess) return E_NO_MEM;
+    const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;
+    rc = mn_allreduce(src, tmp, total, dtype, op, stream);
+    if (!rc && recvcounts[w.grank])
+        rc = hipMemcpy(recvbuf, tmp + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+    hipFree(tmp);
+    return rc;
+}
+
 static int mn_unsupported(const char *what) {
-    MV2_ERR("%s is not supported across nodes (two-level: Allreduce, Reduce, Bcast, Allgather, Barrier)", what);
+    MV2_ERR("%s is not supported across nodes (two-level: Allreduce, Reduce, Reduce_scatter, Bcast, Allgather, Barrier)", what);
     return E_UNSUPPORTED;
 }
 

@@ -4,7 +4,9 @@ TCP (runtime/internode.cpp).  Results are checked bit-exactly against a restatem
 MVAPICH2's two-level structure built from the oracle: node step = the oracle's one-node
 algorithm for the node's ranks, inter-node step = recursive doubling (allreduce, the inter step
 of MPIR_Allreduce_two_level_MV2 / topo-aware hierarchical, allreduce_osu.c:360-630, :2215) or
-binomial reduce (reduce_osu.c:425) over the node leaders, every uop an oracle op-loop call."""
+binomial reduce (reduce_osu.c:425) over the node leaders, every uop an oracle op-loop call;
+reduce-scatter is the two-level allreduce's block (the reference's flat algorithms are not
+restated across nodes)."""
 import numpy as np
 import pytest
 
@@ -79,6 +81,11 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
         cases.append({"id": f"mb{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
                       "seed": seed, "root": root})
         seed += 1
+    for t, op, per in (("MPI_INT", "MPI_SUM", 7001), ("MPI_FLOAT", "MPI_SUM", 100)):
+        counts = [per + (r % 3) for r in range(n)]
+        cases.append({"id": f"ms{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
+                      "count": sum(counts), "seed": seed})
+        seed += 1
     for count in (1000, 100003):
         cases.append({"id": f"mg{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": count,
                       "seed": seed})
@@ -99,6 +106,17 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                                        OPS[case["op"]], 0) for j in range(nodes)]
             want = binomial_leaders(parts, count, t, case["op"], rnode)
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
+        elif k == "reduce_scatter":  # two-level allreduce of the whole operand, then the block
+            counts = case["recvcounts"]
+            parts = [oracle.allreduce_ref(sends[j * ppn:(j + 1) * ppn], count, TYPES[t][0], OPS[case["op"]])[0]
+                     for j in range(nodes)]
+            full = rd_leaders(parts, count, t, case["op"])
+            ext = TYPES[t][3]
+            off = 0
+            for r in range(n):
+                blk = full[r // ppn][off * ext:(off + counts[r]) * ext]
+                assert_bytes_equal(res(cid, r), blk, t, counts[r], f"{cid} reduce_scatter rank {r}")
+                off += counts[r]
         elif k == "bcast":
             want = as_bytes(inputs(case, case["root"]))
             for r in range(n):
