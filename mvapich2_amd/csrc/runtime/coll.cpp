@@ -1139,11 +1139,23 @@ static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int
 static int mn_allreduce(const void *, void *, size_t, int, int, void *);
 static int mn_reduce(const void *, void *, size_t, int, int, int, void *);
 static int mn_unsupported(const char *what);
+// A nonblocking collective across nodes completes at initiation (MPI allows it: the request is
+// complete when MPI_Wait / MPI_Test first sees it); the node steps inside run blocking.
+struct MnBlocking {
+    bool was;
+    MnBlocking() : was(world().defer) { world().defer = false; }
+    ~MnBlocking() {
+        world().defer = was;
+        world().deferred = 0;
+    }
+};
+
 static int mn_reduce_scatter(const void *, void *, const size_t *, int, int, void *);
 
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        MnBlocking nb;
         return mn_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
     }
     pvar_begin();
@@ -1212,7 +1224,8 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
 }
 int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        MnBlocking nb;
         return mn_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
     }
     pvar_begin();
@@ -1316,7 +1329,8 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                         void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        MnBlocking nb;
         return mn_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
     }
     pvar_begin();
@@ -1653,7 +1667,8 @@ static int mn_unsupported(const char *what) {
 
 int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        MnBlocking nb;
         return mn_allgather(sendbuf, recvbuf, bytes, stream);
     }
     return allgather_node(sendbuf, recvbuf, bytes, stream);
@@ -1661,7 +1676,8 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
 
 int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue || world().defer) return mn_unsupported("a nonblocking or stream-ordered collective");
+        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        MnBlocking nb;
         return mn_bcast(buffer, bytes, root, stream);
     }
     return bcast_node(buffer, bytes, root, stream);

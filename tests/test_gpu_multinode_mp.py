@@ -72,6 +72,10 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                          ("MPI_DOUBLE_INT", "MPI_MAXLOC", 5000), ("MPI_UNSIGNED_CHAR", "MPI_BXOR", 4099)):
         cases.append({"id": f"ma{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
         seed += 1
+    # nonblocking across nodes: complete at initiation (integer data: exact in any order)
+    cases.append({"id": f"mi{seed}", "kind": "iallreduce", "type": "MPI_INT", "op": "MPI_SUM", "count": 5000,
+                  "seed": seed})
+    seed += 1
     for t, op, count, root in (("MPI_FLOAT", "MPI_SUM", 1000, n - 1), ("MPI_INT", "MPI_SUM", 70001, 1 % n),
                                ("MPI_DOUBLE", "MPI_MIN", 300, 0)):
         cases.append({"id": f"mr{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
@@ -94,7 +98,7 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        if k == "allreduce":
+        if k in ("allreduce", "iallreduce"):
             parts = [oracle.allreduce_ref(sends[j * ppn:(j + 1) * ppn], count, TYPES[t][0], OPS[case["op"]])[0]
                      for j in range(nodes)]
             want = rd_leaders(parts, count, t, case["op"])
