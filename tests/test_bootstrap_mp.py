@@ -112,3 +112,27 @@ def test_multinode_needs_node_major_ranks():
     rc = q.get(timeout=60)
     p.join()
     assert rc == 44  # MPI_ERR_UNSUPPORTED_OPERATION
+
+
+def test_mv2run_node_emulation_environment(tmp_path):
+    """mv2run --nodes K: node-major local ranks, one boot port for the leaders, the GPU-sharing
+    hint when --share-gpu is given (mvapich2_amd/mv2run.py)."""
+    import json
+    import subprocess
+    import sys
+    out = tmp_path / "env"
+    out.mkdir()
+    child = ("import json, os, sys; k = ['RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'LOCAL_WORLD_SIZE', "
+             "'MV2_COMM_WORLD_LOCAL_RANK', 'MV2AMD_BOOT_PORT', 'MV2AMD_NSHARE', 'MV2AMD_DEVICE', 'MV2AMD_JOBID']; "
+             "open(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write(json.dumps({x: os.environ.get(x) for x in k}))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rc = subprocess.run([sys.executable, "-m", "mvapich2_amd.mv2run", "-n", "6", "--nodes", "3", "--share-gpu",
+                         "--timeout", "60", sys.executable, "-c", child, str(out)], cwd=root, timeout=120).returncode
+    assert rc == 0
+    envs = [json.loads((out / str(r)).read_text()) for r in range(6)]
+    for r, e in enumerate(envs):
+        assert e["RANK"] == str(r) and e["WORLD_SIZE"] == "6"
+        assert e["LOCAL_RANK"] == e["MV2_COMM_WORLD_LOCAL_RANK"] == str(r % 2) and e["LOCAL_WORLD_SIZE"] == "2"
+        assert e["MV2AMD_NSHARE"] == "6" and e["MV2AMD_DEVICE"] == "0"
+    assert len({e["MV2AMD_BOOT_PORT"] for e in envs}) == 1 and envs[0]["MV2AMD_BOOT_PORT"]
+    assert len({e["MV2AMD_JOBID"] for e in envs}) == 1
