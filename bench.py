@@ -462,9 +462,11 @@ def bench_nranks(args, L, rank, size):
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
     tiling = {"grid": m.info("pipe_grid"), "bytes_per_workgroup_round": m.info("pipe_sub"),
+              "remote_stores": "non-temporal" if m.info("pipe_rnt") else "plain",
               "autotuned_at_init": bool(m.info("pipe_tuned")),
               "candidates_max_over_ranks_us": [
-                  {"grid": m.info(f"tune_grid_{k}"), "sub": m.info(f"tune_sub_{k}"), "us": m.info(f"tune_us_{k}")}
+                  {"grid": m.info(f"tune_grid_{k}"), "sub": m.info(f"tune_sub_{k}"),
+                   "nt": m.info(f"tune_rnt_{k}"), "us": m.info(f"tune_us_{k}")}
                   for k in range(m.info("tune_n"))]}
     del sb, rb, rsb
     if args.rccl and m.info("nshare") > 1:

@@ -97,6 +97,7 @@ struct PipeArgs {
     uint64_t *sig_own;
     uint64_t epoch0;                // round k uses epochs epoch0 + 2k and epoch0 + 2k + 1
     int light;                      // 1: signal without the system-scope L2 writeback (uncached data)
+    int rnt;                        // 1: non-temporal stores into peers' arenas, 0: plain (MPI_Init autotune)
     TreeParams tp;
     int *err;
     uint64_t timeout;

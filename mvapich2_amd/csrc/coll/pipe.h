@@ -90,7 +90,7 @@ __device__ __forceinline__ size_t head_bytes(const char *p, size_t len) {
 }
 
 template <bool LocalDst>
-__device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
+__device__ __forceinline__ void blk_copy_jobs(const Jobs &jb, bool rnt = true) {
     constexpr int U = 4;
     __shared__ JobTable t;
     __syncthreads();  // previous users of the table are done
@@ -139,7 +139,7 @@ __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
                 const size_t fu = f + (size_t)u * kPipeThreads;
                 if (fu < NV) {
                     job_addr(t, fu, s, d);
-                    if (LocalDst) *d = cur[u];
+                    if (LocalDst || !rnt) *d = cur[u];
                     else st_nt(d, cur[u]);
                 }
             }
@@ -165,7 +165,7 @@ __device__ __forceinline__ void blk_copy_jobs(const Jobs &jb) {
 // Block-wide copy of nbytes from one source to every non-null destination.
 // src and every destination share the same alignment mod 16: a scalar head up to the
 // first 16-byte boundary, then the 16-byte body, then the tail.
-__device__ __forceinline__ void blk_copy_multi(const Dsts &dd, const char *src0, size_t nbytes0) {
+__device__ __forceinline__ void blk_copy_multi(const Dsts &dd, const char *src0, size_t nbytes0, bool rnt = true) {
     constexpr int U = 4;
     const size_t h = head_bytes(src0, nbytes0);
     if (threadIdx.x < h) {
@@ -203,7 +203,7 @@ __device__ __forceinline__ void blk_copy_multi(const Dsts &dd, const char *src0,
                     for (int u = 0; u < U; ++u)
                         if (x + (size_t)u * kPipeThreads < nv) {
                             v4u *q = (v4u *)d.p[k] + x + (size_t)u * kPipeThreads;
-                            if (k == kMaxRanks) *q = cur[u];  // own recv buffer
+                            if (k == kMaxRanks || !rnt) *q = cur[u];  // own recv buffer / plain remote stores
                             else st_nt(q, cur[u]);
                         }
                 }
@@ -288,7 +288,7 @@ __device__ __forceinline__ void blk_reduce(const PipeArgs &a, const char *const 
 #pragma unroll
                     for (int k = 0; k < kMaxRanks + 1; ++k)
                         if (d.p[k]) {
-                            if (k == kMaxRanks) ((v4u *)d.p[k])[xu] = r;  // own recv buffer
+                            if (k == kMaxRanks || !a.rnt) ((v4u *)d.p[k])[xu] = r;  // own recv / plain remote
                             else st_nt((v4u *)d.p[k] + xu, r);
                         }
                 }
@@ -373,7 +373,7 @@ __device__ __forceinline__ void scatter_round(const PipeArgs &a, uint64_t round0
             jb.len[j] = range_len(a, j, rbase);
         }
     }
-    blk_copy_jobs<false>(jb);
+    blk_copy_jobs<false>(jb, a.rnt != 0);
 }
 
 // P2 of round k: reduce my segment's range from the n RS slots (own operand
@@ -505,7 +505,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a, uint64_t epoch0, ui
                 for (int j = 0; j < kMaxRanks; ++j)
                     if (j < n && j != me) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff + (a.seg_off[me] & 15);
                 if (a.send != a.recv + a.recv_off[me]) d.p[kMaxRanks] = a.recv + a.recv_off[me] + rbase;
-                blk_copy_multi(d, a.send + rbase, len);
+                blk_copy_multi(d, a.send + rbase, len, a.rnt != 0);
             }
             signal_peers(a.sig_peer, n, me, b, E, a.light);
             if (!wait_mask(a.sig_own, all, b, E, a.err, a.timeout, a.light != 0)) return;
@@ -523,7 +523,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a, uint64_t epoch0, ui
                             jb.len[j] = rlen(j);
                         }
                     }
-                    blk_copy_jobs<false>(jb);
+                    blk_copy_jobs<false>(jb, a.rnt != 0);
                 }
                 const size_t l = rlen(root);
                 if (l) {
@@ -531,7 +531,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a, uint64_t epoch0, ui
 #pragma unroll
                     for (int j = 0; j < kMaxRanks; ++j)
                         if (j < n && j != root) d.p[j] = pslot(a.ag_peer.p[j], par, root) + soff;
-                    blk_copy_multi(d, a.send + a.seg_off[root] + rbase, l);
+                    blk_copy_multi(d, a.send + a.seg_off[root] + rbase, l, a.rnt != 0);
                 }
                 signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout, a.light != 0)) return;
@@ -544,7 +544,7 @@ __device__ __forceinline__ void pipe_body(const PipeArgs &a, uint64_t epoch0, ui
 #pragma unroll
                     for (int j = 0; j < kMaxRanks; ++j)
                         if (j < n && j != me && j != root) d.p[j] = pslot(a.ag_peer.p[j], par, me) + soff;
-                    blk_copy_multi(d, pslot(a.rs_peer.p[me], par, root) + soff, l);
+                    blk_copy_multi(d, pslot(a.rs_peer.p[me], par, root) + soff, l, a.rnt != 0);
                 }
                 signal_peers(a.sig_peer, n, me, b, E + 1, a.light);
                 if (!wait_mask(a.sig_own, all, b, E + 1, a.err, a.timeout, a.light != 0)) return;

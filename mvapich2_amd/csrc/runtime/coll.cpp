@@ -406,6 +406,7 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
     a.tsub = g.tsub;
     a.tseg = g.tseg;
     a.nrounds = g.nrounds;
+    a.rnt = w.pipe_rnt;
     if (w.graph) {  // graph lane: own arenas and flags; epochs and parities from the device
         a.rs_peer = w.g_peer_rs;
         a.ag_peer = w.g_peer_ag;
@@ -543,21 +544,27 @@ int pipe_autotune() {
     }
     hipMemset(sb, 0, count * 4);
     hipDeviceSynchronize();
+    // tilings x the flavour of the stores into peers' arenas (non-temporal or plain: how the
+    // fabric combines them is a property of the links, measured rather than assumed)
     static const int kGrid[] = {256, 256, 256, 128, 128, 64};
     static const size_t kSub[] = {128 << 10, 64 << 10, 32 << 10, 256 << 10, 128 << 10, 512 << 10};
-    const int g0 = w.pipe_grid;
+    constexpr int kTilings = (int)(sizeof(kGrid) / sizeof(kGrid[0]));
+    const int g0 = w.pipe_grid, r0 = w.pipe_rnt;
     const size_t s0 = w.pipe_sub;
     int nc = 0;
     int rc = 0;
-    for (int c = 0; c < (int)(sizeof(kGrid) / sizeof(kGrid[0])) && nc < kTuneMax; ++c) {
-        w.pipe_grid = kGrid[c];
-        w.pipe_sub = kSub[c];
+    for (int c = 0; c < 2 * kTilings && nc < kTuneMax; ++c) {
+        w.pipe_grid = kGrid[c % kTilings];
+        w.pipe_sub = kSub[c % kTilings];
+        w.pipe_rnt = c < kTilings ? 1 : 0;
         const PipeGeom g = pipe_geom((count * 4 + w.size - 1) / w.size);
         bool dup = false;  // the grid cap of a shared GPU can fold candidates together
-        for (int k = 0; k < nc; ++k) dup |= w.tune_grid[k] == g.grid && w.tune_sub[k] == g.tsub;
+        for (int k = 0; k < nc; ++k)
+            dup |= w.tune_grid[k] == g.grid && w.tune_sub[k] == g.tsub && w.tune_rnt[k] == w.pipe_rnt;
         if (dup) continue;
         w.tune_grid[nc] = g.grid;
         w.tune_sub[nc] = g.tsub;
+        w.tune_rnt[nc] = w.pipe_rnt;
         double best = 1e30;
         for (int it = 0; it < 4 && !rc; ++it) {  // the first call warms the tiling up
             host_barrier();
@@ -575,6 +582,7 @@ int pipe_autotune() {
     host_barrier();  // every rank's timings are in the control segment
     w.pipe_grid = g0;
     w.pipe_sub = s0;
+    w.pipe_rnt = r0;
     if (rc) {
         MV2_ERR("pipe autotune: probe allreduce failed");
         return rc;
@@ -590,8 +598,10 @@ int pipe_autotune() {
     w.tune_n = nc;
     w.pipe_grid = w.tune_grid[pick];
     w.pipe_sub = w.tune_sub[pick];
+    w.pipe_rnt = w.tune_rnt[pick];
     w.pipe_tuned = 1;
-    MV2_DEBUG("pipe autotune: grid %d sub %zu (%.1f us of %d candidates)", w.pipe_grid, w.pipe_sub, w.tune_us[pick], nc);
+    MV2_DEBUG("pipe autotune: grid %d sub %zu %s stores (%.1f us of %d candidates)", w.pipe_grid, w.pipe_sub,
+              w.pipe_rnt ? "non-temporal" : "plain", w.tune_us[pick], nc);
     return 0;
 }
 
@@ -672,12 +682,15 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "pipe_sub")) *value = (long)w.pipe_sub;
     else if (!strcmp(key, "pipe_tuned")) *value = w.pipe_tuned;
     else if (!strcmp(key, "tune_n")) *value = w.tune_n;
-    else if (!strncmp(key, "tune_", 5) && strlen(key) > 7 && key[strlen(key) - 2] == '_') {
-        // tune_grid_<k> / tune_sub_<k> / tune_us_<k>: candidate k of pipe_autotune
-        const int k = key[strlen(key) - 1] - '0';
-        if (k < 0 || k >= w.tune_n) return E_ARG;
+    else if (!strcmp(key, "pipe_rnt")) *value = w.pipe_rnt;
+    else if (!strncmp(key, "tune_", 5) && strrchr(key, '_') && strrchr(key, '_')[1]) {
+        // tune_grid_<k> / tune_sub_<k> / tune_rnt_<k> / tune_us_<k>: candidate k of pipe_autotune
+        char *end = nullptr;
+        const long k = strtol(strrchr(key, '_') + 1, &end, 10);
+        if (!end || *end || k < 0 || k >= w.tune_n) return E_ARG;
         if (!strncmp(key, "tune_grid_", 10)) *value = w.tune_grid[k];
         else if (!strncmp(key, "tune_sub_", 9)) *value = (long)w.tune_sub[k];
+        else if (!strncmp(key, "tune_rnt_", 9)) *value = w.tune_rnt[k];
         else if (!strncmp(key, "tune_us_", 8)) *value = (long)(w.tune_us[k] + 0.5);
         else return E_ARG;
     } else return E_ARG;

@@ -52,7 +52,7 @@ struct alignas(64) P2PChan {
     P2PRec rec[kP2PSlots];
 };
 
-constexpr int kTuneMax = 8;  // pipe_autotune candidates
+constexpr int kTuneMax = 16;  // pipe_autotune candidates
 
 struct alignas(64) ShmRank {
     std::atomic<uint64_t> arrive;  // host barrier generation
@@ -141,6 +141,8 @@ struct World {
     size_t pipe_sub = kPipeMaxSub;                // bytes per workgroup per segment per round
     int light_release = 1;                        // signal without L2 writeback (arena data is uncached)
     int pipe_tuned = 0;                           // 1: pipe_grid / pipe_sub chosen by pipe_autotune
+    int pipe_rnt = 1;                             // stores into peers' arenas: 1 non-temporal, 0 plain
+    int tune_rnt[kTuneMax] = {};
     int tune_n = 0;                               // candidates timed by pipe_autotune
     int tune_grid[kTuneMax] = {};
     size_t tune_sub[kTuneMax] = {};
