@@ -467,7 +467,10 @@ def bench_nranks(args, L, rank, size):
               "candidates_max_over_ranks_us": [
                   {"grid": m.info(f"tune_grid_{k}"), "sub": m.info(f"tune_sub_{k}"),
                    "nt": m.info(f"tune_rnt_{k}"), "us": m.info(f"tune_us_{k}")}
-                  for k in range(m.info("tune_n"))]}
+                  for k in range(m.info("tune_n"))],
+              "oneshot_max_bytes": m.info("oneshot_max"),
+              "oneshot_vs_pipe_us": [{"bytes": (32 << 10) << i, "oneshot": m.info(f"os_tune_one_{i}"),
+                                      "pipe": m.info(f"os_tune_pipe_{i}")} for i in range(m.info("os_tune_n"))]}
     del sb, rb, rsb
     if args.rccl and m.info("nshare") > 1:
         extra["rccl_comparator"] = {"skipped": "ranks share one GPU: RCCL refuses several ranks on one device"}

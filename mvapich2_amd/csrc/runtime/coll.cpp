@@ -526,6 +526,8 @@ int coll_selftest() {
 // order is fixed per element by the plan.  Runs with one rank per GPU (xGMI) unless
 // MV2AMD_PIPE_AUTOTUNE=0, or on a shared GPU with MV2AMD_PIPE_AUTOTUNE=1; an explicit
 // MV2AMD_PIPE_GRID / MV2AMD_PIPE_SUB disables it.
+int oneshot_autotune();
+
 int pipe_autotune() {
     World &w = world();
     const char *ev = getenv("MV2AMD_PIPE_AUTOTUNE");
@@ -602,6 +604,65 @@ int pipe_autotune() {
     w.pipe_tuned = 1;
     MV2_DEBUG("pipe autotune: grid %d sub %zu %s stores (%.1f us of %d candidates)", w.pipe_grid, w.pipe_sub,
               w.pipe_rnt ? "non-temporal" : "plain", w.tune_us[pick], nc);
+    return oneshot_autotune();
+}
+
+// The one-shot kernel pushes a rank's whole operand to every peer (n-1 times the link bytes of
+// the pipelined kernel) but needs one flag exchange instead of two per round: where it stops
+// paying is again a property of the links.  Probe 32 KiB .. the arena slot with both kernels
+// (max over ranks) and keep the one-shot path up to the largest size it wins, scanning up.
+// The path never changes a result: both kernels evaluate the call's plan.
+int oneshot_autotune() {
+    World &w = world();
+    const int MPI_FLOAT_H = 0x4c00040a, MPI_SUM_H = 0x58000003;
+    const size_t top = w.oneshot_max < w.slot_bytes ? w.oneshot_max : w.slot_bytes;
+    void *sb = nullptr, *rb = nullptr;
+    if (top < ((size_t)32 << 10) || hipMalloc(&sb, top) != hipSuccess || hipMalloc(&rb, top) != hipSuccess) {
+        if (sb) hipFree(sb);
+        return 0;
+    }
+    hipMemset(sb, 0, top);
+    hipDeviceSynchronize();
+    const size_t keep = w.oneshot_max;
+    size_t sizes[kTuneMax / 2];
+    int ns = 0;
+    for (size_t b = (size_t)32 << 10; b <= top && ns < kTuneMax / 2; b <<= 1) sizes[ns++] = b;
+    int rc = 0;
+    for (int i = 0; i < ns && !rc; ++i) {
+        for (int path = 0; path < 2 && !rc; ++path) {  // 0: one-shot, 1: pipelined
+            w.oneshot_max = path ? 0 : keep;
+            double best = 1e30;
+            for (int it = 0; it < 6 && !rc; ++it) {
+                host_barrier();
+                const auto t0 = std::chrono::steady_clock::now();
+                rc = ::allreduce_entry(sb, rb, sizes[i] / 4, MPI_FLOAT_H, MPI_SUM_H, nullptr);
+                const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+                if (it) best = std::min(best, us);
+            }
+            w.shm->r[w.rank].tune_us[2 * i + path] = best;
+        }
+    }
+    hipFree(sb);
+    hipFree(rb);
+    w.oneshot_max = keep;
+    host_barrier();
+    if (rc) return rc;
+    size_t thr = 0;
+    for (int i = 0; i < ns; ++i) {
+        double one = 0, pipe = 0;
+        for (int j = 0; j < w.size; ++j) {
+            one = std::max(one, w.shm->r[j].tune_us[2 * i]);
+            pipe = std::max(pipe, w.shm->r[j].tune_us[2 * i + 1]);
+        }
+        w.os_tune_us[i][0] = one;
+        w.os_tune_us[i][1] = pipe;
+    }
+    for (int i = 0; i < ns && w.os_tune_us[i][0] <= w.os_tune_us[i][1]; ++i) thr = sizes[i];  // wins from the bottom
+    host_barrier();
+    w.os_tune_n = ns;
+    if (thr) w.oneshot_max = thr;  // below 32 KiB the one-shot kernel is kept
+    else w.oneshot_max = (size_t)16 << 10;
+    MV2_DEBUG("one-shot autotune: one-shot up to %zu bytes", w.oneshot_max);
     return 0;
 }
 
@@ -683,6 +744,12 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "pipe_tuned")) *value = w.pipe_tuned;
     else if (!strcmp(key, "tune_n")) *value = w.tune_n;
     else if (!strcmp(key, "pipe_rnt")) *value = w.pipe_rnt;
+    else if (!strcmp(key, "os_tune_n")) *value = w.os_tune_n;
+    else if (!strncmp(key, "os_tune_one_", 12) || !strncmp(key, "os_tune_pipe_", 13)) {
+        const long i = strtol(strrchr(key, '_') + 1, nullptr, 10);
+        if (i < 0 || i >= w.os_tune_n) return E_ARG;
+        *value = (long)(w.os_tune_us[i][key[8] == 'o' ? 0 : 1] + 0.5);
+    }
     else if (!strncmp(key, "tune_", 5) && strrchr(key, '_') && strrchr(key, '_')[1]) {
         // tune_grid_<k> / tune_sub_<k> / tune_rnt_<k> / tune_us_<k>: candidate k of pipe_autotune
         char *end = nullptr;

@@ -143,6 +143,8 @@ struct World {
     int pipe_tuned = 0;                           // 1: pipe_grid / pipe_sub chosen by pipe_autotune
     int pipe_rnt = 1;                             // stores into peers' arenas: 1 non-temporal, 0 plain
     int tune_rnt[kTuneMax] = {};
+    int os_tune_n = 0;                            // one-shot threshold probe: sizes 32 KiB << i
+    double os_tune_us[kTuneMax / 2][2] = {};      // [size][one-shot, pipelined], max over ranks
     int tune_n = 0;                               // candidates timed by pipe_autotune
     int tune_grid[kTuneMax] = {};
     size_t tune_sub[kTuneMax] = {};

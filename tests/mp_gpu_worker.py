@@ -273,7 +273,7 @@ def main():
         elif k == "enqueue_seq":  # stream-ordered collectives (MPIX_*_enqueue) mixed with a blocking call
             res = enqueue_seq(L, case, rank, n)
         elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)
-            keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n", "pipe_rnt"]
+            keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n", "pipe_rnt", "oneshot_max", "os_tune_n"]
             res = np.array([m.info(key) for key in keys], dtype=np.int64)
         elif k == "mpit_counts":  # MPI_T: start every counter, run the calls, read the counters
             prov = ctypes.c_int()

@@ -440,13 +440,18 @@ def test_pipe_autotune_agrees_and_keeps_results(n, tmp_path):
     rank pairs with workgroup b), and the calls after it stay bit-exact with the oracle (the
     tiling never changes the reduction order)."""
     cases = [{"id": "ti", "kind": "tiling_info"}]
+    # sizes around the one-shot threshold the probe picks (16 KiB .. 256 KiB): the path never
+    # changes a result
     for seed, (t, op, count) in enumerate((("MPI_FLOAT", "MPI_SUM", 1 << 21), ("MPI_DOUBLE", "MPI_SUM", 300007),
-                                           ("MPI_FLOAT", "MPI_SUM", 70001)), start=600):
+                                           ("MPI_FLOAT", "MPI_SUM", 70001), ("MPI_FLOAT", "MPI_SUM", 5000),
+                                           ("MPI_FLOAT", "MPI_SUM", 12000), ("MPI_DOUBLE", "MPI_MAX", 20000),
+                                           ("MPI_FLOAT", "MPI_SUM", 65536)), start=600):
         cases.append({"id": f"at{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
     res = run_workers(n, cases, tmp_path, extra_env={"MV2AMD_PIPE_AUTOTUNE": "1",
                                                      "MV2AMD_PIPE_AUTOTUNE_BYTES": str(16 << 20)})
     infos = [res("ti", r).view(np.int64) for r in range(n)]
-    assert infos[0][0] == 1 and infos[0][3] >= 1, infos[0]
+    assert infos[0][0] == 1 and infos[0][3] >= 1 and infos[0][6] >= 1, infos[0]
+    assert (16 << 10) <= infos[0][5] <= (256 << 10), infos[0]
     for r in range(1, n):
         assert np.array_equal(infos[r], infos[0]), (r, infos[r], infos[0])
     for case in cases[1:]:
