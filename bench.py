@@ -501,6 +501,9 @@ def bench_nranks(args, L, rank, size):
                    "latency_8B_us": round(lat_avg * 1e6, 2), "latency_8B_max_over_ranks_us": round(lat_s * 1e6, 2),
                    "latency_8B_kernel_us": round(lat_k_ms * 1e3, 2),
                    "allreduce_8B_stream_ordered_us_per_call": round(sq_s * 1e6, 2),
+                   **({"stream_ordered_note": "ranks share one GPU: each rank's queued kernels spin until the other "
+                       "processes' queues are scheduled (DESIGN.md §4 Stream order); not a one-GPU-per-rank figure"}
+                      if nshare > 1 else {}),
                    "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing",
                    "pipe_tiling": tiling},
         "roofline": ({"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
