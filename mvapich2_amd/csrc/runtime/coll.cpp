@@ -1236,7 +1236,10 @@ int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, 
     if (world().nnodes > 1) {
         if (world().enqueue) return mn_unsupported("a stream-ordered collective");
         MnBlocking nb;
-        return mn_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+        pvar_begin();
+        const int rc = mn_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+        pvar_end(rc == 0);
+        return rc;
     }
     pvar_begin();
     const int rc = allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream);
@@ -1306,7 +1309,10 @@ int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int
     if (world().nnodes > 1) {
         if (world().enqueue) return mn_unsupported("a stream-ordered collective");
         MnBlocking nb;
-        return mn_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
+        pvar_begin();
+        const int rc = mn_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
+        pvar_end(rc == 0);
+        return rc;
     }
     pvar_begin();
     const int rc = reduce_entry(sendbuf, recvbuf, count, dtype, op, root, stream);
@@ -1617,6 +1623,10 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     if (rc || count == 0) return rc;
     const DtypeInfo *dt = dtype_lookup(dtype);
     const size_t bytes = count * (size_t)dt->extent;
+    // MPI_T: MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) with the leaders' recursive
+    // doubling (MPIR_Allreduce_pt2pt_rd_MV2 :366); the node step's own plan is not counted
+    const int chain[2] = {PV_AR_2LVL, PV_AR_SHM_RD};
+    pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
     // node step: every rank of the node holds the node's partial
     if ((rc = allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream))) return rc;
     if (w.rank == 0) {
@@ -1655,6 +1665,9 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     const int rnode = root / w.size, rlocal = root % w.size;
     const bool me_root = w.grank == root;
     const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;  // IN_PLACE: at the root only
+    // MPI_T: MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2039) with the leaders' binomial (:450)
+    const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
+    pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
     if ((rc = mn_reserve(bytes))) return rc;
     // node step: the leader's partial lands in g_mn.d0 (a non-root's recvbuf is not significant)
     if ((rc = reduce_entry(src, w.rank == 0 ? g_mn.d0 : nullptr, count, dtype, op, 0, stream))) return rc;

@@ -135,6 +135,12 @@ void pvar_note_id(int id) {
     push(id);
 }
 
+void pvar_note_ids(const int *ids, int n) {
+    if (t_rec.depth != 1 || t_rec.noted || nbc_kind() != NBC_NONE) return;
+    t_rec.noted = true;
+    for (int i = 0; i < n; ++i) push(ids[i]);
+}
+
 void pvar_note(int coll, const Plan &p, bool in_place, size_t count, int n) {
     // nonblocking initiations run the MPI_I* schedules, whose mv2_coll_i* counters are not
     // among these variables

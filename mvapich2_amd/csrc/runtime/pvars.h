@@ -40,6 +40,7 @@ enum { PV_COLL_ALLREDUCE = 0, PV_COLL_REDUCE = 1, PV_COLL_REDUCE_SCATTER = 2 };
 void pvar_begin();
 void pvar_note(int coll, const Plan &p, bool in_place, size_t count, int n);
 void pvar_note_id(int id);
+void pvar_note_ids(const int *ids, int n);  // a whole chain; later notes in the call are ignored
 void pvar_end(bool ok);
 
 }  // namespace mv2

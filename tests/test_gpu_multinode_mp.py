@@ -129,3 +129,23 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
             want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
             for r in range(n):
                 assert np.array_equal(res(cid, r), want), (cid, r)
+
+
+@pytest.mark.timeout(200)
+def test_mpit_counts_across_nodes(tmp_path):
+    """MPI_T across nodes: Allreduce counts MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) and,
+    on the node leaders, the leaders' recursive doubling (pt2pt_rd :366); Reduce counts the
+    two-level helper (reduce_osu.c:2039) and the leaders' binomial (:450); Reduce_scatter across
+    nodes is not one of the reference's counted chains, so it counts nothing."""
+    import json
+    n, ppn = 4, 2
+    calls = [{"coll": "allreduce", "type": "MPI_FLOAT", "count": 300},
+             {"coll": "reduce", "type": "MPI_INT", "count": 1000, "root": n - 1},
+             {"coll": "reduce_scatter", "type": "MPI_FLOAT", "count": 100}]
+    res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path, ppn=ppn)
+    for r in range(n):
+        want = {"mv2_coll_allreduce_2lvl": 1, "mv2_coll_reduce_two_level_helper": 1}
+        if r % ppn == 0:
+            want.update({"mv2_coll_allreduce_shm_rd": 1, "mv2_coll_reduce_binomial": 1})
+        got = json.loads(res("mpit", r).tobytes().decode())
+        assert {k: v for k, v in got.items() if v} == want, (r, got)
