@@ -1743,13 +1743,12 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
     }
     if (total == 0) return 0;
     const size_t ext = (size_t)dt->extent;
-    char *tmp = nullptr;
-    if (hipMalloc((void **)&tmp, total * ext) != hipSuccess) return E_NO_MEM;
+    char *tmp = (char *)get_scratch(5, total * ext);
+    if (!tmp) return E_NO_MEM;
     const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;
-    rc = mn_allreduce(src, tmp, total, dtype, op, stream);
-    if (!rc && recvcounts[w.grank])
+    if ((rc = mn_allreduce(src, tmp, total, dtype, op, stream))) return rc;
+    if (recvcounts[w.grank])
         rc = hipMemcpy(recvbuf, tmp + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
-    hipFree(tmp);
     return rc;
 }
 

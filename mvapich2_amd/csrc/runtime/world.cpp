@@ -444,7 +444,7 @@ int world_finalize() {
         munmap(w.shm, sizeof(ShmSeg));
         w.shm = nullptr;
     }
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < (int)(sizeof(w.scratch) / sizeof(w.scratch[0])); ++i)
         if (w.scratch[i]) hipFree(w.scratch[i]);
     if (w.sig) hipFree(w.sig);
     if (w.arena) hipFree(w.arena);
