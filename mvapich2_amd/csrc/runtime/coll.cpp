@@ -1617,10 +1617,102 @@ static int mn_require_device_reduction(int dtype, int op) {
     return kind_supported(dt);
 }
 
-static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+// MPIR_Allreduce_index_tuned_intra_MV2's gates ahead of the tables (allreduce_osu.c:3155-3160) over
+// the whole job: the small-message shortcuts (:118-160) win, else the flat ring wrapper (:163-171)
+// when the message is large and ppn low.
+static bool mn_use_ring(long nbytes, size_t count, bool in_place) {
+    const World &w = world();
+    const Knobs &K = knobs();
+    if (K.allred_skip_small) {
+        if (nbytes <= K.topo_allred_max && nbytes >= K.topo_allred_min && K.enable_topo && K.use_topo_allreduce)
+            return false;  // topology-aware path or `goto use_tables`: no ring
+        if (K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr) return false;
+    }
+    // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise it
+    // runs pt2pt_rs over every rank, whose order is not restated across nodes (two-level instead)
+    return K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes && w.size <= K.allred_ring_ppn &&
+           !in_place && count >= (size_t)w.gsize;
+}
+
+static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
+
+// Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
+// chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
+// the accumulator always inout (uop(comp_chunk, recv_chunk), :3958).  Here each node gathers its
+// ranks' operands, and the node leaders pass partial chunks round the ring of nodes: group g (the
+// chunks of node g's ranks) starts at node g with the ranks from the chunk's own onwards, crosses
+// every other node whole, and ends at node g with the ranks before it.  Every uop is one device
+// Reduce_local.  The wrapper's remainder (count % n elements, pt2pt_rs over every rank, :3800-3818)
+// takes the two-level order.
+static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     World &w = world();
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const size_t ext = (size_t)dt->extent, S = count * ext;
+    const int L = w.size, K = w.nnodes, n = w.gsize;
+    const size_t cc = count / (size_t)n, cb = cc * ext, sect = (size_t)L * cb, main_bytes = (size_t)K * sect;
+    const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
+    pvar_note_ids(chain, count % (size_t)n ? 3 : 2);
+    char *G = (char *)get_scratch(6, (size_t)L * S);  // the node's operands, local rank order
+    if (!G) return E_NO_MEM;
+    int rc = allgather_node(sendbuf, G, S, stream);
+    if (rc) return rc;
+    if (w.rank == 0) {
+        if ((rc = mn_reserve(std::max(main_bytes, sect)))) return rc;
+        char *A = g_mn.d0;  // partial chunks of the group in hand
+        auto X = [&](int l, size_t byte_off) { return (const char *)G + (size_t)l * S + byte_off; };
+        const int me = w.node, right = (me + 1) % K, left = (me - 1 + K) % K;
+        // round 0: this node's group, from each chunk's own rank to the node's last
+        for (int l = 0; l < L; ++l) {
+            const size_t off = ((size_t)me * L + l) * cb;
+            if (hipMemcpy(A + (size_t)l * cb, X(l, off), cb, hipMemcpyDeviceToDevice) != hipSuccess) return E_INTERN;
+            for (int m = l + 1; m < L; ++m)
+                if ((rc = mv2h_reduce_local(X(m, off), A + (size_t)l * cb, cc, dtype, op, nullptr))) return rc;
+        }
+        for (int t = 1; t <= K; ++t) {
+            if ((rc = mn_d2h(g_mn.h0, A, sect)) || (rc = net_shift(right, g_mn.h0, sect, left, g_mn.h1, sect)) ||
+                (rc = mn_h2d(A, g_mn.h1, sect)))
+                return rc;
+            const int g = (me - t + K) % K;
+            if (t < K) {  // a whole node: its ranks in order, all of the group's chunks at once
+                for (int m = 0; m < L; ++m)
+                    if ((rc = mv2h_reduce_local(X(m, (size_t)g * sect), A, cc * (size_t)L, dtype, op, nullptr)))
+                        return rc;
+            } else {  // back home: the ranks before each chunk's own
+                for (int l = 0; l < L; ++l)
+                    for (int m = 0; m < l; ++m)
+                        if ((rc = mv2h_reduce_local(X(m, ((size_t)me * L + l) * cb), A + (size_t)l * cb, cc, dtype,
+                                                    op, nullptr)))
+                            return rc;
+            }
+        }
+        // allgather of the groups over the leaders (data movement only), then into recvbuf
+        if ((rc = mn_d2h(g_mn.h1 + (size_t)me * sect, A, sect))) return rc;
+        for (int k = 0; k < K - 1; ++k) {
+            const int so = (me - k + K) % K, ro = (me - k - 1 + K) % K;
+            if ((rc = net_shift(right, g_mn.h1 + (size_t)so * sect, sect, left, g_mn.h1 + (size_t)ro * sect, sect)))
+                return rc;
+        }
+        if ((rc = mn_h2d(recvbuf, g_mn.h1, main_bytes))) return rc;
+    }
+    if ((rc = bcast_node(recvbuf, main_bytes, 0, stream))) return rc;
+    if (count % (size_t)n == 0) return 0;
+    return mn_allreduce_2lvl((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
+                             dtype, op, stream);
+}
+
+static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     int rc = mn_require_device_reduction(dtype, op);
     if (rc || count == 0) return rc;
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const bool in_place = sendbuf == (const void *)-1;
+    if (mn_use_ring((long)(count * (size_t)dt->size), count, in_place))
+        return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+    return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
+}
+
+static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    World &w = world();
+    int rc = 0;
     const DtypeInfo *dt = dtype_lookup(dtype);
     const size_t bytes = count * (size_t)dt->extent;
     // MPI_T: MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) with the leaders' recursive

@@ -167,8 +167,8 @@ struct World {
     double last_ms = 0.0;
 
     // scratch device buffers (host-buffer staging, misalignment, Reduce non-roots)
-    void *scratch[6] = {};  // 5: multi-node Reduce_scatter's whole-operand result
-    size_t scratch_bytes[6] = {};
+    void *scratch[7] = {};  // 5: multi-node Reduce_scatter's result, 6: multi-node ring's node operands
+    size_t scratch_bytes[7] = {};
 };
 
 World &world();

@@ -62,6 +62,29 @@ def binomial_leaders(parts, count, t, op, root):
     return acc[0]
 
 
+def ring_flat(sends, count, t, op):
+    """MPIR_Allreduce_pt2pt_ring_MV2 over every rank of the job (allreduce_osu.c:3916-3968): chunk c
+    = x_c (+) x_{c+1} (+) ... (+) x_{c-1}, the accumulator inout (uop(comp_chunk, recv_chunk))"""
+    n = len(sends)
+    cc = count // n
+    cb = cc * TYPES[t][3]
+    out = np.empty(n * cb, dtype=np.uint8)
+    for c in range(n):
+        acc = sends[c][c * cb:(c + 1) * cb].copy()
+        for j in range(1, n):
+            acc = uop(sends[(c + j) % n][c * cb:(c + 1) * cb].copy(), acc, cc, t, op)
+        out[c * cb:(c + 1) * cb] = acc
+    return out
+
+
+def two_level(sends, count, t, op, ppn):
+    """node allreduce (the oracle's one-node algorithm), recursive doubling over the leaders"""
+    nodes = len(sends) // ppn
+    parts = [oracle.allreduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0], OPS[op])[0]
+             for j in range(nodes)]
+    return rd_leaders(parts, count, t, op)
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("n,ppn", [(4, 2), (6, 2), (3, 1), (8, 4)])
 def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
@@ -71,6 +94,12 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                          ("MPI_FLOAT", "MPI_SUM", 70001), ("MPI_INT", "MPI_SUM", 100003),
                          ("MPI_DOUBLE_INT", "MPI_MAXLOC", 5000), ("MPI_UNSIGNED_CHAR", "MPI_BXOR", 4099)):
         cases.append({"id": f"ma{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
+        seed += 1
+    # from 2 MiB (MV2_ALLREDUCE_RING_ALGO_THRESHOLD) the flat ring over every rank; the remainder
+    # (count % n elements) takes the two-level order
+    for t, op, count in (("MPI_FLOAT", "MPI_SUM", 840 * 1000), ("MPI_FLOAT", "MPI_SUM", 840 * 1000 + 5),
+                         ("MPI_DOUBLE", "MPI_SUM", 300001)):
+        cases.append({"id": f"mR{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
         seed += 1
     # nonblocking across nodes: complete at initiation (integer data: exact in any order)
     cases.append({"id": f"mi{seed}", "kind": "iallreduce", "type": "MPI_INT", "op": "MPI_SUM", "count": 5000,
@@ -98,10 +127,15 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        if k in ("allreduce", "iallreduce"):
-            parts = [oracle.allreduce_ref(sends[j * ppn:(j + 1) * ppn], count, TYPES[t][0], OPS[case["op"]])[0]
-                     for j in range(nodes)]
-            want = rd_leaders(parts, count, t, case["op"])
+        if k == "allreduce" and count * TYPES[t][2] >= 2 << 20:
+            main = ring_flat(sends, count, t, case["op"])
+            rem = count % n
+            tail = two_level([x[len(main):] for x in sends], rem, t, case["op"], ppn) if rem else None
+            for r in range(n):
+                want = np.concatenate([main, tail[r // ppn]]) if rem else main
+                assert_bytes_equal(res(cid, r), want, t, count, f"{cid} ring {t} {case['op']} rank {r}")
+        elif k in ("allreduce", "iallreduce"):
+            want = two_level(sends, count, t, case["op"], ppn)
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r // ppn], t, count, f"{cid} {t} {case['op']} rank {r}")
         elif k == "reduce":
@@ -135,16 +169,19 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
 def test_mpit_counts_across_nodes(tmp_path):
     """MPI_T across nodes: Allreduce counts MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) and,
     on the node leaders, the leaders' recursive doubling (pt2pt_rd :366); Reduce counts the
-    two-level helper (reduce_osu.c:2039) and the leaders' binomial (:450); Reduce_scatter across
-    nodes is not one of the reference's counted chains, so it counts nothing."""
+    two-level helper (reduce_osu.c:2039) and the leaders' binomial (:450); a 2.4 MB Allreduce the
+    flat ring wrapper and ring (:3761, :3898); Reduce_scatter across nodes is not one of the
+    reference's counted chains, so it counts nothing."""
     import json
     n, ppn = 4, 2
     calls = [{"coll": "allreduce", "type": "MPI_FLOAT", "count": 300},
              {"coll": "reduce", "type": "MPI_INT", "count": 1000, "root": n - 1},
-             {"coll": "reduce_scatter", "type": "MPI_FLOAT", "count": 100}]
+             {"coll": "reduce_scatter", "type": "MPI_FLOAT", "count": 100},
+             {"coll": "allreduce", "type": "MPI_FLOAT", "count": 600000}]  # the flat ring (wrapper, :3761)
     res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path, ppn=ppn)
     for r in range(n):
-        want = {"mv2_coll_allreduce_2lvl": 1, "mv2_coll_reduce_two_level_helper": 1}
+        want = {"mv2_coll_allreduce_2lvl": 1, "mv2_coll_reduce_two_level_helper": 1,
+                "mv2_coll_allreduce_pt2pt_ring_wrapper": 1, "mv2_coll_allreduce_pt2pt_ring": 1}
         if r % ppn == 0:
             want.update({"mv2_coll_allreduce_shm_rd": 1, "mv2_coll_reduce_binomial": 1})
         got = json.loads(res("mpit", r).tobytes().decode())
