@@ -1635,6 +1635,7 @@ static bool mn_use_ring(long nbytes, size_t count, bool in_place) {
 }
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
+static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
 
 // Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
 // chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
@@ -1643,7 +1644,7 @@ static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, i
 // chunks of node g's ranks) starts at node g with the ranks from the chunk's own onwards, crosses
 // every other node whole, and ends at node g with the ranks before it.  Every uop is one device
 // Reduce_local.  The wrapper's remainder (count % n elements, pt2pt_rs over every rank, :3800-3818)
-// takes the two-level order.
+// is that flat algorithm for jobs of up to kMaxRanks ranks, else the two-level order.
 static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     World &w = world();
     const DtypeInfo *dt = dtype_lookup(dtype);
@@ -1696,8 +1697,61 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     }
     if ((rc = bcast_node(recvbuf, main_bytes, 0, stream))) return rc;
     if (count % (size_t)n == 0) return 0;
+    if (n <= kMaxRanks)  // the wrapper's pt2pt_rs over every rank (recursive doubling: rem < n)
+        return mn_flat_allreduce((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
+                                 dtype, op, stream);
     return mn_allreduce_2lvl((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
                              dtype, op, stream);
+}
+
+// The tuning tables (allreduce_osu.c:3162-3373) between the shortcuts and the ring.  From 3 ranks
+// per node MVAPICH2 reads its 16-ppn table, whose first entry (numproc 16) serves every job of up
+// to 16 ranks — the entry the one-node selection reads for `size` ranks — so that plan decides:
+// where it names pt2pt_rs / pt2pt_rd the job runs MPIR_Allreduce_pt2pt_rs_MV2 flat over every
+// rank (is_two_level 0).  Restated for jobs of up to kMaxRanks ranks (the program evaluator's
+// operand limit); the 2-ppn and 1-ppn tables' multi-node entries are not restated (two-level).
+static bool mn_use_flat(size_t count, const DtypeInfo *dt, bool in_place) {
+    const World &w = world();
+    if (w.size < 3 || w.gsize > kMaxRanks) return false;
+    Plan p;
+    if (plan_allreduce(w.size, w.rank, count, dt->size, dt->extent, in_place, 0, &p)) return false;
+    return p.algo == ALG_PT2PT_RS || p.algo == ALG_PT2PT_RD;
+}
+
+// Flat pt2pt_rs over every rank (allreduce_osu.c:633-1054): every rank's operand reaches every rank
+// (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
+// evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
+// differ between ranks where the op is not commutative in its bits (MAX/MIN ties of ±0, NaN
+// payloads), as the reference's do.
+static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+    World &w = world();
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const bool in_place = sendbuf == (const void *)-1;
+    const size_t S = count * (size_t)dt->extent, sect = (size_t)w.size * S;
+    const int n = w.gsize, K = w.nnodes;
+    Plan p;
+    int rc = plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, ALG_PT2PT_RS, &p);
+    if (rc) return rc;
+    pvar_note(PV_COLL_ALLREDUCE, p, in_place, count, n);
+    char *W = (char *)get_scratch(6, (size_t)n * S);  // every rank's operand, global rank order
+    if (!W || (rc = mn_reserve((size_t)n * S))) return rc ? rc : E_NO_MEM;
+    if ((rc = allgather_node(in_place ? recvbuf : sendbuf, W + (size_t)w.node * sect, S, stream))) return rc;
+    if (w.rank == 0) {
+        const int me = w.node, right = (me + 1) % K, left = (me - 1 + K) % K;
+        if ((rc = mn_d2h(g_mn.h0 + (size_t)me * sect, W + (size_t)me * sect, sect))) return rc;
+        for (int k = 0; k < K - 1; ++k) {
+            const int so = (me - k + K) % K, ro = (me - k - 1 + K) % K;
+            if ((rc = net_shift(right, g_mn.h0 + (size_t)so * sect, sect, left, g_mn.h0 + (size_t)ro * sect, sect)))
+                return rc;
+        }
+        if ((rc = mn_h2d(W, g_mn.h0, (size_t)n * S))) return rc;
+    }
+    if ((rc = bcast_node(W, (size_t)n * S, 0, stream))) return rc;
+    const void *srcs[kMaxRanks];
+    for (int r = 0; r < n; ++r) srcs[r] = W + (size_t)r * S;
+    if ((rc = mv2h_reduce_n_prog(srcs, n, g_mn.d1, count, dtype, op, (const mv2h_progset *)&p.ps, nullptr)))
+        return rc;
+    return hipMemcpy(recvbuf, g_mn.d1, S, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
 }
 
 static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
@@ -1707,6 +1761,7 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     const bool in_place = sendbuf == (const void *)-1;
     if (mn_use_ring((long)(count * (size_t)dt->size), count, in_place))
         return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+    if (mn_use_flat(count, dt, in_place)) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
     return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
 }
 

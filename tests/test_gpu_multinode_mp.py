@@ -4,9 +4,10 @@ TCP (runtime/internode.cpp).  Results are checked bit-exactly against a restatem
 MVAPICH2's two-level structure built from the oracle: node step = the oracle's one-node
 algorithm for the node's ranks, inter-node step = recursive doubling (allreduce, the inter step
 of MPIR_Allreduce_two_level_MV2 / topo-aware hierarchical, allreduce_osu.c:360-630, :2215) or
-binomial reduce (reduce_osu.c:425) over the node leaders, every uop an oracle op-loop call;
-reduce-scatter is the two-level allreduce's block (the reference's flat algorithms are not
-restated across nodes)."""
+binomial reduce (reduce_osu.c:425) over the node leaders, every uop an oracle op-loop call.
+Allreduce from 2 MiB is the flat ring over every rank, and where the 16-ppn table names it the
+flat pt2pt_rs over every rank (expected_allreduce); reduce-scatter is the allreduce's block (the
+reference's flat reduce-scatter algorithms are not restated across nodes)."""
 import numpy as np
 import pytest
 
@@ -77,6 +78,26 @@ def ring_flat(sends, count, t, op):
     return out
 
 
+def expected_allreduce(sends, count, t, op, ppn):
+    """per-rank results of MPI_Allreduce across nodes, by the selection coll.cpp mn_allreduce
+    restates: flat ring from 2 MiB (remainder: flat pt2pt_rs over every rank for n <= 8), the flat
+    pt2pt_rs where the 16-ppn table names it (ppn >= 3, n <= 8), else two-level"""
+    n = len(sends)
+    if count * TYPES[t][2] >= 2 << 20 and count >= n:
+        main = ring_flat(sends, count, t, op)
+        rem = count % n
+        if not rem:
+            return [main] * n
+        tails = [x[len(main):].copy() for x in sends]
+        tail = oracle.allreduce(tails, rem, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index("pt2pt_rs")) if n <= 8 \
+            else [x for x in two_level(tails, rem, t, op, ppn) for _ in range(ppn)]
+        return [np.concatenate([main, tail[r]]) for r in range(n)]
+    if ppn >= 3 and n <= 8 and oracle.ALGOS[oracle.allreduce_select(ppn, count, TYPES[t][0])] in ("pt2pt_rs",
+                                                                                                   "pt2pt_rd"):
+        return oracle.allreduce_ref([x.copy() for x in sends], count, TYPES[t][0], OPS[op])
+    return [x for x in two_level(sends, count, t, op, ppn) for _ in range(ppn)]
+
+
 def two_level(sends, count, t, op, ppn):
     """node allreduce (the oracle's one-node algorithm), recursive doubling over the leaders"""
     nodes = len(sends) // ppn
@@ -86,7 +107,7 @@ def two_level(sends, count, t, op, ppn):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 2), (3, 1), (8, 4)])
+@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 2), (3, 1), (8, 4), (6, 3)])
 def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     nodes = n // ppn
     cases, seed = [], 300
@@ -127,32 +148,23 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        if k == "allreduce" and count * TYPES[t][2] >= 2 << 20:
-            main = ring_flat(sends, count, t, case["op"])
-            rem = count % n
-            tail = two_level([x[len(main):] for x in sends], rem, t, case["op"], ppn) if rem else None
+        if k in ("allreduce", "iallreduce"):
+            want = expected_allreduce(sends, count, t, case["op"], ppn)
             for r in range(n):
-                want = np.concatenate([main, tail[r // ppn]]) if rem else main
-                assert_bytes_equal(res(cid, r), want, t, count, f"{cid} ring {t} {case['op']} rank {r}")
-        elif k in ("allreduce", "iallreduce"):
-            want = two_level(sends, count, t, case["op"], ppn)
-            for r in range(n):
-                assert_bytes_equal(res(cid, r), want[r // ppn], t, count, f"{cid} {t} {case['op']} rank {r}")
+                assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
         elif k == "reduce":
             rnode = case["root"] // ppn
             parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0],
                                        OPS[case["op"]], 0) for j in range(nodes)]
             want = binomial_leaders(parts, count, t, case["op"], rnode)
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
-        elif k == "reduce_scatter":  # two-level allreduce of the whole operand, then the block
+        elif k == "reduce_scatter":  # the allreduce of the whole operand, then the block
             counts = case["recvcounts"]
-            parts = [oracle.allreduce_ref(sends[j * ppn:(j + 1) * ppn], count, TYPES[t][0], OPS[case["op"]])[0]
-                     for j in range(nodes)]
-            full = rd_leaders(parts, count, t, case["op"])
+            full = expected_allreduce(sends, count, t, case["op"], ppn)
             ext = TYPES[t][3]
             off = 0
             for r in range(n):
-                blk = full[r // ppn][off * ext:(off + counts[r]) * ext]
+                blk = full[r][off * ext:(off + counts[r]) * ext]
                 assert_bytes_equal(res(cid, r), blk, t, counts[r], f"{cid} reduce_scatter rank {r}")
                 off += counts[r]
         elif k == "bcast":
