@@ -1620,7 +1620,7 @@ static int mn_require_device_reduction(int dtype, int op) {
 // MPIR_Allreduce_index_tuned_intra_MV2's gates ahead of the tables (allreduce_osu.c:3155-3160) over
 // the whole job: the small-message shortcuts (:118-160) win, else the flat ring wrapper (:163-171)
 // when the message is large and ppn low.
-static bool mn_use_ring(long nbytes, size_t count, bool in_place) {
+static bool mn_use_ring(long nbytes) {
     const World &w = world();
     const Knobs &K = knobs();
     if (K.allred_skip_small) {
@@ -1628,10 +1628,7 @@ static bool mn_use_ring(long nbytes, size_t count, bool in_place) {
             return false;  // topology-aware path or `goto use_tables`: no ring
         if (K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr) return false;
     }
-    // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise it
-    // runs pt2pt_rs over every rank, whose order is not restated across nodes (two-level instead)
-    return K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes && w.size <= K.allred_ring_ppn &&
-           !in_place && count >= (size_t)w.gsize;
+    return K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes && w.size <= K.allred_ring_ppn;
 }
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
@@ -1759,8 +1756,16 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     if (rc || count == 0) return rc;
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
-    if (mn_use_ring((long)(count * (size_t)dt->size), count, in_place))
-        return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+    if (mn_use_ring((long)(count * (size_t)dt->size))) {
+        // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise
+        // it runs pt2pt_rs over every rank (restated up to kMaxRanks ranks, else two-level)
+        if (!in_place && count >= (size_t)world().gsize)
+            return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+        const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
+        pvar_note_ids(chain, 2);
+        if (world().gsize <= kMaxRanks) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+        return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
+    }
     if (mn_use_flat(count, dt, in_place)) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
     return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
 }

@@ -78,12 +78,15 @@ def ring_flat(sends, count, t, op):
     return out
 
 
-def expected_allreduce(sends, count, t, op, ppn):
+def expected_allreduce(sends, count, t, op, ppn, in_place=False):
     """per-rank results of MPI_Allreduce across nodes, by the selection coll.cpp mn_allreduce
     restates: flat ring from 2 MiB (remainder: flat pt2pt_rs over every rank for n <= 8), the flat
     pt2pt_rs where the 16-ppn table names it (ppn >= 3, n <= 8), else two-level"""
     n = len(sends)
-    if count * TYPES[t][2] >= 2 << 20 and count >= n:
+    if count * TYPES[t][2] >= 2 << 20 and (in_place or count < n) and n <= 8:  # the wrapper's pt2pt_rs
+        return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op],
+                                algo=oracle.ALGOS.index("pt2pt_rs"))
+    if count * TYPES[t][2] >= 2 << 20 and count >= n and not in_place:
         main = ring_flat(sends, count, t, op)
         rem = count % n
         if not rem:
@@ -92,9 +95,9 @@ def expected_allreduce(sends, count, t, op, ppn):
         tail = oracle.allreduce(tails, rem, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index("pt2pt_rs")) if n <= 8 \
             else [x for x in two_level(tails, rem, t, op, ppn) for _ in range(ppn)]
         return [np.concatenate([main, tail[r]]) for r in range(n)]
-    if ppn >= 3 and n <= 8 and oracle.ALGOS[oracle.allreduce_select(ppn, count, TYPES[t][0])] in ("pt2pt_rs",
-                                                                                                   "pt2pt_rd"):
-        return oracle.allreduce_ref([x.copy() for x in sends], count, TYPES[t][0], OPS[op])
+    if ppn >= 3 and n <= 8 and oracle.ALGOS[oracle.allreduce_select(ppn, count, TYPES[t][0], in_place)] in (
+            "pt2pt_rs", "pt2pt_rd"):
+        return oracle.allreduce_ref([x.copy() for x in sends], count, TYPES[t][0], OPS[op], in_place=in_place)
     return [x for x in two_level(sends, count, t, op, ppn) for _ in range(ppn)]
 
 
@@ -122,6 +125,10 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                          ("MPI_DOUBLE", "MPI_SUM", 300001)):
         cases.append({"id": f"mR{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
         seed += 1
+    for count in (600000, 70001):  # IN_PLACE: from 2 MiB the wrapper's pt2pt_rs over every rank
+        cases.append({"id": f"mP{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
+                      "count": count, "seed": seed})
+        seed += 1
     # nonblocking across nodes: complete at initiation (integer data: exact in any order)
     cases.append({"id": f"mi{seed}", "kind": "iallreduce", "type": "MPI_INT", "op": "MPI_SUM", "count": 5000,
                   "seed": seed})
@@ -148,8 +155,8 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        if k in ("allreduce", "iallreduce"):
-            want = expected_allreduce(sends, count, t, case["op"], ppn)
+        if k in ("allreduce", "iallreduce", "allreduce_inplace"):
+            want = expected_allreduce(sends, count, t, case["op"], ppn, in_place=k == "allreduce_inplace")
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
         elif k == "reduce":
