@@ -1617,22 +1617,31 @@ static int mn_require_device_reduction(int dtype, int op) {
     return kind_supported(dt);
 }
 
-// MPIR_Allreduce_index_tuned_intra_MV2's gates ahead of the tables (allreduce_osu.c:3155-3160) over
-// the whole job: the small-message shortcuts (:118-160) win, else the flat ring wrapper (:163-171)
-// when the message is large and ppn low.
-static bool mn_use_ring(long nbytes) {
+// MPIR_Allreduce_index_tuned_intra_MV2's selection (allreduce_osu.c:3015-3373) over the whole job.
+// Returns 0 (two-level), 1 (flat ring wrapper), or ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every
+// rank).  The small-message shortcuts (:118-160) keep the two-level structure; the skip-large gate
+// (:163-171) takes the ring wrapper; then the tuning tables (orders.cpp mn_allreduce_table).
+static int mn_select(long nbytes) {
     const World &w = world();
     const Knobs &K = knobs();
+    bool tables = false;
     if (K.allred_skip_small) {
-        if (nbytes <= K.topo_allred_max && nbytes >= K.topo_allred_min && K.enable_topo && K.use_topo_allreduce)
-            return false;  // topology-aware path or `goto use_tables`: no ring
-        if (K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr) return false;
+        if (nbytes <= K.topo_allred_max && nbytes >= K.topo_allred_min && K.enable_topo && K.use_topo_allreduce) {
+            if (w.size >= K.topo_allred_ppn) return 0;  // topology-aware hierarchical
+            tables = true;                              // goto use_tables
+        }
+        if (!tables && K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr) return 0;
     }
-    return K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes && w.size <= K.allred_ring_ppn;
+    if (!tables && K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes &&
+        w.size <= K.allred_ring_ppn)
+        return 1;
+    const int t = mn_allreduce_table(w.size, w.gsize, nbytes);
+    return t > 0 && w.gsize <= kMaxRanks ? t : 0;  // flat programs: up to kMaxRanks operands
 }
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
-static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
+static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                             int algo);
 
 // Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
 // chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
@@ -1696,38 +1705,25 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     if (count % (size_t)n == 0) return 0;
     if (n <= kMaxRanks)  // the wrapper's pt2pt_rs over every rank (recursive doubling: rem < n)
         return mn_flat_allreduce((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
-                                 dtype, op, stream);
+                                 dtype, op, stream, ALG_PT2PT_RS);
     return mn_allreduce_2lvl((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
                              dtype, op, stream);
 }
 
-// The tuning tables (allreduce_osu.c:3162-3373) between the shortcuts and the ring.  From 3 ranks
-// per node MVAPICH2 reads its 16-ppn table, whose first entry (numproc 16) serves every job of up
-// to 16 ranks — the entry the one-node selection reads for `size` ranks — so that plan decides:
-// where it names pt2pt_rs / pt2pt_rd the job runs MPIR_Allreduce_pt2pt_rs_MV2 flat over every
-// rank (is_two_level 0).  Restated for jobs of up to kMaxRanks ranks (the program evaluator's
-// operand limit); the 2-ppn and 1-ppn tables' multi-node entries are not restated (two-level).
-static bool mn_use_flat(size_t count, const DtypeInfo *dt, bool in_place) {
-    const World &w = world();
-    if (w.size < 3 || w.gsize > kMaxRanks) return false;
-    Plan p;
-    if (plan_allreduce(w.size, w.rank, count, dt->size, dt->extent, in_place, 0, &p)) return false;
-    return p.algo == ALG_PT2PT_RS || p.algo == ALG_PT2PT_RD;
-}
-
-// Flat pt2pt_rs over every rank (allreduce_osu.c:633-1054): every rank's operand reaches every rank
+// Flat pt2pt_rs / pt2pt_rd over every rank (allreduce_osu.c:633-1054, :360-630): every rank's operand reaches every rank
 // (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
 // evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
 // differ between ranks where the op is not commutative in its bits (MAX/MIN ties of ±0, NaN
 // payloads), as the reference's do.
-static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                             int algo) {
     World &w = world();
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
     const size_t S = count * (size_t)dt->extent, sect = (size_t)w.size * S;
     const int n = w.gsize, K = w.nnodes;
     Plan p;
-    int rc = plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, ALG_PT2PT_RS, &p);
+    int rc = plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
     if (rc) return rc;
     pvar_note(PV_COLL_ALLREDUCE, p, in_place, count, n);
     char *W = (char *)get_scratch(6, (size_t)n * S);  // every rank's operand, global rank order
@@ -1756,17 +1752,20 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     if (rc || count == 0) return rc;
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
-    if (mn_use_ring((long)(count * (size_t)dt->size))) {
+    const int sel = mn_select((long)(count * (size_t)dt->size));
+    if (sel == 1) {
         // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise
         // it runs pt2pt_rs over every rank (restated up to kMaxRanks ranks, else two-level)
         if (!in_place && count >= (size_t)world().gsize)
             return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
         const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
         pvar_note_ids(chain, 2);
-        if (world().gsize <= kMaxRanks) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+        if (world().gsize <= kMaxRanks)
+            return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, ALG_PT2PT_RS);
         return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
     }
-    if (mn_use_flat(count, dt, in_place)) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
+    if (sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD)
+        return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, sel);
     return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
 }
 

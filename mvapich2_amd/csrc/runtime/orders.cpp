@@ -666,6 +666,44 @@ static int plan_allreduce_build(int n, int me, size_t count, int tsize, int text
     return allreduce_fill(p, e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS, n, me, count, opk);
 }
 
+// Several nodes: the tuning-table step of MPIR_Allreduce_index_tuned_intra_MV2 (:3162-3290) for
+// `ppn` ranks per node and `gsize` ranks in all.  The 16-ppn table (ppn >= 3) is restated by its
+// first entry (numproc 16: jobs up to 16 ranks); the 2-ppn and 1-ppn tables
+// (nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{2,1}ppn.h) by their numproc 2 / 4 / 8 entries (jobs up
+// to 8 ranks; comm_size_index :3210-3228 over minimum numproc 2).  Returns 0 (is_two_level),
+// ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every rank), or -1 (entry not restated).  The multicast
+// entries fall back to recursive doubling (:3324-3338).
+int mn_allreduce_table(int ppn, int gsize, long nbytes) {
+    const int idx = table_index(nbytes, 1, 18);
+    if (ppn_conf(ppn) == 2) {
+        if (gsize > 16) return -1;
+        return kAr16.two_level[idx] ? 0 : (kAr16.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS);
+    }
+    if (gsize < 2 || gsize > 8) return -1;
+    int ci = 0;  // comm_size_index: log2(floor_pof2(gsize) / 2)
+    for (int v = gsize / 2; v > 1; v >>= 1) ++ci;
+    struct Entry {
+        int two_level[18];
+        int inter[18];
+    };
+    static const Entry k2ppn[3] = {
+        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0},
+         {A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS}},
+        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0},
+         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}},
+        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0},
+         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS}}};
+    static const Entry k1ppn[3] = {
+        {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RD, A_RS, A_RS, A_RS}},
+        {{0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},  // idx 1: multicast -> RD, two-level
+         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}},
+        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 0, 0},
+         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}}};
+    const Entry &e = ppn_conf(ppn) == 1 ? k2ppn[ci] : k1ppn[ci];
+    return e.two_level[idx] ? 0 : (e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS);
+}
+
 // ---------------------------------------------------------------------------
 // MPI_Reduce_scatter (commutative ops; red_scat_osu.c:1859-1896)
 // ---------------------------------------------------------------------------

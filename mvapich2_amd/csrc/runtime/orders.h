@@ -106,6 +106,8 @@ enum OpKind : int { OPK_BUILTIN = 0, OPK_USER_COMM = 1, OPK_USER_NONCOMM = 2 };
 // reference's selection, else an Algo to run (ring wrapper parts).
 int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *out,
                    int opk = OPK_BUILTIN);
+// several nodes: the allreduce tuning-table choice (0 two-level, ALG_PT2PT_RS / _RD flat, -1 unknown)
+int mn_allreduce_table(int ppn, int gsize, long nbytes);
 int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *out, int opk = OPK_BUILTIN);
 // counts[n] per-rank block counts; elements are indexed over the whole operand
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *out,

@@ -48,12 +48,16 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None):
         so = socket.socket()
         so.bind(("127.0.0.1", 0))
         boot = {"MV2AMD_BOOT_ADDR": "127.0.0.1", "MV2AMD_BOOT_PORT": str(so.getsockname()[1]),
-                "MV2AMD_NSHARE": str(n)}  # every emulated node's ranks share the one GPU
+                "MV2AMD_NSHARE": str(n),  # every emulated node's ranks share the one GPU
+                # emulated nodes oversubscribe the one GPU's queues: a slow box can stall a node's
+                # step for tens of seconds while another node's leader waits on its socket
+                "MV2AMD_TIMEOUT_S": "90"}
+        timeout = max(timeout, 240)
         so.close()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r % ppn), LOCAL_WORLD_SIZE=str(ppn),
-                   MV2AMD_JOBID=jobid, MV2AMD_TIMEOUT_S="30", **boot, **(extra_env or {}))
+                   MV2AMD_JOBID=jobid, **{"MV2AMD_TIMEOUT_S": "30", **boot}, **(extra_env or {}))
         env.pop("MV2AMD_DEVICE", None)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), str(spec),
                                        str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))

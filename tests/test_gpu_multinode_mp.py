@@ -78,6 +78,32 @@ def ring_flat(sends, count, t, op):
     return out
 
 
+# multi-node entries of the default allreduce tables (allreduce_tuning.c fall-back,
+# tuning/allreduce/nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{2,1}ppn.h), numproc 2 / 4 / 8: per
+# message-size index, 0 = two-level, else the flat inter-leader function (multicast -> rd)
+_T2 = ["rd rd rd rs rs rs rd rd rd rd rs rs | rs rs rs rs rs rs",
+       "rd rd rd rd rd rd rd rd rd rd rd rd rd | rs rs rs rs rs",
+       "rs rd rd rd rd rd rd rd rd rd rd rd | rs rs rs rs rs rs"]
+_T1 = ["| rd rd rd rd rd rd rd rd rd rd rd rd rd rs rd rs rs rs",
+       "rs | rd . rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs",
+       "rs rd rd rd rd rd rd rd rd rd rd | rd rd . . rs rs rs"]
+
+
+def table_flat(ppn, n, nbytes):
+    """None (two-level) or the flat algorithm MVAPICH2's tables pick across nodes"""
+    idx = min(17, max(0, nbytes.bit_length() - 1))
+    if ppn >= 3:  # 16-ppn table, first entry: the one-node selection for ppn ranks reads it too
+        a = oracle.ALGOS[oracle.allreduce_select(ppn, max(1, nbytes // 4), TYPES["MPI_FLOAT"][0])]
+        return a if a in ("pt2pt_rs", "pt2pt_rd") else None
+    ci = (n // 2).bit_length() - 1
+    row = (_T2 if ppn == 2 else _T1)[ci]
+    # "|" splits the two-level prefix from the flat suffix, "." marks further two-level entries
+    head, tail = row.split("|")
+    cells = [("2l", c) for c in head.split()] + [("flat", c) for c in tail.split()]
+    kind, fn = cells[idx]
+    return None if kind == "2l" or fn == "." else "pt2pt_" + fn
+
+
 def expected_allreduce(sends, count, t, op, ppn, in_place=False):
     """per-rank results of MPI_Allreduce across nodes, by the selection coll.cpp mn_allreduce
     restates: flat ring from 2 MiB (remainder: flat pt2pt_rs over every rank for n <= 8), the flat
@@ -95,9 +121,11 @@ def expected_allreduce(sends, count, t, op, ppn, in_place=False):
         tail = oracle.allreduce(tails, rem, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index("pt2pt_rs")) if n <= 8 \
             else [x for x in two_level(tails, rem, t, op, ppn) for _ in range(ppn)]
         return [np.concatenate([main, tail[r]]) for r in range(n)]
-    if ppn >= 3 and n <= 8 and oracle.ALGOS[oracle.allreduce_select(ppn, count, TYPES[t][0], in_place)] in (
-            "pt2pt_rs", "pt2pt_rd"):
-        return oracle.allreduce_ref([x.copy() for x in sends], count, TYPES[t][0], OPS[op], in_place=in_place)
+    nbytes = count * TYPES[t][2]
+    flat = table_flat(ppn, n, nbytes) if nbytes > 2048 and n <= 8 else None  # topo-aware up to 2 KiB
+    if flat:
+        return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op],
+                                algo=oracle.ALGOS.index(flat))
     return [x for x in two_level(sends, count, t, op, ppn) for _ in range(ppn)]
 
 
