@@ -701,7 +701,10 @@ int mn_allreduce_table(int ppn, int gsize, long nbytes) {
         {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 0, 0},
          {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}}};
     const Entry &e = ppn_conf(ppn) == 1 ? k2ppn[ci] : k1ppn[ci];
-    return e.two_level[idx] ? 0 : (e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS);
+    // one rank per node: the two-level algorithm is its leaders' algorithm over every rank
+    // (MPIR_Allreduce_two_level_MV2 :1750-1780 with nothing to reduce or broadcast in a node)
+    if (e.two_level[idx] && ppn > 1) return 0;
+    return e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
 }
 
 // ---------------------------------------------------------------------------

@@ -84,9 +84,10 @@ def ring_flat(sends, count, t, op):
 _T2 = ["rd rd rd rs rs rs rd rd rd rd rs rs | rs rs rs rs rs rs",
        "rd rd rd rd rd rd rd rd rd rd rd rd rd | rs rs rs rs rs",
        "rs rd rd rd rd rd rd rd rd rd rd rd | rs rs rs rs rs rs"]
+# 1 ppn: a two-level entry is its leaders' function over every rank, so every cell is flat
 _T1 = ["| rd rd rd rd rd rd rd rd rd rd rd rd rd rs rd rs rs rs",
-       "rs | rd . rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs",
-       "rs rd rd rd rd rd rd rd rd rd rd | rd rd . . rs rs rs"]
+       "| rs rd rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs",
+       "| rs rd rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs"]
 
 
 def table_flat(ppn, n, nbytes):
