@@ -139,7 +139,7 @@ def two_level(sends, count, t, op, ppn):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 2), (3, 1), (8, 4), (6, 3)])
+@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 2), (3, 1), (8, 4), (6, 3), (4, 1)])
 def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     nodes = n // ppn
     cases, seed = [], 300
