@@ -225,11 +225,13 @@ def test_mpit_counts_across_nodes(tmp_path):
     calls = [{"coll": "allreduce", "type": "MPI_FLOAT", "count": 300},
              {"coll": "reduce", "type": "MPI_INT", "count": 1000, "root": n - 1},
              {"coll": "reduce_scatter", "type": "MPI_FLOAT", "count": 100},
-             {"coll": "allreduce", "type": "MPI_FLOAT", "count": 600000}]  # the flat ring (wrapper, :3761)
+             {"coll": "allreduce", "type": "MPI_FLOAT", "count": 600000},  # the flat ring (wrapper, :3761)
+             {"coll": "allreduce", "type": "MPI_FLOAT", "count": 70001}]  # 2-ppn table: flat pt2pt_rs
     res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path, ppn=ppn)
     for r in range(n):
         want = {"mv2_coll_allreduce_2lvl": 1, "mv2_coll_reduce_two_level_helper": 1,
-                "mv2_coll_allreduce_pt2pt_ring_wrapper": 1, "mv2_coll_allreduce_pt2pt_ring": 1}
+                "mv2_coll_allreduce_pt2pt_ring_wrapper": 1, "mv2_coll_allreduce_pt2pt_ring": 1,
+                "mv2_coll_allreduce_shm_rs": 1}
         if r % ppn == 0:
             want.update({"mv2_coll_allreduce_shm_rd": 1, "mv2_coll_reduce_binomial": 1})
         got = json.loads(res("mpit", r).tobytes().decode())
