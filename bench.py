@@ -305,6 +305,61 @@ def rccl_comparator(L, world, rank, size, steps, timeout=150):
     return None
 
 
+def user_op_lines(L, world, sb, rb, size):
+    """configs[4]'s user-op allreduce on MPI_Type_vector(nb, 4, 8, MPI_FLOAT) operands, 16 MiB of
+    payload (32 MiB span): `count` elements of nb blocks.  count >= n takes the reference's ring
+    (each rank evaluates its own chunk, allreduce_osu.c:3925-3958); count = 1 leaves the ring
+    nothing and runs recursive doubling (every rank its own tree).  The op is C (tools/osu/
+    uop_vsum.c, as an OSU-style application's would be) or numpy through ctypes (round 2's line).
+    Results are checked exactly on a slice (integer-valued operands)."""
+    F32 = TYPES["MPI_FLOAT"][0]
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+    clib = ctypes.CDLL(os.path.join(ROOT, "tools", "osu", "libuop_vsum.so"))
+    out, ok = [], True
+    for name, nb, count, kind in (("allreduce_user_op_vector", 4096, 256, "c"),
+                                  ("allreduce_user_op_vector_numpy_op", 4096, 256, "py"),
+                                  ("allreduce_user_op_vector_rd", 1 << 20, 1, "py")):
+        ext = (nb - 1) * 8 + 4  # floats
+        vt = ctypes.c_int()
+        m.check(L.MPI_Type_vector(nb, 4, 8, F32, ctypes.byref(vt)), "MPI_Type_vector")
+        m.check(L.MPI_Type_commit(ctypes.byref(vt)), "MPI_Type_commit")
+        keep = None
+        if kind == "c":
+            clib.uop_vsum_blocks(ctypes.c_long(nb))
+            fnp = ctypes.cast(clib.uop_vsum, ctypes.c_void_p)
+        else:
+            def _vsum(inp, io, ln, dt, nb=nb, ext=ext):  # io += in on the type map of ln[0] elements
+                c = ln[0]
+                a = np.lib.stride_tricks.as_strided(
+                    np.ctypeslib.as_array((ctypes.c_float * (c * ext)).from_address(inp)), (c, nb, 4), (ext * 4, 32, 4))
+                b = np.lib.stride_tricks.as_strided(
+                    np.ctypeslib.as_array((ctypes.c_float * (c * ext)).from_address(io)), (c, nb, 4), (ext * 4, 32, 4))
+                b += a
+            keep = UF(_vsum)
+            fnp = ctypes.cast(keep, ctypes.c_void_p)
+        uop = ctypes.c_int()
+        m.check(L.MPI_Op_create(fnp, 1, ctypes.byref(uop)), "MPI_Op_create")
+        # operand: x_r[k] = (k % 61) + r over the span (exact sums in fp32)
+        span = count * ext
+        sb.upload(((np.arange(span, dtype=np.int64) % 61) + L.mv2h_rank()).astype(np.float32))
+        call = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, count, vt.value, uop.value, world)  # noqa: E731
+        s_, _ = _timed(L, world, call, 3, 1)
+        got = rb.download(np.float32, count=min(span, 1 << 20))
+        k = np.arange(len(got), dtype=np.int64)
+        onmap = (k % ext) % 8 < 4
+        want = (size * (k % 61) + size * (size - 1) // 2).astype(np.float32)
+        ok = ok and bool(np.array_equal(got[onmap], want[onmap]))
+        L.MPI_Op_free(ctypes.byref(uop))
+        L.MPI_Type_free(ctypes.byref(vt))
+        del keep
+        algo = "ring (own chunk per rank)" if count >= size else "recursive doubling (every rank its own tree)"
+        out.append({"name": name, "s": s_, "payload": count * nb * 16,
+                    "what": f"configs[4]: commutative user op ({'C' if kind == 'c' else 'numpy via ctypes'}) on "
+                            f"{count} x MPI_Type_vector({nb},4,8,MPI_FLOAT), {count * nb * 16 >> 20} MiB payload, {algo}"})
+    return {"ok": ok, "lines": out}
+
+
 def bench_nranks(args, L, rank, size):
     world = 0x44000000
     F32, F64, DINT = TYPES["MPI_FLOAT"][0], TYPES["MPI_DOUBLE"][0], TYPES["MPI_DOUBLE_INT"][0]
@@ -343,31 +398,10 @@ def bench_nranks(args, L, rank, size):
     ml = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, nrec, DINT, MAXLOC, world)  # noqa: E731
     ml_s, ml_k = _timed(L, world, ml, ks, 2)
 
-    # configs[4]: a commutative user op on MPI_Type_vector(N, 4, 8, MPI_FLOAT) operands (the
-    # reference rejects predefined ops on derived types); the op runs on the host in the
-    # selected algorithm's order (recursive doubling for user ops), as in the reference
-    nbv = 1 << 20
-    vt = ctypes.c_int()
-    m.check(L.MPI_Type_vector(nbv, 4, 8, F32, ctypes.byref(vt)), "MPI_Type_vector")
-    m.check(L.MPI_Type_commit(ctypes.byref(vt)), "MPI_Type_commit")
-    vspan = ((nbv - 1) * 8 + 4) * 4
-    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
-                          ctypes.POINTER(ctypes.c_int))
-
-    def _vsum(inp, io, ln, dt):  # io += in on the type map of ln[0] vector elements
-        for e in range(ln[0]):
-            a = np.ctypeslib.as_array((ctypes.c_float * (vspan // 4)).from_address(inp + e * vspan))
-            b = np.ctypeslib.as_array((ctypes.c_float * (vspan // 4)).from_address(io + e * vspan))
-            bv = np.lib.stride_tricks.as_strided(b, (nbv, 4), (32, 4))
-            av = np.lib.stride_tricks.as_strided(a, (nbv, 4), (32, 4))
-            bv += av
-    ufn = UF(_vsum)
-    uop = ctypes.c_int()
-    m.check(L.MPI_Op_create(ctypes.cast(ufn, ctypes.c_void_p), 1, ctypes.byref(uop)), "MPI_Op_create")
-    uv = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, 1, vt.value, uop.value, world)  # noqa: E731
-    uv_s, _ = _timed(L, world, uv, 2, 1)
-    L.MPI_Op_free(ctypes.byref(uop))
-    L.MPI_Type_free(ctypes.byref(vt))
+    # configs[4]: a commutative user op on MPI_Type_vector(nb, 4, 8, MPI_FLOAT) operands (the
+    # reference rejects predefined ops on derived types); the op runs on the host in the selected
+    # algorithm's order (mpi/user_coll.cpp: packed operands, each ring chunk evaluated by its owner)
+    uops = user_op_lines(L, world, sb, rb, size)
 
     # 8-byte latency (OSU: small-message iterations, skip 100)
     s8 = m.DeviceBuffer(8)
@@ -445,13 +479,16 @@ def bench_nranks(args, L, rank, size):
 
     # max over ranks through the library itself (device allreduce MAX)
     vals = np.array([step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat / args.lat_iters,
-                     float(np.median(lat_k)), 0.0 if (ok and lat_ok) else 1.0, p2p_s, uv_s, sq_s], dtype=np.float64)
+                     float(np.median(lat_k)), 0.0 if (ok and lat_ok and uops["ok"]) else 1.0, p2p_s, sq_s]
+                    + [u["s"] for u in uops["lines"]], dtype=np.float64)
     dm = m.DeviceBuffer(vals.nbytes)
     dm.upload(vals)
     dr = m.DeviceBuffer(vals.nbytes)
     m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, len(vals), F64, MAX, world), "max")
-    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad, p2p_s,
-     uv_s, sq_s) = dr.download(np.float64)
+    got = dr.download(np.float64)
+    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad, p2p_s, sq_s) = got[:15]
+    for u, t in zip(uops["lines"], got[15:]):
+        u["s"] = float(t)
     f = (size - 1) / size
     busbw = 2.0 * f * S_BYTES / step_s / 1e9
     kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
@@ -467,13 +504,25 @@ def bench_nranks(args, L, rank, size):
         "allgather_char": line4(ag_s, ag_k, f * S_BYTES),
         "bcast_char": line4(bc_s, bc_k, S_BYTES),
         "allreduce_maxloc_double_int": line4(ml_s, ml_k, 2.0 * f * nrec * 12),
-        "allreduce_user_op_vector": {"payload_busbw_GBps": round(2.0 * f * nbv * 16 / uv_s / 1e9, 2),
-                                     "ms": round(uv_s * 1e3, 3),
-                                     "what": "configs[4]: commutative user op (host callback) on MPI_Type_vector(1Mi,4,8,"
-                                             "MPI_FLOAT), 16 MiB payload, recursive-doubling order"},
+        **{u["name"]: {"payload_busbw_GBps": round(2.0 * f * u["payload"] / u["s"] / 1e9, 2), "ms": round(u["s"] * 1e3, 3),
+                       "what": u["what"]} for u in uops["lines"]},
         "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
+    # HBM traffic of k_pipe (PIPE_AR) per launch on one rank: the PMC ratio of the newest committed
+    # pass (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE in separate passes, 2 ranks; tools/pmc_summary.py)
+    # times this call's per-rank algorithmic HBM bytes 2S(1 + 2(n-1)/n): reads of the operand, the
+    # RS and the AG slots; writes of the peers' RS pushes, the own segment, the peers' AG pushes and
+    # the gathered segments
+    pipe_alg = 2.0 * S_BYTES * (1.0 + 2.0 * (size - 1) / size)
+    pipe_traffic, pipe_tsrc = None, None
+    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.startswith("pmc_pipe_allreduce_"))
+    if cands:
+        pipe_tsrc = os.path.join("profiles", cands[-1])
+        try:
+            pipe_traffic = round(json.load(open(os.path.join(ROOT, pipe_tsrc)))["traffic_over_algorithmic"] * pipe_alg)
+        except Exception:
+            pipe_traffic, pipe_tsrc = None, None
     tiling = {"grid": m.info("pipe_grid"), "bytes_per_workgroup_round": m.info("pipe_sub"),
               "remote_stores": "non-temporal" if m.info("pipe_rnt") else "plain",
               "autotuned_at_init": bool(m.info("pipe_tuned")),
@@ -482,6 +531,9 @@ def bench_nranks(args, L, rank, size):
                    "nt": m.info(f"tune_rnt_{k}"), "us": m.info(f"tune_us_{k}")}
                   for k in range(m.info("tune_n"))],
               "oneshot_max_bytes": m.info("oneshot_max"),
+              "mpi_init_ms_rank0": round(m.info("init_us") / 1e3, 1),
+              "mpi_init_selftest_ms": round(m.info("selftest_us") / 1e3, 1),
+              "mpi_init_autotune_ms": round(m.info("autotune_us") / 1e3, 1),
               "oneshot_vs_pipe_us": [{"bytes": (32 << 10) << i, "oneshot": m.info(f"os_tune_one_{i}"),
                                       "pipe": m.info(f"os_tune_pipe_{i}")} for i in range(m.info("os_tune_n"))]}
     del sb, rb, rsb
@@ -507,11 +559,13 @@ def bench_nranks(args, L, rank, size):
                    "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing",
                    "pipe_tiling": tiling},
         "roofline": ({"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
-                      "frac": round(kbus / peak_all, 4), "traffic": None,
+                      "frac": round(kbus / peak_all, 4), "traffic": pipe_traffic, "traffic_source": pipe_tsrc,
+                      "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg),
                       "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
                       "kernel_ms": round(kms, 4)} if nshare == 1 else
                      {"bound": "shared-gpu", "achieved": round(kbus, 1), "peak": None, "unit": "GB/s", "frac": None,
-                      "traffic": None, "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)", "kernel_ms": round(kms, 4),
+                      "traffic": pipe_traffic, "traffic_source": pipe_tsrc,
+                      "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)", "kernel_ms": round(kms, 4),
                       "note": f"{nshare} ranks share one GPU: every 'remote' store lands in the same HBM, no xGMI "
                               "link is used, so no xGMI roofline fraction applies"}),
         "cpu_baseline": None,

@@ -115,6 +115,9 @@ int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long l
 int mv2h_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req);
 int mv2h_p2p_test(unsigned long long req, int *done, int *source, int *tag, size_t *bytes);
 int mv2h_p2p_wait(unsigned long long req, int *source, int *tag, size_t *bytes);
+/* progress, then *done = whether `req` has completed, without completing it (MPI_Testall's
+ * all-or-nothing check, MPI-3.1 §3.7.5) */
+int mv2h_p2p_peek(unsigned long long req, int *done);
 int mv2h_p2p_progress(void);
 
 int mv2h_defer_begin(void);
@@ -185,6 +188,12 @@ enum mv2h_nbc {
 int mv2h_nbc_begin(int kind);
 int mv2h_nbc_end(void);
 int mv2h_knobs_reload(void);
+/* Intra-node topology levels of the topology-aware shm tree (create_2level_comm.c:
+ * 916-986): colors[l * n + r] = local rank r's cluster id at level l (its NUMA node, then its
+ * socket), which MPI_Init derives from every rank's CPU binding; set = override for the plans
+ * computed afterwards (tests, tools).  nlevels <= 4, n <= 8. */
+int mv2h_set_topology(int nlevels, const int *colors, int n);
+int mv2h_get_topology(int *nlevels, int *colors, int n);
 /* dst = reduce(srcs[0..nsrc-1]) by the programs of *ps (single GPU; order tests) */
 int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t count, int dtype, int op,
                        const mv2h_progset *ps, void *stream);
@@ -202,7 +211,8 @@ double mv2h_last_kernel_ms(void);
 int mv2h_set_tuning(const char *key, long value);
 /* runtime facts: "nshare" (most ranks sharing one GPU), "device", "cus", "light_release", "oneshot_max",
  * "pipe_grid" / "pipe_sub" (pipelined kernels' tiling), "pipe_tuned" (1: chosen by the MPI_Init
- * autotune), "tune_n" and per candidate k "tune_grid_<k>", "tune_sub_<k>", "tune_us_<k>" (max over ranks) */
+ * autotune), "tune_n" and per candidate k "tune_grid_<k>", "tune_sub_<k>", "tune_us_<k>" (max over ranks),
+ * "init_us" / "selftest_us" / "autotune_us" (this rank's MPI_Init wall time and its parts) */
 int mv2h_get_info(const char *key, long *value);
 
 #ifdef __cplusplus

@@ -62,6 +62,8 @@ constexpr int kDoneStride = 1024;  // counter spacing in words (4 KiB: separate 
 constexpr int kDoneSub = 64;       // first-level counters (blockIdx % 64)
 constexpr int kDoneCtrs = kDoneSub + 8 + 1;  // + per-XCD group (blockIdx % 8) + groups done
 constexpr size_t kDoneBytes = (size_t)kDoneCtrs * kDoneStride * sizeof(uint32_t);
+// ints in the pinned error word block (wait_mask records a timeout's context there)
+constexpr int kErrWords = 64;
 struct Done {
     uint32_t *ctr;   // kDoneCtrs counters, kDoneStride words apart; all 0 between launches
     uint64_t *flag;  // pinned host word
@@ -127,23 +129,38 @@ __device__ __forceinline__ void signal_peers(const SigTable &sig, int n, int me,
 // read with non-temporal loads (L1 bypassed, uncached memory not held in L2),
 // so the system-scope acquire (an L1 + L2 invalidate, >= 1.7 us) is skipped;
 // the MPI_Init self-test checks the pairing of light release and light acquire.
+// On timeout the error word block (pinned host, kErrWords ints) records what was awaited:
+// [1] workgroup, [2..3] epoch, [4] mask, [8 + 2j .. 9 + 2j] the last flag value seen from rank j
+// (several timed-out workgroups may interleave their records; each field is one of theirs).
 __device__ __forceinline__ bool wait_mask(uint64_t *own_sig, unsigned mask, int blk, uint64_t epoch,
                                           int *err, uint64_t timeout_ticks, bool light = false) {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int j = threadIdx.x;
         bool ok = j >= kMaxRanks || !((mask >> j) & 1u);
+        uint64_t seen = 0;
         const uint64_t t0 = wall_clock64();
         bool timed_out = false;
         while (!__all(ok)) {
-            if (!ok) ok = flag_load(own_sig + (size_t)j * kMaxBlocks + blk) >= epoch;
+            if (!ok) {
+                seen = flag_load(own_sig + (size_t)j * kMaxBlocks + blk);
+                ok = seen >= epoch;
+            }
             if (__all(ok)) break;
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > timeout_ticks) { timed_out = true; break; }
         }
+        if (timed_out && j < kMaxRanks && ((mask >> j) & 1u)) {
+            __hip_atomic_store(err + 8 + 2 * j, (int)(uint32_t)seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(err + 9 + 2 * j, (int)(uint32_t)(seen >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (threadIdx.x == 0) {
             if (timed_out) {
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(err + 1, blk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(err + 2, (int)(uint32_t)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(err + 3, (int)(uint32_t)(epoch >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(err + 4, (int)mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(err, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 s_ok = 0;
             } else {
                 if (!light) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");

@@ -200,7 +200,26 @@ int pack_impl(const char *in, int count, MPI_Datatype dt, char *out, bool unpack
     const std::vector<Seg> &segs = d ? d->segs : bsegs;
     const bool din = mv2h_is_device_ptr(in), dout = mv2h_is_device_ptr(out);
     if (!din && !dout) {
-        // host <-> host: reference semantics, host copies
+        // host <-> host: reference semantics, host copies; a regular layout (vectors) moves
+        // fixed-size blocks without a call per block
+        long nb = 0, blk = 0, stride = 0;
+        if (d && regular(d, ext, count, nb, blk, stride) && (blk == 4 || blk == 8 || blk == 16 || blk == 32)) {
+            for (long i = 0; i < nb; ++i) {
+                char *dst = unpack ? out + i * stride : out + i * blk;
+                const char *src = unpack ? in + i * blk : in + i * stride;
+                switch (blk) {
+                case 4: memcpy(dst, src, 4); break;
+                case 8: memcpy(dst, src, 8); break;
+                case 16: memcpy(dst, src, 16); break;
+                default: memcpy(dst, src, 32); break;
+                }
+            }
+            return MPI_SUCCESS;
+        }
+        if (segs.size() == 1 && segs[0].off == 0 && segs[0].len == ext) {  // contiguous
+            memcpy(out, in, (size_t)count * ext);
+            return MPI_SUCCESS;
+        }
         long pos = 0;
         for (int e = 0; e < count; ++e)
             for (const Seg &s : segs) {
@@ -311,6 +330,15 @@ void dtype_merge_typemap(char *dst, const char *src, MPI_Datatype dt, long count
     if (!type_segs(dt, segs, extent, size)) return;
     for (long e = 0; e < count; ++e)
         for (const Seg &sg : segs) memcpy(dst + e * extent + sg.off, src + e * extent + sg.off, (size_t)sg.len);
+}
+
+int dtype_pack(const void *in, int count, MPI_Datatype dt, void *out) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    return count > 0 ? pack_impl((const char *)in, count, dt, (char *)out, false) : MPI_SUCCESS;
+}
+int dtype_unpack(const void *in, int count, MPI_Datatype dt, void *out) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    return count > 0 ? pack_impl((const char *)in, count, dt, (char *)out, true) : MPI_SUCCESS;
 }
 
 long dtype_span(MPI_Datatype dt, int count) {

@@ -12,3 +12,7 @@ long dtype_span(MPI_Datatype dt, int count);
 // copy only the type-map bytes of `count` elements from src to dst (both laid out from
 // element 0 at offset 0): what MPIR_Localcopy / Segment_unpack write into a buffer
 void dtype_merge_typemap(char *dst, const char *src, MPI_Datatype dt, long count);
+// MPI_Pack / MPI_Unpack of `count` elements without the position bookkeeping (no int limit
+// on the packed size); either side may be device or host memory, device work is synchronous
+int dtype_pack(const void *in, int count, MPI_Datatype dt, void *out);
+int dtype_unpack(const void *in, int count, MPI_Datatype dt, void *out);

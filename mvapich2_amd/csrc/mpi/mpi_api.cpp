@@ -26,6 +26,7 @@
 #include "../runtime/pvars.h"
 #include "../runtime/world.h"
 #include "datatype.h"
+#include "user_coll.h"
 
 using namespace mv2;
 
@@ -94,47 +95,8 @@ bool op_valid(MPI_Op op) { return is_builtin_op(op) || user_op(op) != nullptr; }
 bool is_dev(const void *p) { return p && p != MPI_IN_PLACE && mv2h_is_device_ptr(p); }
 
 // ---- user-op path: user functions are host callbacks (the reference also
-// calls them on host copies of device buffers, reduce_local.c:54-164) ----
-// Host staging of the host-side paths (user ops, x87): pinned buffers kept per
-// slot and grown on demand, so a call pays neither page faults nor a zero
-// fill, and the device copies run as DMA from pinned memory.  These paths run
-// under the global critical section; each concurrent use takes its own slot.
-enum HostSlot { HS_OPERANDS, HS_RESULT, HS_MINE, HS_IN, HS_INOUT, HS_COUNT };
-class HostBuf {
-  public:
-    explicit HostBuf(int slot) : slot_(slot) {}
-    void resize(size_t n) {
-        static char *buf[HS_COUNT];
-        static size_t cap[HS_COUNT];
-        static bool pinned[HS_COUNT];
-        if (n > cap[slot_]) {
-            if (buf[slot_]) {
-                if (pinned[slot_]) (void)hipHostFree(buf[slot_]);
-                else free(buf[slot_]);
-            }
-            const size_t want = std::max(n, 2 * cap[slot_]);
-            void *q = nullptr;
-            pinned[slot_] = hipHostMalloc(&q, want, hipHostMallocDefault) == hipSuccess;
-            if (!pinned[slot_]) {
-                (void)hipGetLastError();
-                q = malloc(want);  // no GPU (host-buffer x87 calls): plain memory
-            }
-            buf[slot_] = (char *)q;
-            cap[slot_] = q ? want : 0;
-        }
-        p_ = buf[slot_];
-        n_ = n;
-    }
-    char *data() { return p_; }
-    const char *data() const { return p_; }
-    size_t size() const { return n_; }
-
-  private:
-    int slot_;
-    char *p_ = nullptr;
-    size_t n_ = 0;
-};
-
+// calls them on host copies of device buffers, reduce_local.c:54-164); the
+// collectives' host evaluation is user_coll.cpp ----
 int copy_to_host(HostBuf &h, const void *p, size_t bytes) {
     h.resize(bytes ? bytes : 1);
     if (!h.data()) return MPI_ERR_NO_MEM;
@@ -237,82 +199,6 @@ int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, U
     return copy_from_host(inout, hio, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
 
-// ---- user ops through the reference's algorithm orders (orders.cpp plans) ----
-// Every rank's operand is gathered to host memory; the plan's programs then
-// run with the user function, step dst <- src being fn(in = W[src], inout =
-// W[dst]) on the block's elements, exactly the uop calls the reference makes
-// (its own user-op path also runs on host copies of device buffers).  Only
-// the type-map bytes of the result are written back (MPIR_Localcopy /
-// Segment_unpack semantics): gap bytes of a strided recvbuf stay untouched.
-int gather_operands(const void *src, long span, HostBuf &all) {
-    World &w = world();
-    const int n = w.size;
-    HostBuf mine(HS_MINE);
-    if (copy_to_host(mine, src, span)) return MPI_ERR_OTHER;
-    all.resize((size_t)span * n + 1);
-    if (!all.data()) return MPI_ERR_NO_MEM;
-    if (n > 1) return mv2h_allgather(mine.data(), all.data(), (size_t)span, nullptr);
-    memcpy(all.data(), mine.data(), span);
-    return MPI_SUCCESS;
-}
-
-// Run ps over elements [e_begin, e_end) of the n operands in W (span bytes
-// each, element e at e*extent); merge the type-map bytes of the result into
-// out, whose element 0 is element e_begin.
-void eval_plan(const ProgSet &ps, HostBuf &W, long span, long e_begin, long e_end, MPI_Datatype dt,
-               long extent, UserOp *u, char *out) {
-    long e = e_begin;
-    while (e < e_end) {
-        int b = 0;
-        long be = e_end;
-        if (ps.nprog > 1) {
-            b = (int)std::min<long>((long)(e / (long)ps.blk), ps.nprog - 1);
-            if (b < ps.nprog - 1) be = std::min<long>(e_end, (long)(b + 1) * (long)ps.blk);
-        }
-        const Prog &p = ps.p[b];
-        int cnt = (int)(be - e);
-        MPI_Datatype d = dt;
-        const size_t off = (size_t)e * extent;
-        for (int s = 0; s < p.nsteps; ++s)
-            u->fn(W.data() + (size_t)p.src[s] * span + off, W.data() + (size_t)p.dst[s] * span + off, &cnt, &d);
-        dtype_merge_typemap(out + (size_t)(e - e_begin) * extent, W.data() + (size_t)p.res * span + off, dt, cnt);
-        e = be;
-    }
-}
-
-int user_allreduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
-    World &w = world();
-    const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
-    if (span < 0) return MPI_ERR_TYPE;
-    const int n = w.size, me = w.rank;
-    const bool in_place = sendbuf == MPI_IN_PLACE;
-    HostBuf W(HS_OPERANDS), result(HS_RESULT);
-    int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
-    if (rc) return rc;
-    if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
-    Plan p;
-    if (n == 1) {
-        dtype_merge_typemap(result.data(), W.data(), dt, count);
-    } else if ((rc = plan_allreduce(n, me, (size_t)count, (int)tsize, (int)extent, in_place, 0, &p, opk))) {
-        return rc;
-    } else if (pvar_note(PV_COLL_ALLREDUCE, p, in_place, (size_t)count, n), p.algo != ALG_RING) {
-        eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
-    } else {
-        // ring wrapper (allreduce_osu.c:3758-3818): ring over (count/n)*n elements unless
-        // IN_PLACE or count < n, pt2pt_rs (recursive doubling for user ops) on the rest
-        const long main = in_place ? 0 : (long)(count / n) * n;
-        if (main) eval_plan(p.ps, W, span, 0, main, dt, extent, u, result.data());
-        if (main < count) {
-            Plan r;
-            if ((rc = plan_allreduce(n, me, (size_t)(count - main), (int)tsize, (int)extent, in_place, ALG_PT2PT_RS,
-                                     &r, opk)))
-                return rc;
-            eval_plan(r.ps, W, span, main, count, dt, extent, u, result.data() + (size_t)main * extent);
-        }
-    }
-    return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
-}
-
 // one MPI_T-counted call (runtime/pvars.h)
 int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
     if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
@@ -320,32 +206,9 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
         return MPI_ERR_UNSUPPORTED_OPERATION;
     }
     pvar_begin();
-    const int rc = user_allreduce_body(sendbuf, recvbuf, count, dt, u, opk);
+    const int rc = host_allreduce(sendbuf, recvbuf, count, dt, HostOp{u->fn, opk});
     pvar_end(rc == MPI_SUCCESS);
     return rc;
-}
-
-// MPI_Reduce with a user op: the root evaluates the plan of
-// MPIR_Reduce_index_tuned_intra_MV2 (binomial / knomial / shmem / ...)
-int user_reduce_body(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
-    World &w = world();
-    const long span = dtype_span(dt, count), extent = dtype_extent(dt), tsize = dtype_size(dt);
-    if (span < 0) return MPI_ERR_TYPE;
-    const int n = w.size, me = w.rank;
-    const bool in_place = sendbuf == MPI_IN_PLACE;
-    HostBuf W(HS_OPERANDS), result(HS_RESULT);
-    int rc = gather_operands(in_place ? recvbuf : sendbuf, span, W);
-    if (rc) return rc;
-    Plan p;
-    if (n > 1) {
-        if ((rc = plan_reduce(n, me, root, (size_t)count, (int)tsize, (int)extent, &p, opk))) return rc;
-        pvar_note(PV_COLL_REDUCE, p, in_place, (size_t)count, n);  // every rank runs the algorithm
-    }
-    if (me != root) return MPI_SUCCESS;
-    if (copy_to_host(result, recvbuf, span)) return MPI_ERR_OTHER;
-    if (n == 1) dtype_merge_typemap(result.data(), W.data(), dt, count);
-    else eval_plan(p.ps, W, span, 0, count, dt, extent, u, result.data());
-    return copy_from_host(recvbuf, result, span) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
 
 // one MPI_T-counted call (runtime/pvars.h)
@@ -355,7 +218,7 @@ int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
         return MPI_ERR_UNSUPPORTED_OPERATION;
     }
     pvar_begin();
-    const int rc = user_reduce_body(sendbuf, recvbuf, count, dt, u, root, opk);
+    const int rc = host_reduce(sendbuf, recvbuf, count, dt, HostOp{u->fn, opk}, root);
     pvar_end(rc == MPI_SUCCESS);
     return rc;
 }
@@ -366,53 +229,6 @@ extern "C" int PMPI_Type_get_extent(MPI_Datatype dt, MPI_Aint *lb, MPI_Aint *ext
 
 namespace {
 
-// Reduce_scatter with a user op.  Commutative: the order of
-// MPIR_Reduce_scatter_MV2's choice for this rank's block (ring, recursive
-// halving, pairwise or reduce + scatter).  Non-commutative
-// (MPIR_Reduce_scatter_non_comm_MV2, not restated): the canonical rank order
-// x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
-// associative op, applied as fn(in = x_i, inout = acc).
-int user_reduce_scatter_body(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
-    World &w = world();
-    const int n = w.size, me = w.rank;
-    const long extent = dtype_extent(dt), tsize = dtype_size(dt);
-    if (extent <= 0) return MPI_ERR_TYPE;
-    long total = 0, disp = 0;
-    std::vector<size_t> cz(n);
-    for (int j = 0; j < n; ++j) {
-        if (j == me) disp = total;
-        total += counts[j];
-        cz[j] = (size_t)counts[j];
-    }
-    const long span = dtype_span(dt, (int)total);
-    if (span < 0) return MPI_ERR_TYPE;
-    HostBuf W(HS_OPERANDS), result(HS_RESULT);
-    int rc = gather_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, span, W);
-    if (rc) return rc;
-    Plan p;
-    if (opk != OPK_USER_NONCOMM) {
-        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)tsize, (int)extent, &p, opk))) return rc;
-        pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
-    } else if (n > 1) {
-        pvar_note_id(PV_RS_NON_COMM);
-    }
-    const int c = counts[me];
-    if (c == 0) return MPI_SUCCESS;
-    const long bspan = dtype_span(dt, c);
-    if (copy_to_host(result, recvbuf, bspan)) return MPI_ERR_OTHER;
-    if (opk != OPK_USER_NONCOMM) {
-        eval_plan(p.ps, W, span, disp, disp + c, dt, extent, u, result.data());
-    } else {
-        auto X = [&](int r) { return W.data() + (size_t)r * span + (size_t)disp * extent; };
-        int cc = c;
-        MPI_Datatype d = dt;
-        std::vector<char> acc(X(n - 1), X(n - 1) + bspan);
-        for (int i = n - 2; i >= 0; --i) u->fn(X(i), acc.data(), &cc, &d);
-        dtype_merge_typemap(result.data(), acc.data(), dt, c);
-    }
-    return copy_from_host(recvbuf, result, bspan) ? MPI_ERR_OTHER : MPI_SUCCESS;
-}
-
 // one MPI_T-counted call (runtime/pvars.h)
 int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
     if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
@@ -420,7 +236,7 @@ int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
         return MPI_ERR_UNSUPPORTED_OPERATION;
     }
     pvar_begin();
-    const int rc = user_reduce_scatter_body(sendbuf, recvbuf, counts, dt, u, opk);
+    const int rc = host_reduce_scatter(sendbuf, recvbuf, counts, dt, HostOp{u->fn, opk});
     pvar_end(rc == MPI_SUCCESS);
     return rc;
 }
@@ -1021,6 +837,7 @@ struct MReq {
     int tmp_bytes = 0;
     void *ubuf = nullptr;
     MPI_Datatype dt = MPI_DATATYPE_NULL;
+    int err = MPI_SUCCESS;  // a collective's error found by a peek (MPI_Testall), reported at completion
 };
 std::vector<MReq> g_mreqs;
 constexpr MPI_Request kReqBase = (MPI_Request)0xac000000;
@@ -1080,7 +897,7 @@ int req_finish(MReq &r, int rc, int src, int tag, size_t bytes, MPI_Status *st) 
 int req_wait(MReq &r, MPI_Status *st) {
     int src = MPI_ANY_SOURCE, tag = MPI_ANY_TAG, rc = MPI_SUCCESS;
     size_t bytes = 0;
-    if (r.kind == RQ_COLL) rc = mv2h_wait_ticket(r.id);
+    if (r.kind == RQ_COLL) rc = r.err ? r.err : mv2h_wait_ticket(r.id);
     else if (r.kind == RQ_P2P) rc = mv2h_p2p_wait(r.id, &src, &tag, &bytes);
     return req_finish(r, rc, src, tag, bytes, st);
 }
@@ -1088,7 +905,7 @@ int req_wait(MReq &r, MPI_Status *st) {
 int req_test(MReq &r, int *flag, MPI_Status *st) {
     int src = MPI_ANY_SOURCE, tag = MPI_ANY_TAG, rc = MPI_SUCCESS, done = 1;
     size_t bytes = 0;
-    if (r.kind == RQ_COLL) rc = mv2h_test_ticket(r.id, &done);
+    if (r.kind == RQ_COLL) rc = r.err ? r.err : mv2h_test_ticket(r.id, &done);
     else if (r.kind == RQ_P2P) rc = mv2h_p2p_test(r.id, &done, &src, &tag, &bytes);
     *flag = done;
     if (!done && rc == MPI_SUCCESS) return MPI_SUCCESS;
@@ -1337,15 +1154,29 @@ int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]) WEAK(M
 int PMPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     if (count < 0 || !flag || (count && !requests)) return err_return(MPI_COMM_WORLD, MPI_ERR_ARG, "MPI_Testall");
-    // Requests found complete are completed (set to MPI_REQUEST_NULL) even when
-    // others are still pending: a point-to-point request cannot be peeked
-    // without completing it.  *flag = 1 once all of them are complete.
-    int rc_all = MPI_SUCCESS;
-    bool any_pending = false;
+    // MPI-3.1 §3.7.5: flag = true only if all requests have completed, and then all of them
+    // are completed (deallocated, statuses set); otherwise no request is modified.  First a
+    // peek (progress without completing), then completion of all of them.
     for (int i = 0; i < count; ++i) {
         if (requests[i] == MPI_REQUEST_NULL) continue;
         MReq *r = req_get(requests[i]);
-        int f = 0;
+        if (!r) continue;  // reported below
+        int d = 1;
+        if (r->kind == RQ_COLL) {
+            const int rc = mv2h_test_ticket(r->id, &d);  // reads the completion word only
+            if (rc) r->err = rc, d = 1;                  // a failed collective has completed
+        } else if (r->kind == RQ_P2P && mv2h_p2p_peek(r->id, &d)) {
+            d = 1;  // the request's own test reports the error
+        }
+        if (!d) {
+            *flag = 0;
+            return MPI_SUCCESS;
+        }
+    }
+    int rc_all = MPI_SUCCESS;
+    for (int i = 0; i < count; ++i) {
+        if (requests[i] == MPI_REQUEST_NULL) continue;
+        MReq *r = req_get(requests[i]);
         MPI_Status *st = (!statuses || statuses == MPI_STATUSES_IGNORE) ? MPI_STATUS_IGNORE : &statuses[i];
         if (!r) {
             status_set(st, MPI_ANY_SOURCE, MPI_ANY_TAG, 0, MPI_ERR_REQUEST);
@@ -1353,15 +1184,11 @@ int PMPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status status
             rc_all = MPI_ERR_IN_STATUS;
             continue;
         }
-        const int rc = req_test(*r, &f, st);
-        if (f) {
-            requests[i] = MPI_REQUEST_NULL;
-            if (rc) rc_all = MPI_ERR_IN_STATUS;
-        } else {
-            any_pending = true;
-        }
+        const int rc = req_wait(*r, st);  // complete: returns at once
+        requests[i] = MPI_REQUEST_NULL;
+        if (rc) rc_all = MPI_ERR_IN_STATUS;
     }
-    *flag = any_pending ? 0 : 1;
+    *flag = 1;
     return err_return(MPI_COMM_WORLD, rc_all, "MPI_Testall");
 }
 int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]) WEAK(MPI_Testall);

@@ -1,0 +1,345 @@
+// user_coll.cpp — host-evaluated reductions (user MPI_Op, x87 builtin ops; see user_coll.h).
+//
+// Data path.  Operands travel packed: each rank packs its operand on the device (the strided
+// / run-table pack kernels; a host operand is packed on the host and uploaded) and the packed
+// operands are allgathered device to device.  The host then fetches only the element slices it
+// evaluates, unpacks them into the type's layout — the user function is called on the derived
+// type's layout, as the reference calls it on (char *)buf + disp * extent — runs the plan's
+// programs (one uop(in, inout) call per program step and element block, the calls the
+// reference's algorithm makes), packs the result's type-map bytes and returns them to the
+// device, where one unpack writes the type map of recvbuf.  Gap bytes of recvbuf are never
+// written (MPIR_Localcopy / Segment_unpack semantics, helper_fns.h:62-250).
+//
+// Work split.  Where every rank's program for an element is the same, every rank ends with the
+// same bits and nobody needs to evaluate an element twice: the ring (chunk c is reduced by rank
+// c and allgathered, allreduce_osu.c:3925-4005), the shmem / tree / two-level orders (reduced at
+// local rank 0 and broadcast) and MPI_Reduce (only the root's result counts).  Those elements
+// are split in n ranges, rank r evaluates range r (in the ring: its own chunk, as in the
+// reference) and the packed results are allgathered, so each rank makes uop calls over (n-1)/n
+// of the operand instead of n-1 whole operands.  Where the programs differ between ranks
+// (recursive doubling, :360-630: each rank's own bracketing) every rank evaluates its own
+// result over every element, from the packed operands.
+#include "user_coll.h"
+
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../../include/mv2h.h"
+#include "../common.h"
+#include "../runtime/orders.h"
+#include "../runtime/pvars.h"
+#include "../runtime/world.h"
+#include "datatype.h"
+
+namespace mv2 {
+
+void HostBuf::resize(size_t n) {
+    static char *buf[HS_COUNT];
+    static size_t cap[HS_COUNT];
+    static bool pinned[HS_COUNT];
+    if (n > cap[slot_]) {
+        if (buf[slot_]) {
+            if (pinned[slot_]) (void)hipHostFree(buf[slot_]);
+            else free(buf[slot_]);
+        }
+        const size_t want = std::max(n, 2 * cap[slot_]);
+        void *q = nullptr;
+        pinned[slot_] = hipHostMalloc(&q, want, hipHostMallocDefault) == hipSuccess;
+        if (!pinned[slot_]) {
+            (void)hipGetLastError();
+            q = malloc(want);  // no GPU (host-buffer x87 calls): plain memory
+        }
+        buf[slot_] = (char *)q;
+        cap[slot_] = q ? want : 0;
+    }
+    p_ = buf[slot_];
+    n_ = n;
+}
+
+namespace {
+
+// device scratch kept between calls, grown on demand
+enum DevSlot { DS_MINE, DS_ALL, DS_RES_MINE, DS_RES_ALL, DS_COUNT };
+char *dev_scratch(int slot, size_t bytes) {
+    static void *p[DS_COUNT];
+    static size_t cap[DS_COUNT];
+    if (bytes == 0) bytes = 1;
+    if (bytes > cap[slot]) {
+        if (p[slot]) mv2h_free(p[slot]);
+        p[slot] = nullptr;
+        cap[slot] = 0;
+        if (mv2h_malloc(&p[slot], bytes)) return (char *)(p[slot] = nullptr);
+        cap[slot] = bytes;
+    }
+    return (char *)p[slot];
+}
+
+struct Typed {
+    MPI_Datatype dt;
+    long tsize, extent;
+    bool contig;  // the packed layout is the type's layout
+};
+
+Typed typed(MPI_Datatype dt) {
+    Typed t{dt, dtype_size(dt), dtype_extent(dt), false};
+    t.contig = dtype_is_contiguous(dt) && t.tsize == t.extent;
+    return t;
+}
+
+// every rank's operand, packed, on the device: rank j's at all + j * P
+struct Operands {
+    Typed t;
+    int n;
+    size_t P;
+    const char *all;
+};
+
+int stage_operands(const void *src, int count, const Typed &t, Operands &o) {
+    World &w = world();
+    o.t = t;
+    o.n = w.size;
+    o.P = (size_t)count * (size_t)t.tsize;
+    char *mine = dev_scratch(DS_MINE, o.P);
+    char *all = dev_scratch(DS_ALL, o.P * (size_t)o.n);
+    if (!mine || !all) return MPI_ERR_NO_MEM;
+    int rc;
+    if (mv2h_is_device_ptr(src)) {
+        rc = dtype_pack(src, count, t.dt, mine);
+    } else {
+        HostBuf h(HS_PACKED);
+        h.resize(o.P + 1);
+        if (!h.data()) return MPI_ERR_NO_MEM;
+        rc = dtype_pack(src, count, t.dt, h.data());
+        if (!rc && mv2h_memcpy_htod(mine, h.data(), o.P)) rc = MPI_ERR_OTHER;
+    }
+    if (!rc) rc = o.n > 1 ? mv2h_allgather(mine, all, o.P, nullptr) : (mv2h_memcpy_dtod(all, mine, o.P) ? MPI_ERR_OTHER : 0);
+    o.all = all;
+    return rc;
+}
+
+// Elements [b, e) of every rank's operand in the type's layout (element b at offset 0),
+// operand j at W + j * rspan
+int fetch(const Operands &o, long b, long e, HostBuf &W, long &rspan) {
+    const Typed &t = o.t;
+    const int cnt = (int)(e - b);
+    rspan = dtype_span(t.dt, cnt);
+    const size_t rb = (size_t)cnt * (size_t)t.tsize;
+    W.resize((size_t)rspan * (size_t)o.n + 1);
+    if (!W.data()) return MPI_ERR_NO_MEM;
+    const char *src = o.all + (size_t)b * (size_t)t.tsize;
+    if (t.contig)  // the slices land in place: one strided copy
+        return hipMemcpy2D(W.data(), (size_t)rspan, src, o.P, rb, (size_t)o.n, hipMemcpyDeviceToHost) == hipSuccess
+                   ? 0 : MPI_ERR_OTHER;
+    HostBuf pk(HS_PACKED);
+    pk.resize(rb * (size_t)o.n + 1);
+    if (!pk.data()) return MPI_ERR_NO_MEM;
+    if (hipMemcpy2D(pk.data(), rb, src, o.P, rb, (size_t)o.n, hipMemcpyDeviceToHost) != hipSuccess) return MPI_ERR_OTHER;
+    for (int j = 0; j < o.n; ++j) {
+        const int rc = dtype_unpack(pk.data() + (size_t)j * rb, cnt, t.dt, W.data() + (size_t)j * (size_t)rspan);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+// Run ps over elements [b, e) held in W (element b at offset 0 of each operand, rspan bytes
+// apart); program blocks count from element `pbase`.  Step s is fn(in = w[src], inout = w[dst]).
+// The result's type-map bytes are packed into out (element b first).
+int eval_range(const ProgSet &ps, long pbase, char *W, long rspan, long b, long e, const Typed &t,
+               MPI_User_function *fn, char *out) {
+    for (long x = b; x < e;) {
+        int k = 0;
+        long xe = e;
+        if (ps.nprog > 1) {
+            k = (int)std::min<long>((x - pbase) / (long)ps.blk, ps.nprog - 1);
+            if (k < ps.nprog - 1) xe = std::min<long>(e, pbase + (long)(k + 1) * (long)ps.blk);
+        }
+        const Prog &p = ps.p[k];
+        const size_t off = (size_t)(x - b) * (size_t)t.extent;
+        for (int s = 0; s < p.nsteps; ++s) {
+            int cnt = (int)(xe - x);
+            MPI_Datatype d = t.dt;
+            fn(W + (size_t)p.src[s] * rspan + off, W + (size_t)p.dst[s] * rspan + off, &cnt, &d);
+        }
+        const int rc = dtype_pack(W + (size_t)p.res * rspan + off, (int)(xe - x), t.dt, out + (size_t)(x - b) * t.tsize);
+        if (rc) return rc;
+        x = xe;
+    }
+    return 0;
+}
+
+bool same_progs(const ProgSet &a, const ProgSet &b) {
+    if (a.nprog != b.nprog || (a.nprog > 1 && a.blk != b.blk)) return false;
+    for (int k = 0; k < a.nprog; ++k) {
+        const Prog &p = a.p[k], &q = b.p[k];
+        if (p.nsteps != q.nsteps || p.res != q.res) return false;
+        for (int s = 0; s < p.nsteps; ++s)
+            if (p.dst[s] != q.dst[s] || p.src[s] != q.src[s]) return false;
+    }
+    return true;
+}
+
+// Elements [0, U) have the same programs on every rank (uni) and are split over the ranks;
+// [U, count) are this rank's own (own, program blocks counted from own_base)
+struct Split {
+    const ProgSet *uni;
+    long U;
+    const ProgSet *own;
+    long own_base;
+};
+
+int run_split(const Operands &o, int count, const Split &sp, MPI_User_function *fn, void *recvbuf, bool deliver) {
+    const Typed &t = o.t;
+    const int n = o.n, me = world().rank;
+    const long chunk = sp.U ? (sp.U + n - 1) / n : 0;
+    const long mb = std::min<long>(sp.U, (long)me * chunk), me_e = std::min<long>(sp.U, mb + chunk);
+    char *res_all = dev_scratch(DS_RES_ALL, (size_t)std::max<long>((long)n * chunk, count) * (size_t)t.tsize);
+    if (!res_all) return MPI_ERR_NO_MEM;
+    HostBuf W(HS_OPERANDS), R(HS_RESULT);
+    long rspan = 0;
+    int rc = 0;
+    if (sp.U > 0) {
+        const size_t cb = (size_t)chunk * (size_t)t.tsize;
+        char *res_mine = dev_scratch(DS_RES_MINE, cb);
+        R.resize(cb + 1);
+        if (!res_mine || !R.data()) return MPI_ERR_NO_MEM;
+        if (me_e > mb) {
+            if ((rc = fetch(o, mb, me_e, W, rspan))) return rc;
+            if ((rc = eval_range(*sp.uni, 0, W.data(), rspan, mb, me_e, t, fn, R.data()))) return rc;
+            if (mv2h_memcpy_htod(res_mine, R.data(), (size_t)(me_e - mb) * t.tsize)) return MPI_ERR_OTHER;
+        }
+        // a short (or empty) last range leaves its padding at or after element U, where the
+        // own part below (or nothing) lands
+        if ((rc = mv2h_allgather(res_mine, res_all, cb, nullptr))) return rc;
+    }
+    if (sp.U < count) {
+        const size_t ob = (size_t)(count - sp.U) * (size_t)t.tsize;
+        if ((rc = fetch(o, sp.U, count, W, rspan))) return rc;
+        R.resize(ob + 1);
+        if (!R.data()) return MPI_ERR_NO_MEM;
+        if ((rc = eval_range(*sp.own, sp.own_base, W.data(), rspan, sp.U, count, t, fn, R.data()))) return rc;
+        if (mv2h_memcpy_htod(res_all + (size_t)sp.U * t.tsize, R.data(), ob)) return MPI_ERR_OTHER;
+    }
+    return deliver ? dtype_unpack(res_all, count, t.dt, recvbuf) : 0;
+}
+
+// one rank: recvbuf's type map <- src's
+int copy_typemap(const void *src, void *recvbuf, int count, const Typed &t) {
+    char *tmp = dev_scratch(DS_MINE, (size_t)count * (size_t)t.tsize);
+    if (!tmp) return MPI_ERR_NO_MEM;
+    const int rc = dtype_pack(src, count, t.dt, tmp);
+    return rc ? rc : dtype_unpack(tmp, count, t.dt, recvbuf);
+}
+
+}  // namespace
+
+int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, const HostOp &op) {
+    World &w = world();
+    const Typed t = typed(dt);
+    if (t.tsize < 0 || t.extent < 0) return MPI_ERR_TYPE;
+    const int n = w.size, me = w.rank;
+    const bool in_place = sendbuf == MPI_IN_PLACE;
+    const void *src = in_place ? recvbuf : sendbuf;
+    if (n == 1) return in_place ? MPI_SUCCESS : copy_typemap(src, recvbuf, count, t);
+    Plan p, rem;
+    int rc = plan_allreduce(n, me, (size_t)count, (int)t.tsize, (int)t.extent, in_place, 0, &p, op.opk);
+    if (rc) return rc;
+    pvar_note(PV_COLL_ALLREDUCE, p, in_place, (size_t)count, n);
+    Split sp{&p.ps, 0, &p.ps, 0};
+    if (p.algo == ALG_RING) {
+        // ring wrapper (allreduce_osu.c:3758-3818): the ring over (count / n) * n elements unless
+        // IN_PLACE, pt2pt_rs (recursive doubling for user ops) on the rest
+        sp.U = in_place ? 0 : (long)(count / n) * n;
+        if (sp.U < count) {
+            rc = plan_allreduce(n, me, (size_t)(count - sp.U), (int)t.tsize, (int)t.extent, in_place, ALG_PT2PT_RS, &rem,
+                                op.opk);
+            if (rc) return rc;
+            sp.own = &rem.ps;
+            sp.own_base = sp.U;
+        }
+    } else {
+        bool uniform = true;
+        for (int j = 0; j < n && uniform; ++j) {
+            if (j == me) continue;
+            Plan q;
+            if ((rc = plan_allreduce(n, j, (size_t)count, (int)t.tsize, (int)t.extent, in_place, 0, &q, op.opk))) return rc;
+            uniform = same_progs(q.ps, p.ps);
+        }
+        sp.U = uniform ? count : 0;
+    }
+    Operands o;
+    if ((rc = stage_operands(src, count, t, o))) return rc;
+    return run_split(o, count, sp, op.fn, recvbuf, true);
+}
+
+// MPI_Reduce: the root's programs (MPIR_Reduce_index_tuned_intra_MV2's choice, binomial /
+// knomial / shmem / ...) evaluated over ranges split across every rank
+int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, const HostOp &op, int root) {
+    World &w = world();
+    const Typed t = typed(dt);
+    if (t.tsize < 0 || t.extent < 0) return MPI_ERR_TYPE;
+    const int n = w.size, me = w.rank;
+    const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+    if (n == 1) return sendbuf == MPI_IN_PLACE ? MPI_SUCCESS : copy_typemap(src, recvbuf, count, t);
+    Plan p, pr;
+    int rc = plan_reduce(n, me, root, (size_t)count, (int)t.tsize, (int)t.extent, &p, op.opk);
+    if (rc) return rc;
+    pvar_note(PV_COLL_REDUCE, p, sendbuf == MPI_IN_PLACE, (size_t)count, n);  // every rank runs the algorithm
+    if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
+    Operands o;
+    if ((rc = stage_operands(src, count, t, o))) return rc;
+    const Split sp{&pr.ps, count, &pr.ps, 0};
+    return run_split(o, count, sp, op.fn, recvbuf, me == root);
+}
+
+// Reduce_scatter.  Commutative: the order of MPIR_Reduce_scatter_MV2's choice for this rank's
+// block (ring, recursive halving, pairwise or reduce + scatter).  Non-commutative
+// (MPIR_Reduce_scatter_non_comm_MV2, not restated): the canonical rank order
+// x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an associative op,
+// applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block.
+int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, const HostOp &op) {
+    World &w = world();
+    const Typed t = typed(dt);
+    if (t.tsize < 0 || t.extent <= 0) return MPI_ERR_TYPE;
+    const int n = w.size, me = w.rank;
+    long total = 0, disp = 0;
+    std::vector<size_t> cz(n);
+    for (int j = 0; j < n; ++j) {
+        if (j == me) disp = total;
+        total += counts[j];
+        cz[j] = (size_t)counts[j];
+    }
+    ProgSet ps{};
+    Plan p;
+    int rc;
+    if (op.opk != OPK_USER_NONCOMM) {
+        if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)t.tsize, (int)t.extent, &p, op.opk))) return rc;
+        pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
+        ps = p.ps;
+    } else {
+        if (n > 1) pvar_note_id(PV_RS_NON_COMM);
+        ps.nprog = 1;
+        ps.p[0].nsteps = (uint8_t)(n - 1);
+        ps.p[0].res = (uint8_t)(n - 1);
+        for (int s = 0; s < n - 1; ++s) {
+            ps.p[0].dst[s] = (uint8_t)(n - 1);
+            ps.p[0].src[s] = (uint8_t)(n - 2 - s);
+        }
+    }
+    Operands o;
+    if ((rc = stage_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, (int)total, t, o))) return rc;
+    const int c = counts[me];
+    if (c == 0) return MPI_SUCCESS;
+    HostBuf W(HS_OPERANDS), R(HS_RESULT);
+    long rspan = 0;
+    if ((rc = fetch(o, disp, disp + c, W, rspan))) return rc;
+    R.resize((size_t)c * (size_t)t.tsize + 1);
+    if (!R.data()) return MPI_ERR_NO_MEM;
+    if ((rc = eval_range(ps, 0, W.data(), rspan, disp, disp + c, t, op.fn, R.data()))) return rc;
+    return dtype_unpack(R.data(), c, t.dt, recvbuf);
+}
+
+}  // namespace mv2

@@ -157,14 +157,30 @@ static hipError_t wait_done(hipStream_t st, uint64_t want) {
     }
 }
 
+// A kernel gave up waiting for a peer (device_util.h wait_mask): report what it waited for —
+// the epoch, the ranks and the flag values it last saw from each, next to this rank's host
+// counters — so a failure tells a late peer (flag = an earlier epoch of the same call
+// sequence) from a peer whose call sequence diverged (flags of another call's epochs).
 static int check_err_word() {
     World &w = world();
-    if (w.h_err && __atomic_load_n(w.h_err, __ATOMIC_ACQUIRE)) {
-        MV2_ERR("device collective timed out waiting for a peer (MV2AMD_TIMEOUT_S)");
-        __atomic_store_n(w.h_err, 0, __ATOMIC_RELEASE);
-        return E_OTHER;
-    }
-    return 0;
+    if (!w.h_err || !__atomic_load_n(w.h_err, __ATOMIC_ACQUIRE)) return 0;
+    int *e = w.h_err;
+    const uint64_t ep = (uint64_t)(uint32_t)e[2] | ((uint64_t)(uint32_t)e[3] << 32);
+    char seen[256];
+    int o = 0;
+    for (int j = 0; j < kMaxRanks && o < (int)sizeof(seen) - 40; ++j)
+        if (((unsigned)e[4] >> j) & 1u) {
+            const uint64_t v = (uint64_t)(uint32_t)e[8 + 2 * j] | ((uint64_t)(uint32_t)e[9 + 2 * j] << 32);
+            o += snprintf(seen + o, sizeof(seen) - o, " r%d=%llu", j, (unsigned long long)v);
+        }
+    seen[o] = 0;
+    MV2_ERR("device collective timed out waiting for a peer (MV2AMD_TIMEOUT_S): workgroup %d waited for epoch "
+            "%llu from ranks 0x%x; flags seen:%s; host epoch %llu, round %llu, one-shot calls %llu, call %llu",
+            e[1], (unsigned long long)ep, (unsigned)e[4], seen, (unsigned long long)w.epoch, (unsigned long long)w.round,
+            (unsigned long long)w.os_calls, (unsigned long long)w.done_seq);
+    memset(e + 1, 0, (kErrWords - 1) * sizeof(int));
+    __atomic_store_n(e, 0, __ATOMIC_RELEASE);
+    return E_OTHER;
 }
 
 static int finish(hipStream_t st, bool timed) {
@@ -194,11 +210,7 @@ static int finish(hipStream_t st, bool timed) {
         hipEventElapsedTime(&ms, w.ev0, w.ev1);
         w.last_ms = ms;
     }
-    if (w.h_err && __atomic_load_n(w.h_err, __ATOMIC_ACQUIRE)) {
-        MV2_ERR("device collective timed out waiting for a peer (MV2AMD_TIMEOUT_S)");
-        __atomic_store_n(w.h_err, 0, __ATOMIC_RELEASE);
-        return E_OTHER;
-    }
+    if (check_err_word()) return E_OTHER;
     hp_done();
     return 0;
 }
@@ -528,6 +540,11 @@ int coll_selftest() {
 // MV2AMD_PIPE_GRID / MV2AMD_PIPE_SUB disables it.
 int oneshot_autotune();
 
+static long env_long_coll(const char *name, long dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atol(v) : dflt;
+}
+
 int pipe_autotune() {
     World &w = world();
     const char *ev = getenv("MV2AMD_PIPE_AUTOTUNE");
@@ -555,7 +572,20 @@ int pipe_autotune() {
     const size_t s0 = w.pipe_sub;
     int nc = 0;
     int rc = 0;
+    // time budget (MV2AMD_PIPE_AUTOTUNE_BUDGET_MS, default 3 s of MPI_Init): rank 0 ends the
+    // probe when it is spent and every rank stops at the same candidate (one barrier publishes
+    // the decision, a second one keeps rank 0 from rewriting it before every rank has read it)
+    const double budget_ms = (double)env_long_coll("MV2AMD_PIPE_AUTOTUNE_BUDGET_MS", 3000);
+    const auto t_begin = std::chrono::steady_clock::now();
     for (int c = 0; c < 2 * kTilings && nc < kTuneMax; ++c) {
+        if (w.rank == 0)
+            w.shm->tune_stop.store(
+                nc > 0 && std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count() >
+                              budget_ms ? 1 : 0);
+        host_barrier();
+        const bool stop = w.shm->tune_stop.load() != 0;
+        host_barrier();
+        if (stop) break;
         w.pipe_grid = kGrid[c % kTilings];
         w.pipe_sub = kSub[c % kTilings];
         w.pipe_rnt = c < kTilings ? 1 : 0;
@@ -745,6 +775,9 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "tune_n")) *value = w.tune_n;
     else if (!strcmp(key, "pipe_rnt")) *value = w.pipe_rnt;
     else if (!strcmp(key, "os_tune_n")) *value = w.os_tune_n;
+    else if (!strcmp(key, "init_us")) *value = (long)(w.init_ms * 1e3 + 0.5);
+    else if (!strcmp(key, "selftest_us")) *value = (long)(w.selftest_ms * 1e3 + 0.5);
+    else if (!strcmp(key, "autotune_us")) *value = (long)(w.tune_ms * 1e3 + 0.5);
     else if (!strncmp(key, "os_tune_one_", 12) || !strncmp(key, "os_tune_pipe_", 13)) {
         const long i = strtol(strrchr(key, '_') + 1, nullptr, 10);
         if (i < 0 || i >= w.os_tune_n) return E_ARG;
@@ -948,6 +981,26 @@ int mv2h_nbc_end(void) {
 
 int mv2h_knobs_reload(void) {
     knobs_reload();
+    return 0;
+}
+
+int mv2h_set_topology(int nlevels, const int *colors, int n) {
+    if (nlevels < 0 || nlevels > kTopoLevels || n < 0 || n > kMaxRanks || (nlevels && !colors)) return E_ARG;
+    Topo t{};
+    t.nlevels = nlevels;
+    for (int l = 0; l < nlevels; ++l)
+        for (int r = 0; r < n; ++r) t.color[l][r] = colors[l * n + r];
+    topo_set(t);
+    return 0;
+}
+
+int mv2h_get_topology(int *nlevels, int *colors, int n) {
+    if (!nlevels || n < 0 || n > kMaxRanks) return E_ARG;
+    const Topo &t = topo();
+    *nlevels = t.nlevels;
+    if (colors)
+        for (int l = 0; l < t.nlevels; ++l)
+            for (int r = 0; r < n; ++r) colors[l * n + r] = t.color[l][r];
     return 0;
 }
 
@@ -1523,7 +1576,8 @@ struct MnBufs {
 };
 MnBufs g_mn;
 
-int mn_reserve(size_t bytes) {
+// host staging h0 / h1 (node leaders: the inter-node messages) and device d0 / d1
+int mn_reserve_host(size_t bytes) {
     if (bytes > g_mn.hcap) {
         if (g_mn.h0) hipHostFree(g_mn.h0);
         if (g_mn.h1) hipHostFree(g_mn.h1);
@@ -1534,6 +1588,9 @@ int mn_reserve(size_t bytes) {
             return E_NO_MEM;
         g_mn.hcap = bytes;
     }
+    return 0;
+}
+int mn_reserve_dev(size_t bytes) {
     if (bytes > g_mn.dcap) {
         hipDeviceSynchronize();
         if (g_mn.d0) hipFree(g_mn.d0);
@@ -1545,6 +1602,10 @@ int mn_reserve(size_t bytes) {
         g_mn.dcap = bytes;
     }
     return 0;
+}
+int mn_reserve(size_t bytes) {
+    const int rc = mn_reserve_host(bytes);
+    return rc ? rc : mn_reserve_dev(bytes);
 }
 
 int mn_d2h(void *h, const void *d, size_t b) { return hipMemcpy(h, d, b, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN; }
@@ -1641,7 +1702,7 @@ static int mn_select(long nbytes) {
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
 static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
-                             int algo);
+                             int algo, int root = -1);
 
 // Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
 // chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
@@ -1714,21 +1775,26 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
 // (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
 // evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
 // differ between ranks where the op is not commutative in its bits (MAX/MIN ties of ±0, NaN
-// payloads), as the reference's do.
+// payloads), as the reference's do.  algo 0: the plan of the call's own selection (a nonblocking
+// call's: MPIR_Iallreduce_naive = Ireduce to rank 0 + Ibcast, every rank takes rank 0's result).
+// root >= 0 (MPI_Ireduce): only the root evaluates, the plan of MPIR_Ireduce_binomial.
 static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
-                             int algo) {
+                             int algo, int root) {
     World &w = world();
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
     const size_t S = count * (size_t)dt->extent, sect = (size_t)w.size * S;
     const int n = w.gsize, K = w.nnodes;
     Plan p;
-    int rc = plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
+    int rc = root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
+                       : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
     if (rc) return rc;
-    pvar_note(PV_COLL_ALLREDUCE, p, in_place, count, n);
+    pvar_note(root >= 0 ? PV_COLL_REDUCE : PV_COLL_ALLREDUCE, p, in_place, count, n);
     char *W = (char *)get_scratch(6, (size_t)n * S);  // every rank's operand, global rank order
-    if (!W || (rc = mn_reserve((size_t)n * S))) return rc ? rc : E_NO_MEM;
-    if ((rc = allgather_node(in_place ? recvbuf : sendbuf, W + (size_t)w.node * sect, S, stream))) return rc;
+    if (!W) return E_NO_MEM;
+    if ((rc = mn_reserve_dev(S)) || (w.rank == 0 && (rc = mn_reserve_host((size_t)n * S)))) return rc;
+    const void *mine = in_place ? recvbuf : sendbuf;
+    if ((rc = allgather_node(mine, W + (size_t)w.node * sect, S, stream))) return rc;
     if (w.rank == 0) {
         const int me = w.node, right = (me + 1) % K, left = (me - 1 + K) % K;
         if ((rc = mn_d2h(g_mn.h0 + (size_t)me * sect, W + (size_t)me * sect, sect))) return rc;
@@ -1740,6 +1806,7 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
         if ((rc = mn_h2d(W, g_mn.h0, (size_t)n * S))) return rc;
     }
     if ((rc = bcast_node(W, (size_t)n * S, 0, stream))) return rc;
+    if (root >= 0 && w.grank != root) return 0;
     const void *srcs[kMaxRanks];
     for (int r = 0; r < n; ++r) srcs[r] = W + (size_t)r * S;
     if ((rc = mv2h_reduce_n_prog(srcs, n, g_mn.d1, count, dtype, op, (const mv2h_progset *)&p.ps, nullptr)))
@@ -1752,17 +1819,30 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     if (rc || count == 0) return rc;
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
+    const int gsize = world().gsize;
+    // MPI_Iallreduce: MVAPICH2's nonblocking schedule is flat over the whole job
+    // (MPIR_Iallreduce_intra_MV2 iallreduce_osu.c:257 -> MPIR_Iallreduce_naive: Ireduce to rank 0,
+    // binomial or redscat_gather, then Ibcast), whatever the nodes
+    if (nbc_kind() == NBC_IALLREDUCE && gsize <= kMaxRanks)
+        return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0);
     const int sel = mn_select((long)(count * (size_t)dt->size));
     if (sel == 1) {
         // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise
-        // it runs pt2pt_rs over every rank (restated up to kMaxRanks ranks, else two-level)
-        if (!in_place && count >= (size_t)world().gsize)
+        // it runs pt2pt_rs over every rank (restated up to kMaxRanks ranks, else two-level).  With
+        // IN_PLACE the body's own fallback is pt2pt_rs over (count / n) * n elements (:4095-4100),
+        // then the wrapper's pt2pt_rs on the remainder (:3800-3818): two calls, as on one node
+        if (!in_place && count >= (size_t)gsize)
             return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
         const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
         pvar_note_ids(chain, 2);
-        if (world().gsize <= kMaxRanks)
-            return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, ALG_PT2PT_RS);
-        return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
+        if (gsize > kMaxRanks) return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
+        const size_t main = in_place ? (count / (size_t)gsize) * (size_t)gsize : 0;
+        if (main && main < count) {
+            if ((rc = mn_flat_allreduce(sendbuf, recvbuf, main, dtype, op, stream, ALG_PT2PT_RS))) return rc;
+            const size_t off = main * (size_t)dt->extent;
+            return mn_flat_allreduce(sendbuf, (char *)recvbuf + off, count - main, dtype, op, stream, ALG_PT2PT_RS);
+        }
+        return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, ALG_PT2PT_RS);
     }
     if (sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD)
         return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, sel);
@@ -1817,9 +1897,13 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     const bool me_root = w.grank == root;
     const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;  // IN_PLACE: at the root only
     // MPI_T: MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2039) with the leaders' binomial (:450)
+    // MPI_Ireduce: MVAPICH2's nonblocking schedule (MPIR_Ireduce_binomial, ireduce_osu.c) is flat
+    // over the whole job
+    if (nbc_kind() == NBC_IREDUCE && w.gsize <= kMaxRanks)
+        return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root);
     const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
     pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
-    if ((rc = mn_reserve(bytes))) return rc;
+    if ((rc = mn_reserve_dev(bytes)) || (w.rank == 0 && (rc = mn_reserve_host(bytes)))) return rc;
     // node step: the leader's partial lands in g_mn.d0 (a non-root's recvbuf is not significant)
     if ((rc = reduce_entry(src, w.rank == 0 ? g_mn.d0 : nullptr, count, dtype, op, 0, stream))) return rc;
     if (w.rank == 0) {

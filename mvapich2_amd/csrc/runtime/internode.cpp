@@ -43,7 +43,17 @@ struct Hello {
     int32_t node;
     int32_t port;  // the sender's mesh listener
     int32_t nnodes;
+    int32_t ppn;         // ranks per node (the schedules assume the same count everywhere)
+    int32_t pad;
+    uint64_t knob_hash;  // FNV-1a of the MV2_* selection knobs (every node must select alike)
 };
+
+uint64_t knob_hash() {
+    const unsigned char *p = (const unsigned char *)&knobs();
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(Knobs); ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+}
 struct Entry {
     char ip[64];
     int32_t port;
@@ -249,6 +259,7 @@ int net_init() {
             MV2_ERR("leader rendezvous: cannot listen on port %d", port);
             return E_OTHER;
         }
+        bool mismatch = false;
         for (int k = 1; k < nn; ++k) {
             const int fd = accept_timed(g_net.listen_fd);
             Hello h{};
@@ -258,6 +269,11 @@ int net_init() {
                 if (fd >= 0) close(fd);
                 return E_OTHER;
             }
+            if (h.ppn != w.size || h.knob_hash != knob_hash()) {
+                MV2_ERR("node %d differs from node 0 in %s: the nodes would run different schedules", h.node,
+                        h.ppn != w.size ? "ranks per node" : "its MV2_* collective selection knobs");
+                mismatch = true;
+            }
             sockaddr_in sa{};
             socklen_t len = sizeof(sa);
             getpeername(fd, (sockaddr *)&sa, &len);
@@ -265,8 +281,11 @@ int net_init() {
             table[h.node].port = h.port;
             g_net.fd[h.node] = fd;
         }
+        if (mismatch)  // port -1: every leader refuses the job instead of pairing mismatched schedules
+            for (Entry &e : table) e.port = -1;
         for (int j = 1; j < nn; ++j)
             if (xfer(g_net.fd[j], (const char *)table.data(), table.size() * sizeof(Entry), nullptr, 0)) return E_OTHER;
+        if (mismatch) return E_OTHER;
     } else {
         int myport = 0;
         g_net.listen_fd = open_listener(nullptr, 0, &myport);
@@ -276,9 +295,14 @@ int net_init() {
             MV2_ERR("leader of node %d: cannot reach the rendezvous %s:%d", me, host.c_str(), port);
             return E_OTHER;
         }
-        Hello h{kMagic, me, myport, nn};
+        Hello h{kMagic, me, myport, nn, w.size, 0, knob_hash()};
         if (xfer(fd, (const char *)&h, sizeof(h), nullptr, 0) ||
             xfer(fd, nullptr, 0, (char *)table.data(), table.size() * sizeof(Entry))) {
+            close(fd);
+            return E_OTHER;
+        }
+        if (table[0].port == -1) {
+            MV2_ERR("leader of node %d: node 0 refused the job (ranks per node or MV2_* knobs differ between nodes)", me);
             close(fd);
             return E_OTHER;
         }
@@ -286,7 +310,7 @@ int net_init() {
         // mesh among nodes 1..nn-1: connect down, accept up
         for (int j = 1; j < me; ++j) {
             const int c = connect_retry(table[j].ip, table[j].port);
-            Hello hj{kMagic, me, myport, nn};
+            Hello hj{kMagic, me, myport, nn, w.size, 0, knob_hash()};
             if (c < 0 || xfer(c, (const char *)&hj, sizeof(hj), nullptr, 0)) {
                 MV2_ERR("leader of node %d: cannot connect to node %d", me, j);
                 return E_OTHER;

@@ -22,7 +22,16 @@ namespace mv2 {
 // ---------------------------------------------------------------------------
 static Knobs g_knobs;
 static bool g_knobs_ok = false;
-static uint64_t g_knobs_gen = 0;  // bumped by knobs_reload: invalidates cached plans
+static uint64_t g_knobs_gen = 0;  // bumped by knobs_reload / topo_set: invalidates cached plans
+static Topo g_topo{};
+
+const Topo &topo() { return g_topo; }
+void topo_set(const Topo &t) {
+    g_topo = t;
+    if (g_topo.nlevels < 0) g_topo.nlevels = 0;
+    if (g_topo.nlevels > kTopoLevels) g_topo.nlevels = kTopoLevels;
+    ++g_knobs_gen;
+}
 
 static bool env_set(const char *name, const char **v) {
     *v = getenv(name);
@@ -207,21 +216,48 @@ bool prog_linear(int n, ProgSet &ps) {
     return single_expr(s, acc, ps);
 }
 
-// mv2_shm_tree_reduce (ch3_shmem_coll.c:4272-4359) rooted at local rank 0:
-// every rank with local_rank % deg == 0 reduces members g+1 .. g+deg-1 in
-// order; the root then reduces the group leaders deg, 2deg, ... in order
+// mv2_shm_tree_reduce (ch3_shmem_coll.c:4272-4359) over the members m[0..cnt) of one
+// communicator (in its rank order), rooted at m[0]: every member with index % deg == 0 reduces
+// members g+1 .. g+deg-1 in order; the root then reduces the group leaders deg, 2deg, ... in
+// order.  val[r] = the expression rank r holds; the result lands in val[m[0]].
+void shm_tree_sym(Sym &s, std::vector<int> &val, const int *m, int cnt, int deg) {
+    for (int g = 0; g < cnt; g += deg)
+        for (int i = g + 1; i < g + deg && i < cnt; ++i) val[m[g]] = s.op(val[m[g]], val[m[i]]);
+    for (int g = deg; g < cnt; g += deg) val[m[0]] = s.op(val[m[0]], val[m[g]]);
+}
+
+// The topology-aware reduce to local rank 0 (allreduce_osu.c:2340-2361): one shm tree per
+// level.  At level l the current communicator (all ranks at level 0, then the previous level's
+// group leaders, in rank order) splits by each member's colour at l (0 past the levels); each
+// group reduces into its first member, which leads it into level l+1; one group ends the walk
+// (create_2level_comm.c:836-846: no leader communicator).
 bool prog_tree(int n, int deg, ProgSet &ps) {
     if (deg < 1) deg = 1;
+    const Topo &t = topo();
     Sym s;
-    std::vector<int> grp(n, -1);
-    for (int g = 0; g < n; g += deg) {
-        int acc = s.leaf(g);
-        for (int i = g + 1; i < g + deg && i < n; ++i) acc = s.op(acc, s.leaf(i));
-        grp[g] = acc;
+    std::vector<int> val(n);
+    for (int r = 0; r < n; ++r) val[r] = s.leaf(r);
+    std::vector<int> cur(n);
+    for (int r = 0; r < n; ++r) cur[r] = r;
+    for (int lvl = 0;; ++lvl) {
+        auto color = [&](int r) { return lvl < t.nlevels ? t.color[lvl][r] : 0; };
+        std::vector<int> leaders;
+        std::vector<bool> seen(cur.size(), false);
+        for (size_t i = 0; i < cur.size(); ++i) {
+            if (seen[i]) continue;
+            int m[kMaxRanks], cnt = 0;
+            for (size_t j = i; j < cur.size(); ++j)
+                if (!seen[j] && color(cur[j]) == color(cur[i])) {
+                    seen[j] = true;
+                    m[cnt++] = cur[j];
+                }
+            shm_tree_sym(s, val, m, cnt, deg);
+            leaders.push_back(cur[i]);
+        }
+        if (leaders.size() == 1) return single_expr(s, val[leaders[0]], ps);
+        if (lvl > kTopoLevels) return false;
+        cur = leaders;
     }
-    int acc = grp[0];
-    for (int g = deg; g < n; g += deg) acc = s.op(acc, grp[g]);
-    return single_expr(s, acc, ps);
 }
 
 // MPIR_Reduce_binomial_MV2 (reduce_osu.c:577-643), commutative: relrank =

@@ -77,6 +77,23 @@ struct Knobs {
 const Knobs &knobs();  // parsed from the environment on first use
 void knobs_reload();   // re-read the environment (tests)
 
+// Intra-node topology levels of the topology-aware collectives.  The reference splits the node's
+// communicator level by level (create_intra_node_multi_level_topo_comm, create_2level_comm.c:
+// 916-986, with create_intra_node_topo_comm_at_level :666-900): at level l every rank takes its
+// own cluster id mv2_intra_node_cluster_at_level[l] (hwloc_bind.c:83) as the split colour — the
+// NUMA node it is bound to when the node has several (smpi_identify_my_numa_id :2252-2298), then
+// its socket when there are several and its NUMA node is not inside it (smpi_identify_my_sock_id
+// :2180-2250); levels past a rank's own count read 0 — and the first rank of each group leads it
+// into the next level.  mv2_shm_tree_reduce runs once per level (allreduce_osu.c:2340-2361,
+// reduce_osu.c:272-296).  color[l][r] = rank r's cluster id at level l, for l < nlevels.
+constexpr int kTopoLevels = 4;
+struct Topo {
+    int nlevels;
+    int color[kTopoLevels][kMaxRanks];
+};
+const Topo &topo();           // default: no level (one group: the node)
+void topo_set(const Topo &t); // MPI_Init (runtime/world.cpp) or a test; invalidates cached plans
+
 // Plan::via: how the reference reached the algorithm (for the MPI_T counters
 // of its call chain, runtime/pvars.cpp)
 enum : int {

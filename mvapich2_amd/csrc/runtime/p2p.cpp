@@ -328,6 +328,18 @@ int mv2h_p2p_test(unsigned long long id, int *done, int *source, int *tag, size_
     return err;
 }
 
+int mv2h_p2p_peek(unsigned long long id, int *done) {
+    auto it = g_reqs.find(id);
+    if (it == g_reqs.end()) return E_REQUEST;
+    if (!it->second->done) {
+        bool moved;
+        const int rc = progress(&moved);
+        if (rc) return rc;
+    }
+    *done = it->second->done ? 1 : 0;
+    return 0;
+}
+
 int mv2h_p2p_wait(unsigned long long id, int *source, int *tag, size_t *bytes) {
     if (g_reqs.find(id) == g_reqs.end()) return E_REQUEST;
     const auto t0 = std::chrono::steady_clock::now();

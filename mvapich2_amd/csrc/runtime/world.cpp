@@ -16,6 +16,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <thread>
 
@@ -127,8 +128,8 @@ static int setup_device_common() {
     w.sync_mode = (int)env_long("MV2AMD_SYNC", w.sync_mode);
     // blocking stream: orders after legacy null-stream work (buffer readiness)
     if (hipStreamCreate(&w.stream) != hipSuccess) return E_OTHER;
-    if (hipHostMalloc((void **)&w.h_err, 64, hipHostMallocDefault) != hipSuccess) return E_OTHER;
-    memset(w.h_err, 0, 64);
+    if (hipHostMalloc((void **)&w.h_err, kErrWords * sizeof(int), hipHostMallocDefault) != hipSuccess) return E_OTHER;
+    memset(w.h_err, 0, kErrWords * sizeof(int));
     if (hipMalloc((void **)&w.done_ctr, kDoneBytes) != hipSuccess || hipMemset(w.done_ctr, 0, kDoneBytes) != hipSuccess ||
         hipHostMalloc((void **)&w.done_flag, 64, hipHostMallocDefault) != hipSuccess) {
         w.done_ctr = nullptr;
@@ -161,9 +162,137 @@ int ensure_init_for_device() {
     return setup_device_common();
 }
 
+
+// ---------------------------------------------------------------------------
+// Intra-node topology levels (orders.h Topo): this rank's cluster id per level as the reference
+// derives them at MPI_Init (init.c:255-271 -> smpi_identify_my_numa_id, hwloc_bind.c:2252-2298,
+// then smpi_identify_my_sock_id :2180-2250), from this process's CPU binding (the reference reads
+// its own, hwloc_get_proc_cpubind) and the sysfs view of the NUMA nodes and packages.  The
+// reference binds its ranks itself first (MV2_ENABLE_AFFINITY, bunch policy); this library does
+// not bind, so unbound ranks all intersect the first NUMA node and form one group (one level).
+// MV2AMD_TOPO="c0,c1,...[;d0,d1,...]" gives every local rank's ids per level instead.
+// ---------------------------------------------------------------------------
+static bool read_cpulist(const char *path, std::vector<int> &cpus) {
+    FILE *f = fopen(path, "r");
+    if (!f) return false;
+    char buf[4096];
+    const bool ok = fgets(buf, sizeof(buf), f) != nullptr;
+    fclose(f);
+    if (!ok) return false;
+    for (char *p = buf; *p && *p != '\n';) {
+        char *e = nullptr;
+        const long a = strtol(p, &e, 10);
+        if (e == p) break;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            p = e;
+        }
+        for (long c = a; c <= b; ++c) cpus.push_back((int)c);
+        if (*p == ',') ++p;
+    }
+    return true;
+}
+
+static int my_topology(int *color, int max_levels) {
+    int n = 0;
+    cpu_set_t mine;
+    CPU_ZERO(&mine);
+    if (sched_getaffinity(0, sizeof(mine), &mine) != 0) return 0;
+    std::vector<int> online;
+    if (!read_cpulist("/sys/devices/system/cpu/online", online)) return 0;
+    auto intersects = [&](const std::vector<int> &cs) {
+        for (int c : cs)
+            if (c < CPU_SETSIZE && CPU_ISSET(c, &mine)) return true;
+        return false;
+    };
+    // NUMA nodes in index order (hwloc logical order = OS order here)
+    std::vector<int> nodes;
+    read_cpulist("/sys/devices/system/node/online", nodes);
+    std::vector<std::vector<int>> node_cpus(nodes.size());
+    int my_numa = -1;
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        char path[128];
+        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", nodes[i]);
+        read_cpulist(path, node_cpus[i]);
+        if (my_numa < 0 && intersects(node_cpus[i])) my_numa = (int)i;
+    }
+    if (nodes.size() > 1 && n < max_levels) color[n++] = my_numa;
+    // packages: sorted physical ids; the first one this binding intersects
+    std::vector<int> pkg_ids, pkg_of(online.size(), -1);
+    for (size_t k = 0; k < online.size(); ++k) {
+        char path[128];
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/physical_package_id", online[k]);
+        FILE *f = fopen(path, "r");
+        int id = -1;
+        if (f) {
+            if (fscanf(f, "%d", &id) != 1) id = -1;
+            fclose(f);
+        }
+        pkg_of[k] = id;
+        if (id >= 0 && std::find(pkg_ids.begin(), pkg_ids.end(), id) == pkg_ids.end()) pkg_ids.push_back(id);
+    }
+    std::sort(pkg_ids.begin(), pkg_ids.end());
+    int my_sock = -1;
+    std::vector<int> sock_cpus;
+    for (size_t i = 0; i < pkg_ids.size() && my_sock < 0; ++i) {
+        std::vector<int> cs;
+        for (size_t k = 0; k < online.size(); ++k)
+            if (pkg_of[k] == pkg_ids[i]) cs.push_back(online[k]);
+        if (intersects(cs)) {
+            my_sock = (int)i;
+            sock_cpus = cs;
+        }
+    }
+    if (pkg_ids.size() > 1) {
+        // the NUMA node of the last level (0 without one) inside this socket: no socket level
+        const int numa_id = n >= 1 ? color[n - 1] : 0;
+        bool inside = false;
+        if (numa_id >= 0 && (size_t)numa_id < node_cpus.size()) {
+            inside = true;
+            for (int c : node_cpus[numa_id])
+                if (std::find(sock_cpus.begin(), sock_cpus.end(), c) == sock_cpus.end()) inside = false;
+        }
+        if (!inside && n < max_levels) color[n++] = my_sock;
+    }
+    return n;
+}
+
+// MV2AMD_TOPO override: level l's ids are the l-th ';'-separated list, one id per local rank
+static int topo_override(int rank, int *color, int max_levels) {
+    const char *v = getenv("MV2AMD_TOPO");
+    if (!v || !*v) return -1;
+    int n = 0;
+    for (const char *p = v; *p && n < max_levels;) {
+        int idx = 0, val = 0;
+        bool found = false;
+        while (*p && *p != ';') {
+            char *e = nullptr;
+            const long x = strtol(p, &e, 10);
+            if (e == p) break;
+            if (idx == rank) {
+                val = (int)x;
+                found = true;
+            }
+            ++idx;
+            p = e;
+            if (*p == ',') ++p;
+        }
+        color[n++] = found ? val : 0;
+        while (*p && *p != ';') ++p;
+        if (*p == ';') ++p;
+    }
+    return n;
+}
+
 int world_init() {
     World &w = g_world;
     if (w.inited) return 0;
+    const auto t_init = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     const char *rn[] = {"MV2_COMM_WORLD_RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "RANK", nullptr};
     const char *sn[] = {"MV2_COMM_WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "WORLD_SIZE", nullptr};
     const char *ln[] = {"MV2_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", nullptr};
@@ -231,6 +360,8 @@ int world_init() {
             hipDeviceGetAttribute(&me.pci_device, hipDeviceAttributePciDeviceId, w.device);
         }
         memcpy(&me.knobs, &knobs(), sizeof(Knobs));
+        me.topo_nlevels = topo_override(w.rank, me.topo_color, kTopoLevels);
+        if (me.topo_nlevels < 0) me.topo_nlevels = my_topology(me.topo_color, kTopoLevels);
         w.shm->attached.fetch_add(1);
         host_barrier();  // everyone attached and published pid/device/knobs
         // the algorithm choice (and with it the kernels' flag pairing) must agree on every
@@ -240,6 +371,18 @@ int world_init() {
                 MV2_ERR("MV2_* collective selection knobs differ between rank %d and rank %d", w.rank, j);
                 return E_OTHER;
             }
+
+        // topology levels (orders.h Topo): every rank's cluster ids, levels past a rank's
+        // own count read 0 (mv2_intra_node_cluster_at_level is zero-initialised)
+        {
+            Topo t{};
+            for (int j = 0; j < w.size && j < kMaxRanks; ++j) {
+                const ShmRank &q = w.shm->r[j];
+                if (q.topo_nlevels > t.nlevels) t.nlevels = q.topo_nlevels;
+                for (int l = 0; l < kTopoLevels; ++l) t.color[l][j] = l < q.topo_nlevels ? q.topo_color[l] : 0;
+            }
+            topo_set(t);
+        }
 
         // ranks sharing one GPU (tests run several ranks on one device): the
         // maximum over all GPUs, so every rank derives the same kernel grids
@@ -382,25 +525,31 @@ int world_init() {
     }
     w.inited = true;
     if (w.size > 1 && w.size <= kMaxRanks && !control_only && env_long("MV2AMD_SELFTEST", 1) != 0) {
+        const auto t_st = std::chrono::steady_clock::now();
         int rc = coll_selftest();
+        w.selftest_ms = ms_since(t_st);
+        const auto t_tune = std::chrono::steady_clock::now();
         if (!rc) rc = pipe_autotune();
+        w.tune_ms = ms_since(t_tune);
         if (rc) {
             w.inited = false;
             return rc;
         }
     }
     if (w.nnodes > 1) {
-        if (w.rank == 0) {
-            const int rc = net_init();
-            if (rc) {
-                w.inited = false;
-                return rc;
-            }
+        int rc = w.rank == 0 ? net_init() : 0;
+        if (w.shm && w.rank == 0) w.shm->net_rc.store(rc);
+        host_barrier();  // the node's leader is linked to every other node (or failed: all ranks fail)
+        if (w.shm) rc = w.shm->net_rc.load();
+        if (rc) {
+            if (w.rank != 0) MV2_ERR("the node leader's inter-node bootstrap failed");
+            w.inited = false;
+            return rc;
         }
-        host_barrier();  // the node's leader is linked to every other node
     }
-    MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d)", w.grank, w.gsize, w.rank, w.device,
-              w.nshare, w.node, w.nnodes);
+    w.init_ms = ms_since(t_init);
+    MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d): %.1f ms (self-test %.1f, autotune %.1f)",
+              w.grank, w.gsize, w.rank, w.device, w.nshare, w.node, w.nnodes, w.init_ms, w.selftest_ms, w.tune_ms);
     return 0;
 }
 

@@ -73,13 +73,16 @@ struct alignas(64) ShmRank {
     int selftest_ok;  // coll_selftest verdict of this rank (agreed through host_barrier)
     double tune_us[kTuneMax];  // pipe_autotune: this rank's time per candidate tiling
     Knobs knobs;      // MV2_* selection knobs as this rank parsed them (must agree)
+    int topo_nlevels;               // this rank's topology levels (world.cpp my_topology)
+    int topo_color[kTopoLevels];    // its cluster id per level
 };
 
 struct ShmSeg {
     std::atomic<uint64_t> magic;
     std::atomic<int> attached;
     int size;
-    int pad;
+    std::atomic<int> tune_stop;  // pipe_autotune: rank 0 ends the probe once its time budget is spent
+    std::atomic<int> net_rc;     // the leader's inter-node bootstrap result, for the node's other ranks
     ShmRank r[kShmMaxRanks];
     P2PChan chan[kMaxRanks][kMaxRanks];  // [src][dst]
 };
@@ -149,6 +152,7 @@ struct World {
     int tune_grid[kTuneMax] = {};
     size_t tune_sub[kTuneMax] = {};
     double tune_us[kTuneMax] = {};                // max over ranks per candidate
+    double init_ms = 0, selftest_ms = 0, tune_ms = 0;  // MPI_Init wall time and its self-test / autotune parts
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)

@@ -77,6 +77,8 @@ def lib():
         L.oracle_reduce_scatter.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(l), vp, i, i, kp, i]
         L.oracle_iallreduce_select.argtypes = [i, l, i, i, l]
         L.oracle_reduce_scatter_block_select.argtypes = [i, l, i, l]
+        L.oracle_set_topology.argtypes = [i, ctypes.POINTER(i), i]
+        L.oracle_set_topology.restype = None
         _lib = L
     return _lib
 
@@ -220,3 +222,10 @@ def ireduce_ref(sends, count, dtype_handle, op_handle, root, opkind=0):
 
 def reduce_scatter_block_select(n, recvcount, dtype_handle, long_msg=524288):
     return lib().oracle_reduce_scatter_block_select(n, recvcount, dtype_handle, long_msg)
+
+
+def set_topology(levels, n):
+    """Intra-node topology of the topology-aware shm tree: levels = [[cluster id of rank r at level l
+    for r < n] for each level l] (the NUMA node, then the socket); [] = one group."""
+    flat = [c for lv in levels for c in lv]
+    lib().oracle_set_topology(len(levels), (ctypes.c_int * max(1, len(flat)))(*flat), n)

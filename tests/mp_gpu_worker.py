@@ -405,16 +405,17 @@ def main():
             assert L.MPI_Type_vector(nb, 4, 8, TYPES["MPI_FLOAT"][0], ctypes.byref(vt)) == 0
             assert L.MPI_Type_commit(ctypes.byref(vt)) == 0
             ext_f = (nb - 1) * 8 + 4
-            elem = (np.arange(nb)[:, None] * 8 + np.arange(4)[None, :]).ravel()
             FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                                   ctypes.POINTER(ctypes.c_int))
 
-            def uop(inp, io, ln, dt):
+            def uop(inp, io, ln, dt):  # strided views of the c elements' type maps
                 c = ln[0]
-                idx = (np.arange(c)[:, None] * ext_f + elem[None, :]).ravel()
-                a = np.ctypeslib.as_array((ctypes.c_float * (c * ext_f)).from_address(inp))
-                b = np.ctypeslib.as_array((ctypes.c_float * (c * ext_f)).from_address(io))
-                b[idx] = a[idx] * np.float32(0.5) + b[idx] * np.float32(1.5)
+                shape, strides = (c, nb, 4), (ext_f * 4, 32, 4)
+                a = np.lib.stride_tricks.as_strided(
+                    np.ctypeslib.as_array((ctypes.c_float * (c * ext_f)).from_address(inp)), shape, strides)
+                b = np.lib.stride_tricks.as_strided(
+                    np.ctypeslib.as_array((ctypes.c_float * (c * ext_f)).from_address(io)), shape, strides)
+                b[...] = a * np.float32(0.5) + b * np.float32(1.5)
             cb = FN(uop)
             op = ctypes.c_int()
             L.MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), 1, ctypes.byref(op))

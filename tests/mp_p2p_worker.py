@@ -145,6 +145,42 @@ def main():
     rq = ctypes.c_int()
     assert L.MPI_Ibarrier(WORLD, ctypes.byref(rq)) == 0 and L.MPI_Wait(ctypes.byref(rq), None) == 0
 
+    # 8. MPI_Testall is all-or-nothing (MPI-3.1 §3.7.5): with one receive finished and one
+    #    pending it returns flag = 0 and leaves both handles (and the finished one) intact
+    if rank == 1:
+        s20 = m.DeviceBuffer.from_array(pattern(777, 1, 0, 20))
+        assert L.MPI_Send(s20.ptr, 777, BYTE, 0, 20, WORLD) == 0
+        assert L.MPI_Recv(s20.ptr, 4, BYTE, 0, 22, WORLD, None) == 0  # rank 0's go-ahead
+        s21 = m.DeviceBuffer.from_array(pattern(999, 1, 0, 21))
+        assert L.MPI_Send(s21.ptr, 999, BYTE, 0, 21, WORLD) == 0
+    elif rank == 0:
+        import time
+        r20, r21 = m.DeviceBuffer(777), m.DeviceBuffer(999)
+        qa, qb = ctypes.c_int(), ctypes.c_int()
+        assert L.MPI_Irecv(r20.ptr, 777, BYTE, 1, 20, WORLD, ctypes.byref(qa)) == 0
+        assert L.MPI_Irecv(r21.ptr, 999, BYTE, 1, 21, WORLD, ctypes.byref(qb)) == 0
+        pair = (ctypes.c_int * 2)(qa.value, qb.value)
+        flag = ctypes.c_int(1)
+        t_end = time.time() + 0.3
+        while time.time() < t_end:  # the tag-20 message lands meanwhile; tag 21 cannot
+            assert L.MPI_Testall(2, pair, ctypes.byref(flag), None) == 0
+            assert flag.value == 0 and pair[0] == qa.value and pair[1] == qb.value, "Testall touched a request"
+        one = (ctypes.c_int * 1)(qa.value)
+        flag.value = 0
+        while not flag.value:
+            assert L.MPI_Testall(1, one, ctypes.byref(flag), None) == 0
+        assert one[0] == 0x2c000000
+        assert np.array_equal(r20.download(np.uint8, count=777), pattern(777, 1, 0, 20))
+        go = m.DeviceBuffer(4)
+        assert L.MPI_Send(go.ptr, 4, BYTE, 1, 22, WORLD) == 0
+        rest = (ctypes.c_int * 1)(qb.value)
+        flag.value = 0
+        while not flag.value:
+            assert L.MPI_Testall(1, rest, ctypes.byref(flag), None) == 0
+        assert rest[0] == 0x2c000000
+        assert np.array_equal(r21.download(np.uint8, count=999), pattern(999, 1, 0, 21))
+    L.MPI_Barrier(WORLD)
+
     L.MPI_Finalize()
     print(f"rank {rank} p2p ok", flush=True)
 

@@ -136,3 +136,38 @@ def test_mv2run_node_emulation_environment(tmp_path):
         assert e["MV2AMD_NSHARE"] == "6" and e["MV2AMD_DEVICE"] == "0"
     assert len({e["MV2AMD_BOOT_PORT"] for e in envs}) == 1 and envs[0]["MV2AMD_BOOT_PORT"]
     assert len({e["MV2AMD_JOBID"] for e in envs}) == 1
+
+
+def _mn_knob_worker(rank, size, ppn, jobid, port, q):
+    try:
+        os.environ.update(MV2AMD_CONTROL_PLANE_ONLY="1", MV2AMD_JOBID=jobid, RANK=str(rank), WORLD_SIZE=str(size),
+                          LOCAL_RANK=str(rank % ppn), LOCAL_WORLD_SIZE=str(ppn), MV2AMD_BOOT_ADDR="127.0.0.1",
+                          MV2AMD_BOOT_PORT=str(port), MV2AMD_TIMEOUT_S="30")
+        if rank // ppn == 1:  # the second node's ranks agree among themselves, not with node 0
+            os.environ["MV2_ALLRED_USE_RING"] = "0"
+        import mvapich2_amd as m
+        q.put((rank, m.lib().mv2h_init()))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+
+
+def test_multinode_knob_mismatch_fails_every_rank():
+    """Nodes started with different MV2_* selection knobs would pair different schedules: node 0's
+    leader refuses the job at the rendezvous (runtime/internode.cpp Hello.knob_hash) and every rank
+    of every node fails MPI_Init instead of hanging or computing garbage later."""
+    import socket
+    size, ppn = 4, 2
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    jobid = "k" + uuid.uuid4().hex[:12]
+    procs = [ctx.Process(target=_mn_knob_worker, args=(r, size, ppn, jobid, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v not in (0, None) and not isinstance(v, str) for v in res.values()), res

@@ -355,35 +355,46 @@ def test_mv2_selection_knobs(n, tmp_path):
                 assert_bytes_equal(res(case["id"], n - 1), want, case["type"], case["count"], f"{case['id']} {env}")
 
 
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize("n", [2, 3, 8])
 def test_user_op_on_strided_vector_operand(n, tmp_path):
     """configs[4]: MPI_Allreduce with a commutative user op on MPI_Type_vector(N, 4, 8, MPI_FLOAT)
     operands (the reference rejects predefined ops on derived types).  The result follows the
     reference's order for the call and only type-map bytes of recvbuf are written (gap bytes keep
-    their -7.0): MPIR_Localcopy / uop calls touch the type map only."""
+    their -7.0): MPIR_Localcopy / uop calls touch the type map only.  The operands move packed
+    and ring chunks are evaluated by their owner rank only (mpi/user_coll.cpp)."""
     cases = []
-    for seed, (nb, cnt) in enumerate(((64, 3), (1024, 40), (4096, 33)), start=700):
-        # 4096 x 16 B x 33 elements = 2.1 MiB: the ring wrapper with a remainder
+    sizes = [(64, 3), (1024, 40), (4096, 33), (262144, 5)]
+    # 4096 x 16 B x 33 elements = 2.1 MiB: the ring wrapper with a remainder; 5 x 4 MiB: the ring
+    # over 5 // n * n elements, recursive doubling on the rest (all of it at n = 8)
+    if n == 8:
+        sizes.append((4096, 1024))  # 64 MiB of payload (128 MiB span): the ring, one chunk per rank
+    for seed, (nb, cnt) in enumerate(sizes, start=700):
         cases.append({"id": f"uv{seed}", "kind": "user_vector_allreduce", "nblocks": nb, "count": cnt,
                       "seed": seed})
-    res = run_workers(n, cases, tmp_path)
+    res = run_workers(n, cases, tmp_path, timeout=360)
     fn = lambda a, b: (a * np.float32(0.5) + b * np.float32(1.5)).astype(np.float32)
     for case in cases:
         nb, cnt = case["nblocks"], case["count"]
         ext_f = (nb - 1) * 8 + 4
-        elem = (np.arange(nb)[:, None] * 8 + np.arange(4)[None, :]).ravel()
-        idx = (np.arange(cnt)[:, None] * ext_f + elem[None, :]).ravel()
+
+        def typemap(x):  # (cnt, nb, 4) view of the type map
+            return np.lib.stride_tricks.as_strided(x, (cnt, nb, 4), (ext_f * x.itemsize, 32, 4))
+
+        def gaps(x):  # the 4 floats after each block but the last of every element
+            return np.lib.stride_tricks.as_strided(x[4:], (cnt, nb - 1, 4), (ext_f * x.itemsize, 32, 4))
         packed = []
         for r in range(n):
             x = np.random.default_rng(case["seed"] * 1000 + r).standard_normal(cnt * ext_f).astype(np.float32)
-            packed.append(x[idx].reshape(cnt, nb * 4))
+            packed.append(typemap(x).reshape(cnt, nb * 4).copy())
+            del x
         want = ref_user.allreduce(packed, fn, 1, None, cnt, nbytes=cnt * nb * 16)
-        gap = np.ones(cnt * ext_f, bool)
-        gap[idx] = False
+        del packed
         for r in range(n):
             got = res(case["id"], r).view(np.float32)
-            assert np.array_equal(got[idx].view(np.uint32), want[r].ravel().view(np.uint32)), (case["id"], r)
-            assert np.all(got[gap] == -7.0), f"{case['id']} rank {r}: gap bytes of the vector type were written"
+            assert np.array_equal(typemap(got).reshape(cnt, nb * 4).view(np.uint32),
+                                  want[r].reshape(cnt, nb * 4).view(np.uint32)), (case["id"], r)
+            assert np.all(gaps(got) == -7.0), f"{case['id']} rank {r}: gap bytes of the vector type were written"
 
 
 @pytest.mark.timeout(480)
@@ -532,3 +543,32 @@ def test_graph_captured_allreduce(n, tmp_path):
         for r in range(n):
             assert_bytes_equal(got[r][off:off + 4096 * 4], want[r], "MPI_FLOAT", 4096, f"host lane after replay {k} rank {r}")
         off += 4096 * 4
+
+
+@pytest.mark.parametrize("n,topo", [(4, "0,1,0,1"), (8, "0,1,0,1,0,1,0,1"), (8, "0,0,1,1,2,2,3,3;0,0,0,0,1,1,1,1")])
+def test_gpu_topology_levels(n, topo, tmp_path):
+    """The topology-aware shm tree over several levels (MV2AMD_TOPO sets every rank's NUMA / socket
+    ids; MPI_Init publishes them): small allreduces (<= 2 KiB) and topology-aware reduces on the
+    device, bit-exact with the oracle's multi-level simulation (tests/test_topology.py restates the
+    levels on the CPU)."""
+    levels = [[int(c) for c in lv.split(",")] for lv in topo.split(";")]
+    cases = []
+    for seed, (t, op, count) in enumerate((("MPI_FLOAT", "MPI_SUM", 7), ("MPI_DOUBLE", "MPI_SUM", 100),
+                                           ("MPI_FLOAT", "MPI_MAX", 500), ("MPI_FLOAT", "MPI_SUM", 512)), start=950):
+        cases.append({"id": f"tp{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
+        cases.append({"id": f"tr{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "root": n - 1})
+    res = run_workers(n, cases, tmp_path, extra_env={"MV2AMD_TOPO": topo, "MV2_USE_TOPO_AWARE_REDUCE": "1"})
+    oracle.set_topology(levels, n)
+    try:
+        knobs = oracle.default_knobs(use_topo_reduce=1)
+        for case in cases:
+            if case["kind"] == "allreduce":
+                want = expected_allreduce(case, n, knobs)
+                for r in range(n):
+                    assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"], f"{case['id']} {topo} rank {r}")
+            else:
+                want = expected_reduce(case, n, knobs)
+                assert_bytes_equal(res(case["id"], n - 1), want, case["type"], case["count"], f"{case['id']} {topo}")
+    finally:
+        oracle.set_topology([], n)

@@ -111,8 +111,15 @@ def expected_allreduce(sends, count, t, op, ppn, in_place=False):
     pt2pt_rs where the 16-ppn table names it (ppn >= 3, n <= 8), else two-level"""
     n = len(sends)
     if count * TYPES[t][2] >= 2 << 20 and (in_place or count < n) and n <= 8:  # the wrapper's pt2pt_rs
-        return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op],
-                                algo=oracle.ALGOS.index("pt2pt_rs"))
+        rs = oracle.ALGOS.index("pt2pt_rs")
+        main = (count // n) * n if in_place else 0
+        if not main or main == count:
+            return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op], algo=rs)
+        # IN_PLACE: the ring body's own pt2pt_rs on (count / n) * n elements, then the remainder's
+        ext = TYPES[t][3]
+        head = oracle.allreduce([x[:main * ext].copy() for x in sends], main, TYPES[t][0], OPS[op], algo=rs)
+        tail = oracle.allreduce([x[main * ext:].copy() for x in sends], count - main, TYPES[t][0], OPS[op], algo=rs)
+        return [np.concatenate([head[r], tail[r]]) for r in range(n)]
     if count * TYPES[t][2] >= 2 << 20 and count >= n and not in_place:
         main = ring_flat(sends, count, t, op)
         rem = count % n
@@ -154,14 +161,20 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                          ("MPI_DOUBLE", "MPI_SUM", 300001)):
         cases.append({"id": f"mR{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
         seed += 1
-    for count in (600000, 70001):  # IN_PLACE: from 2 MiB the wrapper's pt2pt_rs over every rank
+    for count in (600000, 600005, 70001):  # IN_PLACE: from 2 MiB the wrapper's pt2pt_rs over every rank
         cases.append({"id": f"mP{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
                       "count": count, "seed": seed})
         seed += 1
-    # nonblocking across nodes: complete at initiation (integer data: exact in any order)
-    cases.append({"id": f"mi{seed}", "kind": "iallreduce", "type": "MPI_INT", "op": "MPI_SUM", "count": 5000,
-                  "seed": seed})
-    seed += 1
+    # nonblocking across nodes: MVAPICH2's nonblocking schedules are flat over the job (Iallreduce =
+    # Ireduce to rank 0 + Ibcast, Ireduce = binomial); they complete at initiation here
+    for t, count in (("MPI_INT", 5000), ("MPI_FLOAT", 5000), ("MPI_FLOAT", 70001), ("MPI_DOUBLE", 30)):
+        cases.append({"id": f"mi{seed}", "kind": "iallreduce", "type": t, "op": "MPI_SUM", "count": count,
+                      "seed": seed})
+        seed += 1
+    for count, root in ((1000, n - 1), (70001, 1 % n)):
+        cases.append({"id": f"mj{seed}", "kind": "ireduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
     for t, op, count, root in (("MPI_FLOAT", "MPI_SUM", 1000, n - 1), ("MPI_INT", "MPI_SUM", 70001, 1 % n),
                                ("MPI_DOUBLE", "MPI_MIN", 300, 0)):
         cases.append({"id": f"mr{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
@@ -184,7 +197,14 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        if k in ("allreduce", "iallreduce", "allreduce_inplace"):
+        if k == "iallreduce" and n <= 8:
+            want = oracle.iallreduce_ref(sends, count, TYPES[t][0], OPS[case["op"]])
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} iallreduce rank {r}")
+        elif k == "ireduce":
+            want = oracle.ireduce_ref(sends, count, TYPES[t][0], OPS[case["op"]], case["root"])
+            assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} ireduce root {case['root']}")
+        elif k in ("allreduce", "iallreduce", "allreduce_inplace"):
             want = expected_allreduce(sends, count, t, case["op"], ppn, in_place=k == "allreduce_inplace")
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
