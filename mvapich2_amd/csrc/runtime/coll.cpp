@@ -2071,6 +2071,13 @@ static bool capturing(void *stream) {
 }
 static int enqueue_checks(const void *send, const void *recv, void *stream, bool graph_ok = false) {
     if (!stream) return E_ARG;
+    // a destroyed stream or one of another device is an argument error, not a launch into it
+    int sdev = -1;
+    if (hipStreamGetDevice((hipStream_t)stream, &sdev) != hipSuccess || sdev != world().device) {
+        (void)hipGetLastError();
+        MV2_ERR("stream-ordered call: the stream is not a live stream of this rank's device");
+        return E_ARG;
+    }
     // host-managed epochs and parities would be replayed by a graph: a captured call must take
     // the graph lane (allreduce on 16-byte-aligned device buffers), anything else is refused
     if (capturing(stream)) {

@@ -419,6 +419,18 @@ def test_full_size_baseline_configs(n, tmp_path):
             assert int(res(case["id"], r)[0]) == 0, (case["id"], r, int(res(case["id"], r)[0]))
 
 
+@pytest.mark.timeout(400)
+def test_allreduce_1gib_bit_exact(tmp_path):
+    """configs[2]'s upper end: a 1 GiB fp32 SUM MPI_Allreduce of random N(0,1) operands at 2 ranks
+    (the ring wrapper: 2 chunks of 512 MiB, each 16 rounds of the 32 MiB arena slots), every rank's
+    whole result bit-exact against the oracle's simulation of the reference's ring."""
+    n = 2
+    cases = [{"id": "gb1", "kind": "big_allreduce_rand", "count": 1 << 28, "seed": 11}]
+    res = run_workers(n, cases, tmp_path, timeout=360)
+    for r in range(n):
+        assert int(res("gb1", r)[0]) == 0, (r, int(res("gb1", r)[0]))
+
+
 def test_mpit_counters_follow_the_selection(tmp_path):
     """MPI_T (mpi/mpit.cpp): a started counter handle counts the calls of the algorithms the
     reference's call chain runs for each call (its MPIR_T_PVAR_COUNTER_INC sites), 4 ranks:
