@@ -170,7 +170,8 @@ enum mv2h_coll {
 /* opkind: 0 builtin, 1 commutative user op, 2 non-commutative user op.
  * *algo: 0 none, 1 shmem_linear, 2 pt2pt_rs, 3 pt2pt_rd, 4 ring_wrapper,
  * 5 topo_tree, 6 two_level_p2p, 7 binomial, 8 knomial, 9 redscat_gather,
- * 10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic, 14 reduce_topo.
+ * 10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic, 14 reduce_topo,
+ * 15 rs_noncomm_pof2, 16 rs_noncomm_rd (non-commutative user ops' reduce-scatter).
  * *unpinned = 1 when the reference's own result depends on message arrival. */
 int mv2h_plan(int coll, int n, int rank, int root, size_t count, const size_t *counts, int dtype, int opkind,
               int in_place, int *algo, int *inner, int *unpinned, mv2h_progset *ps);

@@ -295,11 +295,12 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
     return run_split(o, count, sp, op.fn, recvbuf, me == root);
 }
 
-// Reduce_scatter.  Commutative: the order of MPIR_Reduce_scatter_MV2's choice for this rank's
-// block (ring, recursive halving, pairwise or reduce + scatter).  Non-commutative
-// (MPIR_Reduce_scatter_non_comm_MV2, not restated): the canonical rank order
-// x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an associative op,
-// applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block.
+// Reduce_scatter: the order of MPIR_Reduce_scatter_MV2's choice for this rank's block — ring,
+// recursive halving, pairwise or reduce + scatter for commutative ops,
+// MPIR_Reduce_scatter_non_comm_MV2 (mirror-permuted halving or recursive doubling) for
+// non-commutative ones.  The nonblocking non-commutative schedules are not restated: those take
+// the canonical rank order x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
+// associative op, applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block.
 int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, const HostOp &op) {
     World &w = world();
     const Typed t = typed(dt);
@@ -315,12 +316,11 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     ProgSet ps{};
     Plan p;
     int rc;
-    if (op.opk != OPK_USER_NONCOMM) {
+    if (op.opk != OPK_USER_NONCOMM || nbc_kind() == NBC_NONE) {
         if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)t.tsize, (int)t.extent, &p, op.opk))) return rc;
         pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
         ps = p.ps;
     } else {
-        if (n > 1) pvar_note_id(PV_RS_NON_COMM);
         ps.nprog = 1;
         ps.p[0].nsteps = (uint8_t)(n - 1);
         ps.p[0].res = (uint8_t)(n - 1);

@@ -138,7 +138,7 @@ const char *algo_name(int a) {
     static const char *names[ALG_COUNT] = {
         "none", "shmem_linear", "pt2pt_rs", "pt2pt_rd", "ring_wrapper", "topo_tree", "two_level_p2p",
         "binomial", "knomial", "redscat_gather", "rs_ring", "rs_rec_halving", "rs_pairwise", "rs_basic",
-        "reduce_topo"};
+        "reduce_topo", "rs_noncomm_pof2", "rs_noncomm_rd"};
     return (a >= 0 && a < ALG_COUNT) ? names[a] : "?";
 }
 
@@ -479,6 +479,85 @@ int rs_pairwise_expr(Sym &s, int n, int me) {
     return acc;
 }
 
+// MPIR_Reduce_scatter_noncomm_MV2 (red_scat_osu.c:132-290), a power-of-two size with equal
+// counts: the blocks are mirror-permuted (:90-103, :211-222), then at step k rank r and its peer
+// r ^ 2^k split their current range of positions, the higher rank keeping the upper half, and
+// both reduce the kept half as uop(in = the lower rank's partial, inout = the higher rank's)
+// (:260-272).  Rank r ends at position mirror(r), i.e. with block r.
+int rs_noncomm_pof2_expr(Sym &s, int n, int me) {
+    std::vector<std::vector<int>> val(n, std::vector<int>(n));
+    for (int r = 0; r < n; ++r)
+        for (int p = 0; p < n; ++p) val[r][p] = s.leaf(r);
+    std::vector<int> lo(n, 0), sz(n, n);
+    for (int k = 0; (1 << k) < n; ++k) {
+        std::vector<std::vector<int>> nv = val;
+        for (int r = 0; r < n; ++r) {
+            const int q = r ^ (1 << k), half = sz[r] / 2;
+            const int keep = r > q ? lo[r] + half : lo[r];
+            const int hi = std::max(r, q), low = std::min(r, q);
+            for (int p = keep; p < keep + half; ++p) nv[r][p] = s.op(val[hi][p], val[low][p]);
+            lo[r] = keep;
+            sz[r] = half;
+        }
+        val.swap(nv);
+    }
+    return val[me][lo[me]];
+}
+
+// MPIR_Reduce_scatter_non_comm_MV2's recursive doubling (red_scat_osu.c:1478-1722), any size and
+// counts: at mask 2^i every rank exchanges with rank ^ mask all blocks outside the partner's
+// subtree [dst_tree_root, +mask); where the partner subtree is cut off by the size, the ranks of
+// this subtree that got data hand their received blocks down to the others (:1592-1656); then
+// uop(in = received, inout = results) when the partner subtree is the lower one, else
+// uop(in = results, inout = received) (:1668-1720).  Expressions are per block; the result is
+// block `me` on rank me.
+int rs_noncomm_rd_expr(Sym &s, int n, int me) {
+    std::vector<std::vector<int>> res(n, std::vector<int>(n)), rcv(n, std::vector<int>(n, -1));
+    for (int r = 0; r < n; ++r)
+        for (int b = 0; b < n; ++b) res[r][b] = s.leaf(r);
+    for (int mask = 1, i = 0; mask < n; mask <<= 1, ++i) {
+        std::vector<int> dtr(n), mtr(n);
+        std::vector<bool> got(n, false);
+        for (int r = 0; r < n; ++r) {
+            dtr[r] = ((r ^ mask) >> i) << i;
+            mtr[r] = (r >> i) << i;
+        }
+        auto outside = [&](int b, int root) { return b < root || b >= root + mask; };
+        const std::vector<std::vector<int>> snap = res;
+        for (int r = 0; r < n; ++r) {
+            const int dst = r ^ mask;
+            if (dst >= n) continue;
+            for (int b = 0; b < n; ++b)
+                if (outside(b, dtr[r])) rcv[r][b] = snap[dst][b];
+            got[r] = true;
+        }
+        int k = 0;
+        for (int j = mask; j; j >>= 1) ++k;
+        --k;
+        for (int tm = mask >> 1; tm; tm >>= 1, --k) {
+            std::vector<std::pair<int, int>> moves;
+            for (int r = 0; r < n; ++r) {
+                if (dtr[r] + mask <= n) continue;
+                const int npc = n - mtr[r] - mask, d = r ^ tm, root = (r >> k) << k;
+                if (d > r && r < root + npc && d >= root + npc && d < n) moves.push_back({r, d});
+            }
+            for (const auto &mv : moves) {
+                for (int b = 0; b < n; ++b)
+                    if (outside(b, dtr[mv.second])) rcv[mv.second][b] = rcv[mv.first][b];
+                got[mv.second] = true;
+            }
+        }
+        for (int r = 0; r < n; ++r) {
+            if (!got[r]) continue;
+            for (int b = 0; b < n; ++b) {
+                if (!outside(b, dtr[r]) || rcv[r][b] < 0) continue;
+                res[r][b] = dtr[r] < mtr[r] ? s.op(res[r][b], rcv[r][b]) : s.op(rcv[r][b], res[r][b]);
+            }
+        }
+    }
+    return res[me][me];
+}
+
 // tuning-table index of a message size (allreduce_osu.c:3241-3277,
 // reduce_osu.c:2556-2586): 0 below the smallest entry, the last entry above
 // the largest, else log2 of the largest power of two <= nbytes over the smallest
@@ -750,10 +829,27 @@ static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int ts
                                      int opk) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
-    if (opk == OPK_USER_NONCOMM) return E_INTERN;  // MPIR_Reduce_scatter_non_comm_MV2: not restated here
-    const Knobs &K = knobs();
     size_t total = 0;
     for (int j = 0; j < n; ++j) total += counts[j];
+    if (opk == OPK_USER_NONCOMM) {
+        // MPIR_Reduce_scatter_MV2 sends every non-commutative op to MPIR_Reduce_scatter_non_comm_MV2
+        // (red_scat_osu.c:1895-1898): the pof2 / equal-count special case or recursive doubling
+        int pof2 = 1;
+        while (pof2 < n) pof2 <<= 1;
+        bool regular = true;
+        for (int j = 0; j + 1 < n; ++j) regular = regular && counts[j] == counts[j + 1];
+        Sym s;
+        int e;
+        if (pof2 == n && regular) {
+            p->algo = ALG_RS_NONCOMM_POF2;
+            e = rs_noncomm_pof2_expr(s, n, me);
+        } else {
+            p->algo = ALG_RS_NONCOMM_RD;
+            e = rs_noncomm_rd_expr(s, n, me);
+        }
+        return single_expr(s, e, p->ps) ? 0 : E_INTERN;
+    }
+    const Knobs &K = knobs();
     const long nbytes = (long)total * tsize;
     // default table (red_scat_tuning.c:214-287), first entry (numproc 8) for n <= 8
     int algo;

@@ -34,6 +34,8 @@ enum Algo : int {
     ALG_RS_PAIRWISE = 12,    // MPIR_Reduce_scatter_Pair_Wise_MV2 (:786)
     ALG_RS_BASIC = 13,       // MPIR_Reduce_Scatter_Basic_MV2 (:300): MPIR_Reduce_MV2 to 0 + scatter
     ALG_REDUCE_TOPO = 14,    // MPIR_Reduce_topo_aware_hierarchical_MV2 (reduce_osu.c:206)
+    ALG_RS_NONCOMM_POF2 = 15,// MPIR_Reduce_scatter_noncomm_MV2 (red_scat_osu.c:132): pof2, equal counts
+    ALG_RS_NONCOMM_RD = 16,  // MPIR_Reduce_scatter_non_comm_MV2's recursive doubling (:1478)
     ALG_COUNT
 };
 

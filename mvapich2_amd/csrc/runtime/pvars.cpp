@@ -75,6 +75,9 @@ const PvarDesc kDesc[PV_COUNT] = {
     // MPIR_Reduce_scatter_non_comm_MV2 :1394
     {"mv2_coll_reduce_scatter_non_comm", "mv2_coll_timer_reduce_scatter_non_comm", "Reduce_scatter Algorithms",
      "Number of times MV2 non-commutative reduce_scatter algorithm was invoked"},
+    // MPIR_Reduce_scatter_noncomm_MV2 :154 (pof2 size, equal counts, inside the above)
+    {"mv2_coll_reduce_scatter_noncomm", "mv2_coll_timer_reduce_scatter_noncomm", "Reduce_scatter Algorithms",
+     "Number of times MV2 power-of-two non-commutative reduce_scatter algorithm was invoked"},
     // reduce_shmem (allreduce_osu.c:1513) and MPIR_Reduce_shmem_MV2's shmem slot use
     {"mv2_num_shmem_coll_calls", nullptr, "Shmem Collective Calls",
      "Number of times MV2 shared-memory collective calls were invoked"},
@@ -177,6 +180,8 @@ void pvar_note(int coll, const Plan &p, bool in_place, size_t count, int n) {
         case ALG_RS_REC_HALVING: push(PV_RS_REC_HALVING); break;
         case ALG_RS_PAIRWISE: push(PV_RS_PAIRWISE); break;
         case ALG_RS_BASIC: push(PV_RS_BASIC); reduce_chain(p, p.inner); break;
+        case ALG_RS_NONCOMM_POF2: push(PV_RS_NON_COMM); push(PV_RS_NONCOMM); break;
+        case ALG_RS_NONCOMM_RD: push(PV_RS_NON_COMM); break;
         default: break;
         }
         break;

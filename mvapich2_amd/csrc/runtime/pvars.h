@@ -18,7 +18,7 @@ enum PvarId : int {
     PV_AR_SHM_RD, PV_AR_SHM_RS, PV_AR_SHM_INTRA, PV_AR_INTRA_P2P, PV_AR_2LVL, PV_AR_TOPO,
     PV_AR_RING, PV_AR_RING_WRAPPER, PV_AR_RING_INPLACE,
     PV_RED_BINOMIAL, PV_RED_REDSCAT_GATHER, PV_RED_SHMEM, PV_RED_KNOMIAL, PV_RED_TOPO, PV_RED_TWO_LEVEL_HELPER,
-    PV_RS_BASIC, PV_RS_REC_HALVING, PV_RS_PAIRWISE, PV_RS_RING, PV_RS_RING_2LVL, PV_RS_NON_COMM,
+    PV_RS_BASIC, PV_RS_REC_HALVING, PV_RS_PAIRWISE, PV_RS_RING, PV_RS_RING_2LVL, PV_RS_NON_COMM, PV_RS_NONCOMM,
     PV_NUM_SHMEM_COLL_CALLS,
     PV_COUNT
 };

@@ -29,7 +29,7 @@ class Knobs(ctypes.Structure):
 # algorithm ids (include/mv2h.h mv2h_plan)
 ALGOS = ["none", "shmem_linear", "pt2pt_rs", "pt2pt_rd", "ring_wrapper", "topo_tree", "two_level_p2p",
          "binomial", "knomial", "redscat_gather", "rs_ring", "rs_rec_halving", "rs_pairwise", "rs_basic",
-         "reduce_topo"]
+         "reduce_topo", "rs_noncomm_pof2", "rs_noncomm_rd"]
 
 
 def default_knobs(**over):

@@ -234,3 +234,105 @@ def reduce_scatter(xs, fn, dtype_handle, counts):
     else:
         raise NotImplementedError(algo)
     return out
+
+
+def _mirror(x, bits):
+    """mirror_permutation (red_scat_osu.c:90-103): the low `bits` bits reversed"""
+    r = x & ~((1 << bits) - 1)
+    for i in range(bits):
+        r |= ((x >> i) & 1) << (bits - 1 - i)
+    return r
+
+
+def reduce_scatter_noncomm(xs, fn, counts):
+    """MPIR_Reduce_scatter_non_comm_MV2 (red_scat_osu.c:1367-1760) for a non-commutative op: every
+    rank's block, rank by rank.  Power-of-two size with equal counts: MPIR_Reduce_scatter_noncomm_MV2
+    (:132-290), the blocks mirror-permuted then halved; else recursive doubling over the whole
+    buffer with the non-power-of-two hand-off inside subtrees (:1478-1722)."""
+    n = len(xs)
+    pof2, lg = 1, 0
+    while pof2 < n:
+        pof2 <<= 1
+        lg += 1
+    disps = [sum(counts[:r]) for r in range(n)]
+    total = sum(counts)
+    if pof2 == n and len(set(counts)) == 1:
+        bs = counts[0]
+        buf = []  # per rank: the mirror-permuted blocks, then the double buffer's current inout
+        for r in range(n):
+            b = np.empty_like(xs[r][:total])
+            for i in range(n):
+                m = _mirror(i, lg)
+                b[m * bs:(m + 1) * bs] = xs[r][i * bs:(i + 1) * bs]
+            buf.append(b)
+        send_off, recv_off, size = [0] * n, [0] * n, total
+        for k in range(lg):
+            size //= 2
+            snap = [b.copy() for b in buf]
+            for r in range(n):
+                peer = r ^ (1 << k)
+                if r > peer:
+                    recv_off[r] += size
+                else:
+                    send_off[r] += size
+            for r in range(n):
+                peer = r ^ (1 << k)
+                ro = recv_off[r]
+                incoming = snap[peer][ro:ro + size]  # the peer sent its send range = my recv range
+                mine = snap[r][ro:ro + size]
+                # rank > peer: op(received, mine) into mine; else op(mine, received) into received
+                buf[r][ro:ro + size] = fn(incoming, mine) if r > peer else fn(mine, incoming)
+                send_off[r] = recv_off[r]
+        return [buf[r][recv_off[r]:recv_off[r] + counts[r]].copy() for r in range(n)]
+    # recursive doubling
+    res = [x[:total].copy() for x in xs]
+    rcv = [np.empty_like(x[:total]) for x in xs]
+
+    def blocks_outside(root, mask):
+        lo, hi = disps[root] if root < n else total, disps[root + mask] if root + mask < n else total
+        return [(0, lo), (hi, total)]
+
+    mask, i = 1, 0
+    while mask < n:
+        got = [False] * n
+        dtr = [((r ^ mask) >> i) << i for r in range(n)]
+        mtr = [(r >> i) << i for r in range(n)]
+        snap = [x.copy() for x in res]
+        for r in range(n):
+            dst = r ^ mask
+            if dst < n:  # MPIC_Sendrecv: the blocks outside dst's subtree, from dst's results
+                for a, b in blocks_outside(dtr[r], mask):
+                    rcv[r][a:b] = snap[dst][a:b]
+                got[r] = True
+        # non-power-of-two: ranks with data hand their received blocks to the subtree's others
+        k = mask.bit_length() - 1
+        tm = mask >> 1
+        while tm:
+            moves = []
+            for r in range(n):
+                if dtr[r] + mask <= n:
+                    continue
+                npc = n - mtr[r] - mask
+                d = r ^ tm
+                root = (r >> k) << k
+                if d > r and r < root + npc and root + npc <= d < n:
+                    moves.append((r, d))
+            for s, d in moves:
+                for a, b in blocks_outside(dtr[d], mask):
+                    rcv[d][a:b] = rcv[s][a:b]
+                got[d] = True
+            tm >>= 1
+            k -= 1
+        for r in range(n):
+            if not got[r]:
+                continue
+            for a, b in blocks_outside(dtr[r], mask):
+                if b <= a:
+                    continue
+                if dtr[r] < mtr[r]:
+                    res[r][a:b] = fn(rcv[r][a:b], res[r][a:b])
+                else:
+                    res[r][a:b] = fn(res[r][a:b], rcv[r][a:b])
+        mask <<= 1
+        i += 1
+    return [res[r][disps[r]:disps[r] + counts[r]].copy() for r in range(n)]

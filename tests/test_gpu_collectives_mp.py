@@ -290,20 +290,12 @@ def user_allreduce_expected(n, count, commute):
 
 def user_reduce_scatter_expected(n, counts, commute):
     """commutative: MPIR_Reduce_scatter_MV2's choice (ref_user.reduce_scatter); non-commutative:
-    the canonical x_0 op (x_1 op (... op x_{n-1})) (mpi_api.cpp user_reduce_scatter)"""
+    MPIR_Reduce_scatter_non_comm_MV2 (ref_user.reduce_scatter_noncomm)"""
     total = sum(counts)
     xs = [((np.arange(total) + r) % 7).astype(np.int32) for r in range(n)]
     if commute:
         return ref_user.reduce_scatter(xs, ufn, TYPES["MPI_INT"][0], counts)
-    out, off = [], 0
-    for b in range(n):
-        blk = slice(off, off + counts[b])
-        acc = xs[n - 1][blk]
-        for i in range(n - 2, -1, -1):
-            acc = ufn(xs[i][blk], acc)
-        out.append(acc)
-        off += counts[b]
-    return out
+    return ref_user.reduce_scatter_noncomm(xs, ufn, counts)
 
 
 KNOB_RUNS = [

@@ -20,7 +20,8 @@ EXPECTED_COUNTERS = [
     "mv2_coll_reduce_binomial", "mv2_coll_reduce_redscat_gather", "mv2_coll_reduce_shmem", "mv2_coll_reduce_knomial",
     "mv2_coll_reduce_topo_aware_hierarchical", "mv2_coll_reduce_two_level_helper", "mv2_coll_reduce_scatter_basic",
     "mv2_coll_reduce_scatter_rec_halving", "mv2_coll_reduce_scatter_pairwise", "mv2_coll_reduce_scatter_ring",
-    "mv2_coll_reduce_scatter_ring_2lvl", "mv2_coll_reduce_scatter_non_comm", "mv2_num_shmem_coll_calls"]
+    "mv2_coll_reduce_scatter_ring_2lvl", "mv2_coll_reduce_scatter_non_comm", "mv2_coll_reduce_scatter_noncomm",
+    "mv2_num_shmem_coll_calls"]
 
 
 @pytest.fixture
@@ -90,7 +91,7 @@ def test_categories(T):
         names.append((name.value.decode(), nc.value, npv.value))
     assert names[0] == ("Allreduce Algorithms", 0, 18)
     assert names[1] == ("Reduce Algorithms", 0, 12)
-    assert names[2] == ("Reduce_scatter Algorithms", 0, 12)
+    assert names[2] == ("Reduce_scatter Algorithms", 0, 14)
     assert names[3] == ("Shmem Collective Calls", 0, 1)
     assert names[4][0] == "Collective Selection" and names[4][1] > 20
     idx = (ctypes.c_int * 18)()

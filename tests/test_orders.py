@@ -308,6 +308,31 @@ def test_user_op_plans_match_reference_restatement(commute):
                     off += counts[r]
 
 
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8])
+def test_noncommutative_reduce_scatter_matches_reference(n):
+    """MPIR_Reduce_scatter_non_comm_MV2 (red_scat_osu.c:1367-1760) for a non-commutative user op:
+    the power-of-two / equal-count mirror-permuted halving (MPIR_Reduce_scatter_noncomm_MV2
+    :132-290) and the recursive doubling with the non-power-of-two hand-off, against the rank-by-rank
+    restatement tests/ref_user.reduce_scatter_noncomm, with the non-associative, non-commutative
+    fn(in, io) = 2 in + 3 io."""
+    from tests import ref_user
+    fn = lambda a, b: (a * 2 + b * 3).astype(np.int64)
+    h = TYPES["MPI_INT"][0]
+    pof2 = 1 << (n - 1).bit_length()
+    for counts in ([5] * n, [1] * n, [3 + (r % 3) for r in range(n)], [0] + [4] * (n - 1), [7] * (n - 1) + [2]):
+        total = sum(counts)
+        xs = [((np.arange(total) * (r + 3) + r) % 13).astype(np.int64) for r in range(n)]
+        want = ref_user.reduce_scatter_noncomm(xs, fn, counts)
+        off = 0
+        for r in range(n):
+            algo, _, _, progs, blk = m.plan("reduce_scatter", n, r, h, counts=counts, opkind=2)
+            regular = len(set(counts)) == 1
+            assert oracle.ALGOS[algo] == ("rs_noncomm_pof2" if pof2 == n and regular else "rs_noncomm_rd")
+            got = eval_progs_fn(xs, progs, blk, off, off + counts[r], fn)
+            assert np.array_equal(got, want[r]), (n, counts, r, oracle.ALGOS[algo])
+            off += counts[r]
+
+
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 7, 8])
 def test_nonblocking_plans_match_reference(n):
     """MPI_Iallreduce / MPI_Ireduce / MPI_Ireduce_scatter(_block) and the blocking
