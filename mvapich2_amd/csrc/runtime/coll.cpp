@@ -565,8 +565,9 @@ int pipe_autotune() {
     hipDeviceSynchronize();
     // tilings x the flavour of the stores into peers' arenas (non-temporal or plain: how the
     // fabric combines them is a property of the links, measured rather than assumed)
-    static const int kGrid[] = {256, 256, 256, 128, 128, 64};
-    static const size_t kSub[] = {128 << 10, 64 << 10, 32 << 10, 256 << 10, 128 << 10, 512 << 10};
+    // (256 x 16 KiB: 8 rounds of a 32 MiB segment at 8 ranks, the deepest pipeline)
+    static const int kGrid[] = {256, 256, 256, 256, 128, 128, 64};
+    static const size_t kSub[] = {128 << 10, 64 << 10, 32 << 10, 16 << 10, 256 << 10, 128 << 10, 512 << 10};
     constexpr int kTilings = (int)(sizeof(kGrid) / sizeof(kGrid[0]));
     const int g0 = w.pipe_grid, r0 = w.pipe_rnt;
     const size_t s0 = w.pipe_sub;
@@ -2014,6 +2015,7 @@ int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
 // part (3): strided pack / unpack
 // ---------------------------------------------------------------------------
 int mv2h_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride, void *stream) {
+    hp_entry();  // a new API call: the timing events bracket its own launches
     int rc;
     if ((rc = ensure_init_for_device())) return rc;
     hipStream_t st = pick_stream(stream);
@@ -2025,6 +2027,7 @@ int mv2h_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, si
 }
 
 int mv2h_unpack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride, void *stream) {
+    hp_entry();  // a new API call: the timing events bracket its own launches
     int rc;
     if ((rc = ensure_init_for_device())) return rc;
     hipStream_t st = pick_stream(stream);
@@ -2037,6 +2040,7 @@ int mv2h_unpack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
 
 int mv2h_pack_segments(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
                        const int64_t *lens, int nseg, int unpack, void *stream) {
+    hp_entry();  // a new API call: the timing events bracket its own launches
     int rc;
     if ((rc = ensure_init_for_device())) return rc;
     hipStream_t st = pick_stream(stream);

@@ -97,6 +97,44 @@ __global__ __launch_bounds__(T) void k_pack_perm2(const v4u *__restrict__ src, v
     }
 }
 
+// write-only references over the 256 MiB span: every 16-byte unit (whole lines), or the first
+// 16 bytes of every 32-byte sector (the unpack's byte-masked write pattern without its reads)
+template <int T, bool HALF>
+__global__ __launch_bounds__(T) void k_write_only(v4u *__restrict__ dst, size_t units) {
+    const size_t u = (size_t)blockIdx.x * T + threadIdx.x;
+    if (u < units) dst[HALF ? 2 * u : u] = v4u{(unsigned)u, 1u, 2u, 3u};
+}
+// read the packed 128 MiB and write whole 32-byte sectors (payload + zeroed gap): the traffic an
+// unpack would have if it were allowed to overwrite the gaps (not a valid MPI_Unpack)
+template <int T>
+__global__ __launch_bounds__(T) void k_expand_whole(const v4u *__restrict__ src, v4u *__restrict__ dst, size_t rows) {
+    const size_t u = (size_t)blockIdx.x * T + threadIdx.x;
+    if (u < rows) {
+        const v4u v = __builtin_nontemporal_load(src + u);
+        dst[2 * u] = v;
+        dst[2 * u + 1] = v4u{0xA5A5A5A5u, 0xA5A5A5A5u, 0xA5A5A5A5u, 0xA5A5A5A5u};
+    }
+}
+// unpack, one row per lane but each workgroup owning a contiguous 1/8th-of-the-chip slab: the
+// blockIdx -> slab map keeps each XCD's L2 on its own part of the span (XCD = blockIdx % 8)
+template <int U, int T>
+__global__ __launch_bounds__(T) void k_unpack_xcd(const v4u *__restrict__ src, v4u *__restrict__ dst, size_t rows) {
+    const size_t nb = gridDim.x, per = nb / 8;
+    const size_t b = blockIdx.x, slab = (b % 8) * per + b / 8;
+    const size_t base = slab * T * U + threadIdx.x;
+    v4u v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const size_t u = base + (size_t)k * T;
+        if (u < rows) v[k] = __builtin_nontemporal_load(src + u);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const size_t u = base + (size_t)k * T;
+        if (u < rows) dst[2 * u] = v[k];
+    }
+}
+
 struct Res {
     const char *name;
     float ms;
@@ -206,13 +244,33 @@ int main() {
             hipLaunchKernelGGL((k_units_gs<4, 512, true, true>), dim3(g), dim3(512), 0, 0, dpack, dout, rows, su);
         }));
     }
+    UK(2, 256, true, false);
+    UK(1, 1024, true, false);
+    UK(2, 1024, true, false);
+    rs.push_back(time_unpack("unpack xcd-slab U=2 T=512", [&] {
+        hipLaunchKernelGGL((k_unpack_xcd<2, 512>), dim3(rows / 1024), dim3(512), 0, 0, dpack, dout, rows);
+    }));
+    rs.push_back(time_unpack("unpack xcd-slab U=4 T=256", [&] {
+        hipLaunchKernelGGL((k_unpack_xcd<4, 256>), dim3(rows / 1024), dim3(256), 0, 0, dpack, dout, rows);
+    }));
+    // write-only / whole-sector references (traffic floors of the unpack's write side)
+    rs.push_back(time_pack("ref: write-only 256 MiB whole lines", [&] {
+        hipLaunchKernelGGL((k_write_only<512, false>), dim3(span / 16 / 512), dim3(512), 0, 0, dout, span / 16);
+    }));
+    rs.push_back(time_pack("ref: write-only 16 of every 32 bytes over 256 MiB", [&] {
+        hipLaunchKernelGGL((k_write_only<512, true>), dim3(rows / 512), dim3(512), 0, 0, dout, rows);
+    }));
+    rs.push_back(time_pack("ref: read 128 MiB + write 256 MiB whole sectors (gap overwritten)", [&] {
+        hipLaunchKernelGGL((k_expand_whole<512>), dim3(rows / 512), dim3(512), 0, 0, dpack, dout, rows);
+    }));
     // references: contiguous copy of the span and of the packed bytes
     rs.push_back(time_pack("ref: copy 128 MiB contiguous (packed size)", [&] {
         hipMemcpyAsync(dpack, dspan, packed, hipMemcpyDeviceToDevice, 0);
     }));
     for (auto &r : rs) {
         const bool unpack = !strncmp(r.name, "unpack", 6);
-        const double floor_b = unpack ? (double)packed + span : (double)span + packed;
+        double floor_b = unpack ? (double)packed + span : (double)span + packed;
+        if (!strncmp(r.name, "ref: write-only", 15)) floor_b = (double)span;
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"GBps_algorithmic\": %.1f, \"GBps_hbm_floor\": %.1f, \"ok\": %s}\n",
                r.name, r.ms, 2.0 * packed / (r.ms * 1e6), floor_b / (r.ms * 1e6), r.ok ? "true" : "false");
     }
