@@ -49,9 +49,9 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None):
         so.bind(("127.0.0.1", 0))
         boot = {"MV2AMD_BOOT_ADDR": "127.0.0.1", "MV2AMD_BOOT_PORT": str(so.getsockname()[1]),
                 "MV2AMD_NSHARE": str(n),  # every emulated node's ranks share the one GPU
-                # emulated nodes oversubscribe the one GPU's queues: a slow box can stall a node's
-                # step for tens of seconds while another node's leader waits on its socket
-                "MV2AMD_TIMEOUT_S": "90"}
+                # the default 30 s: a device wait that runs out prints the epoch it waited for and
+                # the flags it saw (coll.cpp check_err_word), so a stall names itself
+                "MV2AMD_TIMEOUT_S": "30"}
         timeout = max(timeout, 240)
         so.close()
     procs = []
