@@ -8,6 +8,8 @@
 #include <cstring>
 #include <vector>
 
+#include "../mvapich2_amd/csrc/device_util.h"  // mv2::Done / block_done: the product's completion word
+
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 #define CK(x)                                                                      \
@@ -135,6 +137,29 @@ __global__ __launch_bounds__(T) void k_unpack_xcd(const v4u *__restrict__ src, v
     }
 }
 
+// the product kernel's shape with its end-of-workgroup completion (mv2::block_done: stores
+// drained, sub-counters, host word), one tile per workgroup (GS = 0) or a fixed grid striding
+// over the tiles (GS = grid): the completion's drain is paid once per workgroup
+template <int U, int T, bool UNPACK, bool DONE>
+__global__ __launch_bounds__(T) void k_units_done(const v4u *__restrict__ src, v4u *__restrict__ dst, size_t rows,
+                                                  size_t su, mv2::Done d) {
+    const size_t step = (size_t)gridDim.x * T * U;
+    for (size_t base = (size_t)blockIdx.x * T * U + threadIdx.x; base < rows; base += step) {
+        v4u v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const size_t u = base + (size_t)k * T;
+            if (u < rows) v[k] = __builtin_nontemporal_load(src + (UNPACK ? u : u * su));
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const size_t u = base + (size_t)k * T;
+            if (u < rows) dst[UNPACK ? u * su : u] = v[k];
+        }
+    }
+    if (DONE) mv2::block_done(d);
+}
+
 struct Res {
     const char *name;
     float ms;
@@ -252,6 +277,45 @@ int main() {
     }));
     rs.push_back(time_unpack("unpack xcd-slab U=4 T=256", [&] {
         hipLaunchKernelGGL((k_unpack_xcd<4, 256>), dim3(rows / 1024), dim3(256), 0, 0, dpack, dout, rows);
+    }));
+    // completion-word cost: the product's block_done on the one-tile shape and on fixed grids
+    uint32_t *dctr = nullptr;
+    uint64_t *dflag = nullptr;
+    CK(hipMalloc(&dctr, mv2::kDoneBytes));
+    CK(hipMemset(dctr, 0, mv2::kDoneBytes));
+    CK(hipHostMalloc((void **)&dflag, 64, hipHostMallocDefault));
+    static uint64_t seq = 0;
+#define DV(U, T, UNPACK, DONE, GRID)                                                                          \
+    do {                                                                                                      \
+        char *nm = new char[120];                                                                             \
+        const size_t g_ = (GRID) ? (size_t)(GRID) : (rows + (T) * (U) - 1) / ((T) * (U));                     \
+        snprintf(nm, 120, "%s %s U=%d T=%d grid=%zu", UNPACK ? "unpack" : "pack", DONE ? "done" : "nodone", U, T, g_); \
+        auto fn = [&] {                                                                                       \
+            mv2::Done d_{dctr, dflag, ++seq};                                                                 \
+            hipLaunchKernelGGL((k_units_done<U, T, UNPACK, DONE>), dim3(g_), dim3(T), 0, 0,                   \
+                               UNPACK ? dpack : dspan, UNPACK ? dout : dpack, rows, su, d_);                  \
+        };                                                                                                    \
+        rs.push_back(UNPACK ? time_unpack(nm, fn) : time_pack(nm, fn));                                       \
+    } while (0)
+    DV(2, 512, true, false, 0);
+    DV(2, 512, true, true, 0);
+    DV(1, 1024, true, true, 0);
+    DV(2, 512, false, false, 0);
+    DV(2, 512, false, true, 0);
+    for (int g : {512, 1024, 2048, 4096}) {
+        DV(2, 512, true, true, g);
+        DV(2, 1024, true, true, g);
+        DV(4, 512, true, true, g);
+        DV(2, 512, false, true, g);
+        DV(4, 512, false, true, g);
+    }
+    // MPI_Pack then MPI_Unpack of the same buffers back to back (the pack_overhead probe's
+    // sequence): the pair's time, to compare with the two kernels timed apart
+    rs.push_back(time_pack("pair: pack + unpack alternating (ms per pair)", [&] {
+        mv2::Done d_{dctr, dflag, ++seq};
+        hipLaunchKernelGGL((k_units_done<2, 512, false, true>), dim3(rows / 1024), dim3(512), 0, 0, dspan, dpack, rows, su, d_);
+        mv2::Done e_{dctr, dflag, ++seq};
+        hipLaunchKernelGGL((k_units_done<2, 512, true, true>), dim3(rows / 1024), dim3(512), 0, 0, dpack, dspan, rows, su, e_);
     }));
     // write-only / whole-sector references (traffic floors of the unpack's write side)
     rs.push_back(time_pack("ref: write-only 256 MiB whole lines", [&] {
