@@ -502,6 +502,289 @@ static int t_op_commutative(void) {
     return errs;
 }
 
+/* red3.c / red4.c: MPI_Reduce of permutation matrices with the matrix product, every root,
+ * then in place at the root with NULL receive buffers elsewhere.  red3: rank r < n-1 exchanges
+ * r and r+1, the last rank holds the identity; red4: every rank exchanges r and (r+1) % n.  The
+ * expected answer is the ordered product P_0 ... P_{n-1}, computed here with the same function
+ * (red4.c:16-20: independent of the root). */
+static void swap_perm(int m, int r, int *mat) {
+    memset(mat, 0, sizeof(int) * m * m);
+    for (int i = 0; i < m; ++i) {
+        int j = i;
+        if (i == r) j = (i + 1) % m;
+        else if (i == (r + 1) % m) j = (i + m - 1) % m;
+        mat[i * m + j] = 1;
+    }
+}
+static void red_mat(int red4, int r, int *mat) {
+    const int m = g_size;
+    if (!red4 && r == m - 1) {
+        memset(mat, 0, sizeof(int) * m * m);
+        for (int i = 0; i < m; ++i) mat[i * m + i] = 1;
+    } else {
+        swap_perm(m, r, mat);
+    }
+}
+static int red_noncomm(int red4) {
+    if (g_size < 2 || g_size > 256) return 0;
+    const int m = g_size, bytes = m * m * (int)sizeof(int);
+    g_mat = m;
+    MPI_Op op;
+    MPI_Datatype mt;
+    MPI_Op_create(op_matmul, 0, &op);
+    MPI_Type_contiguous(m * m, MPI_INT, &mt);
+    MPI_Type_commit(&mt);
+    int *want = xmalloc(bytes), *tmp = xmalloc(bytes), *h = xmalloc(bytes), one = 1;
+    red_mat(red4, m - 1, want);
+    for (int r = m - 2; r >= 0; --r) {  /* want = P_r x want */
+        red_mat(red4, r, tmp);
+        op_matmul(tmp, want, &one, &mt);
+    }
+    int errs = 0;
+    int *a = ob_alloc(bytes), *b = ob_alloc(bytes);
+    for (int root = 0; root < m; ++root)
+        for (int pass = 0; pass < 2; ++pass) {
+            red_mat(red4, g_rank, h);
+            ob_put(pass ? b : a, h, bytes);
+            const void *s = pass && g_rank == root ? MPI_IN_PLACE : pass ? (const void *)b : (const void *)a;
+            void *r = pass && g_rank != root ? NULL : b;
+            errs += MPI_Reduce(s, r, 1, mt, op, root, MPI_COMM_WORLD) != MPI_SUCCESS;
+            if (g_rank == root) {
+                ob_get(h, b, bytes);
+                errs += chk(memcmp(h, want, bytes) == 0);
+            }
+        }
+    ob_free(a);
+    ob_free(b);
+    free(want);
+    free(tmp);
+    free(h);
+    MPI_Type_free(&mt);
+    MPI_Op_free(&op);
+    return errs;
+}
+static int t_red3(void) { return red_noncomm(0); }
+static int t_red4(void) { return red_noncomm(1); }
+
+/* longuser.c:16-60: a commutative user sum of doubles (+1 on odd ranks, -1 on even), counts
+ * 1 .. 65536 */
+static void op_dsum(void *in_, void *io_, int *len, MPI_Datatype *dt) {
+    (void)dt;
+    const double *in = (const double *)in_;
+    double *io = (double *)io_;
+    for (int i = 0; i < *len; ++i) io[i] = in[i] + io[i];
+}
+static int t_longuser(void) {
+    MPI_Op op;
+    MPI_Op_create(op_dsum, 1, &op);
+    int errs = 0;
+    const double want = (g_size & 1) ? -1.0 : 0.0;
+    for (int count = 1; count < 100000; count *= 2) {
+        double *h = xmalloc(count * sizeof(double));
+        double *a = ob_alloc(count * sizeof(double)), *b = ob_alloc(count * sizeof(double));
+        for (int i = 0; i < count; ++i) h[i] = (g_rank & 1) ? 1.0 : -1.0;
+        ob_put(a, h, count * sizeof(double));
+        for (int i = 0; i < count; ++i) h[i] = 100.0;
+        ob_put(b, h, count * sizeof(double));
+        errs += MPI_Allreduce(a, b, count, MPI_DOUBLE, op, MPI_COMM_WORLD) != MPI_SUCCESS;
+        ob_get(h, b, count * sizeof(double));
+        for (int i = 0; i < count; ++i) errs += chk(h[i] == want);
+        ob_free(a);
+        ob_free(b);
+        free(h);
+    }
+    MPI_Op_free(&op);
+    return errs;
+}
+
+/* one int operand / result in operand memory */
+static int reduce_int(int v, MPI_Op op, int root, int *out) {
+    int *a = ob_alloc(sizeof(int)), *b = ob_alloc(sizeof(int)), init = -100;
+    ob_put(a, &v, sizeof v);
+    ob_put(b, &init, sizeof init);
+    int errs = MPI_Reduce(a, b, 1, MPI_INT, op, root, MPI_COMM_WORLD) != MPI_SUCCESS;
+    errs += MPI_Bcast(b, 1, MPI_INT, root, MPI_COMM_WORLD) != MPI_SUCCESS;
+    ob_get(out, b, sizeof(int));
+    ob_free(a);
+    ob_free(b);
+    return errs;
+}
+
+/* coll8.c: MPI_Reduce of the rank with SUM, MIN, MAX to rank 0 */
+static int t_coll8(void) {
+    int errs = 0, r = 0;
+    errs += reduce_int(g_rank, MPI_SUM, 0, &r) + chk(r == g_size * (g_size - 1) / 2);
+    errs += reduce_int(g_rank, MPI_MIN, 0, &r) + chk(r == 0);
+    errs += reduce_int(g_rank, MPI_MAX, 0, &r) + chk(r == g_size - 1);
+    return errs;
+}
+
+/* coll9.c: a commutative user sum, MPI_Reduce to rank 0 */
+static int t_coll9(void) {
+    MPI_Op op;
+    MPI_Op_create(op_nc_isum, 1, &op);
+    int r = 0, errs = reduce_int(g_rank, op, 0, &r) + chk(r == g_size * (g_size - 1) / 2);
+    MPI_Op_free(&op);
+    return errs;
+}
+
+/* coll10.c:19-35: IN must always come from lower ranks than INOUT (the computation is in rank
+ * order, independent of the root); a violation yields 100000.  Reduce to rank n-1. */
+static void op_assoc(void *in_, void *io_, int *len, MPI_Datatype *dt) {
+    (void)dt;
+    const int *in = (const int *)in_;
+    int *io = (int *)io_;
+    for (int i = 0; i < *len; ++i) io[i] = io[i] <= in[i] ? 100000 : in[i];
+}
+static int t_coll10(void) {
+    MPI_Op op;
+    MPI_Op_create(op_assoc, 0, &op);
+    int r = 0, errs = reduce_int(g_rank, op, g_size - 1, &r) + chk(r == 0);
+    MPI_Op_free(&op);
+    return errs;
+}
+
+/* coll12.c: MAXLOC (Reduce + Bcast) and MINLOC (Allreduce) of MPI_DOUBLE_INT over a 2-entry
+ * table: entry i is rank + 1 (negated for MINLOC) from rank i on, 0 below; entry i's location
+ * is rank i */
+struct di {
+    double v;
+    int loc;
+};
+static int t_coll12(void) {
+    struct di in[2], out[2];
+    int errs = 0;
+    struct di *a = ob_alloc(sizeof in), *b = ob_alloc(sizeof out);
+    for (int pass = 0; pass < 2; ++pass) {
+        memset(in, 0, sizeof in);
+        for (int i = 0; i < 2; ++i) {
+            in[i].v = i >= g_rank ? (pass ? -1.0 : 1.0) * (g_rank + 1.0) : 0.0;
+            in[i].loc = g_rank;
+        }
+        ob_put(a, in, sizeof in);
+        if (!pass) {
+            errs += MPI_Reduce(a, b, 2, MPI_DOUBLE_INT, MPI_MAXLOC, 0, MPI_COMM_WORLD) != MPI_SUCCESS;
+            errs += MPI_Bcast(b, 2, MPI_DOUBLE_INT, 0, MPI_COMM_WORLD) != MPI_SUCCESS;
+        } else {
+            errs += MPI_Allreduce(a, b, 2, MPI_DOUBLE_INT, MPI_MINLOC, MPI_COMM_WORLD) != MPI_SUCCESS;
+        }
+        ob_get(out, b, sizeof out);
+        for (int i = 0; i < 2; ++i)
+            if (i % g_size == g_rank) errs += chk(out[i].loc == g_rank);
+    }
+    ob_free(a);
+    ob_free(b);
+    return errs;
+}
+
+/* iallred.c: an MPI_Iallreduce left in flight across a blocking MPI_Allreduce */
+static int t_iallred(void) {
+    const int one = 1, two = 2;
+    int *a = ob_alloc(sizeof(int)), *b = ob_alloc(sizeof(int)), *c = ob_alloc(sizeof(int)), *d = ob_alloc(sizeof(int));
+    ob_put(a, &one, sizeof one);
+    ob_put(c, &two, sizeof two);
+    MPI_Request req;
+    int errs = MPI_Iallreduce(a, b, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+    errs += MPI_Allreduce(c, d, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD) != MPI_SUCCESS;
+    errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+    int isum = 0, sum = 0;
+    ob_get(&isum, b, sizeof isum);
+    ob_get(&sum, d, sizeof sum);
+    errs += chk(isum == g_size && sum == 2 * g_size);
+    ob_free(a);
+    ob_free(b);
+    ob_free(c);
+    ob_free(d);
+    return errs;
+}
+
+/* nonblocking2.c (the collectives this library provides): Ibcast of 10 ints and of 17 signed
+ * chars (bytes past them untouched), Ibarrier, Ireduce with MPI_SUM and with a user op freed
+ * before the wait, Iallreduce, Ireduce_scatter and Ireduce_scatter_block (the receive buffer
+ * past the rank's block untouched), Iallgather; COUNT = 10 */
+static int t_nonblocking2(void) {
+    enum { CNT = 10, PRIME = 17 };
+    const int n = g_size, nb = CNT * n * (int)sizeof(int);
+    int *h = xmalloc(nb), *g = xmalloc(nb), *counts = xmalloc(n * sizeof(int));
+    int *buf = ob_alloc(nb), *rbuf = ob_alloc(nb);
+    MPI_Request req;
+    int errs = 0;
+    const int tri = n * (n - 1) / 2;
+    /* Ibcast of COUNT ints */
+    for (int i = 0; i < CNT; ++i) h[i] = g_rank == 0 ? i : -1;
+    ob_put(buf, h, CNT * sizeof(int));
+    errs += MPI_Ibcast(buf, CNT, MPI_INT, 0, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+    errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+    ob_get(h, buf, CNT * sizeof(int));
+    for (int i = 0; i < CNT; ++i) errs += chk(h[i] == i);
+    /* Ibcast of PRIME signed chars inside a larger buffer */
+    signed char *hc = (signed char *)h;
+    for (int i = 0; i < nb; ++i) hc[i] = i < PRIME ? (g_rank == 0 ? (signed char)i : (signed char)0xdb) : (signed char)0xbf;
+    ob_put(buf, h, nb);
+    errs += MPI_Ibcast(buf, PRIME, MPI_SIGNED_CHAR, 0, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+    errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+    ob_get(h, buf, nb);
+    for (int i = 0; i < nb; ++i) errs += chk(hc[i] == (i < PRIME ? (signed char)i : (signed char)0xbf));
+    /* Ibarrier */
+    errs += MPI_Ibarrier(MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+    errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+    /* Ireduce (SUM, then a user sum freed before the wait) and Iallreduce */
+    for (int k = 0; k < 3; ++k) {
+        for (int i = 0; i < CNT; ++i) {
+            h[i] = g_rank + i;
+            g[i] = (int)0xdeadbeef;
+        }
+        ob_put(buf, h, CNT * sizeof(int));
+        ob_put(rbuf, g, CNT * sizeof(int));
+        MPI_Op op = MPI_SUM;
+        if (k == 1) MPI_Op_create(op_nc_isum, 1, &op);
+        if (k < 2) errs += MPI_Ireduce(buf, rbuf, CNT, MPI_INT, op, 0, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+        else errs += MPI_Iallreduce(buf, rbuf, CNT, MPI_INT, op, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+        if (k == 1) MPI_Op_free(&op);
+        errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+        if (k == 2 || g_rank == 0) {
+            ob_get(g, rbuf, CNT * sizeof(int));
+            for (int i = 0; i < CNT; ++i) errs += chk(g[i] == tri + i * n);
+        }
+    }
+    /* Ireduce_scatter / Ireduce_scatter_block: block i of every rank holds rank + i */
+    for (int blk = 0; blk < 2; ++blk) {
+        for (int i = 0; i < n; ++i) {
+            counts[i] = CNT;
+            for (int j = 0; j < CNT; ++j) {
+                h[i * CNT + j] = g_rank + i;
+                g[i * CNT + j] = (int)0xdeadbeef;
+            }
+        }
+        ob_put(buf, h, nb);
+        ob_put(rbuf, g, nb);
+        if (blk) errs += MPI_Ireduce_scatter_block(buf, rbuf, CNT, MPI_INT, MPI_SUM, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+        else errs += MPI_Ireduce_scatter(buf, rbuf, counts, MPI_INT, MPI_SUM, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+        errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+        ob_get(g, rbuf, nb);
+        for (int j = 0; j < CNT; ++j) errs += chk(g[j] == n * g_rank + tri);
+        for (int j = CNT; j < CNT * n; ++j) errs += chk(g[j] == (int)0xdeadbeef);
+    }
+    /* Iallgather */
+    for (int i = 0; i < n * CNT; ++i) {
+        h[i] = g_rank + i;
+        g[i] = (int)0xdeadbeef;
+    }
+    ob_put(buf, h, nb);
+    ob_put(rbuf, g, nb);
+    errs += MPI_Iallgather(buf, CNT, MPI_INT, rbuf, CNT, MPI_INT, MPI_COMM_WORLD, &req) != MPI_SUCCESS;
+    errs += MPI_Wait(&req, MPI_STATUS_IGNORE) != MPI_SUCCESS;
+    ob_get(g, rbuf, nb);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < CNT; ++j) errs += chk(g[i * CNT + j] == i + j);
+    ob_free(buf);
+    ob_free(rbuf);
+    free(h);
+    free(g);
+    free(counts);
+    return errs;
+}
+
 static const struct {
     const char *name;
     int (*fn)(void);
@@ -515,6 +798,11 @@ static const struct {
     {"allgather2", t_allgather2},   {"allgather3", t_allgather3},
     {"bcasttest", t_bcasttest},     {"bcastzerotype", t_bcastzerotype},
     {"op_commutative", t_op_commutative},
+    {"red3", t_red3},               {"red4", t_red4},
+    {"longuser", t_longuser},       {"coll8", t_coll8},
+    {"coll9", t_coll9},             {"coll10", t_coll10},
+    {"coll12", t_coll12},           {"iallred", t_iallred},
+    {"nonblocking2", t_nonblocking2},
 };
 
 static double now_s(void) {

@@ -1,6 +1,7 @@
 """The reference's own collective tests (MPICH test/mpi/coll shipped with MVAPICH2 2.3.7:
 allred2-6, allredmany, uoplong, redscat2/3, red_scat_block2, redscatblk3, reduce, allgather2/3,
-bcasttest, bcastzerotype, op_commutative), restated as one C program
+bcasttest, bcastzerotype, op_commutative, red3/4, longuser, coll8-10, coll12, iallred and the
+nonblocking2 calls this library provides), restated as one C program
 (tests/mpich_coll/coll_suite.c) that links the drop-in libmpi.so like an application and checks
 each test's own closed-form answers.  Run with device-memory operands (the accelerated path)
 and with host-memory operands, at several rank counts sharing the one GPU."""
@@ -15,7 +16,8 @@ SUITE = os.path.join(ROOT, "tests", "mpich_coll")
 EXE = os.path.join(SUITE, "coll_suite")
 CASES = ["allred2", "allred3", "allred4", "allred5", "allred6", "allredmany", "uoplong", "redscat2",
          "red_scat_block2", "redscat3", "redscatblk3", "reduce", "allgather2", "allgather3", "bcasttest",
-         "bcastzerotype", "op_commutative"]
+         "bcastzerotype", "op_commutative", "red3", "red4", "longuser", "coll8", "coll9", "coll10", "coll12", "iallred",
+         "nonblocking2"]
 
 
 def _exe():
