@@ -201,10 +201,6 @@ int user_reduce_local(const void *in, void *inout, int count, MPI_Datatype dt, U
 
 // one MPI_T-counted call (runtime/pvars.h)
 int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int opk) {
-    if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
-        fprintf(stderr, "[mv2amd] user ops and long double types are not supported across nodes\n");
-        return MPI_ERR_UNSUPPORTED_OPERATION;
-    }
     pvar_begin();
     const int rc = host_allreduce(sendbuf, recvbuf, count, dt, HostOp{u->fn, opk});
     pvar_end(rc == MPI_SUCCESS);
@@ -213,10 +209,6 @@ int user_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
 
 // one MPI_T-counted call (runtime/pvars.h)
 int user_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, UserOp *u, int root, int opk) {
-    if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
-        fprintf(stderr, "[mv2amd] user ops and long double types are not supported across nodes\n");
-        return MPI_ERR_UNSUPPORTED_OPERATION;
-    }
     pvar_begin();
     const int rc = host_reduce(sendbuf, recvbuf, count, dt, HostOp{u->fn, opk}, root);
     pvar_end(rc == MPI_SUCCESS);
@@ -231,10 +223,6 @@ namespace {
 
 // one MPI_T-counted call (runtime/pvars.h)
 int user_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, UserOp *u, int opk) {
-    if (world().nnodes > 1) {  // host-evaluated ops: the schedules are restated for one node
-        fprintf(stderr, "[mv2amd] user ops and long double types are not supported across nodes\n");
-        return MPI_ERR_UNSUPPORTED_OPERATION;
-    }
     pvar_begin();
     const int rc = host_reduce_scatter(sendbuf, recvbuf, counts, dt, HostOp{u->fn, opk});
     pvar_end(rc == MPI_SUCCESS);

@@ -19,6 +19,12 @@
 // of the operand instead of n-1 whole operands.  Where the programs differ between ranks
 // (recursive doubling, :360-630: each rank's own bracketing) every rank evaluates its own
 // result over every element, from the packed operands.
+//
+// Several nodes.  The operands travel the same way over the whole job (the packed allgather
+// crosses the leaders' links) and the schedule is the one the device path restates there
+// (runtime/coll.cpp mn_host_schedule): flat schedules are evaluated as above over the job's ranks;
+// a two-level schedule is evaluated in its two stages — each node's partial at its leader (the
+// node step's programs over that node's operands), then the leaders' programs over the partials.
 #include "user_coll.h"
 
 #include <hip/hip_runtime.h>
@@ -78,6 +84,16 @@ char *dev_scratch(int slot, size_t bytes) {
     return (char *)p[slot];
 }
 
+// the ranks a reduction runs over: the node's, or every rank of a job on several nodes
+struct Job {
+    int n, me;
+    bool multi;
+};
+Job job() {
+    const World &w = world();
+    return w.nnodes > 1 ? Job{w.gsize, w.grank, true} : Job{w.size, w.rank, false};
+}
+
 struct Typed {
     MPI_Datatype dt;
     long tsize, extent;
@@ -99,9 +115,8 @@ struct Operands {
 };
 
 int stage_operands(const void *src, int count, const Typed &t, Operands &o) {
-    World &w = world();
     o.t = t;
-    o.n = w.size;
+    o.n = job().n;
     o.P = (size_t)count * (size_t)t.tsize;
     char *mine = dev_scratch(DS_MINE, o.P);
     char *all = dev_scratch(DS_ALL, o.P * (size_t)o.n);
@@ -193,7 +208,7 @@ struct Split {
 
 int run_split(const Operands &o, int count, const Split &sp, MPI_User_function *fn, void *recvbuf, bool deliver) {
     const Typed &t = o.t;
-    const int n = o.n, me = world().rank;
+    const int n = o.n, me = job().me;
     const long chunk = sp.U ? (sp.U + n - 1) / n : 0;
     const long mb = std::min<long>(sp.U, (long)me * chunk), me_e = std::min<long>(sp.U, mb + chunk);
     char *res_all = dev_scratch(DS_RES_ALL, (size_t)std::max<long>((long)n * chunk, count) * (size_t)t.tsize);
@@ -226,6 +241,92 @@ int run_split(const Operands &o, int count, const Split &sp, MPI_User_function *
     return deliver ? dtype_unpack(res_all, count, t.dt, recvbuf) : 0;
 }
 
+// Run ps over elements [b, e) of the nreg operands at W (rspan bytes apart, element b at offset 0),
+// program blocks counted from element pbase, and copy each element's result into dst (the type's
+// layout, element b at offset 0)
+int eval_into(const ProgSet &ps, long pbase, char *W, long rspan, long b, long e, const Typed &t,
+              MPI_User_function *fn, char *dst) {
+    for (long x = b; x < e;) {
+        int k = 0;
+        long xe = e;
+        if (ps.nprog > 1) {
+            k = (int)std::min<long>((x - pbase) / (long)ps.blk, ps.nprog - 1);
+            if (k < ps.nprog - 1) xe = std::min<long>(e, pbase + (long)(k + 1) * (long)ps.blk);
+        }
+        const Prog &p = ps.p[k];
+        const size_t off = (size_t)(x - b) * (size_t)t.extent;
+        for (int s = 0; s < p.nsteps; ++s) {
+            int cnt = (int)(xe - x);
+            MPI_Datatype d = t.dt;
+            fn(W + (size_t)p.src[s] * rspan + off, W + (size_t)p.dst[s] * rspan + off, &cnt, &d);
+        }
+        const long span = dtype_span(t.dt, (int)(xe - x));
+        memcpy(dst + off, W + (size_t)p.res * rspan + off, (size_t)span);
+        x = xe;
+    }
+    return 0;
+}
+
+// A two-level schedule across nodes (MPIR_Allreduce_two_level_MV2 / the two-level reduce helper):
+// every node's partial from its ranks' operands (the node step's programs for local rank 0), then
+// the leaders' programs over the partials.  Result: packed type-map bytes of elements [0, count)
+// in res (device).
+int run_two_level(const Operands &o, int count, const MnSched &sc, MPI_User_function *fn, char *res) {
+    const Typed &t = o.t;
+    const World &w = world();
+    const int L = w.size, K = w.nnodes;
+    HostBuf W(HS_OPERANDS), R(HS_RESULT), Pt(HS_PARTIALS);
+    long rspan = 0;
+    int rc = fetch(o, 0, count, W, rspan);
+    if (rc) return rc;
+    Pt.resize((size_t)rspan * (size_t)K + 1);
+    R.resize((size_t)count * (size_t)t.tsize + 1);
+    if (!Pt.data() || !R.data()) return MPI_ERR_NO_MEM;
+    for (int j = 0; j < K; ++j) {
+        char *nodeW = W.data() + (size_t)j * (size_t)L * (size_t)rspan, *part = Pt.data() + (size_t)j * rspan;
+        if (L == 1) memcpy(part, nodeW, (size_t)rspan);
+        else if ((rc = eval_into(sc.node.ps, 0, nodeW, rspan, 0, count, t, fn, part))) return rc;
+    }
+    if (K == 1) {
+        rc = dtype_pack(Pt.data(), count, t.dt, R.data());
+    } else {
+        rc = eval_range(sc.lead.ps, 0, Pt.data(), rspan, 0, count, t, fn, R.data());
+    }
+    if (rc) return rc;
+    return mv2h_memcpy_htod(res, R.data(), (size_t)count * (size_t)t.tsize) ? MPI_ERR_OTHER : 0;
+}
+
+// every rank's plan_allreduce programs (forced as on this rank) equal `mine`
+bool uniform_over_ranks(int n, int me, int count, const Typed &t, bool in_place, int forced, int opk,
+                        const ProgSet &mine) {
+    for (int j = 0; j < n; ++j) {
+        if (j == me) continue;
+        Plan q;
+        if (plan_allreduce(n, j, (size_t)count, (int)t.tsize, (int)t.extent, in_place, forced, &q, opk)) return false;
+        if (!same_progs(q.ps, mine)) return false;
+    }
+    return true;
+}
+
+// this rank's own programs over two ranges: [0, U) by a, [U, count) by b counted from U
+int run_split2(const Operands &o, int count, const ProgSet &a, long U, const ProgSet &b, MPI_User_function *fn,
+               void *recvbuf) {
+    const Typed &t = o.t;
+    char *res = dev_scratch(DS_RES_ALL, (size_t)count * (size_t)t.tsize);
+    if (!res) return MPI_ERR_NO_MEM;
+    HostBuf W(HS_OPERANDS), R(HS_RESULT);
+    R.resize((size_t)count * (size_t)t.tsize + 1);
+    if (!R.data()) return MPI_ERR_NO_MEM;
+    long rspan = 0;
+    int rc;
+    if ((rc = fetch(o, 0, U, W, rspan)) || (rc = eval_range(a, 0, W.data(), rspan, 0, U, t, fn, R.data()))) return rc;
+    if ((rc = fetch(o, U, count, W, rspan)) ||
+        (rc = eval_range(b, U, W.data(), rspan, U, count, t, fn, R.data() + (size_t)U * t.tsize)))
+        return rc;
+    if (mv2h_memcpy_htod(res, R.data(), (size_t)count * (size_t)t.tsize)) return MPI_ERR_OTHER;
+    return dtype_unpack(res, count, t.dt, recvbuf);
+}
+
 // one rank: recvbuf's type map <- src's
 int copy_typemap(const void *src, void *recvbuf, int count, const Typed &t) {
     char *tmp = dev_scratch(DS_MINE, (size_t)count * (size_t)t.tsize);
@@ -237,18 +338,44 @@ int copy_typemap(const void *src, void *recvbuf, int count, const Typed &t) {
 }  // namespace
 
 int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, const HostOp &op) {
-    World &w = world();
+    const Job J = job();
     const Typed t = typed(dt);
     if (t.tsize < 0 || t.extent < 0) return MPI_ERR_TYPE;
-    const int n = w.size, me = w.rank;
+    const int n = J.n, me = J.me;
     const bool in_place = sendbuf == MPI_IN_PLACE;
     const void *src = in_place ? recvbuf : sendbuf;
     if (n == 1) return in_place ? MPI_SUCCESS : copy_typemap(src, recvbuf, count, t);
     Plan p, rem;
-    int rc = plan_allreduce(n, me, (size_t)count, (int)t.tsize, (int)t.extent, in_place, 0, &p, op.opk);
+    int rc, forced = 0;
+    Split sp{&p.ps, 0, &p.ps, 0};
+    if (J.multi) {
+        MnSched sc;
+        if ((rc = mn_host_schedule(MN_COLL_ALLREDUCE, (size_t)count, (int)t.tsize, (int)t.extent, in_place, op.opk, -1,
+                                   &sc)))
+            return rc == E_UNSUPPORTED ? MPI_ERR_UNSUPPORTED_OPERATION : MPI_ERR_INTERN;
+        Operands o;
+        if ((rc = stage_operands(src, count, t, o))) return rc;
+        if (sc.kind == MN_TWO_LEVEL) {
+            char *res = dev_scratch(DS_RES_ALL, (size_t)count * (size_t)t.tsize);
+            if (!res) return MPI_ERR_NO_MEM;
+            if ((rc = run_two_level(o, count, sc, op.fn, res))) return rc;
+            return dtype_unpack(res, count, t.dt, recvbuf);
+        }
+        p = sc.p;
+        rem = sc.rem;
+        forced = sc.forced;
+        if (forced == ALG_RING) {  // ring chunks [0, U) are uniform, the remainder each rank's own
+            sp = Split{&p.ps, sc.U, &rem.ps, sc.U};
+        } else if (sc.U && sc.U < count) {  // IN_PLACE from 2 MiB: two pt2pt_rs calls, own programs
+            return run_split2(o, count, p.ps, sc.U, rem.ps, op.fn, recvbuf);
+        } else {
+            sp = Split{&p.ps, uniform_over_ranks(n, me, count, t, in_place, forced, op.opk, p.ps) ? count : 0, &p.ps, 0};
+        }
+        return run_split(o, count, sp, op.fn, recvbuf, true);
+    }
+    rc = plan_allreduce(n, me, (size_t)count, (int)t.tsize, (int)t.extent, in_place, 0, &p, op.opk);
     if (rc) return rc;
     pvar_note(PV_COLL_ALLREDUCE, p, in_place, (size_t)count, n);
-    Split sp{&p.ps, 0, &p.ps, 0};
     if (p.algo == ALG_RING) {
         // ring wrapper (allreduce_osu.c:3758-3818): the ring over (count / n) * n elements unless
         // IN_PLACE, pt2pt_rs (recursive doubling for user ops) on the rest
@@ -261,14 +388,7 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
             sp.own_base = sp.U;
         }
     } else {
-        bool uniform = true;
-        for (int j = 0; j < n && uniform; ++j) {
-            if (j == me) continue;
-            Plan q;
-            if ((rc = plan_allreduce(n, j, (size_t)count, (int)t.tsize, (int)t.extent, in_place, 0, &q, op.opk))) return rc;
-            uniform = same_progs(q.ps, p.ps);
-        }
-        sp.U = uniform ? count : 0;
+        sp.U = uniform_over_ranks(n, me, count, t, in_place, 0, op.opk, p.ps) ? count : 0;
     }
     Operands o;
     if ((rc = stage_operands(src, count, t, o))) return rc;
@@ -278,14 +398,33 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
 // MPI_Reduce: the root's programs (MPIR_Reduce_index_tuned_intra_MV2's choice, binomial /
 // knomial / shmem / ...) evaluated over ranges split across every rank
 int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, const HostOp &op, int root) {
-    World &w = world();
+    const Job J = job();
     const Typed t = typed(dt);
     if (t.tsize < 0 || t.extent < 0) return MPI_ERR_TYPE;
-    const int n = w.size, me = w.rank;
+    const int n = J.n, me = J.me;
     const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
     if (n == 1) return sendbuf == MPI_IN_PLACE ? MPI_SUCCESS : copy_typemap(src, recvbuf, count, t);
     Plan p, pr;
-    int rc = plan_reduce(n, me, root, (size_t)count, (int)t.tsize, (int)t.extent, &p, op.opk);
+    int rc;
+    if (J.multi) {
+        MnSched sc;
+        if ((rc = mn_host_schedule(MN_COLL_REDUCE, (size_t)count, (int)t.tsize, (int)t.extent, sendbuf == MPI_IN_PLACE,
+                                   op.opk, root, &sc)))
+            return rc == E_UNSUPPORTED ? MPI_ERR_UNSUPPORTED_OPERATION : MPI_ERR_INTERN;
+        Operands o;
+        if ((rc = stage_operands(src, count, t, o))) return rc;
+        if (sc.kind == MN_TWO_LEVEL) {  // only the root's result counts: the root evaluates it
+            if (me != root) return MPI_SUCCESS;
+            char *res = dev_scratch(DS_RES_ALL, (size_t)count * (size_t)t.tsize);
+            if (!res) return MPI_ERR_NO_MEM;
+            if ((rc = run_two_level(o, count, sc, op.fn, res))) return rc;
+            return dtype_unpack(res, count, t.dt, recvbuf);
+        }
+        if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
+        const Split sp{&pr.ps, count, &pr.ps, 0};
+        return run_split(o, count, sp, op.fn, recvbuf, me == root);
+    }
+    rc = plan_reduce(n, me, root, (size_t)count, (int)t.tsize, (int)t.extent, &p, op.opk);
     if (rc) return rc;
     pvar_note(PV_COLL_REDUCE, p, sendbuf == MPI_IN_PLACE, (size_t)count, n);  // every rank runs the algorithm
     if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
@@ -302,10 +441,11 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
 // the canonical rank order x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
 // associative op, applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block.
 int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, const HostOp &op) {
-    World &w = world();
+    const Job J = job();
     const Typed t = typed(dt);
     if (t.tsize < 0 || t.extent <= 0) return MPI_ERR_TYPE;
-    const int n = w.size, me = w.rank;
+    const int n = J.n, me = J.me;
+    if (n > kMaxRanks) return MPI_ERR_UNSUPPORTED_OPERATION;  // programs over the job's ranks
     long total = 0, disp = 0;
     std::vector<size_t> cz(n);
     for (int j = 0; j < n; ++j) {

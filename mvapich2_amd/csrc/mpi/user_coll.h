@@ -12,7 +12,7 @@ namespace mv2 {
 
 // Pinned host staging kept per slot and grown on demand (no page faults or zero fill per
 // call; device copies run as DMA).  Used under the global critical section.
-enum HostSlot { HS_IN, HS_INOUT, HS_PACKED, HS_OPERANDS, HS_RESULT, HS_COUNT };
+enum HostSlot { HS_IN, HS_INOUT, HS_PACKED, HS_OPERANDS, HS_RESULT, HS_PARTIALS, HS_COUNT };
 class HostBuf {
   public:
     explicit HostBuf(int slot) : slot_(slot) {}

@@ -1471,7 +1471,10 @@ int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvco
     if (world().nnodes > 1) {
         if (world().enqueue) return mn_unsupported("a stream-ordered collective");
         MnBlocking nb;
-        return mn_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
+        pvar_begin();
+        const int rc = mn_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
+        pvar_end(rc == 0);
+        return rc;
     }
     pvar_begin();
     const int rc = reduce_scatter_entry(sendbuf, recvbuf, recvcounts, dtype, op, stream);
@@ -1683,9 +1686,11 @@ static int mn_require_device_reduction(int dtype, int op) {
 // Returns 0 (two-level), 1 (flat ring wrapper), or ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every
 // rank).  The small-message shortcuts (:118-160) keep the two-level structure; the skip-large gate
 // (:163-171) takes the ring wrapper; then the tuning tables (orders.cpp mn_allreduce_table).
-static int mn_select(long nbytes) {
+static int mn_select(long nbytes, int *intra, int *inter) {
     const World &w = world();
     const Knobs &K = knobs();
+    *intra = MN_INTRA_NODE;  // the shortcuts' node step is the node's own small-message order
+    *inter = ALG_PT2PT_RD;   // and their leaders' step recursive doubling (:2215-2262, :147-153)
     bool tables = false;
     if (K.allred_skip_small) {
         if (nbytes <= K.topo_allred_max && nbytes >= K.topo_allred_min && K.enable_topo && K.use_topo_allreduce) {
@@ -1697,11 +1702,18 @@ static int mn_select(long nbytes) {
     if (!tables && K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes &&
         w.size <= K.allred_ring_ppn)
         return 1;
-    const int t = mn_allreduce_table(w.size, w.gsize, nbytes);
+    int in = MN_INTRA_NODE, it = ALG_PT2PT_RD;
+    const int t = mn_allreduce_table(w.size, w.gsize, nbytes, &in, &it);
+    if (t == 0) {
+        *intra = in;
+        *inter = it;
+        return 0;
+    }
     return t > 0 && w.gsize <= kMaxRanks ? t : 0;  // flat programs: up to kMaxRanks operands
 }
 
-static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream);
+static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                             int intra = MN_INTRA_NODE, int inter = ALG_PT2PT_RD);
 static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
                              int algo, int root = -1);
 
@@ -1772,29 +1784,17 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
                              dtype, op, stream);
 }
 
-// Flat pt2pt_rs / pt2pt_rd over every rank (allreduce_osu.c:633-1054, :360-630): every rank's operand reaches every rank
-// (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
-// evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
-// differ between ranks where the op is not commutative in its bits (MAX/MIN ties of ±0, NaN
-// payloads), as the reference's do.  algo 0: the plan of the call's own selection (a nonblocking
-// call's: MPIR_Iallreduce_naive = Ireduce to rank 0 + Ibcast, every rank takes rank 0's result).
-// root >= 0 (MPI_Ireduce): only the root evaluates, the plan of MPIR_Ireduce_binomial.
-static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
-                             int algo, int root) {
+// Every rank's S-byte operand onto every rank, in global rank order (*out: device scratch of
+// gsize * S bytes): node allgather into the node's section, a ring of sections over the leaders,
+// node broadcast.  The data movement of the flat algorithms restated across nodes.
+static int mn_gather_all(const void *mine, size_t S, char **out, void *stream) {
     World &w = world();
-    const DtypeInfo *dt = dtype_lookup(dtype);
-    const bool in_place = sendbuf == (const void *)-1;
-    const size_t S = count * (size_t)dt->extent, sect = (size_t)w.size * S;
     const int n = w.gsize, K = w.nnodes;
-    Plan p;
-    int rc = root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
-                       : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
-    if (rc) return rc;
-    pvar_note(root >= 0 ? PV_COLL_REDUCE : PV_COLL_ALLREDUCE, p, in_place, count, n);
-    char *W = (char *)get_scratch(6, (size_t)n * S);  // every rank's operand, global rank order
+    const size_t sect = (size_t)w.size * S;
+    char *W = (char *)get_scratch(6, (size_t)n * S);
     if (!W) return E_NO_MEM;
-    if ((rc = mn_reserve_dev(S)) || (w.rank == 0 && (rc = mn_reserve_host((size_t)n * S)))) return rc;
-    const void *mine = in_place ? recvbuf : sendbuf;
+    int rc = 0;
+    if (w.rank == 0 && (rc = mn_reserve_host((size_t)n * S))) return rc;
     if ((rc = allgather_node(mine, W + (size_t)w.node * sect, S, stream))) return rc;
     if (w.rank == 0) {
         const int me = w.node, right = (me + 1) % K, left = (me - 1 + K) % K;
@@ -1807,6 +1807,31 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
         if ((rc = mn_h2d(W, g_mn.h0, (size_t)n * S))) return rc;
     }
     if ((rc = bcast_node(W, (size_t)n * S, 0, stream))) return rc;
+    *out = W;
+    return 0;
+}
+
+// Flat pt2pt_rs / pt2pt_rd over every rank (allreduce_osu.c:633-1054, :360-630): every rank's operand reaches every rank
+// (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
+// evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
+// differ between ranks where the op is not commutative in its bits (MAX/MIN ties of ±0, NaN
+// payloads), as the reference's do.  algo 0: the plan of the call's own selection (a nonblocking
+// call's: MPIR_Iallreduce_naive = Ireduce to rank 0 + Ibcast, every rank takes rank 0's result).
+// root >= 0 (MPI_Ireduce): only the root evaluates, the plan of MPIR_Ireduce_binomial.
+static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                             int algo, int root) {
+    World &w = world();
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const bool in_place = sendbuf == (const void *)-1;
+    const size_t S = count * (size_t)dt->extent;
+    const int n = w.gsize;
+    Plan p;
+    int rc = root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
+                       : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
+    if (rc) return rc;
+    pvar_note(root >= 0 ? PV_COLL_REDUCE : PV_COLL_ALLREDUCE, p, in_place, count, n);
+    char *W = nullptr;  // every rank's operand, global rank order
+    if ((rc = mn_reserve_dev(S)) || (rc = mn_gather_all(in_place ? recvbuf : sendbuf, S, &W, stream))) return rc;
     if (root >= 0 && w.grank != root) return 0;
     const void *srcs[kMaxRanks];
     for (int r = 0; r < n; ++r) srcs[r] = W + (size_t)r * S;
@@ -1826,7 +1851,8 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     // binomial or redscat_gather, then Ibcast), whatever the nodes
     if (nbc_kind() == NBC_IALLREDUCE && gsize <= kMaxRanks)
         return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0);
-    const int sel = mn_select((long)(count * (size_t)dt->size));
+    int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD;
+    const int sel = mn_select((long)(count * (size_t)dt->size), &intra, &inter);
     if (sel == 1) {
         // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise
         // it runs pt2pt_rs over every rank (restated up to kMaxRanks ranks, else two-level).  With
@@ -1847,23 +1873,87 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     }
     if (sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD)
         return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, sel);
-    return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
+    return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream, intra, inter);
 }
 
-static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
+// The node step of a two-level table entry: the entry's intra-node function over the node's ranks
+// (MPIR_Allreduce_two_level_MV2 :1727-1745; the leader's result is what the leaders reduce, and the
+// node broadcast that ends the call overwrites every other rank's).  MN_INTRA_NODE: the node's own
+// one-node selection, which reads the same table entry (16 ppn) or is the shortcut's order.
+static int node_allreduce_intra(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                                int intra) {
+    if (intra == MN_INTRA_NODE) return allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream);
+    const DtypeInfo *dt = nullptr;
+    int rc = check_op_dtype(op, dtype, &dt);
+    if (rc || count == 0) return rc;
+    if ((rc = kind_supported(dt)) || (rc = require_world())) return rc;
+    World &w = world();
+    const int n = w.size, me = w.rank, oi = op_index(op);
+    const bool in_place = sendbuf == (const void *)-1;
+    if (n == 1 || oi == OP_NO_OP || oi == OP_REPLACE)
+        return allreduce_impl(sendbuf, recvbuf, count, dt, oi, pick_stream(stream), tree_base(n));
+    Plan p;
+    if (intra == MN_INTRA_P2P) {  // MPIR_Reduce_MV2 to local rank 0 (the node's reduce selection)
+        rc = plan_reduce(n, me, 0, count, dt->size, dt->extent, &p);
+        p.inner = p.algo;
+        p.algo = ALG_TWO_LEVEL_P2P;
+    } else {
+        rc = plan_allreduce(n, me, count, dt->size, dt->extent, in_place,
+                            intra == MN_INTRA_RS ? ALG_PT2PT_RS : ALG_SHMEM_LINEAR, &p);
+    }
+    if (rc) return rc;
+    log_plan("allreduce (node step)", p, count);
+    return allreduce_impl(sendbuf, recvbuf, count, dt, oi, pick_stream(stream), tree_from_plan(p, n, count, me));
+}
+
+namespace {
+// leaders: MPIR_Allreduce_pt2pt_rs_MV2 (:633-1054; recursive doubling for count < pof2, :802) with
+// the nodes as ranks, MPI_IN_PLACE on `acc`.  Every leader's partial reaches every leader (a ring
+// over the leaders) and each evaluates that algorithm's per-element programs for its own node
+// index on the device; more than kMaxRanks nodes keep recursive doubling (not restated).
+int leader_prog(char *acc, size_t count, int dtype, int op, size_t bytes, int algo) {
+    World &w = world();
+    const int K = w.nnodes, me = w.node;
+    if (K > kMaxRanks) return leader_rd(acc, count, dtype, op, bytes);
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    Plan p;
+    int rc = plan_allreduce(K, me, count, dt->size, dt->extent, true, algo, &p);
+    if (rc) return rc;
+    char *W = (char *)get_scratch(6, (size_t)K * bytes);
+    if (!W) return E_NO_MEM;
+    if ((rc = mn_reserve_host((size_t)K * bytes)) || (rc = mn_d2h(g_mn.h0 + (size_t)me * bytes, acc, bytes)))
+        return rc;
+    const int right = (me + 1) % K, left = (me - 1 + K) % K;
+    for (int k = 0; k < K - 1; ++k) {
+        const int so = (me - k + K) % K, ro = (me - k - 1 + K) % K;
+        if ((rc = net_shift(right, g_mn.h0 + (size_t)so * bytes, bytes, left, g_mn.h0 + (size_t)ro * bytes, bytes)))
+            return rc;
+    }
+    if ((rc = mn_h2d(W, g_mn.h0, (size_t)K * bytes))) return rc;
+    const void *srcs[kMaxRanks];
+    for (int r = 0; r < K; ++r) srcs[r] = W + (size_t)r * bytes;
+    return mv2h_reduce_n_prog(srcs, K, acc, count, dtype, op, (const mv2h_progset *)&p.ps, nullptr);
+}
+}  // namespace
+
+static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                             int intra, int inter) {
     World &w = world();
     int rc = 0;
     const DtypeInfo *dt = dtype_lookup(dtype);
     const size_t bytes = count * (size_t)dt->extent;
     // MPI_T: MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) with the leaders' recursive
-    // doubling (MPIR_Allreduce_pt2pt_rd_MV2 :366); the node step's own plan is not counted
-    const int chain[2] = {PV_AR_2LVL, PV_AR_SHM_RD};
+    // doubling (MPIR_Allreduce_pt2pt_rd_MV2 :366) or pt2pt_rs (:639); the node step's own plan is
+    // not counted
+    const int chain[2] = {PV_AR_2LVL, inter == ALG_PT2PT_RS ? PV_AR_SHM_RS : PV_AR_SHM_RD};
     pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
-    // node step: every rank of the node holds the node's partial
-    if ((rc = allreduce_entry(sendbuf, recvbuf, count, dtype, op, stream))) return rc;
+    // node step: the leader holds the node's partial
+    if ((rc = node_allreduce_intra(sendbuf, recvbuf, count, dtype, op, stream, intra))) return rc;
     if (w.rank == 0) {
         if ((rc = mn_reserve(bytes))) return rc;
-        if ((rc = mn_h2d(g_mn.d0, recvbuf, bytes)) || (rc = leader_rd(g_mn.d0, count, dtype, op, bytes)) ||
+        if ((rc = mn_h2d(g_mn.d0, recvbuf, bytes)) ||
+            (rc = inter == ALG_PT2PT_RS ? leader_prog(g_mn.d0, count, dtype, op, bytes, ALG_PT2PT_RS)
+                                        : leader_rd(g_mn.d0, count, dtype, op, bytes)) ||
             (rc = mn_d2h(recvbuf, g_mn.d0, bytes)))
             return rc;
     }
@@ -1962,10 +2052,13 @@ static int mn_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *
     return bcast_node(recvbuf, total, 0, stream);
 }
 
-// Reduce_scatter across nodes: the two-level allreduce of the whole operand, then this rank's
-// block.  The reference runs its flat reduce-scatter algorithms over all ranks here (red_scat_osu.c
-// :1859-1896), whose fp order is not restated across nodes; integer, logical, bitwise and LOC
-// results are exact.
+// Reduce_scatter across nodes: MPIR_Reduce_scatter_MV2 runs its flat algorithms over every rank of
+// the job (red_scat_osu.c:1771-1900: ring / basic / recursive halving / pairwise by total size, the
+// non-commutative forms for non-commutative ops; MPI_Ireduce_scatter: pairwise).  Every operand
+// reaches every rank (mn_gather_all) and each rank evaluates its own block's programs of the
+// selected algorithm over the job's ranks (orders.cpp plan_reduce_scatter, the same restatement as
+// on one node).  Jobs above kMaxRanks ranks: the two-level allreduce of the whole operand, then the
+// block (integer, logical, bitwise and LOC results exact; the fp order not restated).
 static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                              void *stream) {
     World &w = world();
@@ -1978,15 +2071,122 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
         total += recvcounts[j];
     }
     if (total == 0) return 0;
-    const size_t ext = (size_t)dt->extent;
-    char *tmp = (char *)get_scratch(5, total * ext);
-    if (!tmp) return E_NO_MEM;
-    const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;
-    if ((rc = mn_allreduce(src, tmp, total, dtype, op, stream))) return rc;
-    if (recvcounts[w.grank])
-        rc = hipMemcpy(recvbuf, tmp + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
-    return rc;
+    const size_t ext = (size_t)dt->extent, S = total * ext;
+    const bool in_place = sendbuf == (const void *)-1;
+    const void *src = in_place ? recvbuf : sendbuf;
+    if (w.gsize > kMaxRanks) {
+        char *tmp = (char *)get_scratch(5, S);
+        if (!tmp) return E_NO_MEM;
+        if ((rc = mn_allreduce(src, tmp, total, dtype, op, stream))) return rc;
+        if (recvcounts[w.grank])
+            rc = hipMemcpy(recvbuf, tmp + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess
+                     ? 0 : E_INTERN;
+        return rc;
+    }
+    Plan p;
+    if ((rc = plan_reduce_scatter(w.gsize, w.grank, recvcounts, dt->size, dt->extent, &p))) return rc;
+    log_plan("reduce_scatter (flat over the job)", p, total);
+    pvar_note(PV_COLL_REDUCE_SCATTER, p, in_place, total, w.gsize);
+    char *W = nullptr;
+    if ((rc = mn_reserve_dev(S)) || (rc = mn_gather_all(src, S, &W, stream))) return rc;
+    if (!recvcounts[w.grank]) return 0;
+    const void *srcs[kMaxRanks];
+    for (int r = 0; r < w.gsize; ++r) srcs[r] = W + (size_t)r * S;
+    if (p.algo == ALG_NONE) {  // REPLACE / NO_OP: nothing to reduce
+        return hipMemcpy(recvbuf, (const char *)srcs[w.grank] + off * ext, recvcounts[w.grank] * ext,
+                         hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+    }
+    if ((rc = mv2h_reduce_n_prog(srcs, w.gsize, g_mn.d1, total, dtype, op, (const mv2h_progset *)&p.ps, nullptr)))
+        return rc;
+    return hipMemcpy(recvbuf, g_mn.d1 + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess
+               ? 0 : E_INTERN;
 }
+
+}  // extern "C" (a C++ entry point for mpi/user_coll.cpp)
+
+// Host-evaluated reductions across nodes (user ops, x87 types; mpi/user_coll.cpp): the schedule the
+// device path above runs, as programs.  Allreduce: a non-commutative op fails every shortcut and
+// every two-level test and runs recursive doubling over the job (allreduce_osu.c:3359-3368);
+// MPI_Iallreduce the flat naive schedule; else mn_select's choice (flat ring wrapper / flat
+// pt2pt_rs or _rd / two-level with the entry's intra and inter functions).  Reduce: the flat
+// binomial for a non-commutative op (the two-level helper needs a commutative one,
+// reduce_osu.c:2628-2636) and for MPI_Ireduce, else the two-level helper (node reduce to local rank
+// 0, binomial over the leaders to the root's node).  Flat schedules need the job's ranks as
+// program registers (up to kMaxRanks).
+int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool in_place, int opk, int root, MnSched *s) {
+    const World &w = world();
+    const int n = w.gsize, me = w.grank, L = w.size, K = w.nnodes;
+    memset(s, 0, sizeof(*s));
+    s->kind = MN_FLAT;
+    s->U = 0;
+    int rc = 0;
+    if (coll == MN_COLL_REDUCE) {
+        if (opk == OPK_USER_NONCOMM || nbc_kind() == NBC_IREDUCE) {
+            if (n > kMaxRanks) return E_UNSUPPORTED;
+            rc = plan_reduce(n, me, root, count, tsize, textent, &s->p, opk);
+            if (!rc) pvar_note(PV_COLL_REDUCE, s->p, in_place, count, n);
+            return rc;
+        }
+        s->kind = MN_TWO_LEVEL;
+        const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
+        pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
+        if ((rc = plan_reduce(L, 0, 0, count, tsize, textent, &s->node, opk))) return rc;
+        return plan_binomial(K, root / L, &s->lead);
+    }
+    if (opk == OPK_USER_NONCOMM || (nbc_kind() == NBC_IALLREDUCE && n <= kMaxRanks)) {
+        if (n > kMaxRanks) return E_UNSUPPORTED;
+        if ((rc = plan_allreduce(n, me, count, tsize, textent, in_place, 0, &s->p, opk))) return rc;
+        pvar_note(PV_COLL_ALLREDUCE, s->p, in_place, count, n);
+        return 0;
+    }
+    int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD;
+    const int sel = mn_select((long)count * tsize, &intra, &inter);
+    if (sel == 1 && n <= kMaxRanks) {  // the flat ring wrapper over every rank
+        const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
+        if (!in_place && count >= (size_t)n) {
+            pvar_note_ids(chain, count % (size_t)n ? 3 : 2);
+            s->forced = ALG_RING;
+            s->U = (long)(count / n) * n;
+            if ((rc = plan_allreduce(n, me, (size_t)s->U, tsize, textent, false, ALG_RING, &s->p, opk))) return rc;
+        } else {
+            const int rs_chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
+            pvar_note_ids(rs_chain, 2);
+            s->forced = ALG_PT2PT_RS;
+            s->U = in_place ? (long)(count / n) * n : 0;  // IN_PLACE: two pt2pt_rs calls (:4095, :3800)
+            if (s->U && (rc = plan_allreduce(n, me, (size_t)s->U, tsize, textent, true, ALG_PT2PT_RS, &s->p, opk)))
+                return rc;
+        }
+        if ((size_t)s->U < count)
+            rc = plan_allreduce(n, me, count - (size_t)s->U, tsize, textent, in_place, ALG_PT2PT_RS, &s->rem, opk);
+        if (!s->U) s->p = s->rem;
+        return rc;
+    }
+    if ((sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD) && n <= kMaxRanks) {
+        s->forced = sel;
+        if ((rc = plan_allreduce(n, me, count, tsize, textent, in_place, sel, &s->p, opk))) return rc;
+        pvar_note(PV_COLL_ALLREDUCE, s->p, in_place, count, n);
+        return 0;
+    }
+    // two-level (also the fall-back of a flat choice over more than kMaxRanks ranks)
+    s->kind = MN_TWO_LEVEL;
+    if (sel != 0) {
+        intra = MN_INTRA_NODE;
+        inter = ALG_PT2PT_RD;
+    }
+    const int chain[2] = {PV_AR_2LVL, inter == ALG_PT2PT_RS ? PV_AR_SHM_RS : PV_AR_SHM_RD};
+    pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
+    if (K > kMaxRanks) return E_UNSUPPORTED;
+    switch (intra) {
+    case MN_INTRA_P2P: rc = plan_reduce(L, 0, 0, count, tsize, textent, &s->node, opk); break;
+    case MN_INTRA_SHMEM: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, ALG_SHMEM_LINEAR, &s->node, opk); break;
+    case MN_INTRA_RS: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, ALG_PT2PT_RS, &s->node, opk); break;
+    default: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, 0, &s->node, opk); break;
+    }
+    if (rc) return rc;
+    return plan_allreduce(K, w.node, count, tsize, textent, true, inter, &s->lead, opk);
+}
+
+extern "C" {
 
 static int mn_unsupported(const char *what) {
     MV2_ERR("%s is not supported across nodes (two-level: Allreduce, Reduce, Reduce_scatter, Bcast, Allgather, Barrier)", what);

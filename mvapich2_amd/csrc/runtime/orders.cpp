@@ -788,11 +788,18 @@ static int plan_allreduce_build(int n, int me, size_t count, int tsize, int text
 // to 8 ranks; comm_size_index :3210-3228 over minimum numproc 2).  Returns 0 (is_two_level),
 // ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every rank), or -1 (entry not restated).  The multicast
 // entries fall back to recursive doubling (:3324-3338).
-int mn_allreduce_table(int ppn, int gsize, long nbytes) {
+int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) {
     const int idx = table_index(nbytes, 1, 18);
+    auto two_level = [&](int in, int a) {
+        if (intra) *intra = in;
+        if (inter) *inter = a == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
+        return 0;
+    };
     if (ppn_conf(ppn) == 2) {
         if (gsize > 16) return -1;
-        return kAr16.two_level[idx] ? 0 : (kAr16.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS);
+        // the node's one-node plan (ppn >= 3 ranks) reads this same entry's intra function
+        if (kAr16.two_level[idx]) return two_level(MN_INTRA_NODE, kAr16.inter[idx]);
+        return kAr16.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
     }
     if (gsize < 2 || gsize > 8) return -1;
     int ci = 0;  // comm_size_index: log2(floor_pof2(gsize) / 2)
@@ -800,25 +807,34 @@ int mn_allreduce_table(int ppn, int gsize, long nbytes) {
     struct Entry {
         int two_level[18];
         int inter[18];
+        int intra[18];
     };
+    enum { SH = MN_INTRA_SHMEM, PP = MN_INTRA_P2P, RS = MN_INTRA_RS };
+    // nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_2ppn.h numproc 2 / 4 / 8 (inter-leader and intra-node lists)
     static const Entry k2ppn[3] = {
         {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0},
-         {A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS}},
+         {A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS},
+         {SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, PP, PP, PP, PP, PP, PP}},
         {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0},
-         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}},
+         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS},
+         {SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, PP, PP, PP, PP, PP}},
         {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0},
-         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS}}};
+         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS},
+         {SH, SH, SH, SH, SH, SH, RS, SH, SH, SH, SH, SH, PP, PP, PP, PP, PP, PP}}};
     static const Entry k1ppn[3] = {
         {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RD, A_RS, A_RS, A_RS}},
+         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RD, A_RS, A_RS, A_RS},
+         {}},
         {{0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},  // idx 1: multicast -> RD, two-level
-         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}},
+         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS},
+         {}},
         {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 0, 0},
-         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS}}};
+         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS},
+         {}}};
     const Entry &e = ppn_conf(ppn) == 1 ? k2ppn[ci] : k1ppn[ci];
     // one rank per node: the two-level algorithm is its leaders' algorithm over every rank
     // (MPIR_Allreduce_two_level_MV2 :1750-1780 with nothing to reduce or broadcast in a node)
-    if (e.two_level[idx] && ppn > 1) return 0;
+    if (e.two_level[idx] && ppn > 1) return two_level(e.intra[idx], e.inter[idx]);
     return e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
 }
 
@@ -1008,6 +1024,12 @@ int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, P
                       [&] { return plan_ireduce_build(n, root, count, p, opk); });
     return cached(make_key(1, n, me, root, count, nullptr, tsize, textent, false, 0, opk), p,
                   [&] { return plan_reduce_build(n, me, root, count, tsize, textent, p, opk); });
+}
+
+int plan_binomial(int n, int root, Plan *p, bool noncomm) {
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    return reduce_fill(p, ALG_BINOMIAL, n, root, 0, 0, noncomm);
 }
 
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *p, int opk) {

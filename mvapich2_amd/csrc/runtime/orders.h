@@ -125,9 +125,20 @@ enum OpKind : int { OPK_BUILTIN = 0, OPK_USER_COMM = 1, OPK_USER_NONCOMM = 2 };
 // reference's selection, else an Algo to run (ring wrapper parts).
 int plan_allreduce(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced, Plan *out,
                    int opk = OPK_BUILTIN);
-// several nodes: the allreduce tuning-table choice (0 two-level, ALG_PT2PT_RS / _RD flat, -1 unknown)
-int mn_allreduce_table(int ppn, int gsize, long nbytes);
+// several nodes: the allreduce tuning-table choice (0 two-level, ALG_PT2PT_RS / _RD flat, -1 unknown).
+// For a two-level entry *intra / *inter name the entry's node step (MN_INTRA_*) and the leaders'
+// algorithm (ALG_PT2PT_RD / ALG_PT2PT_RS) of MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1687-1800).
+enum MnIntra : int {
+    MN_INTRA_NODE = 0,    // the node's own one-node selection reads the same table entry (16 ppn)
+    MN_INTRA_SHMEM = 1,   // MPIR_Allreduce_reduce_shmem_MV2: ((x0 . x1) . x2) ... at the leader
+    MN_INTRA_P2P = 2,     // MPIR_Allreduce_reduce_p2p_MV2: MPIR_Reduce_MV2 to local rank 0 (:1614-1684)
+    MN_INTRA_RS = 3,      // MPIR_Allreduce_pt2pt_rs_MV2 over the node's communicator, leader's result
+};
+int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra = nullptr, int *inter = nullptr);
 int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *out, int opk = OPK_BUILTIN);
+// MPIR_Reduce_binomial_MV2 (reduce_osu.c:425) to `root`, whatever the selection (the leaders' step
+// of MPIR_Reduce_two_level_helper_MV2 across nodes)
+int plan_binomial(int n, int root, Plan *out, bool noncomm = false);
 // counts[n] per-rank block counts; elements are indexed over the whole operand
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *out,
                         int opk = OPK_BUILTIN);
@@ -147,6 +158,25 @@ enum NbcKind : int {
 };
 void nbc_set(int kind);
 int nbc_kind();
+
+// Several nodes: the schedule of a host-evaluated reduction (user MPI_Op, x87 types) over the job,
+// as runtime/coll.cpp restates it for the device path (mn_select, MPIR_Allreduce_two_level_MV2,
+// MPIR_Reduce_two_level_helper_MV2, the flat algorithms over every rank).  MN_FLAT: `p` holds this
+// rank's programs over the job's ranks (forced: the plan_allreduce / plan_reduce argument that
+// reproduces any rank's; for the ring, elements [0, U) take `p` and [U, count) `rem`, counted from
+// U; ranges split over the ranks when every rank's programs agree).  MN_TWO_LEVEL: `node` = the
+// node step's programs for local rank 0 over the node's ranks, `lead` = the leaders' programs over
+// the nodes' partials for the leader whose result this rank takes (its own node's, or for
+// MPI_Reduce the root's node).
+enum : int { MN_FLAT = 0, MN_TWO_LEVEL = 1 };
+enum : int { MN_COLL_ALLREDUCE = 0, MN_COLL_REDUCE = 1 };
+struct MnSched {
+    int kind;
+    int forced;
+    long U;
+    Plan p, rem, node, lead;
+};
+int mn_host_schedule(int coll, size_t count, int tsize, int textent, bool in_place, int opk, int root, MnSched *s);
 
 const char *algo_name(int algo);
 

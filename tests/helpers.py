@@ -32,9 +32,18 @@ def np_dtype(type_name):
     return np.dtype(desc)
 
 
-def rand_typed(type_name, count, rng, edges=True, small=False):
-    """Seeded random operand of `count` elements (as a byte-backed numpy array)."""
+def rand_typed(type_name, count, rng, edges=True, small=False, ties=False):
+    """Seeded random operand of `count` elements (as a byte-backed numpy array).  ties: floating
+    values drawn from {+-0, +-1, two NaN payloads}, so every element's MAX / MIN result depends on
+    which operand is the accumulator (signed-zero ties keep inout, NaN against NaN keeps inout)."""
     dt = np_dtype(type_name)
+    if ties and dt.kind == "f":
+        pool = np.array([0.0, -0.0, 1.0, -1.0, np.nan, np.nan], dtype=dt)
+        if dt.itemsize == 4:
+            pool[4:] = np.array([0x7FC00011, 0xFFC00022], dtype=np.uint32).view(np.float32)
+        else:
+            pool[4:] = np.array([0x7FF8000000000011, 0xFFF8000000000022], dtype=np.uint64).view(np.float64)
+        return pool[rng.integers(0, len(pool), count)]
     if type_name == "MPI_C_BOOL":  # _Bool objects hold only 0 / 1 (other bytes are UB in C)
         return rng.integers(0, 2, count).astype(dt)
     if dt.names:

@@ -20,7 +20,8 @@ WORLD = 0x44000000
 
 def inputs(case, rank):
     rng = np.random.default_rng(case["seed"] * 1000 + rank)
-    return rand_typed(case["type"], case["count"], rng, small=case.get("small", False))
+    return rand_typed(case["type"], case["count"], rng, small=case.get("small", False),
+                      ties=case.get("ties", False))
 
 
 def enqueue_seq(L, case, rank, n):
@@ -373,6 +374,25 @@ def main():
             sb = m.DeviceBuffer.from_array(x)
             rb = m.DeviceBuffer(count * 4)
             rc = L.MPI_Allreduce(sb.ptr, rb.ptr, count, TYPES["MPI_INT"][0], op.value, WORLD)
+            assert rc == 0, (case["id"], rc)
+            res = rb.download(np.uint8, count=count * 4)
+            L.MPI_Op_free(ctypes.byref(op))
+        elif k == "user_reduce":
+            FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(ctypes.c_int))
+
+            def uop(inp, io, ln, dt):
+                c = ln[0]
+                a = np.ctypeslib.as_array((ctypes.c_int * c).from_address(inp))
+                b = np.ctypeslib.as_array((ctypes.c_int * c).from_address(io))
+                b[:] = a * 2 + b * 3
+            cb = FN(uop)
+            op = ctypes.c_int()
+            L.MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), case["commute"], ctypes.byref(op))
+            x = (np.arange(count, dtype=np.int32) + rank) % 7
+            sb = m.DeviceBuffer.from_array(x)
+            rb = m.DeviceBuffer(count * 4)
+            rc = L.MPI_Reduce(sb.ptr, rb.ptr, count, TYPES["MPI_INT"][0], op.value, case["root"], WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=count * 4)
             L.MPI_Op_free(ctypes.byref(op))

@@ -27,7 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def inputs(case, rank):
     rng = np.random.default_rng(case["seed"] * 1000 + rank)
-    return rand_typed(case["type"], case["count"], rng, small=case.get("small", False))
+    return rand_typed(case["type"], case["count"], rng, small=case.get("small", False),
+                      ties=case.get("ties", False))
 
 
 GEOMS = {"default": {}, "small": {"MV2AMD_PIPE_GRID": "3", "MV2AMD_PIPE_SUB": "4096"}}

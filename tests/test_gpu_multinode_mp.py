@@ -2,17 +2,20 @@
 n / ppn nodes, each with its own control segment and IPC world, the node leaders linked over
 TCP (runtime/internode.cpp).  Results are checked bit-exactly against a restatement of
 MVAPICH2's two-level structure built from the oracle: node step = the oracle's one-node
-algorithm for the node's ranks, inter-node step = recursive doubling (allreduce, the inter step
-of MPIR_Allreduce_two_level_MV2 / topo-aware hierarchical, allreduce_osu.c:360-630, :2215) or
-binomial reduce (reduce_osu.c:425) over the node leaders, every uop an oracle op-loop call.
-Allreduce from 2 MiB is the flat ring over every rank, and where the 16-ppn table names it the
-flat pt2pt_rs over every rank (expected_allreduce); reduce-scatter is the allreduce's block (the
-reference's flat reduce-scatter algorithms are not restated across nodes)."""
+algorithm for the node's ranks (the small-message shortcuts, and 16-ppn table entries, whose
+intra function the one-node selection reads too) or the 2-ppn table entry's reduce_shmem,
+inter-node step = the table's recursive doubling or pt2pt_rs over the node leaders (the inter step
+of MPIR_Allreduce_two_level_MV2 / topo-aware hierarchical, allreduce_osu.c:360-630, :633-1054,
+:1750-1780, :2215) or binomial reduce (reduce_osu.c:425) over the node leaders, every uop an
+oracle op-loop call.  Allreduce from 2 MiB is the flat ring over every rank, and where the tables
+name it the flat pt2pt_rs / pt2pt_rd over every rank (expected_allreduce); reduce-scatter is
+MPIR_Reduce_scatter_MV2's flat selection over every rank (red_scat_osu.c:1771-1900)."""
 import numpy as np
 import pytest
 
 from mvapich2_amd.consts import OPS, TYPES
 from oracle import oracle
+from tests import ref_user
 from tests.helpers import as_bytes, assert_bytes_equal
 from tests.test_gpu_collectives_mp import inputs, run_workers
 
@@ -90,25 +93,25 @@ _T1 = ["| rd rd rd rd rd rd rd rd rd rd rd rd rd rs rd rs rs rs",
        "| rs rd rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs"]
 
 
-def table_flat(ppn, n, nbytes):
-    """None (two-level) or the flat algorithm MVAPICH2's tables pick across nodes"""
+def table_entry(ppn, n, nbytes, knobs=None):
+    """("2l", inter) for a two-level entry or ("flat", algorithm) of MVAPICH2's tables across nodes"""
     idx = min(17, max(0, nbytes.bit_length() - 1))
     if ppn >= 3:  # 16-ppn table, first entry: the one-node selection for ppn ranks reads it too
-        a = oracle.ALGOS[oracle.allreduce_select(ppn, max(1, nbytes // 4), TYPES["MPI_FLOAT"][0])]
-        return a if a in ("pt2pt_rs", "pt2pt_rd") else None
+        a = oracle.ALGOS[oracle.allreduce_select(ppn, max(1, nbytes // 4), TYPES["MPI_FLOAT"][0], knobs=knobs)]
+        return ("flat", a) if a in ("pt2pt_rs", "pt2pt_rd") else ("2l", "pt2pt_rs")  # its inter list: all rs
     ci = (n // 2).bit_length() - 1
     row = (_T2 if ppn == 2 else _T1)[ci]
-    # "|" splits the two-level prefix from the flat suffix, "." marks further two-level entries
+    # "|" splits the two-level prefix from the flat suffix
     head, tail = row.split("|")
     cells = [("2l", c) for c in head.split()] + [("flat", c) for c in tail.split()]
     kind, fn = cells[idx]
-    return None if kind == "2l" or fn == "." else "pt2pt_" + fn
+    return kind, "pt2pt_" + fn
 
 
 def expected_allreduce(sends, count, t, op, ppn, in_place=False):
     """per-rank results of MPI_Allreduce across nodes, by the selection coll.cpp mn_allreduce
     restates: flat ring from 2 MiB (remainder: flat pt2pt_rs over every rank for n <= 8), the flat
-    pt2pt_rs where the 16-ppn table names it (ppn >= 3, n <= 8), else two-level"""
+    pt2pt_rs / pt2pt_rd where the tables name it (n <= 8), else two-level"""
     n = len(sends)
     if count * TYPES[t][2] >= 2 << 20 and (in_place or count < n) and n <= 8:  # the wrapper's pt2pt_rs
         rs = oracle.ALGOS.index("pt2pt_rs")
@@ -127,22 +130,32 @@ def expected_allreduce(sends, count, t, op, ppn, in_place=False):
             return [main] * n
         tails = [x[len(main):].copy() for x in sends]
         tail = oracle.allreduce(tails, rem, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index("pt2pt_rs")) if n <= 8 \
-            else [x for x in two_level(tails, rem, t, op, ppn) for _ in range(ppn)]
+            else two_level(tails, rem, t, op, ppn)
         return [np.concatenate([main, tail[r]]) for r in range(n)]
     nbytes = count * TYPES[t][2]
-    flat = table_flat(ppn, n, nbytes) if nbytes > 2048 and n <= 8 else None  # topo-aware up to 2 KiB
-    if flat:
-        return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op],
-                                algo=oracle.ALGOS.index(flat))
-    return [x for x in two_level(sends, count, t, op, ppn) for _ in range(ppn)]
+    if nbytes > 2048 and n <= 8:  # the topology-aware shortcut up to 2 KiB, then the tables
+        kind, fn = table_entry(ppn, n, nbytes)
+        if kind == "flat":
+            return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op],
+                                    algo=oracle.ALGOS.index(fn))
+        return two_level(sends, count, t, op, ppn, inter=fn, pair_shmem=ppn == 2)
+    return two_level(sends, count, t, op, ppn)
 
 
-def two_level(sends, count, t, op, ppn):
-    """node allreduce (the oracle's one-node algorithm), recursive doubling over the leaders"""
+def two_level(sends, count, t, op, ppn, inter="pt2pt_rd", pair_shmem=False, knobs=None):
+    """MPIR_Allreduce_two_level_MV2: node step (the oracle's one-node algorithm, or for a 2-ppn table
+    entry its reduce_shmem: x0 (+) x1 at the leader), the leaders' inter algorithm, node broadcast"""
     nodes = len(sends) // ppn
-    parts = [oracle.allreduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0], OPS[op])[0]
-             for j in range(nodes)]
-    return rd_leaders(parts, count, t, op)
+    if pair_shmem:
+        parts = [uop(sends[2 * j + 1], sends[2 * j], count, t, op) for j in range(nodes)]
+    else:
+        parts = [oracle.allreduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0], OPS[op],
+                                      knobs=knobs)[0] for j in range(nodes)]
+    if inter == "pt2pt_rd":
+        lead = rd_leaders(parts, count, t, op)
+    else:
+        lead = oracle.allreduce(parts, count, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index(inter))
+    return [lead[r // ppn] for r in range(len(sends))]
 
 
 @pytest.mark.timeout(300)
@@ -184,11 +197,37 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
         cases.append({"id": f"mb{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
                       "seed": seed, "root": root})
         seed += 1
+    # 4-8 KiB: the 2-ppn table's numproc 4 entry is two-level (reduce_shmem + recursive doubling);
+    # signed zeros and NaN payloads make the operand order visible in MAX / MIN
+    for t, op, count in (("MPI_DOUBLE", "MPI_MAX", 600), ("MPI_FLOAT", "MPI_MIN", 1500)):
+        cases.append({"id": f"mt{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "ties": True})
+        seed += 1
+    # reduce-scatter over every rank: basic (<= 256 B), recursive halving, pairwise, ring (>= 128 KiB)
+    for t, op, per, ties in (("MPI_FLOAT", "MPI_SUM", 7, False), ("MPI_DOUBLE", "MPI_MAX", 150, True),
+                             ("MPI_FLOAT", "MPI_SUM", 1500, False), ("MPI_FLOAT", "MPI_SUM", 12000, False)):
+        counts = [per + (r % 2) for r in range(n)]
+        cases.append({"id": f"ms{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
+                      "count": sum(counts), "seed": seed, "ties": ties})
+        seed += 1
     for t, op, per in (("MPI_INT", "MPI_SUM", 7001), ("MPI_FLOAT", "MPI_SUM", 100)):
         counts = [per + (r % 3) for r in range(n)]
         cases.append({"id": f"ms{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
                       "count": sum(counts), "seed": seed})
         seed += 1
+    # x87 long double across nodes: host-evaluated in 80-bit on the same schedules (mpi/user_coll.cpp)
+    for kind, op, count in (("allreduce", "MPI_SUM", 100), ("allreduce", "MPI_SUM", 70001),
+                            ("allreduce", "MPI_MAX", 1000), ("allreduce", "MPI_SUM", 140001)):
+        cases.append({"id": f"mx{seed}", "kind": kind, "type": "MPI_LONG_DOUBLE", "op": op, "count": count,
+                      "seed": seed})
+        seed += 1
+    cases.append({"id": f"mx{seed}", "kind": "reduce", "type": "MPI_LONG_DOUBLE", "op": "MPI_SUM", "count": 30001,
+                  "seed": seed, "root": n - 1})
+    seed += 1
+    xc = [3000 + r for r in range(n)]
+    cases.append({"id": f"mx{seed}", "kind": "reduce_scatter", "type": "MPI_LONG_DOUBLE", "op": "MPI_SUM",
+                  "recvcounts": xc, "count": sum(xc), "seed": seed})
+    seed += 1
     for count in (1000, 100003):
         cases.append({"id": f"mg{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": count,
                       "seed": seed})
@@ -214,13 +253,13 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                                        OPS[case["op"]], 0) for j in range(nodes)]
             want = binomial_leaders(parts, count, t, case["op"], rnode)
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
-        elif k == "reduce_scatter":  # the allreduce of the whole operand, then the block
+        elif k == "reduce_scatter":  # MPIR_Reduce_scatter_MV2 flat over every rank
             counts = case["recvcounts"]
-            full = expected_allreduce(sends, count, t, case["op"], ppn)
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
             ext = TYPES[t][3]
             off = 0
             for r in range(n):
-                blk = full[r][off * ext:(off + counts[r]) * ext]
+                blk = full[off * ext:(off + counts[r]) * ext]
                 assert_bytes_equal(res(cid, r), blk, t, counts[r], f"{cid} reduce_scatter rank {r}")
                 off += counts[r]
         elif k == "bcast":
@@ -233,13 +272,122 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                 assert np.array_equal(res(cid, r), want), (cid, r)
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,ppn", [(6, 3), (8, 4), (4, 2)])
+def test_two_level_table_entries_across_nodes(n, ppn, tmp_path):
+    """With the small-message shortcuts off (MV2_ENABLE_TOPO_AWARE_COLLECTIVES=0,
+    MV2_ENABLE_SKIP_TUNING_TABLE_SEARCH=0) small allreduces read the tables' two-level entries: at
+    >= 3 ranks per node the 16-ppn entry's intra function (reduce_shmem, or reduce_p2p = the node's
+    MPIR_Reduce_MV2 to local rank 0 from 256 B) and pt2pt_rs over the leaders (recursive doubling
+    for count < pof2); at 2 ranks per node the 2-ppn entry's reduce_shmem and recursive doubling."""
+    env = {"MV2_ENABLE_TOPO_AWARE_COLLECTIVES": "0", "MV2_ENABLE_SKIP_TUNING_TABLE_SEARCH": "0"}
+    k = oracle.default_knobs(enable_topo=0, enable_skip_search=0)
+    cases, seed = [], 900
+    for t, op, count, ties in (("MPI_FLOAT", "MPI_SUM", 100, False), ("MPI_DOUBLE", "MPI_MAX", 50, True),
+                               ("MPI_FLOAT", "MPI_SUM", 60, False), ("MPI_FLOAT", "MPI_MIN", 60, True),
+                               ("MPI_INT", "MPI_SUM", 3, False), ("MPI_DOUBLE", "MPI_MAX", 1, True)):
+        cases.append({"id": f"mk{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "ties": ties})
+        seed += 1
+    res = run_workers(n, cases, tmp_path, ppn=ppn, extra_env=env)
+    for case in cases:
+        cid, t, count = case["id"], case["type"], case["count"]
+        sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+        kind, fn = table_entry(ppn, n, count * TYPES[t][2], knobs=k)
+        assert kind == "2l", (cid, kind, fn)
+        want = two_level(sends, count, t, case["op"], ppn, inter=fn, pair_shmem=ppn == 2, knobs=k)
+        for r in range(n):
+            assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
+
+
+def _ufn(a, b):
+    """the workers' user op: inout = 2 in + 3 inout (int32, wrapping; neither commutative nor associative)"""
+    return (a.astype(np.int64) * 2 + b.astype(np.int64) * 3).astype(np.int32)
+
+
+def user_allreduce_across(xs, commute, count, ppn):
+    """MPI_Allreduce with a user op across nodes (coll.cpp mn_host_schedule): non-commutative ->
+    recursive doubling over every rank; commutative -> mn_select's schedule: the topology-aware
+    shortcut up to 2 KiB (node tree, leaders' recursive doubling), a 2-ppn two-level entry
+    (reduce_shmem + recursive doubling), else the tables' flat pt2pt_rs, which a user op turns into
+    recursive doubling (allreduce_osu.c:802)"""
+    n = len(xs)
+    F = TYPES["MPI_INT"][0]
+    if not commute:
+        return ref_user.rd(xs, _ufn, False)
+    nbytes = count * 4
+    if nbytes <= 2048 and ppn == 1:
+        parts = [x.copy() for x in xs]
+    elif nbytes <= 2048:
+        parts = [ref_user.allreduce(xs[j * ppn:(j + 1) * ppn], _ufn, True, F, count)[0] for j in range(n // ppn)]
+    else:
+        kind, fn = table_entry(ppn, n, nbytes)
+        if kind == "flat":
+            return ref_user.rd(xs, _ufn, True)
+        parts = [ref_user.linear(xs[j * ppn:(j + 1) * ppn], _ufn) for j in range(n // ppn)]
+    lead = ref_user.rd(parts, _ufn, True)
+    return [lead[r // ppn] for r in range(n)]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 3), (8, 4), (3, 1)])
+def test_user_ops_across_nodes(n, ppn, tmp_path):
+    """User MPI_Ops across nodes (host-evaluated, mpi/user_coll.cpp): the device path's schedule
+    over the job's ranks — two-level (node step, leaders' step) or flat — with operands that travel
+    packed over the leaders' links; MPI_Reduce: the two-level helper (node reduce to local rank 0,
+    binomial over the leaders) for a commutative op, the flat binomial for a non-commutative one;
+    MPI_Reduce_scatter: MPIR_Reduce_scatter_MV2's flat selection (non_comm forms included)."""
+    cases, seed = [], 700
+    for commute in (1, 0):
+        for count in (100, 2000, 33):
+            cases.append({"id": f"ua{seed}", "kind": "user_allreduce", "commute": commute, "count": count,
+                          "type": "MPI_INT", "seed": seed})
+            seed += 1
+        for count, root in ((100, n - 1), (3000, 1 % n)):
+            cases.append({"id": f"ur{seed}", "kind": "user_reduce", "commute": commute, "count": count,
+                          "type": "MPI_INT", "seed": seed, "root": root})
+            seed += 1
+        for per in (3, 400):
+            counts = [per] * n if not commute else [per + (r % 2) for r in range(n)]
+            cases.append({"id": f"us{seed}", "kind": "user_reduce_scatter", "commute": commute, "count": sum(counts),
+                          "recvcounts": counts, "type": "MPI_INT", "seed": seed})
+            seed += 1
+    res = run_workers(n, cases, tmp_path, ppn=ppn)
+    for case in cases:
+        cid, k, count, commute = case["id"], case["kind"], case["count"], bool(case["commute"])
+        if k == "user_allreduce":
+            xs = [(np.arange(count, dtype=np.int32) + r) % 7 for r in range(n)]
+            want = user_allreduce_across(xs, commute, count, ppn)
+            for r in range(n):
+                assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
+        elif k == "user_reduce":
+            xs = [(np.arange(count, dtype=np.int32) + r) % 7 for r in range(n)]
+            root = case["root"]
+            if commute and ppn == 1:
+                want = ref_user.binomial(xs, _ufn, root, True)
+            elif commute:
+                parts = [ref_user.reduce(xs[j * ppn:(j + 1) * ppn], _ufn, True, TYPES["MPI_INT"][0], count, 0)
+                         for j in range(n // ppn)]
+                want = ref_user.binomial(parts, _ufn, root // ppn, True)
+            else:
+                want = ref_user.reduce(xs, _ufn, False, TYPES["MPI_INT"][0], count, root)
+            assert np.array_equal(res(cid, root).view(np.int32), want), (cid, root)
+        else:
+            counts = case["recvcounts"]
+            xs = [((np.arange(sum(counts)) + r) % 7).astype(np.int32) for r in range(n)]
+            want = ref_user.reduce_scatter(xs, _ufn, TYPES["MPI_INT"][0], counts) if commute else \
+                ref_user.reduce_scatter_noncomm(xs, _ufn, counts)
+            for r in range(n):
+                assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
+
+
 @pytest.mark.timeout(200)
 def test_mpit_counts_across_nodes(tmp_path):
     """MPI_T across nodes: Allreduce counts MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) and,
     on the node leaders, the leaders' recursive doubling (pt2pt_rd :366); Reduce counts the
     two-level helper (reduce_osu.c:2039) and the leaders' binomial (:450); a 2.4 MB Allreduce the
-    flat ring wrapper and ring (:3761, :3898); Reduce_scatter across nodes is not one of the
-    reference's counted chains, so it counts nothing."""
+    flat ring wrapper and ring (:3761, :3898); Reduce_scatter (400 floats over 4 ranks) its flat
+    recursive halving (red_scat_osu.c:449)."""
     import json
     n, ppn = 4, 2
     calls = [{"coll": "allreduce", "type": "MPI_FLOAT", "count": 300},
@@ -250,7 +398,7 @@ def test_mpit_counts_across_nodes(tmp_path):
     res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path, ppn=ppn)
     for r in range(n):
         want = {"mv2_coll_allreduce_2lvl": 1, "mv2_coll_reduce_two_level_helper": 1,
-                "mv2_coll_allreduce_pt2pt_ring_wrapper": 1, "mv2_coll_allreduce_pt2pt_ring": 1,
+                "mv2_coll_reduce_scatter_rec_halving": 1, "mv2_coll_allreduce_pt2pt_ring_wrapper": 1, "mv2_coll_allreduce_pt2pt_ring": 1,
                 "mv2_coll_allreduce_shm_rs": 1}
         if r % ppn == 0:
             want.update({"mv2_coll_allreduce_shm_rd": 1, "mv2_coll_reduce_binomial": 1})
