@@ -1717,6 +1717,25 @@ static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, i
 static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
                              int algo, int root = -1);
 
+// The node's S-byte operands at its leader only (G: L * S bytes, local rank order; unused on the
+// other ranks), over the node's device point-to-point channels in the library's collective context
+static int gather_node_leader(const void *mine, char *G, size_t S) {
+    World &w = world();
+    const int L = w.size;
+    unsigned long long req[kMaxRanks] = {};
+    int rc = 0;
+    if (w.rank != 0) {
+        if ((rc = p2p_isend(mine, S, 0, kCollTagBase - 2, &req[0]))) return rc;
+        return mv2h_p2p_wait(req[0], nullptr, nullptr, nullptr);
+    }
+    for (int l = 1; l < L; ++l)
+        if ((rc = p2p_irecv(G + (size_t)l * S, S, l, kCollTagBase - 2, &req[l]))) return rc;
+    if (hipMemcpy(G, mine, S, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+    for (int l = 1; l < L; ++l)
+        if ((rc = mv2h_p2p_wait(req[l], nullptr, nullptr, nullptr))) return rc;
+    return 0;
+}
+
 // Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
 // chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
 // the accumulator always inout (uop(comp_chunk, recv_chunk), :3958).  Here each node gathers its
@@ -1733,11 +1752,11 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     const size_t cc = count / (size_t)n, cb = cc * ext, sect = (size_t)L * cb, main_bytes = (size_t)K * sect;
     const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
     pvar_note_ids(chain, count % (size_t)n ? 3 : 2);
-    char *G = (char *)get_scratch(6, (size_t)L * S);  // the node's operands, local rank order
-    if (!G) return E_NO_MEM;
-    int rc = allgather_node(sendbuf, G, S, stream);
-    if (rc) return rc;
+    int rc = 0;
     if (w.rank == 0) {
+        char *G = (char *)get_scratch(6, (size_t)L * S);  // the node's operands, local rank order
+        if (!G) return E_NO_MEM;
+        if ((rc = gather_node_leader(sendbuf, G, S))) return rc;
         if ((rc = mn_reserve(std::max(main_bytes, sect)))) return rc;
         char *A = g_mn.d0;  // partial chunks of the group in hand
         auto X = [&](int l, size_t byte_off) { return (const char *)G + (size_t)l * S + byte_off; };
@@ -1774,6 +1793,8 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
                 return rc;
         }
         if ((rc = mn_h2d(recvbuf, g_mn.h1, main_bytes))) return rc;
+    } else if ((rc = gather_node_leader(sendbuf, nullptr, S))) {
+        return rc;
     }
     if ((rc = bcast_node(recvbuf, main_bytes, 0, stream))) return rc;
     if (count % (size_t)n == 0) return 0;
@@ -2019,11 +2040,11 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     // the root is not the leader: the node's device point-to-point channel carries the result
     unsigned long long req = 0;
     if (w.rank == 0) {
-        if ((rc = mv2h_isend(g_mn.d0, bytes, rlocal, 0x7d01, &req))) return rc;
+        if ((rc = p2p_isend(g_mn.d0, bytes, rlocal, kCollTagBase - 1, &req))) return rc;
         return mv2h_p2p_wait(req, nullptr, nullptr, nullptr);
     }
     if (me_root) {
-        if ((rc = mv2h_irecv(recvbuf, bytes, 0, 0x7d01, &req))) return rc;
+        if ((rc = p2p_irecv(recvbuf, bytes, 0, kCollTagBase - 1, &req))) return rc;
         return mv2h_p2p_wait(req, nullptr, nullptr, nullptr);
     }
     return 0;

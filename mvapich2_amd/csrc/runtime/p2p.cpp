@@ -85,7 +85,9 @@ std::list<Unexp *> g_unexp;            // unexpected messages in arrival order
 Arrival g_in[kMaxRanks];
 
 bool matches(const Req *r, int src, int tag) {
-    return (r->src_want == MV2H_ANY_SOURCE || r->src_want == src) && (r->tag_want == MV2H_ANY_TAG || r->tag_want == tag);
+    // MPI_ANY_TAG matches application tags only (>= 0), never the library's collective context
+    return (r->src_want == MV2H_ANY_SOURCE || r->src_want == src) &&
+           (r->tag_want == tag || (r->tag_want == MV2H_ANY_TAG && tag >= 0));
 }
 
 char *slot_ptr(char *arena, int src, uint64_t pos) {
@@ -242,14 +244,11 @@ uint64_t add_req(Req *r) {
 
 using namespace mv2;
 
-extern "C" {
-
-int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req) {
+int mv2::p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req) {
     int rc = ready();
     if (rc) return rc;
     World &w = world();
     if (dest < 0 || dest >= w.size) return E_RANK;
-    if (tag < 0) return E_TAG;
     if (bytes && !buf) return E_BUFFER;
     Req *r = new Req{};
     r->send = true;
@@ -264,12 +263,11 @@ int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long l
     return progress(&moved);  // eager: start pushing right away
 }
 
-int mv2h_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req) {
+int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req) {
     int rc = ready();
     if (rc) return rc;
     World &w = world();
     if (source != MV2H_ANY_SOURCE && (source < 0 || source >= w.size)) return E_RANK;
-    if (tag < 0 && tag != MV2H_ANY_TAG) return E_TAG;
     if (cap && !buf) return E_BUFFER;
     Req *r = new Req{};
     r->send = false;
@@ -304,6 +302,18 @@ int mv2h_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *r
     g_posted.push_back(r);
     bool moved;
     return progress(&moved);
+}
+
+extern "C" {
+
+int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req) {
+    if (tag < 0) return E_TAG;
+    return p2p_isend(buf, bytes, dest, tag, req);
+}
+
+int mv2h_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req) {
+    if (tag < 0 && tag != MV2H_ANY_TAG) return E_TAG;
+    return p2p_irecv(buf, cap, source, tag, req);
 }
 
 int mv2h_p2p_test(unsigned long long id, int *done, int *source, int *tag, size_t *bytes) {

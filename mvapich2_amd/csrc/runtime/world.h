@@ -185,5 +185,11 @@ void *get_scratch(int idx, size_t bytes);
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
 int pipe_autotune();  // coll.cpp: init-time choice of the pipelined kernels' tiling
 void host_prof_report();  // coll.cpp: MV2AMD_HOST_PROFILE summary
+// The library's own messages on the node's point-to-point channels (the steps of the multi-node
+// collectives) carry tags below kCollTagBase: the collective context of MPICH's comm (context_id +
+// MPID_CONTEXT_INTRA_COLL), so no application receive, MPI_ANY_TAG included, can match them.
+constexpr int kCollTagBase = -0x100;
+int p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req);  // runtime/p2p.cpp
+int p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req);
 
 }  // namespace mv2
