@@ -103,12 +103,14 @@ int mv2h_enqueue_check(void);
  * order (one stream).  mv2h_wait_ticket blocks; mv2h_test_ticket sets *done.  Both return
  * the collective's error class (e.g. a peer timeout), 0 on success. */
 /* ---- point-to-point (runtime/p2p.cpp; reference ch3 eager/IPC path, ch3u_recvq.c matching) ----
- * Byte messages between the ranks of the node; buffers may be device or host memory.
- * A send completes when its last chunk is in the receiver's arena (buffer reusable); a
- * receive completes when the matched message is in `buf` (E_TRUNCATE if it was longer
- * than cap: the first cap bytes are delivered).  Matching: posting order against arrival
- * order, MV2H_ANY_SOURCE / MV2H_ANY_TAG wildcards, non-overtaking per (source, tag).
- * Progress happens inside every isend/irecv/test/wait call. */
+ * Byte messages between ranks (global ranks, MPI_COMM_WORLD numbering); buffers may be device
+ * or host memory.  Within a node a send completes when its last chunk is in the receiver's
+ * arena; to a rank on another node (the rank mesh, TCP) when its bytes are in the socket
+ * (buffer reusable either way).  A receive completes when the matched message is in `buf`
+ * (E_TRUNCATE if it was longer than cap: the first cap bytes are delivered).  Matching:
+ * posting order against arrival order, MV2H_ANY_SOURCE / MV2H_ANY_TAG wildcards (application
+ * tags >= 0 only), non-overtaking per (source, tag).  Progress happens inside every
+ * isend/irecv/test/wait call. */
 #define MV2H_ANY_SOURCE (-2)
 #define MV2H_ANY_TAG (-1)
 int mv2h_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req);

@@ -922,10 +922,6 @@ int start_coll(MPI_Request *request, const char *fn, F &&call, int nbc = MV2H_NB
 
 int p2p_checks(MPI_Comm comm, int count, MPI_Datatype dt, int tag, bool recv) {
     if (!g_initialized) return MPI_ERR_OTHER;
-    if (world().nnodes > 1) {  // device channels connect the ranks of one node
-        fprintf(stderr, "[mv2amd] point-to-point is not supported across nodes\n");
-        return MPI_ERR_UNSUPPORTED_OPERATION;
-    }
     if (comm != MPI_COMM_WORLD) return comm_index(comm) < 0 ? MPI_ERR_COMM : MPI_ERR_UNSUPPORTED_OPERATION;
     if (count < 0) return MPI_ERR_COUNT;
     if (!dtype_valid(dt)) return MPI_ERR_TYPE;
@@ -941,7 +937,7 @@ int isend_impl(const void *buf, int count, MPI_Datatype dt, int dest, int tag, M
         *request = req_new(r);
         return MPI_SUCCESS;
     }
-    if (dest < 0 || dest >= world().size) return MPI_ERR_RANK;
+    if (dest < 0 || dest >= world().gsize) return MPI_ERR_RANK;
     r.kind = RQ_P2P;
     const void *src = buf;
     size_t bytes = (size_t)dtype_span(dt, count);
@@ -980,7 +976,7 @@ int irecv_impl(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_R
         *request = req_new(r);
         return MPI_SUCCESS;
     }
-    if (source != MPI_ANY_SOURCE && (source < 0 || source >= world().size)) return MPI_ERR_RANK;
+    if (source != MPI_ANY_SOURCE && (source < 0 || source >= world().gsize)) return MPI_ERR_RANK;
     r.kind = RQ_P2P;
     void *dst = buf;
     size_t cap = (size_t)dtype_span(dt, count);

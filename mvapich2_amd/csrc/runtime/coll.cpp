@@ -1721,15 +1721,15 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
 // other ranks), over the node's device point-to-point channels in the library's collective context
 static int gather_node_leader(const void *mine, char *G, size_t S) {
     World &w = world();
-    const int L = w.size;
+    const int L = w.size, base = w.node * w.size;  // point-to-point takes global ranks
     unsigned long long req[kMaxRanks] = {};
     int rc = 0;
     if (w.rank != 0) {
-        if ((rc = p2p_isend(mine, S, 0, kCollTagBase - 2, &req[0]))) return rc;
+        if ((rc = p2p_isend(mine, S, base, kCollTagBase - 2, &req[0]))) return rc;
         return mv2h_p2p_wait(req[0], nullptr, nullptr, nullptr);
     }
     for (int l = 1; l < L; ++l)
-        if ((rc = p2p_irecv(G + (size_t)l * S, S, l, kCollTagBase - 2, &req[l]))) return rc;
+        if ((rc = p2p_irecv(G + (size_t)l * S, S, base + l, kCollTagBase - 2, &req[l]))) return rc;
     if (hipMemcpy(G, mine, S, hipMemcpyDefault) != hipSuccess) return E_INTERN;
     for (int l = 1; l < L; ++l)
         if ((rc = mv2h_p2p_wait(req[l], nullptr, nullptr, nullptr))) return rc;
@@ -2040,11 +2040,11 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     // the root is not the leader: the node's device point-to-point channel carries the result
     unsigned long long req = 0;
     if (w.rank == 0) {
-        if ((rc = p2p_isend(g_mn.d0, bytes, rlocal, kCollTagBase - 1, &req))) return rc;
+        if ((rc = p2p_isend(g_mn.d0, bytes, root, kCollTagBase - 1, &req))) return rc;
         return mv2h_p2p_wait(req, nullptr, nullptr, nullptr);
     }
     if (me_root) {
-        if ((rc = p2p_irecv(recvbuf, bytes, 0, kCollTagBase - 1, &req))) return rc;
+        if ((rc = p2p_irecv(recvbuf, bytes, w.node * w.size, kCollTagBase - 1, &req))) return rc;
         return mv2h_p2p_wait(req, nullptr, nullptr, nullptr);
     }
     return 0;

@@ -64,8 +64,21 @@ struct Net {
     std::vector<int> fd;  // fd[node] (-1: self / not connected)
     int listen_fd = -1;
     bool up = false;
+    std::vector<std::string> ip;  // every node's address (the rendezvous' view; node 0: the boot host)
 };
 Net g_net;
+
+// rank mesh: one TCP stream between every pair of ranks on different nodes (point-to-point
+// across nodes, runtime/p2p.cpp)
+struct Mesh {
+    std::vector<int> fd;  // fd[global rank] (-1: same node / not connected)
+    int listen_fd = -1;
+};
+Mesh g_mesh;
+struct MeshHello {
+    int32_t magic;
+    int32_t grank;
+};
 
 double now_s() {
     timespec t;
@@ -286,6 +299,8 @@ int net_init() {
         for (int j = 1; j < nn; ++j)
             if (xfer(g_net.fd[j], (const char *)table.data(), table.size() * sizeof(Entry), nullptr, 0)) return E_OTHER;
         if (mismatch) return E_OTHER;
+        g_net.ip.assign((size_t)nn, host);
+        for (int j = 1; j < nn; ++j) g_net.ip[j] = table[j].ip;
     } else {
         int myport = 0;
         g_net.listen_fd = open_listener(nullptr, 0, &myport);
@@ -307,6 +322,8 @@ int net_init() {
             return E_OTHER;
         }
         g_net.fd[0] = fd;
+        g_net.ip.assign((size_t)nn, host);
+        for (int j = 1; j < nn; ++j) g_net.ip[j] = table[j].ip;
         // mesh among nodes 1..nn-1: connect down, accept up
         for (int j = 1; j < me; ++j) {
             const int c = connect_retry(table[j].ip, table[j].port);
@@ -349,7 +366,81 @@ int net_barrier() {
     return 0;
 }
 
+int mesh_setup() {
+    World &w = world();
+    const int L = w.size, K = w.nnodes, n = w.gsize;
+    if (K <= 1 || n > kMeshMaxRanks) return 0;  // no rank mesh: point-to-point stays within nodes
+    int port = 0;
+    g_mesh.listen_fd = open_listener(nullptr, 0, &port);
+    int rc = g_mesh.listen_fd < 0 ? E_OTHER : 0;
+    if (w.shm) w.shm->r[w.rank].mesh_port = rc ? -1 : port;
+    host_barrier();
+    std::vector<int32_t> all((size_t)n, -1);
+    std::vector<std::string> ip((size_t)K);
+    if (w.rank == 0) {
+        // every node's listener ports: a ring of per-node sections over the leaders
+        for (int l = 0; l < L; ++l) all[(size_t)w.node * L + l] = w.shm ? w.shm->r[l].mesh_port : port;
+        const int me = w.node, right = (me + 1) % K, left = (me - 1 + K) % K;
+        const size_t sect = (size_t)L * sizeof(int32_t);
+        for (int k = 0; k < K - 1 && !rc; ++k) {
+            const int so = (me - k + K) % K, ro = (me - k - 1 + K) % K;
+            rc = net_shift(right, &all[(size_t)so * L], sect, left, &all[(size_t)ro * L], sect);
+        }
+        for (int g = 0; g < n && !rc; ++g)
+            if (all[g] < 0) rc = E_OTHER;
+        if (w.shm) {
+            for (int g = 0; g < n; ++g) w.shm->mesh_port[g] = all[g];
+            for (int j = 0; j < K; ++j) snprintf(w.shm->node_ip[j], sizeof(w.shm->node_ip[j]), "%s", g_net.ip[j].c_str());
+            w.shm->net_rc.store(rc);
+        }
+        for (int j = 0; j < K; ++j) ip[j] = g_net.ip[j];
+    }
+    host_barrier();
+    if (w.shm) {
+        rc = w.shm->net_rc.load();
+        for (int g = 0; g < n; ++g) all[g] = w.shm->mesh_port[g];
+        for (int j = 0; j < K; ++j) ip[j] = w.shm->node_ip[j];
+    }
+    if (rc) {
+        MV2_ERR("rank mesh: a node's listener ports could not be exchanged");
+        return rc;
+    }
+    // connect to every rank of a lower node, accept every rank of a higher one
+    g_mesh.fd.assign((size_t)n, -1);
+    for (int g = 0; g < w.node * L; ++g) {
+        const int c = connect_retry(ip[g / L].c_str(), all[g]);
+        const MeshHello h{kMagic, w.grank};
+        if (c < 0 || xfer(c, (const char *)&h, sizeof(h), nullptr, 0)) {
+            MV2_ERR("rank mesh: cannot connect to rank %d (%s:%d)", g, ip[g / L].c_str(), all[g]);
+            return E_OTHER;
+        }
+        g_mesh.fd[g] = c;
+    }
+    for (int k = (w.node + 1) * L; k < n; ++k) {
+        const int c = accept_timed(g_mesh.listen_fd);
+        MeshHello h{};
+        if (c < 0 || xfer(c, nullptr, 0, (char *)&h, sizeof(h)) || h.magic != kMagic || h.grank < (w.node + 1) * L ||
+            h.grank >= n || g_mesh.fd[h.grank] >= 0) {
+            MV2_ERR("rank mesh: bad or missing connection from a higher node");
+            if (c >= 0) close(c);
+            return E_OTHER;
+        }
+        g_mesh.fd[h.grank] = c;
+    }
+    MV2_DEBUG("rank mesh up: rank %d linked to %d ranks of other nodes", w.grank, n - L);
+    return 0;
+}
+
+int mesh_fd(int grank) { return grank >= 0 && grank < (int)g_mesh.fd.size() ? g_mesh.fd[grank] : -1; }
+
 void net_finalize() {
+    for (int &fd : g_mesh.fd)
+        if (fd >= 0) {
+            close(fd);
+            fd = -1;
+        }
+    if (g_mesh.listen_fd >= 0) close(g_mesh.listen_fd);
+    g_mesh.listen_fd = -1;
     for (int &fd : g_net.fd)
         if (fd >= 0) {
             close(fd);

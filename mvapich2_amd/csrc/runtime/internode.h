@@ -17,4 +17,11 @@ int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t r
 // one ring step: send to `to` while receiving from `from`, both directions in flight together
 int net_shift(int to, const void *sbuf, size_t sbytes, int from, void *rbuf, size_t rbytes);
 
+// Rank mesh (every rank, after the leaders' bootstrap): one TCP stream between every pair of
+// ranks on different nodes, for point-to-point across nodes (runtime/p2p.cpp).  The ports travel
+// through the node's control segment and the leaders' links.  Jobs above kMeshMaxRanks ranks get
+// no mesh.  mesh_fd: the stream to global rank g, or -1.
+int mesh_setup();
+int mesh_fd(int grank);
+
 }  // namespace mv2

@@ -23,6 +23,12 @@
 //   * progress is made inside Wait/Test of any request (and blocking calls).
 // Copies run on their own stream so a pending nonblocking collective never
 // blocks point-to-point progress.
+//
+// Ranks are global.  Between nodes (the reference's netmod path) a message
+// travels on the rank mesh (internode.cpp mesh_setup: one TCP stream per pair of ranks on
+// different nodes): a 24-byte header {source, tag, bytes}, then the payload, staged through host
+// memory on both sides; the receiver matches the header against the same posted / unexpected
+// queues, so MPI_ANY_SOURCE and per-(source, tag) order hold across both transports.
 #include <hip/hip_runtime.h>
 #include <sched.h>
 #include <stdlib.h>
@@ -35,7 +41,11 @@
 #include <unordered_map>
 #include <vector>
 
+#include <errno.h>
+#include <sys/socket.h>
+
 #include "../../../include/mv2h.h"
+#include "internode.h"
 #include "log.h"
 #include "world.h"
 
@@ -84,6 +94,35 @@ std::list<Req *> g_posted;             // unmatched receives in posting order
 std::list<Unexp *> g_unexp;            // unexpected messages in arrival order
 Arrival g_in[kMaxRanks];
 
+// rank mesh (ranks on other nodes)
+struct NetHdr {
+    int32_t magic;
+    int32_t src;  // sender's global rank
+    int32_t tag;
+    int32_t pad;
+    uint64_t bytes;
+};
+constexpr int32_t kNetMagic = 0x6d763270;  // "mv2p"
+struct NetOut {
+    Req *r;
+    std::vector<char> buf;  // header + payload (staged to host at MPI_Isend)
+    size_t off;
+};
+struct NetIn {
+    NetHdr hdr;
+    size_t hgot = 0;
+    bool body = false;
+    std::vector<char> stage;  // the payload, host
+    size_t got = 0;
+    Req *req = nullptr;    // matched receive, or
+    Unexp *ux = nullptr;   // unexpected message (filled when the payload is complete)
+};
+std::deque<NetOut> g_netq[kMeshMaxRanks];
+NetIn g_netin[kMeshMaxRanks];
+
+int node_base() { return world().node * world().size; }
+bool on_node(int g) { return g >= node_base() && g < node_base() + world().size; }
+
 bool matches(const Req *r, int src, int tag) {
     // MPI_ANY_TAG matches application tags only (>= 0), never the library's collective context
     return (r->src_want == MV2H_ANY_SOURCE || r->src_want == src) &&
@@ -96,13 +135,126 @@ char *slot_ptr(char *arena, int src, uint64_t pos) {
 
 int ready() {
     World &w = world();
-    if (!w.inited || !w.shm || !w.p2p) {
+    if (!w.inited || !w.p2p || (w.size > 1 && !w.shm)) {
         MV2_ERR("point-to-point needs MPI_Init and at most %d ranks on the node", kMaxRanks);
         return E_OTHER;
     }
     // created on first use: an idle extra stream still costs a hardware queue, and
     // collective-only jobs (several ranks sharing a GPU in tests) measured slower with it
     if (!w.p2p_stream && hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
+    return 0;
+}
+
+// a header from global rank src: the receive it matches (posting order), else an unexpected
+// message; the payload lands in `stage` and is delivered when complete
+void net_header(NetIn &in, int src) {
+    in.req = nullptr;
+    in.ux = nullptr;
+    for (auto it = g_posted.begin(); it != g_posted.end(); ++it) {
+        if (matches(*it, src, in.hdr.tag)) {
+            in.req = *it;
+            g_posted.erase(it);
+            break;
+        }
+    }
+    if (in.req) {
+        in.req->src = src;
+        in.req->rtag = in.hdr.tag;
+        in.req->total = in.hdr.bytes;
+    } else {
+        in.ux = new Unexp{src, in.hdr.tag, (size_t)in.hdr.bytes};
+        g_unexp.push_back(in.ux);
+    }
+    in.stage.resize(in.hdr.bytes);
+    in.got = 0;
+    in.body = true;
+}
+
+int net_deliver(NetIn &in) {
+    in.body = false;
+    in.hgot = 0;
+    if (in.req) {
+        Req *r = in.req;
+        const size_t n = std::min(r->total, r->cap);
+        if (n && hipMemcpy(r->rbuf, in.stage.data(), n, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+        if (r->total > r->cap) r->err = E_TRUNCATE;
+        r->done = true;
+    } else if (in.ux) {
+        in.ux->data.swap(in.stage);
+        if (in.ux->data.empty()) in.ux->data.resize(1);
+        in.ux->got = in.ux->total;
+        in.ux->complete = true;
+    }
+    in.req = nullptr;
+    in.ux = nullptr;
+    in.stage.clear();
+    return 0;
+}
+
+// non-blocking pass over the rank mesh: write queued messages, read headers and payloads
+int net_progress(bool *moved) {
+    World &w = world();
+    if (w.nnodes <= 1) return 0;
+    for (int g = 0; g < w.gsize && g < kMeshMaxRanks; ++g) {
+        const int fd = mesh_fd(g);
+        if (fd < 0) continue;
+        while (!g_netq[g].empty()) {
+            NetOut &o = g_netq[g].front();
+            const ssize_t k = send(fd, o.buf.data() + o.off, o.buf.size() - o.off, MSG_DONTWAIT | MSG_NOSIGNAL);
+            if (k < 0) {
+                if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
+                MV2_ERR("point-to-point to rank %d: connection lost", g);
+                return E_OTHER;
+            }
+            o.off += (size_t)k;
+            *moved = *moved || k > 0;
+            if (o.off < o.buf.size()) break;
+            o.r->done = true;
+            g_netq[g].pop_front();
+        }
+        NetIn &in = g_netin[g];
+        for (;;) {
+            char *dst;
+            size_t want;
+            if (!in.body) {
+                dst = (char *)&in.hdr + in.hgot;
+                want = sizeof(NetHdr) - in.hgot;
+            } else {
+                dst = in.stage.data() + in.got;
+                want = in.stage.size() - in.got;
+            }
+            if (want) {
+                const ssize_t k = recv(fd, dst, want, MSG_DONTWAIT);
+                if (k == 0) {
+                    MV2_ERR("point-to-point from rank %d: connection closed", g);
+                    return E_OTHER;
+                }
+                if (k < 0) {
+                    if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
+                    MV2_ERR("point-to-point from rank %d: connection lost", g);
+                    return E_OTHER;
+                }
+                *moved = true;
+                if (!in.body) in.hgot += (size_t)k;
+                else in.got += (size_t)k;
+                if ((!in.body && in.hgot < sizeof(NetHdr)) || (in.body && in.got < in.stage.size())) continue;
+            }
+            if (!in.body) {
+                if (in.hdr.magic != kNetMagic || in.hdr.src != g) {
+                    MV2_ERR("point-to-point from rank %d: stream out of sequence", g);
+                    return E_INTERN;
+                }
+                net_header(in, g);
+                if (in.stage.empty()) {  // empty message: complete at its header
+                    const int rc = net_deliver(in);
+                    if (rc) return rc;
+                }
+            } else {
+                const int rc = net_deliver(in);
+                if (rc) return rc;
+            }
+        }
+    }
     return 0;
 }
 
@@ -132,6 +284,8 @@ int progress(bool *moved) {
     };
     std::vector<SendPub> sp;
     std::vector<RecvPub> rp;
+    const int base = node_base();
+    if (!w.shm) return net_progress(moved);
 
     for (int d = 0; d < n; ++d) {
         if (g_sendq[d].empty()) continue;
@@ -171,18 +325,18 @@ int progress(bool *moved) {
                 a.active = true;
                 a.total = rec.total;
                 for (auto it = g_posted.begin(); it != g_posted.end(); ++it) {
-                    if (matches(*it, s, rec.tag)) {
+                    if (matches(*it, base + s, rec.tag)) {
                         a.req = *it;
                         g_posted.erase(it);
                         break;
                     }
                 }
                 if (a.req) {
-                    a.req->src = s;
+                    a.req->src = base + s;
                     a.req->rtag = rec.tag;
                     a.req->total = rec.total;
                 } else {
-                    a.ux = new Unexp{s, rec.tag, (size_t)rec.total};
+                    a.ux = new Unexp{base + s, rec.tag, (size_t)rec.total};
                     a.ux->data.resize(rec.total ? rec.total : 1);
                     g_unexp.push_back(a.ux);
                 }
@@ -207,6 +361,8 @@ int progress(bool *moved) {
         }
     }
 
+    int rc = net_progress(moved);
+    if (rc) return rc;
     if (sp.empty() && rp.empty()) return 0;
     *moved = true;
     if (hipStreamSynchronize(w.p2p_stream) != hipSuccess) {
@@ -248,7 +404,7 @@ int mv2::p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned lo
     int rc = ready();
     if (rc) return rc;
     World &w = world();
-    if (dest < 0 || dest >= w.size) return E_RANK;
+    if (dest < 0 || dest >= w.gsize) return E_RANK;
     if (bytes && !buf) return E_BUFFER;
     Req *r = new Req{};
     r->send = true;
@@ -257,7 +413,41 @@ int mv2::p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned lo
     r->peer = dest;
     r->tag = tag;
     r->msg = ++g_msg_seq;
-    g_sendq[dest].push_back(r);
+    if (!on_node(dest)) {  // rank mesh: header + payload staged to host now, written by progress
+        if (mesh_fd(dest) < 0) {
+            delete r;
+            MV2_ERR("no point-to-point link to rank %d on another node (jobs up to %d ranks)", dest, kMeshMaxRanks);
+            return E_UNSUPPORTED;
+        }
+        NetOut o{r, std::vector<char>(sizeof(NetHdr) + bytes), 0};
+        const NetHdr h{kNetMagic, w.grank, tag, 0, (uint64_t)bytes};
+        memcpy(o.buf.data(), &h, sizeof(h));
+        if (bytes && hipMemcpy(o.buf.data() + sizeof(h), buf, bytes, hipMemcpyDefault) != hipSuccess) {
+            delete r;
+            return E_INTERN;
+        }
+        g_netq[dest].push_back(std::move(o));
+        *req = add_req(r);
+        bool moved = false;
+        return net_progress(&moved);
+    }
+    if (!w.shm) {  // a node of one rank sending to itself: matched and delivered right here
+        NetIn in;
+        in.hdr = NetHdr{kNetMagic, w.grank, tag, 0, (uint64_t)bytes};
+        net_header(in, w.grank);
+        if (bytes && hipMemcpy(in.stage.data(), buf, bytes, hipMemcpyDefault) != hipSuccess) {
+            delete r;
+            return E_INTERN;
+        }
+        if ((rc = net_deliver(in))) {
+            delete r;
+            return rc;
+        }
+        r->done = true;
+        *req = add_req(r);
+        return 0;
+    }
+    g_sendq[dest - node_base()].push_back(r);
     *req = add_req(r);
     bool moved;
     return progress(&moved);  // eager: start pushing right away
@@ -267,7 +457,7 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
     int rc = ready();
     if (rc) return rc;
     World &w = world();
-    if (source != MV2H_ANY_SOURCE && (source < 0 || source >= w.size)) return E_RANK;
+    if (source != MV2H_ANY_SOURCE && (source < 0 || source >= w.gsize)) return E_RANK;
     if (cap && !buf) return E_BUFFER;
     Req *r = new Req{};
     r->send = false;
@@ -289,9 +479,14 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
         if (u->complete) {
             if (u->total > cap) r->err = E_TRUNCATE;
             r->done = true;
+        } else if (!on_node(u->src)) {
+            // still arriving on the rank mesh: the payload goes to this receive when complete
+            NetIn &in = g_netin[u->src];
+            in.ux = nullptr;
+            in.req = r;
         } else {
             // still arriving: the rest of its chunks go straight to the user buffer
-            Arrival &a = g_in[u->src];
+            Arrival &a = g_in[u->src - node_base()];
             a.ux = nullptr;
             a.req = r;
         }

@@ -546,6 +546,10 @@ int world_init() {
             w.inited = false;
             return rc;
         }
+        if ((rc = mesh_setup())) {  // every rank linked to the ranks of the other nodes (p2p)
+            w.inited = false;
+            return rc;
+        }
     }
     w.init_ms = ms_since(t_init);
     MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d): %.1f ms (self-test %.1f, autotune %.1f)",
@@ -569,7 +573,7 @@ int world_finalize() {
     host_prof_report();
     if (w.nnodes > 1) {
         global_barrier();
-        if (w.rank == 0) net_finalize();
+        net_finalize();  // the rank mesh on every rank, the leaders' links on the leaders
     }
     if (w.size > 1 && w.shm) {
         host_barrier();

@@ -75,7 +75,10 @@ struct alignas(64) ShmRank {
     Knobs knobs;      // MV2_* selection knobs as this rank parsed them (must agree)
     int topo_nlevels;               // this rank's topology levels (world.cpp my_topology)
     int topo_color[kTopoLevels];    // its cluster id per level
+    int mesh_port;                  // this rank's rank-mesh listener (internode.cpp mesh_setup)
 };
+
+constexpr int kMeshMaxRanks = 64;  // jobs up to this many ranks get the rank mesh (p2p across nodes)
 
 struct ShmSeg {
     std::atomic<uint64_t> magic;
@@ -85,6 +88,8 @@ struct ShmSeg {
     std::atomic<int> net_rc;     // the leader's inter-node bootstrap result, for the node's other ranks
     ShmRank r[kShmMaxRanks];
     P2PChan chan[kMaxRanks][kMaxRanks];  // [src][dst]
+    int mesh_port[kMeshMaxRanks];        // every rank's rank-mesh listener (the leader fills it in)
+    char node_ip[kMeshMaxRanks][48];     // every node's address
 };
 
 struct World {
