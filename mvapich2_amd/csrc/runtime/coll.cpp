@@ -1270,9 +1270,18 @@ static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int
     if ((rc = require_world())) return rc;
     return allreduce_select(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
 }
+// A stream-ordered call across nodes (MPIX_*_enqueue): the leaders' steps are host-driven, so the
+// call waits for the caller's stream, then runs as the blocking call and returns complete; work
+// queued on the stream afterwards sees the result.  Stream order without the overlap (graph
+// capture stays refused, enqueue_checks).  The EnqueueScope of the entry point clears the flag.
+static int mn_stream_order(void **stream) {
+    if (hipStreamSynchronize((hipStream_t)*stream) != hipSuccess) return E_INTERN;
+    world().enqueue = false;
+    *stream = nullptr;
+    return 0;
+}
 static int mn_allreduce(const void *, void *, size_t, int, int, void *);
 static int mn_reduce(const void *, void *, size_t, int, int, int, void *);
-static int mn_unsupported(const char *what);
 // A nonblocking collective across nodes completes at initiation (MPI allows it: the request is
 // complete when MPI_Wait / MPI_Test first sees it); the node steps inside run blocking.
 struct MnBlocking {
@@ -1288,7 +1297,8 @@ static int mn_reduce_scatter(const void *, void *, const size_t *, int, int, voi
 
 int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        int rc0 = 0;
+        if (world().enqueue && (rc0 = mn_stream_order(&stream))) return rc0;
         MnBlocking nb;
         pvar_begin();
         const int rc = mn_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
@@ -1361,7 +1371,8 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
 }
 int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        int rc0 = 0;
+        if (world().enqueue && (rc0 = mn_stream_order(&stream))) return rc0;
         MnBlocking nb;
         pvar_begin();
         const int rc = mn_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
@@ -1469,7 +1480,8 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                         void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        int rc0 = 0;
+        if (world().enqueue && (rc0 = mn_stream_order(&stream))) return rc0;
         MnBlocking nb;
         pvar_begin();
         const int rc = mn_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
@@ -2209,14 +2221,10 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
 
 extern "C" {
 
-static int mn_unsupported(const char *what) {
-    MV2_ERR("%s is not supported across nodes (two-level: Allreduce, Reduce, Reduce_scatter, Bcast, Allgather, Barrier)", what);
-    return E_UNSUPPORTED;
-}
-
 int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        int rc0 = 0;
+        if (world().enqueue && (rc0 = mn_stream_order(&stream))) return rc0;
         MnBlocking nb;
         return mn_allgather(sendbuf, recvbuf, bytes, stream);
     }
@@ -2225,7 +2233,8 @@ int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *strea
 
 int mv2h_bcast(void *buffer, size_t bytes, int root, void *stream) {
     if (world().nnodes > 1) {
-        if (world().enqueue) return mn_unsupported("a stream-ordered collective");
+        int rc0 = 0;
+        if (world().enqueue && (rc0 = mn_stream_order(&stream))) return rc0;
         MnBlocking nb;
         return mn_bcast(buffer, bytes, root, stream);
     }
@@ -2337,7 +2346,7 @@ int mv2h_reduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dt
     if (!count) return 0;
     const World &w = world();
     // recvbuf is significant at the root only
-    int rc = enqueue_checks(sendbuf, w.rank == root ? recvbuf : (sendbuf == (const void *)-1 ? nullptr : sendbuf),
+    int rc = enqueue_checks(sendbuf, w.grank == root ? recvbuf : (sendbuf == (const void *)-1 ? nullptr : sendbuf),
                             stream);
     if (rc) return rc;
     EnqueueScope q;

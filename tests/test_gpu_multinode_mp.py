@@ -381,6 +381,51 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
                 assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,ppn", [(4, 2), (3, 1)])
+def test_stream_ordered_across_nodes(n, ppn, tmp_path):
+    """MPIX_*_enqueue across nodes: the call waits for the caller's stream, runs the blocking
+    multi-node schedule and returns complete, so the chain of tests/mp_gpu_worker.py enqueue_seq
+    (y = Allreduce(x), z = Allreduce(y) in stream order, Bcast, Reduce_scatter, Allgather, a
+    blocking Allreduce between, Reduce MAX to 0) gives the blocking calls' results; capture stays
+    refused."""
+    F = TYPES["MPI_FLOAT"][0]
+    cases = []
+    for seed, c in ((511, 1000), (512, (1 << 20) + 5)):
+        counts = [c // n + (1 if r < c % n else 0) for r in range(n)]
+        cases.append({"id": f"eq{seed}", "kind": "enqueue_seq", "type": "MPI_FLOAT", "count": c, "seed": seed,
+                      "recvcounts": counts, "per": c // n})
+    res = run_workers(n, cases, tmp_path, ppn=ppn)
+    for case in cases:
+        c, counts, per = case["count"], case["recvcounts"], case["per"]
+        xs = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+        y = expected_allreduce(xs, c, "MPI_FLOAT", "MPI_SUM", ppn)
+        z = expected_allreduce([y[r].copy() for r in range(n)], c, "MPI_FLOAT", "MPI_SUM", ppn)
+        rs_full = oracle.reduce_scatter_ref([x.copy() for x in xs], counts, F, OPS["MPI_SUM"])
+        ag = np.concatenate([x[:per * 4] for x in xs])
+        parts0 = [oracle.reduce_ref([x.copy() for x in xs[j * ppn:(j + 1) * ppn]], c, F, OPS["MPI_MAX"], 0)
+                  for j in range(n // ppn)]
+        red = binomial_leaders(parts0, c, "MPI_FLOAT", "MPI_MAX", 0)
+        for r in range(n):
+            got = res(case["id"], r)
+            o, parts = 0, {}
+            for name, nb in (("y", c * 4), ("z", c * 4), ("xb", c * 4), ("w", c * 4), ("rs", counts[r] * 4),
+                             ("ag", per * n * 4), ("r", c * 4), ("w2", c * 4)):
+                parts[name] = got[o:o + nb]
+                o += nb
+            tag = f"{case['id']} rank {r}"
+            assert_bytes_equal(parts["y"], y[r], "MPI_FLOAT", c, tag + " y")
+            assert_bytes_equal(parts["z"], z[r], "MPI_FLOAT", c, tag + " z")
+            assert np.array_equal(parts["xb"], xs[1 % n]), tag + " bcast"
+            assert_bytes_equal(parts["w"], y[r], "MPI_FLOAT", c, tag + " blocking w")
+            assert_bytes_equal(parts["w2"], y[r], "MPI_FLOAT", c, tag + " w2")
+            off = sum(counts[:r]) * 4
+            assert_bytes_equal(parts["rs"], rs_full[off:off + counts[r] * 4], "MPI_FLOAT", counts[r], tag + " rs")
+            assert np.array_equal(parts["ag"], ag), tag + " allgather"
+            if r == 0:
+                assert_bytes_equal(parts["r"], red, "MPI_FLOAT", c, tag + " reduce")
+
+
 @pytest.mark.timeout(200)
 def test_mpit_counts_across_nodes(tmp_path):
     """MPI_T across nodes: Allreduce counts MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) and,
