@@ -160,6 +160,32 @@ def big_case(L, case, rank, n):
             full = oracle.reduce_scatter_ref([x.view(np.uint8) for x in xs], counts, F, OPS["MPI_SUM"]).view(np.uint32)
             want = full[off:off + counts[rank]]
         return np.array([np.count_nonzero(got != want)])
+    if k == "huge":  # operands above 4 GiB: 64-bit byte offsets through every kernel and copy
+        cnt = case["count"]
+        D = TYPES["MPI_DOUBLE"][0]
+        i = np.arange(cnt, dtype=np.int64)
+        base = (i % 1000).astype(np.float64)
+        del i
+        sb = m.DeviceBuffer.from_array(base * (rank + 1))
+        rb = m.DeviceBuffer(cnt * 8)
+        assert L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, D, OPS["MPI_SUM"], WORLD) == 0  # ring wrapper + remainder
+        bad_ar = np.count_nonzero(rb.download(np.float64, count=cnt) != base * (n * (n + 1) // 2))
+        rb.upload(np.zeros(cnt, np.float64) if rank != 1 % n else base * (1 % n + 1))
+        assert L.MPI_Bcast(rb.ptr, cnt, D, 1 % n, WORLD) == 0
+        bad_bc = np.count_nonzero(rb.download(np.float64, count=cnt) != base * (1 % n + 1))
+        rb.upload(base)
+        assert L.MPI_Reduce_local(sb.ptr, rb.ptr, cnt, D, OPS["MPI_SUM"]) == 0
+        bad_rl = np.count_nonzero(rb.download(np.float64, count=cnt) != base * (rank + 2))
+        # reduce_scatter / allgather with blocks of cnt // n doubles: results past 4 GiB in total
+        per = cnt // n
+        counts = (ctypes.c_int * n)(*([per] * n))
+        assert L.MPI_Reduce_scatter(sb.ptr, rb.ptr, counts, D, OPS["MPI_SUM"], WORLD) == 0
+        want = base[rank * per:(rank + 1) * per] * (n * (n + 1) // 2)
+        bad_rs = np.count_nonzero(rb.download(np.float64, count=per) != want)
+        assert L.MPI_Allgather(sb.ptr, per, D, rb.ptr, per, D, WORLD) == 0
+        got = rb.download(np.float64, count=per * n)
+        bad_ag = sum(np.count_nonzero(got[r * per:(r + 1) * per] != base[:per] * (r + 1)) for r in range(n))
+        return np.array([bad_ar, bad_bc, bad_rl, bad_rs, bad_ag])
     if k == "big_reduce_scatter":  # configs[3]: OMB recvcounts = size/n (+1 for the first size%n)
         tot = case["count"]
         counts = [tot // n + (1 if r < tot % n else 0) for r in range(n)]
@@ -447,7 +473,7 @@ def main():
             res = rb.download(np.uint8, count=cnt * ext_f * 4)
             L.MPI_Op_free(ctypes.byref(op))
             L.MPI_Type_free(ctypes.byref(vt))
-        elif k.startswith("big_"):
+        elif k.startswith("big_") or k == "huge":
             res = big_case(L, case, rank, n)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)

@@ -424,6 +424,20 @@ def test_allreduce_1gib_bit_exact(tmp_path):
         assert int(res("gb1", r)[0]) == 0, (r, int(res("gb1", r)[0]))
 
 
+@pytest.mark.timeout(600)
+def test_operands_above_4gib(tmp_path):
+    """MPI_Allreduce / MPI_Bcast / MPI_Reduce_local on 2^29 + 3 doubles (4 GiB + 24 B) at 2 ranks,
+    MPI_Reduce_scatter / MPI_Allgather with 2 GiB + 8 B blocks: byte offsets past 32 bits in the
+    pipelined kernels (ring chunks of 2 GiB + 8 B, the second starting off a 16-byte boundary), the
+    one-element pt2pt_rs remainder and the streaming Reduce_local; exact closed-form results
+    checked over every element in each rank."""
+    n = 2
+    cases = [{"id": "hg1", "kind": "huge", "count": (1 << 29) + 3, "seed": 1}]
+    res = run_workers(n, cases, tmp_path, timeout=540)
+    for r in range(n):
+        assert [int(v) for v in res("hg1", r)] == [0] * 5, (r, res("hg1", r))
+
+
 def test_mpit_counters_follow_the_selection(tmp_path):
     """MPI_T (mpi/mpit.cpp): a started counter handle counts the calls of the algorithms the
     reference's call chain runs for each call (its MPIR_T_PVAR_COUNTER_INC sites), 4 ranks:
