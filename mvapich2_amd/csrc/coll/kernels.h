@@ -29,25 +29,6 @@ struct DevSeq {
     uint32_t pad[9];
 };
 
-// Command block of a lingering one-shot kernel (coll.cpp linger_*; pinned host memory).  After
-// its call a single-workgroup one-shot kernel stays resident for a short window and polls `seq`:
-// the host posts the next small allreduce of the same shape (same op, type, count and order)
-// here instead of launching a kernel, and the kernel runs it with the new buffers, epoch, arena
-// half and completion value.  op 2 (or the window running out) ends the kernel, which reports
-// the last command it ran.
-struct alignas(64) LingerCmd {
-    uint64_t seq;       // last command posted (the host stores it last, release)
-    uint64_t op;        // 1: run, 2: exit
-    uint64_t send, recv;
-    uint64_t epoch;
-    uint64_t poff;      // arena half, bytes
-    uint64_t done_seq;  // completion-word value of the command
-    uint64_t pad0;
-    uint64_t exit_inst; // kernel -> host: the instance that ended ...
-    uint64_t exit_last; // ... and the last command it ran
-    uint64_t pad1[6];
-};
-
 struct OneShotArgs {
     const char *send;
     char *recv;
@@ -67,11 +48,6 @@ struct OneShotArgs {
     // block at run time (arena_peer / arena_own then point at half 0; `half` = bytes per half)
     DevSeq *dseq;
     size_t half;
-    size_t poff0;       // host lane: this call's arena half (arena_peer / arena_own point at half 0)
-    // lingering (grid 1, host lane): command block, this kernel's instance, the command number
-    // of this launch's own call, and the window in wall-clock ticks (0: no lingering)
-    LingerCmd *lcmd;
-    uint64_t linst, lseq0, linger;
 };
 
 // ---------------------------------------------------------------------------

@@ -272,15 +272,14 @@ __device__ __forceinline__ void dseq_advance(DevSeq *d, uint64_t de, uint64_t dr
 }
 
 template <class Rd, bool PROG>
-__device__ __forceinline__ void oneshot_body(const OneShotArgs &a, const char *sendp, char *recvp, uint64_t epoch,
-                                             size_t poff) {
+__device__ __forceinline__ void oneshot_body(const OneShotArgs &a, uint64_t epoch, size_t poff) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const int blk = blockIdx.x, G = gridDim.x;
     const size_t per = (a.nvec + G - 1) / G;
     const size_t vb = (size_t)blk * per;
     const size_t ve = vb + per < a.nvec ? vb + per : a.nvec;
-    const v4u *send = (const v4u *)sendp;
+    const v4u *send = (const v4u *)a.send;
     // phase A: push my data to every peer's slot (me)
     for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
         const v4u x = send[i];
@@ -291,7 +290,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, const char *s
     const size_t tail0 = a.nvec * N;
     if (blk == 0) {
         for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {
-            const T x = ((const T *)sendp)[e];
+            const T x = ((const T *)a.send)[e];
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
                 if (j < a.n && j != a.me) ((T *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes))[e] = x;
@@ -317,7 +316,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, const char *s
         for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
             v4u v[kMaxRanks];
             load(i, v);
-            ((v4u *)recvp)[i] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
+            ((v4u *)a.recv)[i] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
         }
     } else {
         // a butterfly owner that is constant over this workgroup's range is fixed once (no
@@ -330,7 +329,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, const char *s
         for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
             v4u v[kMaxRanks];
             load(i, v);
-            ((v4u *)recvp)[i] = vreduce_n<Rd>(v, a.n, tp, i * N);
+            ((v4u *)a.recv)[i] = vreduce_n<Rd>(v, a.n, tp, i * N);
         }
     }
     if (blk == 0) {
@@ -338,73 +337,26 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, const char *s
             T col[kMaxRanks];
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j)
-                col[j] = (j >= a.n || j == a.me) ? ((const T *)sendp)[e]
+                col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e]
                                                  : ld_nt_elem((const T *)(arena_own + (size_t)j * a.slot_bytes) + e);
-            if constexpr (PROG) ((T *)recvp)[e] = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, e)]);
-            else ((T *)recvp)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
+            if constexpr (PROG) ((T *)a.recv)[e] = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, e)]);
+            else ((T *)a.recv)[e] = tree_reduce<Rd>(col, a.n, a.tp.linear, a.tp.pof2, a.tp.rem, elem_owner<Rd>(a.tp, e));
         }
-    }
-}
-
-// A lingering one-shot kernel (grid 1): wait up to a.linger ticks for the host's next command
-// (LingerCmd, pinned host memory), run it, repeat; on op 2 or a quiet window, report and end.
-// Only the buffers, the epoch, the arena half and the completion value change between commands.
-template <class Rd, bool PROG>
-__device__ __forceinline__ void oneshot_linger(const OneShotArgs &a) {
-    __shared__ uint64_t s_cmd[6];
-    uint64_t want = a.lseq0 + 1;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            LingerCmd *c = a.lcmd;
-            const uint64_t t0 = wall_clock64();
-            uint64_t op = 2;
-            for (;;) {
-                if (__hip_atomic_load(&c->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) {
-                    op = __hip_atomic_load(&c->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                if (wall_clock64() - t0 > a.linger) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            s_cmd[0] = op;
-            if (op == 1) {
-                s_cmd[1] = __hip_atomic_load(&c->send, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_cmd[2] = __hip_atomic_load(&c->recv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_cmd[3] = __hip_atomic_load(&c->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_cmd[4] = __hip_atomic_load(&c->poff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_cmd[5] = __hip_atomic_load(&c->done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            } else {
-                __hip_atomic_store(&c->exit_last, want - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&c->exit_inst, a.linst, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        __syncthreads();
-        if (s_cmd[0] != 1) return;
-        const char *send = (const char *)s_cmd[1];
-        char *recv = (char *)s_cmd[2];
-        const uint64_t epoch = s_cmd[3];
-        const size_t poff = (size_t)s_cmd[4];
-        const Done dn{a.done.ctr, a.done.flag, s_cmd[5]};
-        __syncthreads();  // every thread has its copy before thread 0 polls again
-        oneshot_body<Rd, PROG>(a, send, recv, epoch, poff);
-        block_done(dn);
-        ++want;
     }
 }
 
 template <class Rd, bool PROG>
 __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
     uint64_t epoch = a.epoch;
-    size_t poff = a.poff0;
+    size_t poff = 0;
     if (a.dseq) {  // graph lane: this replay's epoch and arena half
         const SeqBase q = dseq_read(a.dseq);
         epoch = q.epoch + 1;
         poff = (q.os & 1) * a.half;
     }
-    oneshot_body<Rd, PROG>(a, a.send, a.recv, epoch, poff);
+    oneshot_body<Rd, PROG>(a, epoch, poff);
     if (a.dseq) dseq_advance(a.dseq, 1, 0, 1);
     block_done(a.done);
-    if (a.lcmd && gridDim.x == 1) oneshot_linger<Rd, PROG>(a);
 }
 
 template <int OP, int K>

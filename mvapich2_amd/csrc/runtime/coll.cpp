@@ -49,10 +49,8 @@ bool log_debug_on() {
 // a stream other than the previous one first waits for it.  Calls that stay on one stream
 // pay nothing for the order.  (A caller's stream handle reused after hipStreamDestroy is
 // safe: the destroy drains the stream's queue first.)
-static void linger_stop();
 static hipStream_t pick_stream(void *s) {
     World &w = world();
-    if (w.l_live && !w.l_hold) linger_stop();  // any other call first ends a lingering one-shot kernel
     hipStream_t st = s ? (hipStream_t)s : w.stream;
     if (w.graph) return st;  // graph lane: disjoint arenas and epochs, ordered by the graph itself
     if (w.last_st && st != w.last_st) {
@@ -215,111 +213,6 @@ static int finish(hipStream_t st, bool timed) {
     if (check_err_word()) return E_OTHER;
     hp_done();
     return 0;
-}
-
-// ---------------------------------------------------------------------------
-// Lingering one-shot kernel.  A blocking small allreduce costs a kernel launch (2.2 us of host
-// time on MI355X, tools/query_probe.hip) plus the kernel's start-up before any byte moves.  A
-// single-workgroup one-shot kernel can stay resident for MV2AMD_LINGER_US (0 = off, the default)
-// after its call, on a non-blocking stream of its own, polling a pinned command block
-// (kernels.h LingerCmd); the next small allreduce of the same shape (op, type, count, order) is
-// posted there — new buffers, epoch, arena half and completion value — instead of launched.
-// The protocol with the peers is the launched kernel's (same epochs and arena halves in call
-// order), so ranks may mix posted and launched calls.  A call is posted only when the legacy
-// null stream and the library's stream are idle (a launched kernel on the library's blocking
-// stream would have waited for them; hipStreamQuery costs 0.07 us on an idle stream), its
-// buffers need no staging, and the kernel's window has at least half left by the host's clock;
-// a command the kernel did not take (it reported its exit first) is launched instead.  Every
-// other call ends the kernel first (pick_stream), so nothing queues behind it, and an
-// application's hipDeviceSynchronize waits at most one window for it.
-// ---------------------------------------------------------------------------
-static bool linger_ready() {
-    World &w = world();
-    if (w.l_window_ns == 0 || w.sync_mode != 0 || !w.done_flag) return false;
-    if (!w.lcmd) {
-        if (hipHostMalloc((void **)&w.lcmd, sizeof(LingerCmd), hipHostMallocDefault) != hipSuccess) {
-            w.lcmd = nullptr;
-            w.l_window_ns = 0;
-            return false;
-        }
-        memset((void *)w.lcmd, 0, sizeof(LingerCmd));
-    }
-    if (!w.svc_stream && hipStreamCreateWithFlags(&w.svc_stream, hipStreamNonBlocking) != hipSuccess) {
-        w.svc_stream = nullptr;
-        w.l_window_ns = 0;
-        return false;
-    }
-    return true;
-}
-
-static void linger_stop() {
-    World &w = world();
-    if (!w.l_live) return;
-    w.l_live = false;
-    LingerCmd *c = w.lcmd;
-    if (__atomic_load_n(&c->exit_inst, __ATOMIC_ACQUIRE) == w.l_inst) return;  // its window ran out
-    c->op = 2;
-    __atomic_store_n(&c->seq, ++w.l_posted, __ATOMIC_RELEASE);
-    const uint64_t t0 = now_ns();
-    while (__atomic_load_n(&c->exit_inst, __ATOMIC_ACQUIRE) != w.l_inst) {
-        if (now_ns() - t0 > 2000000000ull) {  // not seen in 2 s: the stream says when it has ended
-            hipStreamSynchronize(w.svc_stream);
-            break;
-        }
-    }
-}
-
-void linger_end() { linger_stop(); }
-
-// may this call be posted to the lingering kernel?
-static bool linger_match(int oi, int kind, size_t count, size_t esize, const TreeParams &tp, hipStream_t st,
-                         bool staged) {
-    World &w = world();
-    if (!w.l_live || !w.l_hold || staged || st != w.stream || w.last_st != w.stream || w.graph || w.enqueue ||
-        w.defer || w.timing)
-        return false;
-    if (oi != w.l_oi || kind != w.l_kind || count != w.l_count || esize != w.l_esize || w.size != w.l_n ||
-        w.light_release != w.l_light || memcmp(&tp, &w.l_tp, sizeof(TreeParams)) != 0)
-        return false;
-    if (!w.l_nomargin && now_ns() - w.l_tdone > w.l_window_ns / 2) return false;
-    return hipStreamQuery(nullptr) == hipSuccess && hipStreamQuery(w.stream) == hipSuccess;
-}
-
-// post one call; 0 = done, 1 = the kernel had already ended (launch it), else an error class
-static int linger_post(const char *send, char *recv, uint64_t epoch, size_t poff, uint64_t want) {
-    World &w = world();
-    LingerCmd *c = w.lcmd;
-    c->op = 1;
-    c->send = (uint64_t)(uintptr_t)send;
-    c->recv = (uint64_t)(uintptr_t)recv;
-    c->epoch = epoch;
-    c->poff = poff;
-    c->done_seq = want;
-    const uint64_t mine = ++w.l_posted;
-    __atomic_store_n(&c->seq, mine, __ATOMIC_RELEASE);
-    uint64_t next_query = now_ns() + 100000000ull;
-    for (unsigned spins = 0;; ++spins) {
-        if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) break;
-        if (__atomic_load_n(&c->exit_inst, __ATOMIC_ACQUIRE) == w.l_inst) {
-            if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) break;
-            if (__atomic_load_n(&c->exit_last, __ATOMIC_RELAXED) < mine) {
-                w.l_live = false;
-                return 1;
-            }
-        }
-        if ((spins & 1023u) == 0 && now_ns() > next_query) {  // every 100 ms: is the kernel still there?
-            next_query = now_ns() + 100000000ull;
-            const hipError_t q = hipStreamQuery(w.svc_stream);
-            if (q != hipErrorNotReady && __atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) < want &&
-                __atomic_load_n(&c->exit_inst, __ATOMIC_ACQUIRE) != w.l_inst) {
-                MV2_ERR("lingering one-shot kernel ended without reporting (%s)", hipGetErrorString(q));
-                w.l_live = false;
-                return E_INTERN;
-            }
-        }
-    }
-    w.l_tdone = now_ns();
-    return check_err_word() ? E_OTHER : 0;
 }
 
 // kernel-time events bracket the call's first launch to its last (calls made of several
@@ -832,10 +725,7 @@ int mv2h_memcpy_htod(void *d, const void *s, size_t b) { return hipMemcpy(d, s, 
 int mv2h_memcpy_dtoh(void *d, const void *s, size_t b) { return hipMemcpy(d, s, b, hipMemcpyDeviceToHost) == hipSuccess ? 0 : E_INTERN; }
 int mv2h_memcpy_dtod(void *d, const void *s, size_t b) { return hipMemcpy(d, s, b, hipMemcpyDeviceToDevice) == hipSuccess ? 0 : E_INTERN; }
 int mv2h_memset(void *d, int v, size_t b) { return hipMemset(d, v, b) == hipSuccess ? 0 : E_INTERN; }
-int mv2h_device_synchronize(void) {
-    linger_stop();  // a lingering one-shot kernel would hold hipDeviceSynchronize for its window
-    return hipDeviceSynchronize() == hipSuccess ? 0 : E_INTERN;
-}
+int mv2h_device_synchronize(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : E_INTERN; }
 
 int mv2h_dtype_info(int dtype, size_t *size, size_t *extent) {
     const DtypeInfo *dt = dtype_lookup(dtype);
@@ -889,10 +779,6 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "init_us")) *value = (long)(w.init_ms * 1e3 + 0.5);
     else if (!strcmp(key, "selftest_us")) *value = (long)(w.selftest_ms * 1e3 + 0.5);
     else if (!strcmp(key, "autotune_us")) *value = (long)(w.tune_ms * 1e3 + 0.5);
-    else if (!strcmp(key, "linger_us")) *value = (long)(w.l_window_ns / 1000);
-    else if (!strcmp(key, "linger_posts")) *value = (long)w.l_posts;
-    else if (!strcmp(key, "linger_launches")) *value = (long)w.l_launches;
-    else if (!strcmp(key, "linger_missed")) *value = (long)w.l_missed;
     else if (!strncmp(key, "os_tune_one_", 12) || !strncmp(key, "os_tune_pipe_", 13)) {
         const long i = strtol(strrchr(key, '_') + 1, nullptr, 10);
         if (i < 0 || i >= w.os_tune_n) return E_ARG;
@@ -1275,9 +1161,9 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
             a.dseq = w.dseq;
             a.half = half;
         } else {
-            for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j];  // half 0; poff0 selects
-            a.arena_own = w.arena;
-            a.poff0 = (w.os_calls++ & 1) * half;
+            const size_t par = (w.os_calls++ & 1) * half;
+            for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j] + par;
+            a.arena_own = w.arena + par;
             a.sig_peer = w.peer_sig;
             a.sig_own = w.sig;
             a.epoch = ++w.epoch;
@@ -1291,58 +1177,14 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.err = w.h_err;
         a.timeout = w.timeout_ticks;
         a.light = w.light_release;
+        a.done = arm_done(st);
         int g = (int)((nvec + 511) / 512);
         g = std::max(1, std::min(g, std::min(gcap, 32)));
-        // a small call of the lingering kernel's shape is posted to it; a call it cannot serve
-        // ends it; a single-workgroup call on idle streams is launched as the next one
-        const bool staged = s.copy_back || (!in_place && s.send != (const char *)sendbuf);
-        if (g == 1 && !w.graph && linger_match(oi, dt->kind, count, dt->extent, tp, st, staged)) {
-            const uint64_t want = ++w.done_seq;
-            rc = linger_post(s.send, s.recv, a.epoch, a.poff0, want);
-            if (rc != 1) {  // done (or failed); 1: the kernel had ended, launch this call
-                ++w.l_posts;
-                return rc;
-            }
-            ++w.l_missed;
-            a.done = Done{w.done_ctr, w.done_flag, want};
-            w.pending = want;
-        } else {
-            if (w.l_live) linger_stop();
-            a.done = arm_done(st);
-        }
-        const bool linger = g == 1 && !w.graph && w.l_hold && !staged && st == w.stream && !w.enqueue && !w.defer &&
-                            !w.timing && w.last_st == w.stream && a.done.flag && linger_ready() &&
-                            hipStreamQuery(nullptr) == hipSuccess && hipStreamQuery(w.stream) == hipSuccess;
-        hipStream_t lst = st;
-        if (linger) {
-            a.lcmd = w.lcmd;
-            a.linst = ++w.l_inst;
-            a.lseq0 = w.l_posted;
-            a.linger = w.l_ticks;
-            lst = w.svc_stream;
-        }
-        LaunchCfg cfg = coll_cfg(g, lst);
-        tmark0(lst);
+        LaunchCfg cfg = coll_cfg(g, st);
+        tmark0(st);
         rc = launch_oneshot(oi, dt->kind, a, dt->extent, cfg);
-        tmark1(lst);
+        tmark1(st);
         if (rc) return rc;
-        if (linger) {
-            ++w.l_launches;
-            w.l_live = true;
-            w.l_oi = oi;
-            w.l_kind = dt->kind;
-            w.l_count = count;
-            w.l_esize = dt->extent;
-            w.l_n = n;
-            w.l_light = w.light_release;
-            w.l_tp = tp;
-            const uint64_t want = w.pending;
-            w.pending = 0;
-            const hipError_t e = wait_done(w.svc_stream, want);
-            w.l_tdone = now_ns();
-            if (e != hipSuccess) return E_INTERN;
-            return check_err_word() ? E_OTHER : 0;
-        }
         stage_out(s, st);
         return finish(st, w.timing);
     }
@@ -1426,12 +1268,7 @@ static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int
     if (count == 0) return 0;  // allreduce_osu.c:3730
     if ((rc = kind_supported(dt))) return rc;
     if ((rc = require_world())) return rc;
-    World &w = world();
-    // a single-workgroup one-shot call may be posted to the lingering kernel (allreduce_impl)
-    w.l_hold = !stream && count * (size_t)dt->extent <= 512 * 16;
-    rc = allreduce_select(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
-    w.l_hold = false;
-    return rc;
+    return allreduce_select(sendbuf, recvbuf, count, dt, op_index(op), pick_stream(stream));
 }
 // A stream-ordered call across nodes (MPIX_*_enqueue): the leaders' steps are host-driven, so the
 // call waits for the caller's stream, then runs as the blocking call and returns complete; work

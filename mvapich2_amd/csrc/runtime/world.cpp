@@ -104,7 +104,6 @@ void *get_scratch(int idx, size_t bytes) {
     World &w = g_world;
     if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];
     if (w.scratch[idx]) {
-        linger_end();  // hipFree waits for the whole device
         hipStreamSynchronize(w.stream);
         hipFree(w.scratch[idx]);
         w.scratch[idx] = nullptr;
@@ -145,11 +144,6 @@ static int setup_device_common() {
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, w.device) == hipSuccess && khz > 0)
         w.wall_clock_khz = khz;
     w.timeout_ticks = (uint64_t)(env_long("MV2AMD_TIMEOUT_S", 120) * w.wall_clock_khz * 1000.0);
-    // lingering one-shot kernel window (coll.cpp linger_*): 0 turns it off
-    const long lus = env_long("MV2AMD_LINGER_US", 0);
-    w.l_window_ns = lus > 0 ? (uint64_t)lus * 1000u : 0;
-    w.l_ticks = (uint64_t)((double)w.l_window_ns * w.wall_clock_khz * 1e-6);
-    w.l_nomargin = env_long("MV2AMD_LINGER_TEST_NOMARGIN", 0) != 0;
     w.oneshot_max = (size_t)env_long("MV2AMD_ONESHOT_MAX", (long)w.oneshot_max);
     w.max_grid = (int)env_long("MV2AMD_MAX_GRID", w.max_grid);
     w.pipe_grid = (int)env_long("MV2AMD_PIPE_GRID", w.pipe_grid);
@@ -575,7 +569,6 @@ int global_barrier() {
 int world_finalize() {
     World &w = g_world;
     if (!w.inited || w.finalized) return 0;
-    linger_end();
     if (w.stream) hipStreamSynchronize(w.stream);
     host_prof_report();
     if (w.nnodes > 1) {

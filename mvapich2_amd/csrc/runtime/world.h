@@ -170,21 +170,6 @@ struct World {
     hipEvent_t sw_ev = nullptr;     // recorded on last_st when a call switches streams
     uint64_t deferred = 0;          // ticket of the last deferred call (0: completed at initiation)
 
-    // lingering one-shot kernel (coll.cpp linger_*): small allreduces of one shape posted to a
-    // resident single-workgroup kernel instead of launched (MV2AMD_LINGER_US window, 0 = off)
-    LingerCmd *lcmd = nullptr;          // pinned command block
-    hipStream_t svc_stream = nullptr;   // non-blocking stream of the lingering kernel
-    bool l_live = false;                // a lingering kernel may be polling
-    bool l_hold = false;                // the current call may post to it (pick_stream keeps it)
-    uint64_t l_inst = 0, l_posted = 0;  // kernel instance / last command number
-    uint64_t l_tdone = 0;               // host time (ns) of the last completion seen
-    uint64_t l_window_ns = 20000, l_ticks = 0;
-    bool l_nomargin = false;            // tests: post even when the window may have run out
-    uint64_t l_posts = 0, l_launches = 0, l_missed = 0;  // calls posted / lingering launches / not taken
-    int l_oi = -1, l_kind = -1, l_n = 0, l_light = 0;  // the shape it serves
-    size_t l_count = 0, l_esize = 0;
-    TreeParams l_tp{};
-
     // timing (bench)
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -205,7 +190,6 @@ void *get_scratch(int idx, size_t bytes);
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
 int pipe_autotune();  // coll.cpp: init-time choice of the pipelined kernels' tiling
 void host_prof_report();  // coll.cpp: MV2AMD_HOST_PROFILE summary
-void linger_end();        // coll.cpp: end a lingering one-shot kernel (before device-wide waits)
 // The library's own messages on the node's point-to-point channels (the steps of the multi-node
 // collectives) carry tags below kCollTagBase: the collective context of MPICH's comm (context_id +
 // MPID_CONTEXT_INTRA_COLL), so no application receive, MPI_ANY_TAG included, can match them.

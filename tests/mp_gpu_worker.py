@@ -81,38 +81,6 @@ def enqueue_seq(L, case, rank, n):
     return np.concatenate(out)
 
 
-def linger_seq(L, case, rank, n):
-    """A sequence of small MPI_Allreduce calls that the lingering one-shot kernel serves (same
-    shape back to back: posted, not launched), broken by calls it cannot serve (another shape, a
-    pipelined size, MPI_Reduce_local, a host buffer, a nonblocking call), each with fresh operands
-    from (seed, call index, rank); returns every result, concatenated."""
-    P = ctypes.c_void_p
-    out = []
-    for k, (t, op, c, how) in enumerate(case["calls"]):
-        h = TYPES[t][0]
-        x = rand_typed(t, c, np.random.default_rng(case["seed"] * 100000 + k * 100 + rank), edges=False)
-        ext = TYPES[t][3]
-        if how == "host":
-            r = np.zeros(c * ext, dtype=np.uint8)
-            assert L.MPI_Allreduce(x.ctypes.data, r.ctypes.data, c, h, OPS[op], WORLD) == 0
-            out.append(r)
-            continue
-        sb = m.DeviceBuffer.from_array(x)
-        rb = m.DeviceBuffer(c * ext)
-        if how == "rl":  # MPI_Reduce_local(x, x): inout = x op x
-            assert L.MPI_Reduce_local(sb.ptr, sb.ptr, c, h, OPS[op]) == 0
-            out.append(sb.download(np.uint8, count=c * ext))
-            continue
-        if how == "nb":
-            q = ctypes.c_int()
-            assert L.MPI_Iallreduce(sb.ptr, rb.ptr, c, h, OPS[op], WORLD, ctypes.byref(q)) == 0
-            assert L.MPI_Wait(ctypes.byref(q), None) == 0
-        else:
-            assert L.MPI_Allreduce(sb.ptr, rb.ptr, c, h, OPS[op], WORLD) == 0
-        out.append(rb.download(np.uint8, count=c * ext))
-    return np.concatenate(out)
-
-
 def graph_allreduce(L, case, rank, n):
     """HIP graph capture (graph lane): MPIX_Allreduce_enqueue captured on a stream for each count,
     the graphs instantiated once and replayed `reps` times in an interleaved order with new
@@ -331,8 +299,6 @@ def main():
             res = graph_allreduce(L, case, rank, n)
         elif k == "enqueue_seq":  # stream-ordered collectives (MPIX_*_enqueue) mixed with a blocking call
             res = enqueue_seq(L, case, rank, n)
-        elif k == "linger_seq":  # small allreduces posted to the lingering one-shot kernel
-            res = linger_seq(L, case, rank, n)
         elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)
             keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n", "pipe_rnt", "oneshot_max", "os_tune_n"]
             res = np.array([m.info(key) for key in keys], dtype=np.int64)

@@ -536,50 +536,6 @@ def test_stream_ordered_collectives(n, tmp_path):
                 assert_bytes_equal(parts["r"], red, "MPI_FLOAT", c, tag + " reduce")
 
 
-LINGER_CALLS = ([("MPI_FLOAT", "MPI_SUM", 2, "dev")] * 12 + [("MPI_DOUBLE", "MPI_MAX", 100, "dev")] * 4
-                + [("MPI_FLOAT", "MPI_SUM", 2, "dev")] * 3 + [("MPI_FLOAT", "MPI_SUM", 300007, "dev")]
-                + [("MPI_FLOAT", "MPI_SUM", 2, "dev")] * 3 + [("MPI_FLOAT", "MPI_SUM", 2, "rl")]
-                + [("MPI_FLOAT", "MPI_SUM", 2, "dev")] * 2 + [("MPI_FLOAT", "MPI_SUM", 2, "host")] * 2
-                + [("MPI_FLOAT", "MPI_SUM", 2, "nb")] + [("MPI_FLOAT", "MPI_SUM", 2, "dev")] * 3
-                + [("MPI_INT", "MPI_BXOR", 513, "dev")] * 3 + [("MPI_DOUBLE_INT", "MPI_MAXLOC", 64, "dev")] * 3
-                + [("MPI_FLOAT", "MPI_SUM", 2048, "dev")] * 4)
-
-
-@pytest.mark.parametrize("n,window,nomargin", [(2, "2000", "0"), (3, "2000", "0"), (2, "20", "1"), (3, "0", "0")])
-def test_lingering_oneshot(n, window, nomargin, tmp_path):
-    """Small allreduces posted to the lingering one-shot kernel (coll.cpp linger_*):
-    runs of one shape are served by the resident kernel, other calls (another shape, a pipelined
-    size, MPI_Reduce_local, host buffers, MPI_Iallreduce) end it; MV2AMD_LINGER_TEST_NOMARGIN=1
-    posts even when the window may have run out, so the 'not taken, launch it' path runs; window 0
-    is the launched path.  Every result bit-exact against the oracle."""
-    case = {"id": "lg1", "kind": "linger_seq", "seed": 41, "calls": LINGER_CALLS}
-    res = run_workers(n, [case], tmp_path, extra_env={"MV2AMD_LINGER_US": window,
-                                                      "MV2AMD_LINGER_TEST_NOMARGIN": nomargin})
-    want = []
-    for k, (t, op, c, how) in enumerate(LINGER_CALLS):
-        xs = [rand_typed(t, c, np.random.default_rng(41 * 100000 + k * 100 + r), edges=False).view(np.uint8).ravel()
-              for r in range(n)]
-        if how == "rl":
-            want.append([oracle_rl(x, t, op, c) for x in xs])
-        elif how == "nb":
-            want.append(oracle.iallreduce_ref([x.copy() for x in xs], c, TYPES[t][0], OPS[op]))
-        else:
-            want.append(oracle.allreduce_ref([x.copy() for x in xs], c, TYPES[t][0], OPS[op]))
-    for r in range(n):
-        got = res("lg1", r)
-        o = 0
-        for k, (t, op, c, how) in enumerate(LINGER_CALLS):
-            nb = c * TYPES[t][3]
-            assert_bytes_equal(got[o:o + nb], want[k][r], t, c, f"call {k} ({t} {op} {c} {how}) rank {r}")
-            o += nb
-
-
-def oracle_rl(x, t, op, c):
-    y = x.copy()
-    assert oracle.reduce_local(x.copy(), y, c, TYPES[t][0], OPS[op]) == 0
-    return y
-
-
 @pytest.mark.parametrize("n", [2, 3])
 def test_graph_captured_allreduce(n, tmp_path):
     """MPIX_Allreduce_enqueue captured into HIP graphs (the graph lane: own arenas, epochs and
