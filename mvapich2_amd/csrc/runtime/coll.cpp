@@ -970,6 +970,14 @@ int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t coun
     return finish(st, world().timing);
 }
 
+int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) {
+    int in = -1, it = -1;
+    const int t = mn_allreduce_table(ppn, gsize, nbytes, &in, &it);
+    if (intra) *intra = t == 0 ? in : -1;
+    if (inter) *inter = t == 0 ? it : -1;
+    return t;
+}
+
 int mv2h_nbc_begin(int kind) {
     if (kind < MV2H_NBC_NONE || kind > MV2H_NBC_IREDUCE_SCATTER_BLOCK) return E_ARG;
     nbc_set(kind);
