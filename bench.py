@@ -185,22 +185,24 @@ def bench_n1(args, L):
     extra["MPI_FLOAT:MPI_SUM host buffers (PCIe-inclusive)"] = {"GB/s_call": round(3 * S_BYTES * 3 / (time.perf_counter() - t0) / 1e9, 2)}
     del hx, hy
     extra["MPI_Pack/Unpack MPI_Type_vector(8Mi,4,8,MPI_FLOAT)"] = pack_run(L, max(3, args.steps // 2))
-    # the metric's small-message half at one rank: an 8-byte MPI_Reduce_local (two floats) per call,
-    # OSU-style mean over args.lat_iters back-to-back blocking calls after 100 untimed ones
+    # the metric's small-message half at one rank: an 8-byte MPI_Reduce_local per call, OSU-style
+    # mean over args.lat_iters back-to-back blocking calls after 100 untimed ones.  MPI_UNSIGNED
+    # (2 elements) so that its launches are a kernel instantiation of their own and the rocprof
+    # average of the 256 MiB fp32 kernel stays that kernel's
     s8, r8 = m.DeviceBuffer(8), m.DeviceBuffer(8)
-    s8.upload(np.ones(2, dtype=np.float32))
-    r8.upload(np.zeros(2, dtype=np.float32))
-    F32, SUM = TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]
+    s8.upload(np.ones(2, dtype=np.uint32))
+    r8.upload(np.zeros(2, dtype=np.uint32))
+    U32, SUM = TYPES["MPI_UNSIGNED"][0], OPS["MPI_SUM"]
     for _ in range(100):
-        L.MPI_Reduce_local(s8.ptr, r8.ptr, 2, F32, SUM)
+        L.MPI_Reduce_local(s8.ptr, r8.ptr, 2, U32, SUM)
     t0 = time.perf_counter()
     for _ in range(args.lat_iters):
-        m.check(L.MPI_Reduce_local(s8.ptr, r8.ptr, 2, F32, SUM), "MPI_Reduce_local 8 B")
+        m.check(L.MPI_Reduce_local(s8.ptr, r8.ptr, 2, U32, SUM), "MPI_Reduce_local 8 B")
     lat = (time.perf_counter() - t0) / args.lat_iters
-    ok8 = bool(np.all(r8.download(np.float32, count=2) == 100 + args.lat_iters))
+    ok8 = bool(np.all(r8.download(np.uint32, count=2) == 100 + args.lat_iters))
     extra["reduce_local_8B_latency_us"] = {"us": round(lat * 1e6, 2), "correct": ok8,
-                                           "what": "MPI_Reduce_local fp32 SUM, 2 elements, device buffers, blocking "
-                                                   "call incl. launch and completion word"}
+                                           "what": "MPI_Reduce_local SUM on 2 MPI_UNSIGNED (8 B), device buffers, "
+                                                   "blocking call incl. launch and completion word"}
     del s8, r8
     # HBM traffic of this kernel from the newest committed PMC pass (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py); the file is named in the line
