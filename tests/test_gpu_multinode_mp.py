@@ -210,6 +210,16 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
         cases.append({"id": f"ms{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
                       "count": sum(counts), "seed": seed, "ties": ties})
         seed += 1
+    # MPI_Ireduce_scatter across nodes: its own flat schedule (MPIR_Ireduce_scatter_MV2 -> pairwise)
+    cases.append({"id": f"mn{seed}", "kind": "reduce_scatter", "type": "MPI_FLOAT", "op": "MPI_SUM", "via": "inb",
+                  "recvcounts": [3000 + r for r in range(n)], "count": sum(3000 + r for r in range(n)), "seed": seed})
+    seed += 1
+    # ragged with empty blocks: every other rank receives nothing
+    for t, op, per in (("MPI_FLOAT", "MPI_SUM", 1000), ("MPI_DOUBLE", "MPI_MIN", 40000)):
+        counts = [0 if r % 2 == 0 else per + r for r in range(n)]
+        cases.append({"id": f"mz{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
+                      "count": sum(counts), "seed": seed})
+        seed += 1
     for t, op, per in (("MPI_INT", "MPI_SUM", 7001), ("MPI_FLOAT", "MPI_SUM", 100)):
         counts = [per + (r % 3) for r in range(n)]
         cases.append({"id": f"ms{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
@@ -255,7 +265,8 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
         elif k == "reduce_scatter":  # MPIR_Reduce_scatter_MV2 flat over every rank
             counts = case["recvcounts"]
-            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
+            algo = oracle.ALGOS.index("rs_pairwise") if case.get("via") == "inb" else -1
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]], algo=algo)
             ext = TYPES[t][3]
             off = 0
             for r in range(n):
