@@ -178,9 +178,10 @@ enum mv2h_coll {
 int mv2h_plan(int coll, int n, int rank, int root, size_t count, const size_t *counts, int dtype, int opkind,
               int in_place, int *algo, int *inner, int *unpinned, mv2h_progset *ps);
 /* Several nodes: the allreduce tuning-table entry for ppn ranks per node, gsize ranks and nbytes
- * (allreduce_osu.c:3162-3290 over the default tables).  Returns 0 for a two-level entry (*intra:
- * 0 the node's own selection, 1 reduce_shmem, 2 reduce_p2p, 3 pt2pt_rs; *inter: 2 pt2pt_rs,
- * 3 pt2pt_rd), 2 / 3 for a flat pt2pt_rs / pt2pt_rd over every rank, -1 for an entry not restated. */
+ * (allreduce_osu.c:3162-3290 over every numproc entry of the default 1 / 2 / 16-ppn tables).
+ * Returns 0 for a two-level entry (*intra: 0 the node's own selection, 1 reduce_shmem,
+ * 2 reduce_p2p, 3 pt2pt_rs, 4 pt2pt_rd; *inter: 2 pt2pt_rs, 3 pt2pt_rd), 2 / 3 for a flat
+ * pt2pt_rs / pt2pt_rd over every rank. */
 int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter);
 /* Nonblocking initiation: between mv2h_nbc_begin(kind) and mv2h_nbc_end() on this thread
  * the reducing collectives take the reference's nonblocking selection (MPIR_Iallreduce_MV2,

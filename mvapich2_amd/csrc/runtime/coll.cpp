@@ -1635,46 +1635,121 @@ int mn_reserve(size_t bytes) {
 int mn_d2h(void *h, const void *d, size_t b) { return hipMemcpy(h, d, b, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN; }
 int mn_h2d(void *d, const void *h, size_t b) { return hipMemcpy(d, h, b, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN; }
 
-// leaders: recursive doubling on `acc` (device, `count` elements), allreduce_osu.c:455-600 with
-// the nodes as ranks; every step's uop(tmp, recv) is one device Reduce_local
-int leader_rd(char *acc, size_t count, int dtype, int op, size_t bytes) {
-    World &w = world();
-    const int n = w.nnodes, rank = w.node;
+// The message schedules of MPIR_Allreduce_pt2pt_rd_MV2 (allreduce_osu.c:455-600) and
+// MPIR_Allreduce_pt2pt_rs_MV2 (:740-1054: recursive doubling for count < pof2, :802) run as
+// messages over n ranks, this one `rank`.  acc (device, count elements of ext bytes) holds the
+// operand and ends with the result; tmp (device, as large) receives.  x.xchg(peer, sb, sbytes, rb,
+// rbytes) sends and receives (either side may be empty).  Every uop(tmp, recvbuf) is one device
+// Reduce_local; builtin ops only (commutative, so recursive doubling never swaps its operands).
+struct Xport {
+    virtual int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) = 0;
+};
+int sched_allreduce(Xport &x, int n, int rank, char *acc, char *tmp, size_t count, size_t ext, int dtype, int op,
+                    bool rd) {
     int pof2 = 1;
     while (pof2 * 2 <= n) pof2 *= 2;
     const int rem = n - pof2;
+    const size_t S = count * ext;
     int rc = 0, newrank;
+    auto uop = [&](size_t off, size_t cnt) { return mv2h_reduce_local(tmp + off, acc + off, cnt, dtype, op, nullptr); };
+    // non-power-of-two pre-step: even ranks below 2 * rem hand their operand to rank + 1
     if (rank < 2 * rem) {
         if (rank % 2 == 0) {
-            if ((rc = mn_d2h(g_mn.h0, acc, bytes)) || (rc = net_send(rank + 1, g_mn.h0, bytes))) return rc;
+            if ((rc = x.xchg(rank + 1, acc, S, nullptr, 0))) return rc;
             newrank = -1;
         } else {
-            if ((rc = net_recv(rank - 1, g_mn.h1, bytes)) || (rc = mn_h2d(g_mn.d1, g_mn.h1, bytes)) ||
-                (rc = mv2h_reduce_local(g_mn.d1, acc, count, dtype, op, nullptr)))
-                return rc;
+            if ((rc = x.xchg(rank - 1, nullptr, 0, tmp, S)) || (rc = uop(0, count))) return rc;
             newrank = rank / 2;
         }
     } else {
         newrank = rank - rem;
     }
-    if (newrank != -1) {
+    auto real = [&](int nr) { return nr < rem ? nr * 2 + 1 : nr + rem; };
+    if (newrank != -1 && (rd || count < (size_t)pof2)) {
         for (int mask = 1; mask < pof2; mask <<= 1) {
+            if ((rc = x.xchg(real(newrank ^ mask), acc, S, tmp, S)) || (rc = uop(0, count))) return rc;
+        }
+    } else if (newrank != -1) {
+        // reduce-scatter by recursive halving over pof2 blocks (the last one takes the remainder),
+        // then the recursive-doubling allgather
+        std::vector<size_t> cnts((size_t)pof2, count / (size_t)pof2), disps((size_t)pof2, 0);
+        cnts[(size_t)pof2 - 1] = count - (count / (size_t)pof2) * (size_t)(pof2 - 1);
+        for (int i = 1; i < pof2; ++i) disps[i] = disps[i - 1] + cnts[i - 1];
+        auto span = [&](int a, int b) { return a < b ? disps[b - 1] + cnts[b - 1] - disps[a] : (size_t)0; };
+        int mask = 1, send_idx = 0, recv_idx = 0, last_idx = pof2;
+        while (mask < pof2) {
             const int newdst = newrank ^ mask;
-            const int dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
-            if ((rc = mn_d2h(g_mn.h0, acc, bytes)) || (rc = net_sendrecv(dst, g_mn.h0, bytes, g_mn.h1, bytes)) ||
-                (rc = mn_h2d(g_mn.d1, g_mn.h1, bytes)) ||
-                (rc = mv2h_reduce_local(g_mn.d1, acc, count, dtype, op, nullptr)))  // builtin ops commute
+            size_t scnt, rcnt;
+            if (newrank < newdst) {
+                send_idx = recv_idx + pof2 / (mask * 2);
+                scnt = span(send_idx, last_idx);
+                rcnt = span(recv_idx, send_idx);
+            } else {
+                recv_idx = send_idx + pof2 / (mask * 2);
+                scnt = span(send_idx, recv_idx);
+                rcnt = span(recv_idx, last_idx);
+            }
+            const size_t so = disps[send_idx] * ext, ro = disps[recv_idx] * ext;
+            if ((rc = x.xchg(real(newdst), acc + so, scnt * ext, tmp + ro, rcnt * ext)) || (rc = uop(ro, rcnt)))
                 return rc;
+            send_idx = recv_idx;
+            mask <<= 1;
+            if (mask < pof2) last_idx = recv_idx + pof2 / mask;
+        }
+        for (mask >>= 1; mask > 0; mask >>= 1) {
+            const int newdst = newrank ^ mask;
+            size_t scnt, rcnt;
+            if (newrank < newdst) {
+                if (mask != pof2 / 2) last_idx = last_idx + pof2 / (mask * 2);
+                recv_idx = send_idx + pof2 / (mask * 2);
+                scnt = span(send_idx, recv_idx);
+                rcnt = span(recv_idx, last_idx);
+            } else {
+                recv_idx = send_idx - pof2 / (mask * 2);
+                scnt = span(send_idx, last_idx);
+                rcnt = span(recv_idx, send_idx);
+            }
+            if ((rc = x.xchg(real(newdst), acc + disps[send_idx] * ext, scnt * ext, acc + disps[recv_idx] * ext,
+                             rcnt * ext)))
+                return rc;
+            if (newrank > newdst) send_idx = recv_idx;
         }
     }
-    if (rank < 2 * rem) {
-        if (rank % 2) {
-            if ((rc = mn_d2h(g_mn.h0, acc, bytes)) || (rc = net_send(rank - 1, g_mn.h0, bytes))) return rc;
-        } else {
-            if ((rc = net_recv(rank + 1, g_mn.h1, bytes)) || (rc = mn_h2d(acc, g_mn.h1, bytes))) return rc;
-        }
+    // post-step: the odd ranks below 2 * rem return the result to rank - 1
+    if (rank < 2 * rem) rc = rank % 2 ? x.xchg(rank - 1, acc, S, nullptr, 0) : x.xchg(rank + 1, nullptr, 0, acc, S);
+    return rc;
+}
+
+// the node leaders as ranks (node index), over their TCP links, staged through g_mn.h0 / h1
+struct LeaderLinks : Xport {
+    int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) override {
+        int rc = 0;
+        if (sbytes && (rc = mn_d2h(g_mn.h0, sb, sbytes))) return rc;
+        if (sbytes && rbytes) rc = net_sendrecv(peer, g_mn.h0, sbytes, g_mn.h1, rbytes);
+        else if (sbytes) rc = net_send(peer, g_mn.h0, sbytes);
+        else if (rbytes) rc = net_recv(peer, g_mn.h1, rbytes);
+        return rc || !rbytes ? rc : mn_h2d(rb, g_mn.h1, rbytes);
     }
-    return 0;
+};
+
+// every rank of the job (global rank), over the point-to-point channels in the library's
+// collective context: device IPC within a node, the rank mesh between nodes
+struct RankChannels : Xport {
+    int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) override {
+        unsigned long long sq = 0, rq = 0;
+        int rc = 0;
+        if (rbytes && (rc = p2p_irecv(rb, rbytes, peer, kCollTagBase - 3, &rq))) return rc;
+        if (sbytes && (rc = p2p_isend(sb, sbytes, peer, kCollTagBase - 3, &sq))) return rc;
+        if (sbytes && (rc = mv2h_p2p_wait(sq, nullptr, nullptr, nullptr))) return rc;
+        return rbytes ? mv2h_p2p_wait(rq, nullptr, nullptr, nullptr) : 0;
+    }
+};
+
+// leaders: recursive doubling on `acc` (device, `count` elements) with the nodes as ranks
+int leader_rd(char *acc, size_t count, int dtype, int op, size_t bytes) {
+    World &w = world();
+    LeaderLinks x;
+    return sched_allreduce(x, w.nnodes, w.node, acc, g_mn.d1, count, bytes / count, dtype, op, true);
 }
 
 // leaders: binomial broadcast of the host buffer h from node `root` (MPIR_Bcast_binomial order)
@@ -1729,7 +1804,7 @@ static int mn_select(long nbytes, int *intra, int *inter) {
         *inter = it;
         return 0;
     }
-    return t > 0 && w.gsize <= kMaxRanks ? t : 0;  // flat programs: up to kMaxRanks operands
+    return t;
 }
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
@@ -1763,7 +1838,7 @@ static int gather_node_leader(const void *mine, char *G, size_t S) {
 // chunks of node g's ranks) starts at node g with the ranks from the chunk's own onwards, crosses
 // every other node whole, and ends at node g with the ranks before it.  Every uop is one device
 // Reduce_local.  The wrapper's remainder (count % n elements, pt2pt_rs over every rank, :3800-3818)
-// is that flat algorithm for jobs of up to kMaxRanks ranks, else the two-level order.
+// is that flat algorithm (its programs up to kMaxRanks ranks, its message schedule above).
 static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     World &w = world();
     const DtypeInfo *dt = dtype_lookup(dtype);
@@ -1818,11 +1893,9 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     }
     if ((rc = bcast_node(recvbuf, main_bytes, 0, stream))) return rc;
     if (count % (size_t)n == 0) return 0;
-    if (n <= kMaxRanks)  // the wrapper's pt2pt_rs over every rank (recursive doubling: rem < n)
-        return mn_flat_allreduce((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
-                                 dtype, op, stream, ALG_PT2PT_RS);
-    return mn_allreduce_2lvl((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
-                             dtype, op, stream);
+    // the wrapper's pt2pt_rs over every rank (recursive doubling: rem < n)
+    return mn_flat_allreduce((const char *)sendbuf + main_bytes, (char *)recvbuf + main_bytes, count % (size_t)n,
+                             dtype, op, stream, ALG_PT2PT_RS);
 }
 
 // Every rank's S-byte operand onto every rank, in global rank order (*out: device scratch of
@@ -1852,6 +1925,28 @@ static int mn_gather_all(const void *mine, size_t S, char **out, void *stream) {
     return 0;
 }
 
+// Flat pt2pt_rs / pt2pt_rd over more than kMaxRanks ranks (beyond the programs' registers): the
+// algorithm's message schedule itself (sched_allreduce) over every rank's point-to-point channels,
+// each step's received data reduced into this rank's accumulator (recvbuf, or device scratch when
+// recvbuf is host memory) by one device Reduce_local.
+static int mn_sched_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int algo) {
+    World &w = world();
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const bool in_place = sendbuf == (const void *)-1;
+    const size_t ext = (size_t)dt->extent, S = count * ext;
+    const int id = algo == ALG_PT2PT_RS ? PV_AR_SHM_RS : PV_AR_SHM_RD;
+    pvar_note_ids(&id, 1);
+    int rc = mn_reserve_dev(S);
+    if (rc) return rc;
+    char *acc = is_device(recvbuf) ? (char *)recvbuf : g_mn.d0;
+    const void *src = in_place ? recvbuf : sendbuf;
+    if (src != acc && hipMemcpy(acc, src, S, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+    RankChannels x;
+    if ((rc = sched_allreduce(x, w.gsize, w.grank, acc, g_mn.d1, count, ext, dtype, op, algo == ALG_PT2PT_RD)))
+        return rc;
+    return acc == recvbuf || hipMemcpy(recvbuf, acc, S, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+}
+
 // Flat pt2pt_rs / pt2pt_rd over every rank (allreduce_osu.c:633-1054, :360-630): every rank's operand reaches every rank
 // (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
 // evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
@@ -1866,6 +1961,8 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     const bool in_place = sendbuf == (const void *)-1;
     const size_t S = count * (size_t)dt->extent;
     const int n = w.gsize;
+    if (n > kMaxRanks && root < 0 && (algo == ALG_PT2PT_RS || algo == ALG_PT2PT_RD))
+        return mn_sched_allreduce(sendbuf, recvbuf, count, dtype, op, algo);
     Plan p;
     int rc = root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
                        : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
@@ -1896,14 +1993,13 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     const int sel = mn_select((long)(count * (size_t)dt->size), &intra, &inter);
     if (sel == 1) {
         // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise
-        // it runs pt2pt_rs over every rank (restated up to kMaxRanks ranks, else two-level).  With
+        // it runs pt2pt_rs over every rank.  With
         // IN_PLACE the body's own fallback is pt2pt_rs over (count / n) * n elements (:4095-4100),
         // then the wrapper's pt2pt_rs on the remainder (:3800-3818): two calls, as on one node
         if (!in_place && count >= (size_t)gsize)
             return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
         const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
         pvar_note_ids(chain, 2);
-        if (gsize > kMaxRanks) return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
         const size_t main = in_place ? (count / (size_t)gsize) * (size_t)gsize : 0;
         if (main && main < count) {
             if ((rc = mn_flat_allreduce(sendbuf, recvbuf, main, dtype, op, stream, ALG_PT2PT_RS))) return rc;
@@ -1940,7 +2036,10 @@ static int node_allreduce_intra(const void *sendbuf, void *recvbuf, size_t count
         p.algo = ALG_TWO_LEVEL_P2P;
     } else {
         rc = plan_allreduce(n, me, count, dt->size, dt->extent, in_place,
-                            intra == MN_INTRA_RS ? ALG_PT2PT_RS : ALG_SHMEM_LINEAR, &p);
+                            intra == MN_INTRA_RS   ? ALG_PT2PT_RS
+                            : intra == MN_INTRA_RD ? ALG_PT2PT_RD
+                                                   : ALG_SHMEM_LINEAR,
+                            &p);
     }
     if (rc) return rc;
     log_plan("allreduce (node step)", p, count);
@@ -1951,11 +2050,14 @@ namespace {
 // leaders: MPIR_Allreduce_pt2pt_rs_MV2 (:633-1054; recursive doubling for count < pof2, :802) with
 // the nodes as ranks, MPI_IN_PLACE on `acc`.  Every leader's partial reaches every leader (a ring
 // over the leaders) and each evaluates that algorithm's per-element programs for its own node
-// index on the device; more than kMaxRanks nodes keep recursive doubling (not restated).
+// index on the device; more than kMaxRanks nodes run the algorithm's message schedule itself.
 int leader_prog(char *acc, size_t count, int dtype, int op, size_t bytes, int algo) {
     World &w = world();
     const int K = w.nnodes, me = w.node;
-    if (K > kMaxRanks) return leader_rd(acc, count, dtype, op, bytes);
+    if (K > kMaxRanks) {
+        LeaderLinks x;
+        return sched_allreduce(x, K, me, acc, g_mn.d1, count, bytes / count, dtype, op, algo == ALG_PT2PT_RD);
+    }
     const DtypeInfo *dt = dtype_lookup(dtype);
     Plan p;
     int rc = plan_allreduce(K, me, count, dt->size, dt->extent, true, algo, &p);
@@ -2221,6 +2323,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
     case MN_INTRA_P2P: rc = plan_reduce(L, 0, 0, count, tsize, textent, &s->node, opk); break;
     case MN_INTRA_SHMEM: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, ALG_SHMEM_LINEAR, &s->node, opk); break;
     case MN_INTRA_RS: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, ALG_PT2PT_RS, &s->node, opk); break;
+    case MN_INTRA_RD: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, ALG_PT2PT_RD, &s->node, opk); break;
     default: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, 0, &s->node, opk); break;
     }
     if (rc) return rc;

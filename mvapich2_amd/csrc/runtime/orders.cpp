@@ -782,60 +782,74 @@ static int plan_allreduce_build(int n, int me, size_t count, int tsize, int text
 }
 
 // Several nodes: the tuning-table step of MPIR_Allreduce_index_tuned_intra_MV2 (:3162-3290) for
-// `ppn` ranks per node and `gsize` ranks in all.  The 16-ppn table (ppn >= 3) is restated by its
-// first entry (numproc 16: jobs up to 16 ranks); the 2-ppn and 1-ppn tables
-// (nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{2,1}ppn.h) by their numproc 2 / 4 / 8 entries (jobs up
-// to 8 ranks; comm_size_index :3210-3228 over minimum numproc 2).  Returns 0 (is_two_level),
-// ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every rank), or -1 (entry not restated).  The multicast
-// entries fall back to recursive doubling (:3324-3338).
+// `ppn` ranks per node and `gsize` ranks in all, over every numproc entry of the default tables
+// nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h (the 16-ppn one for ppn >= 3).
+// comm_size_index (:3210-3228): the entry of floor_pof2(gsize), clamped to the table's first and
+// last; the message-size index over 18 entries from 1 byte (:3240-3275).  Returns 0
+// (is_two_level), ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every rank).  The multicast helper falls
+// back to recursive doubling (:3324-3338), keeping a two-level entry two-level.
+namespace {
+struct MnEntry {
+    int numproc;
+    const char *two_level;  // per size index: '1' = MPIR_Allreduce_two_level_MV2
+    const char *inter;      // s = pt2pt_rs, d = pt2pt_rd, m = multicast helper (-> pt2pt_rd)
+    const char *intra;      // h = reduce_shmem, p = reduce_p2p, s = pt2pt_rs, d = pt2pt_rd
+};
+// the tables' per-entry lists, one character per message-size index (1 B, 2 B, ... 128 KiB)
+const MnEntry k1ppnTab[] = {
+    {2, "000000000000000000", "dddddddddddddsdsss", "pppppppppppppppppp"},
+    {4, "010000000000000000", "smdddddddddddsssss", "phpppppppppppppppp"},
+    {8, "111111111110011000", "sddddddddddddsssss", "psshhhssshhpphhppp"},
+    {16, "010101111101111000", "dsssddddmddddsssss", "ppppppdphpppphhppp"},
+    {32, "000001001111111100", "dsdssddddddddsssss", "ppppppppshhshppppp"},
+};
+const MnEntry k2ppnTab[] = {
+    {2, "111111111111000000", "dddsssddddssssssss", "hhhhhhhhhhhhpppppp"},
+    {4, "111111111111100000", "dddddddddddddsssss", "hhhhhhhhhhhhhppppp"},
+    {8, "111111111111000000", "sdddddddddddssssss", "hhhhhhshhhhhpppppp"},
+    {16, "111111111101100000", "smdddddddddddsssss", "hhhdhhddhdphpppppp"},
+    {32, "111111111111110000", "dddddddddddddsssss", "sdsshssshsshshpppp"},
+};
+const MnEntry k16ppnTab[] = {
+    {16, "111111111100000000", "ssssssssssssssssss", "hhhhhhhhpppppppppp"},
+    {32, "111111111111000000", "sdddddddmdddssssss", "hhhhhhhhhpdppppppp"},
+    {64, "111111111111100000", "dddmdddmmddddsssss", "hhhhhhhhhssssppppp"},
+    {128, "111111111111100000", "sddddddddddddsssss", "hhshhshhspdsdppppp"},
+    {256, "111111111111110000", "dmdsddmddmdmdsssss", "dhhpsshhshshsspppp"},
+    {512, "111111111111111000", "dmsdddmmmddddsssss", "shhphphhhsdssppppp"},
+    {1024, "111111111111110000", "dsmdsmddmdmddsssss", "phhphhhshshspppppp"},
+};
+}  // namespace
+
 int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) {
-    const int idx = table_index(nbytes, 1, 18);
-    auto two_level = [&](int in, int a) {
-        if (intra) *intra = in;
-        if (inter) *inter = a == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
-        return 0;
-    };
-    if (ppn_conf(ppn) == 2) {
-        if (gsize > 16) return -1;
-        // the node's one-node plan (ppn >= 3 ranks) reads this same entry's intra function
-        if (kAr16.two_level[idx]) return two_level(MN_INTRA_NODE, kAr16.inter[idx]);
-        return kAr16.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
+    const int conf = ppn_conf(ppn);
+    const MnEntry *tab = conf == 0 ? k1ppnTab : conf == 1 ? k2ppnTab : k16ppnTab;
+    const int ntab = conf == 2 ? (int)(sizeof(k16ppnTab) / sizeof(k16ppnTab[0])) : 5;
+    int ci = 0;  // comm_size_index
+    if (gsize > tab[ntab - 1].numproc) {
+        ci = ntab - 1;
+    } else {
+        for (int v = pof2_of(gsize); v > tab[0].numproc; v >>= 1) ++ci;
     }
-    if (gsize < 2 || gsize > 8) return -1;
-    int ci = 0;  // comm_size_index: log2(floor_pof2(gsize) / 2)
-    for (int v = gsize / 2; v > 1; v >>= 1) ++ci;
-    struct Entry {
-        int two_level[18];
-        int inter[18];
-        int intra[18];
-    };
-    enum { SH = MN_INTRA_SHMEM, PP = MN_INTRA_P2P, RS = MN_INTRA_RS };
-    // nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_2ppn.h numproc 2 / 4 / 8 (inter-leader and intra-node lists)
-    static const Entry k2ppn[3] = {
-        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0},
-         {A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS},
-         {SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, PP, PP, PP, PP, PP, PP}},
-        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0},
-         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS},
-         {SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, SH, PP, PP, PP, PP, PP}},
-        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0},
-         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS, A_RS},
-         {SH, SH, SH, SH, SH, SH, RS, SH, SH, SH, SH, SH, PP, PP, PP, PP, PP, PP}}};
-    static const Entry k1ppn[3] = {
-        {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-         {A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RD, A_RS, A_RS, A_RS},
-         {}},
-        {{0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},  // idx 1: multicast -> RD, two-level
-         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS},
-         {}},
-        {{1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 0, 0},
-         {A_RS, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RD, A_RS, A_RS, A_RS, A_RS, A_RS},
-         {}}};
-    const Entry &e = ppn_conf(ppn) == 1 ? k2ppn[ci] : k1ppn[ci];
+    const MnEntry &e = tab[ci];
+    const int idx = table_index(nbytes, 1, 18);
+    const int a = e.inter[idx] == 's' ? ALG_PT2PT_RS : ALG_PT2PT_RD;
     // one rank per node: the two-level algorithm is its leaders' algorithm over every rank
     // (MPIR_Allreduce_two_level_MV2 :1750-1780 with nothing to reduce or broadcast in a node)
-    if (e.two_level[idx] && ppn > 1) return two_level(e.intra[idx], e.inter[idx]);
-    return e.inter[idx] == A_RD ? ALG_PT2PT_RD : ALG_PT2PT_RS;
+    if (e.two_level[idx] != '1' || ppn <= 1) return a;
+    int in = MN_INTRA_SHMEM;
+    switch (e.intra[idx]) {
+    case 'p': in = MN_INTRA_P2P; break;
+    case 's': in = MN_INTRA_RS; break;
+    case 'd': in = MN_INTRA_RD; break;
+    default: break;
+    }
+    // 16 ppn, numproc 16 entry: the node's one-node plan for its ppn ranks reads this same entry
+    // (same intra function, plus its own checks), so the node step is that plan
+    if (conf == 2 && ci == 0) in = MN_INTRA_NODE;
+    if (intra) *intra = in;
+    if (inter) *inter = a;
+    return 0;
 }
 
 // ---------------------------------------------------------------------------

@@ -133,6 +133,7 @@ enum MnIntra : int {
     MN_INTRA_SHMEM = 1,   // MPIR_Allreduce_reduce_shmem_MV2: ((x0 . x1) . x2) ... at the leader
     MN_INTRA_P2P = 2,     // MPIR_Allreduce_reduce_p2p_MV2: MPIR_Reduce_MV2 to local rank 0 (:1614-1684)
     MN_INTRA_RS = 3,      // MPIR_Allreduce_pt2pt_rs_MV2 over the node's communicator, leader's result
+    MN_INTRA_RD = 4,      // MPIR_Allreduce_pt2pt_rd_MV2 over the node's communicator, leader's result
 };
 int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra = nullptr, int *inter = nullptr);
 int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *out, int opk = OPK_BUILTIN);

@@ -10,6 +10,9 @@ of MPIR_Allreduce_two_level_MV2 / topo-aware hierarchical, allreduce_osu.c:360-6
 oracle op-loop call.  Allreduce from 2 MiB is the flat ring over every rank, and where the tables
 name it the flat pt2pt_rs / pt2pt_rd over every rank (expected_allreduce); reduce-scatter is
 MPIR_Reduce_scatter_MV2's flat selection over every rank (red_scat_osu.c:1771-1900)."""
+import json
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -81,40 +84,47 @@ def ring_flat(sends, count, t, op):
     return out
 
 
-# multi-node entries of the default allreduce tables (allreduce_tuning.c fall-back,
-# tuning/allreduce/nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{2,1}ppn.h), numproc 2 / 4 / 8: per
-# message-size index, 0 = two-level, else the flat inter-leader function (multicast -> rd)
-_T2 = ["rd rd rd rs rs rs rd rd rd rd rs rs | rs rs rs rs rs rs",
-       "rd rd rd rd rd rd rd rd rd rd rd rd rd | rs rs rs rs rs",
-       "rs rd rd rd rd rd rd rd rd rd rd rd | rs rs rs rs rs rs"]
-# 1 ppn: a two-level entry is its leaders' function over every rank, so every cell is flat
-_T1 = ["| rd rd rd rd rd rd rd rd rd rd rd rd rd rs rd rs rs rs",
-       "| rs rd rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs",
-       "| rs rd rd rd rd rd rd rd rd rd rd rd rd rs rs rs rs rs"]
+# the multi-node allreduce tables MVAPICH2 falls back to (allreduce_tuning.c default branch,
+# tuning/allreduce/nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h), as data generated from
+# the headers by tests/golden/gen_mn_allreduce_tables.py
+_TABLES = json.loads((Path(__file__).parent / "golden" / "mn_allreduce_tables.json").read_text())
+_INTRA = {"h": "reduce_shmem", "p": "reduce_p2p", "s": "pt2pt_rs", "d": "pt2pt_rd"}
+
+
+def table_cell(ppn, n, nbytes):
+    """MPIR_Allreduce_index_tuned_intra_MV2's table step (allreduce_osu.c:3200-3290): ("2l", inter,
+    intra) for a two-level entry, ("flat", algorithm, None) for a flat one (multicast -> pt2pt_rd).
+    comm_size_index: the entry of floor_pof2(n), clamped to the table's first and last entries;
+    one rank per node: a two-level entry is its leaders' function over every rank; 16 ppn, first
+    entry: intra "node" (the node's one-node selection reads the same entry)."""
+    tab = _TABLES["1ppn" if ppn <= 1 else "2ppn" if ppn == 2 else "16ppn"]
+    if n > tab[-1]["numproc"]:
+        ci = len(tab) - 1
+    else:
+        p, ci = 1 << (n.bit_length() - 1), 0
+        while p > tab[0]["numproc"]:
+            p, ci = p >> 1, ci + 1
+    e = tab[ci]
+    idx = min(17, max(0, nbytes.bit_length() - 1))
+    fn = "pt2pt_rs" if e["inter"][idx] == "s" else "pt2pt_rd"
+    if e["two_level"][idx] != "1" or ppn <= 1:
+        return "flat", fn, None
+    return "2l", fn, "node" if ppn >= 3 and ci == 0 else _INTRA[e["intra"][idx]]
 
 
 def table_entry(ppn, n, nbytes, knobs=None):
     """("2l", inter) for a two-level entry or ("flat", algorithm) of MVAPICH2's tables across nodes"""
-    idx = min(17, max(0, nbytes.bit_length() - 1))
-    if ppn >= 3:  # 16-ppn table, first entry: the one-node selection for ppn ranks reads it too
-        a = oracle.ALGOS[oracle.allreduce_select(ppn, max(1, nbytes // 4), TYPES["MPI_FLOAT"][0], knobs=knobs)]
-        return ("flat", a) if a in ("pt2pt_rs", "pt2pt_rd") else ("2l", "pt2pt_rs")  # its inter list: all rs
-    ci = (n // 2).bit_length() - 1
-    row = (_T2 if ppn == 2 else _T1)[ci]
-    # "|" splits the two-level prefix from the flat suffix
-    head, tail = row.split("|")
-    cells = [("2l", c) for c in head.split()] + [("flat", c) for c in tail.split()]
-    kind, fn = cells[idx]
-    return kind, "pt2pt_" + fn
+    return table_cell(ppn, n, nbytes)[:2]
 
 
 def expected_allreduce(sends, count, t, op, ppn, in_place=False):
     """per-rank results of MPI_Allreduce across nodes, by the selection coll.cpp mn_allreduce
-    restates: flat ring from 2 MiB (remainder: flat pt2pt_rs over every rank for n <= 8), the flat
-    pt2pt_rs / pt2pt_rd where the tables name it (n <= 8), else two-level"""
+    restates: flat ring from 2 MiB (remainder, IN_PLACE and count < n: the wrapper's flat pt2pt_rs
+    over every rank), the small-message shortcuts' two-level order up to 2 KiB, then the tables'
+    flat pt2pt_rs / pt2pt_rd or two-level entry"""
     n = len(sends)
-    if count * TYPES[t][2] >= 2 << 20 and (in_place or count < n) and n <= 8:  # the wrapper's pt2pt_rs
-        rs = oracle.ALGOS.index("pt2pt_rs")
+    rs = oracle.ALGOS.index("pt2pt_rs")
+    if count * TYPES[t][2] >= 2 << 20 and (in_place or count < n):  # the wrapper's pt2pt_rs
         main = (count // n) * n if in_place else 0
         if not main or main == count:
             return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op], algo=rs)
@@ -129,28 +139,35 @@ def expected_allreduce(sends, count, t, op, ppn, in_place=False):
         if not rem:
             return [main] * n
         tails = [x[len(main):].copy() for x in sends]
-        tail = oracle.allreduce(tails, rem, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index("pt2pt_rs")) if n <= 8 \
-            else two_level(tails, rem, t, op, ppn)
+        tail = oracle.allreduce(tails, rem, TYPES[t][0], OPS[op], algo=rs)
         return [np.concatenate([main, tail[r]]) for r in range(n)]
     nbytes = count * TYPES[t][2]
-    if nbytes > 2048 and n <= 8:  # the topology-aware shortcut up to 2 KiB, then the tables
-        kind, fn = table_entry(ppn, n, nbytes)
+    if nbytes > 2048:  # the topology-aware shortcut up to 2 KiB, then the tables
+        kind, fn, intra = table_cell(ppn, n, nbytes)
         if kind == "flat":
             return oracle.allreduce([x.copy() for x in sends], count, TYPES[t][0], OPS[op],
                                     algo=oracle.ALGOS.index(fn))
-        return two_level(sends, count, t, op, ppn, inter=fn, pair_shmem=ppn == 2)
+        return two_level(sends, count, t, op, ppn, inter=fn, intra=intra)
     return two_level(sends, count, t, op, ppn)
 
 
-def two_level(sends, count, t, op, ppn, inter="pt2pt_rd", pair_shmem=False, knobs=None):
-    """MPIR_Allreduce_two_level_MV2: node step (the oracle's one-node algorithm, or for a 2-ppn table
-    entry its reduce_shmem: x0 (+) x1 at the leader), the leaders' inter algorithm, node broadcast"""
+def node_step(xs, count, t, op, intra, knobs=None):
+    """the leader's partial after a two-level entry's intra-node function over the node's ranks
+    (MPIR_Allreduce_two_level_MV2 :1727-1745)"""
+    if intra == "node":  # the node's own one-node selection
+        return oracle.allreduce_ref(xs, count, TYPES[t][0], OPS[op], knobs=knobs)[0]
+    if intra == "reduce_p2p":  # MPIR_Reduce_MV2 to local rank 0
+        return oracle.reduce_ref(xs, count, TYPES[t][0], OPS[op], 0)
+    algo = "shmem_linear" if intra == "reduce_shmem" else intra
+    return oracle.allreduce(xs, count, TYPES[t][0], OPS[op], algo=oracle.ALGOS.index(algo))[0]
+
+
+def two_level(sends, count, t, op, ppn, inter="pt2pt_rd", intra="node", knobs=None):
+    """MPIR_Allreduce_two_level_MV2: node step (node_step), the leaders' inter algorithm, node
+    broadcast"""
     nodes = len(sends) // ppn
-    if pair_shmem:
-        parts = [uop(sends[2 * j + 1], sends[2 * j], count, t, op) for j in range(nodes)]
-    else:
-        parts = [oracle.allreduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0], OPS[op],
-                                      knobs=knobs)[0] for j in range(nodes)]
+    parts = [node_step([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, t, op, intra, knobs)
+             for j in range(nodes)]
     if inter == "pt2pt_rd":
         lead = rd_leaders(parts, count, t, op)
     else:
@@ -304,9 +321,9 @@ def test_two_level_table_entries_across_nodes(n, ppn, tmp_path):
     for case in cases:
         cid, t, count = case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        kind, fn = table_entry(ppn, n, count * TYPES[t][2], knobs=k)
+        kind, fn, intra = table_cell(ppn, n, count * TYPES[t][2])
         assert kind == "2l", (cid, kind, fn)
-        want = two_level(sends, count, t, case["op"], ppn, inter=fn, pair_shmem=ppn == 2, knobs=k)
+        want = two_level(sends, count, t, case["op"], ppn, inter=fn, intra=intra, knobs=k)
         for r in range(n):
             assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
 
@@ -460,3 +477,60 @@ def test_mpit_counts_across_nodes(tmp_path):
             want.update({"mv2_coll_allreduce_shm_rd": 1, "mv2_coll_reduce_binomial": 1})
         got = json.loads(res("mpit", r).tobytes().decode())
         assert {k: v for k, v in got.items() if v} == want, (r, got)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("n,ppn", [(12, 1), (12, 2), (10, 2), (12, 4)])
+def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
+    """Jobs of more than 8 ranks (at most 12 processes on the one GPU): the flat pt2pt_rs /
+    pt2pt_rd the tables name over every rank, and the ring wrapper's pt2pt_rs remainder, run as
+    the reference's message schedule over the point-to-point channels (coll.cpp sched_allreduce,
+    RankChannels); the small-message shortcut's recursive doubling over more than 8 node leaders
+    (LeaderLinks); the tables' numproc 8 / 16 entries (10 and 12 ranks: comm_size_index of 8)."""
+    cases, seed = [], 1300
+    for t, op, count, ties in (("MPI_FLOAT", "MPI_SUM", 10, False), ("MPI_FLOAT", "MPI_SUM", 300, False),
+                               ("MPI_FLOAT", "MPI_SUM", 700, False), ("MPI_FLOAT", "MPI_SUM", 1500, False),
+                               ("MPI_FLOAT", "MPI_SUM", 5000, False), ("MPI_FLOAT", "MPI_SUM", 70001, False),
+                               ("MPI_INT", "MPI_SUM", 100003, False), ("MPI_DOUBLE", "MPI_MAX", 3000, True),
+                               ("MPI_FLOAT", "MPI_MIN", 1100, True), ("MPI_DOUBLE_INT", "MPI_MAXLOC", 5000, False),
+                               ("MPI_UNSIGNED_CHAR", "MPI_BXOR", 4099, False), ("MPI_DOUBLE", "MPI_SUM", 300001, False),
+                               ("MPI_FLOAT", "MPI_SUM", 840 * 1000 + 5, False)):
+        cases.append({"id": f"m9{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "ties": ties})
+        seed += 1
+    for count in (600005, 3001):
+        cases.append({"id": f"m9{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
+                      "count": count, "seed": seed})
+        seed += 1
+    for count, root in ((1000, n - 1), (70001, 1)):
+        cases.append({"id": f"m9{seed}", "kind": "reduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
+    cases.append({"id": f"m9{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": 70001,
+                  "seed": seed, "root": n - 2})
+    seed += 1
+    cases.append({"id": f"m9{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": 3001,
+                  "seed": seed})
+    seed += 1
+    res = run_workers(n, cases, tmp_path, ppn=ppn)
+    nodes = n // ppn
+    for case in cases:
+        k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
+        sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+        if k in ("allreduce", "allreduce_inplace"):
+            want = expected_allreduce(sends, count, t, case["op"], ppn, in_place=k == "allreduce_inplace")
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
+        elif k == "reduce":
+            parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0],
+                                       OPS[case["op"]], 0) for j in range(nodes)]
+            want = binomial_leaders(parts, count, t, case["op"], case["root"] // ppn)
+            assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
+        elif k == "bcast":
+            want = as_bytes(inputs(case, case["root"]))
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        else:
+            want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
