@@ -458,7 +458,12 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     int rc;
     if (op.opk != OPK_USER_NONCOMM || nbc_kind() == NBC_NONE) {
         if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)t.tsize, (int)t.extent, &p, op.opk))) return rc;
-        pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
+        if (J.multi && p.algo == ALG_RS_BASIC) {  // the reduce inside is the multi-node one
+            const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
+            pvar_note_ids(chain, world().rank == 0 ? 3 : 2);
+        } else {
+            pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
+        }
         ps = p.ps;
     } else {
         ps.nprog = 1;
@@ -472,6 +477,19 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     Operands o;
     if ((rc = stage_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, (int)total, t, o))) return rc;
     const int c = counts[me];
+    if (J.multi && op.opk != OPK_USER_NONCOMM && p.algo == ALG_RS_BASIC) {
+        // MPIR_Reduce_Scatter_Basic_MV2 (red_scat_osu.c:300-413): MPIR_Reduce_MV2 to rank 0 over the
+        // whole job — the two-level reduce helper for a commutative op — then the scatter: every
+        // rank evaluates that reduce's result (a basic operand is at most a few hundred bytes)
+        MnSched sc;
+        if ((rc = mn_host_schedule(MN_COLL_REDUCE, (size_t)total, (int)t.tsize, (int)t.extent, false, op.opk, 0, &sc)))
+            return rc == E_UNSUPPORTED ? MPI_ERR_UNSUPPORTED_OPERATION : MPI_ERR_INTERN;
+        if (c == 0) return MPI_SUCCESS;
+        char *res = dev_scratch(DS_RES_ALL, (size_t)total * (size_t)t.tsize);
+        if (!res) return MPI_ERR_NO_MEM;
+        if (sc.kind != MN_TWO_LEVEL || (rc = run_two_level(o, (int)total, sc, op.fn, res))) return rc ? rc : MPI_ERR_INTERN;
+        return dtype_unpack(res + (size_t)disp * (size_t)t.tsize, c, t.dt, recvbuf);
+    }
     if (c == 0) return MPI_SUCCESS;
     HostBuf W(HS_OPERANDS), R(HS_RESULT);
     long rspan = 0;

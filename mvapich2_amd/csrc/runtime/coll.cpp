@@ -1642,7 +1642,11 @@ int mn_h2d(void *d, const void *h, size_t b) { return hipMemcpy(d, h, b, hipMemc
 // rbytes) sends and receives (either side may be empty).  Every uop(tmp, recvbuf) is one device
 // Reduce_local; builtin ops only (commutative, so recursive doubling never swaps its operands).
 struct Xport {
-    virtual int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) = 0;
+    // send sbytes of sb to `to` while receiving rbytes into rb from `from` (either side may be empty)
+    virtual int shift(int to, const char *sb, size_t sbytes, int from, char *rb, size_t rbytes) = 0;
+    int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) {
+        return shift(peer, sb, sbytes, peer, rb, rbytes);
+    }
 };
 int sched_allreduce(Xport &x, int n, int rank, char *acc, char *tmp, size_t count, size_t ext, int dtype, int op,
                     bool rd) {
@@ -1722,12 +1726,12 @@ int sched_allreduce(Xport &x, int n, int rank, char *acc, char *tmp, size_t coun
 
 // the node leaders as ranks (node index), over their TCP links, staged through g_mn.h0 / h1
 struct LeaderLinks : Xport {
-    int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) override {
+    int shift(int to, const char *sb, size_t sbytes, int from, char *rb, size_t rbytes) override {
         int rc = 0;
         if (sbytes && (rc = mn_d2h(g_mn.h0, sb, sbytes))) return rc;
-        if (sbytes && rbytes) rc = net_sendrecv(peer, g_mn.h0, sbytes, g_mn.h1, rbytes);
-        else if (sbytes) rc = net_send(peer, g_mn.h0, sbytes);
-        else if (rbytes) rc = net_recv(peer, g_mn.h1, rbytes);
+        if (sbytes && rbytes) rc = net_shift(to, g_mn.h0, sbytes, from, g_mn.h1, rbytes);
+        else if (sbytes) rc = net_send(to, g_mn.h0, sbytes);
+        else if (rbytes) rc = net_recv(from, g_mn.h1, rbytes);
         return rc || !rbytes ? rc : mn_h2d(rb, g_mn.h1, rbytes);
     }
 };
@@ -1735,15 +1739,126 @@ struct LeaderLinks : Xport {
 // every rank of the job (global rank), over the point-to-point channels in the library's
 // collective context: device IPC within a node, the rank mesh between nodes
 struct RankChannels : Xport {
-    int xchg(int peer, const char *sb, size_t sbytes, char *rb, size_t rbytes) override {
+    int shift(int to, const char *sb, size_t sbytes, int from, char *rb, size_t rbytes) override {
         unsigned long long sq = 0, rq = 0;
         int rc = 0;
-        if (rbytes && (rc = p2p_irecv(rb, rbytes, peer, kCollTagBase - 3, &rq))) return rc;
-        if (sbytes && (rc = p2p_isend(sb, sbytes, peer, kCollTagBase - 3, &sq))) return rc;
+        if (rbytes && (rc = p2p_irecv(rb, rbytes, from, kCollTagBase - 3, &rq))) return rc;
+        if (sbytes && (rc = p2p_isend(sb, sbytes, to, kCollTagBase - 3, &sq))) return rc;
         if (sbytes && (rc = mv2h_p2p_wait(sq, nullptr, nullptr, nullptr))) return rc;
         return rbytes ? mv2h_p2p_wait(rq, nullptr, nullptr, nullptr) : 0;
     }
 };
+
+// MPI_Reduce_scatter's message schedules over n ranks (commutative ops, every uop one device
+// Reduce_local of the received data `in` into this rank's accumulator `inout`).  in: this rank's
+// whole operand (device, total elements, block j at disps[j]); out: its block (cnts[rank]
+// elements, device or host); t0 / t1: device scratch of the whole operand.
+//
+// MPIR_Reduce_scatter_Rec_Halving_MV2 (red_scat_osu.c:428-780): the non-power-of-two pre-step,
+// recursive halving over pof2 merged blocks (an odd rank below 2 * rem also works its left
+// neighbour's block), the post-step returning the even ranks' blocks.
+int sched_rs_halving(Xport &x, int n, int rank, const size_t *cnts, const size_t *disps, const char *in, char *out,
+                     char *t0, char *t1, size_t ext, int dtype, int op) {
+    const size_t total = disps[n - 1] + cnts[n - 1], S = total * ext;
+    char *res = t0, *tmp = t1;  // tmp_results, tmp_recvbuf
+    if (hipMemcpy(res, in, S, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+    int pof2 = 1;
+    while (pof2 * 2 <= n) pof2 *= 2;
+    const int rem = n - pof2;
+    int rc = 0, newrank;
+    if (rank < 2 * rem) {
+        if (rank % 2 == 0) {
+            if ((rc = x.xchg(rank + 1, res, S, nullptr, 0))) return rc;
+            newrank = -1;
+        } else {
+            if ((rc = x.xchg(rank - 1, nullptr, 0, tmp, S)) ||
+                (rc = mv2h_reduce_local(tmp, res, total, dtype, op, nullptr)))
+                return rc;
+            newrank = rank / 2;
+        }
+    } else {
+        newrank = rank - rem;
+    }
+    auto real = [&](int nr) { return nr < rem ? nr * 2 + 1 : nr + rem; };
+    if (newrank != -1) {
+        std::vector<size_t> ncnt((size_t)pof2), ndisp((size_t)pof2, 0);
+        for (int i = 0; i < pof2; ++i) {
+            const int old = real(i);
+            ncnt[i] = cnts[old] + (old < 2 * rem ? cnts[old - 1] : 0);
+        }
+        for (int i = 1; i < pof2; ++i) ndisp[i] = ndisp[i - 1] + ncnt[i - 1];
+        auto span = [&](int a, int b) {
+            size_t c = 0;
+            for (int i = a; i < b; ++i) c += ncnt[i];
+            return c;
+        };
+        int send_idx = 0, recv_idx = 0, last_idx = pof2;
+        for (int mask = pof2 >> 1; mask > 0; mask >>= 1) {
+            const int newdst = newrank ^ mask;
+            size_t scnt, rcnt;
+            if (newrank < newdst) {
+                send_idx = recv_idx + mask;
+                scnt = span(send_idx, last_idx);
+                rcnt = span(recv_idx, send_idx);
+            } else {
+                recv_idx = send_idx + mask;
+                scnt = span(send_idx, recv_idx);
+                rcnt = span(recv_idx, last_idx);
+            }
+            const size_t so = ndisp[send_idx] * ext, ro = ndisp[recv_idx] * ext;
+            if ((rc = x.xchg(real(newdst), res + so, scnt * ext, tmp + ro, rcnt * ext))) return rc;
+            if (rcnt && (rc = mv2h_reduce_local(tmp + ro, res + ro, rcnt, dtype, op, nullptr))) return rc;
+            send_idx = recv_idx;
+            last_idx = recv_idx + mask;
+        }
+        if (cnts[rank] &&
+            hipMemcpy(out, res + disps[rank] * ext, cnts[rank] * ext, hipMemcpyDefault) != hipSuccess)
+            return E_INTERN;
+    }
+    if (rank < 2 * rem) {
+        if (rank % 2) rc = x.xchg(rank - 1, res + disps[rank - 1] * ext, cnts[rank - 1] * ext, nullptr, 0);
+        else if (is_device(out)) rc = x.xchg(rank + 1, nullptr, 0, out, cnts[rank] * ext);
+        else if (!(rc = x.xchg(rank + 1, nullptr, 0, tmp, cnts[rank] * ext)) && cnts[rank])
+            rc = hipMemcpy(out, tmp, cnts[rank] * ext, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+    }
+    return rc;
+}
+
+// MPIR_Reduce_scatter_Pair_Wise_MV2 (:786-1020): this rank's block starts as its own data; step i
+// sends block (rank + i) to that rank and reduces the block received from rank - i into it
+int sched_rs_pairwise(Xport &x, int n, int rank, const size_t *cnts, const size_t *disps, const char *in, char *out,
+                      char *t0, char *t1, size_t ext, int dtype, int op) {
+    const size_t B = cnts[rank] * ext;
+    if (B && hipMemcpy(t0, in + disps[rank] * ext, B, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+    int rc = 0;
+    for (int i = 1; i < n; ++i) {
+        const int src = (rank - i + n) % n, dst = (rank + i) % n;
+        if ((rc = x.shift(dst, in + disps[dst] * ext, cnts[dst] * ext, src, t1, B))) return rc;
+        if (B && (rc = mv2h_reduce_local(t1, t0, cnts[rank], dtype, op, nullptr))) return rc;
+    }
+    return !B || hipMemcpy(out, t0, B, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+}
+
+// MPIR_Reduce_scatter_ring(_2lvl) (:1026-1180, :1190-1300; its 1 MiB chunking does not change an
+// element's order): at distance d this rank sends block (rank + d) to the right, having reduced the
+// partial received from the left into its own data of that block
+int sched_rs_ring(Xport &x, int n, int rank, const size_t *cnts, const size_t *disps, const char *in, char *out,
+                  char *t0, char *t1, size_t ext, int dtype, int op) {
+    const int right = (rank + 1) % n, left = (rank - 1 + n) % n;
+    int rc = 0;
+    for (int dist = n - 1; dist >= 0; --dist) {
+        const int sr = (rank + dist) % n, rr = (rank + dist - 1 + n) % n;
+        const size_t sc = cnts[sr];
+        if (sc && hipMemcpy(t0, in + disps[sr] * ext, sc * ext, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+        if (dist < n - 1 && sc && (rc = mv2h_reduce_local(t1, t0, sc, dtype, op, nullptr))) return rc;
+        if (dist > 0) {
+            if ((rc = x.shift(right, t0, sc * ext, left, t1, cnts[rr] * ext))) return rc;
+        } else if (sc && hipMemcpy(out, t0, sc * ext, hipMemcpyDefault) != hipSuccess) {
+            return E_INTERN;
+        }
+    }
+    return 0;
+}
 
 // leaders: recursive doubling on `acc` (device, `count` elements) with the nodes as ranks
 int leader_rd(char *acc, size_t count, int dtype, int op, size_t bytes) {
@@ -2200,8 +2315,9 @@ static int mn_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *
 // non-commutative forms for non-commutative ops; MPI_Ireduce_scatter: pairwise).  Every operand
 // reaches every rank (mn_gather_all) and each rank evaluates its own block's programs of the
 // selected algorithm over the job's ranks (orders.cpp plan_reduce_scatter, the same restatement as
-// on one node).  Jobs above kMaxRanks ranks: the two-level allreduce of the whole operand, then the
-// block (integer, logical, bitwise and LOC results exact; the fp order not restated).
+// on one node).  Jobs above kMaxRanks ranks: the algorithm's message schedule itself
+// (sched_rs_halving / _pairwise / _ring over the rank channels).  The basic algorithm at any size
+// is MPIR_Reduce_MV2 over the whole job (the multi-node reduce) and a scatter.
 static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
                              void *stream) {
     World &w = world();
@@ -2217,14 +2333,40 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
     const size_t ext = (size_t)dt->extent, S = total * ext;
     const bool in_place = sendbuf == (const void *)-1;
     const void *src = in_place ? recvbuf : sendbuf;
-    if (w.gsize > kMaxRanks) {
+    const int n = w.gsize, me = w.grank, oi = op_index(op);
+    const size_t mine = recvcounts[me] * ext;
+    if (oi == OP_NO_OP || oi == OP_REPLACE) {  // nothing to reduce: this rank's own block
+        return !mine || hipMemcpy(recvbuf, (const char *)src + off * ext, mine, hipMemcpyDefault) == hipSuccess
+                   ? 0 : E_INTERN;
+    }
+    const int algo = reduce_scatter_algo(n, (long)(total * (size_t)dt->size));
+    if (algo == ALG_RS_BASIC) {
+        // MPIR_Reduce_Scatter_Basic_MV2 (red_scat_osu.c:300-413): MPIR_Reduce_MV2 to rank 0 over
+        // the whole communicator — the multi-node reduce (mn_reduce) — then the blocks scattered
+        const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
+        pvar_note_ids(chain, w.rank == 0 ? 3 : 2);
         char *tmp = (char *)get_scratch(5, S);
         if (!tmp) return E_NO_MEM;
-        if ((rc = mn_allreduce(src, tmp, total, dtype, op, stream))) return rc;
-        if (recvcounts[w.grank])
-            rc = hipMemcpy(recvbuf, tmp + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess
-                     ? 0 : E_INTERN;
-        return rc;
+        if ((rc = mn_reduce(src, tmp, total, dtype, op, 0, stream)) || (rc = mn_bcast(tmp, S, 0, stream))) return rc;
+        return !mine || hipMemcpy(recvbuf, tmp + off * ext, mine, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+    }
+    if (n > kMaxRanks) {
+        // beyond the programs' registers: the algorithm's message schedule over the rank channels
+        const int id = algo == ALG_RS_RING ? PV_RS_RING : algo == ALG_RS_PAIRWISE ? PV_RS_PAIRWISE : PV_RS_REC_HALVING;
+        pvar_note_ids(&id, 1);
+        std::vector<size_t> disps((size_t)n, 0);
+        for (int j = 1; j < n; ++j) disps[j] = disps[j - 1] + recvcounts[j - 1];
+        if ((rc = mn_reserve_dev(S))) return rc;
+        const char *in = (const char *)src;
+        if (!is_device(src)) {  // a host operand: staged to the device once
+            char *stage = (char *)get_scratch(5, S);
+            if (!stage || hipMemcpy(stage, src, S, hipMemcpyDefault) != hipSuccess) return stage ? E_INTERN : E_NO_MEM;
+            in = stage;
+        }
+        // (MPI_IN_PLACE needs no copy: every schedule writes this rank's block after its last read)
+        RankChannels x;
+        auto fn = algo == ALG_RS_RING ? sched_rs_ring : algo == ALG_RS_PAIRWISE ? sched_rs_pairwise : sched_rs_halving;
+        return fn(x, n, me, recvcounts, disps.data(), in, (char *)recvbuf, g_mn.d0, g_mn.d1, ext, dtype, op);
     }
     Plan p;
     if ((rc = plan_reduce_scatter(w.gsize, w.grank, recvcounts, dt->size, dt->extent, &p))) return rc;
@@ -2235,10 +2377,6 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
     if (!recvcounts[w.grank]) return 0;
     const void *srcs[kMaxRanks];
     for (int r = 0; r < w.gsize; ++r) srcs[r] = W + (size_t)r * S;
-    if (p.algo == ALG_NONE) {  // REPLACE / NO_OP: nothing to reduce
-        return hipMemcpy(recvbuf, (const char *)srcs[w.grank] + off * ext, recvcounts[w.grank] * ext,
-                         hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
-    }
     if ((rc = mv2h_reduce_n_prog(srcs, w.gsize, g_mn.d1, total, dtype, op, (const mv2h_progset *)&p.ps, nullptr)))
         return rc;
     return hipMemcpy(recvbuf, g_mn.d1 + off * ext, recvcounts[w.grank] * ext, hipMemcpyDefault) == hipSuccess

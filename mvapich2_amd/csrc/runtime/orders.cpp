@@ -21,6 +21,7 @@ namespace mv2 {
 // knobs
 // ---------------------------------------------------------------------------
 static Knobs g_knobs;
+static thread_local int t_nbc = NBC_NONE;  // nonblocking initiation in progress (nbc_set)
 static bool g_knobs_ok = false;
 static uint64_t g_knobs_gen = 0;  // bumped by knobs_reload / topo_set: invalidates cached plans
 static Topo g_topo{};
@@ -855,6 +856,35 @@ int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) 
 // ---------------------------------------------------------------------------
 // MPI_Reduce_scatter (commutative ops; red_scat_osu.c:1859-1896)
 // ---------------------------------------------------------------------------
+// MPIR_Reduce_scatter_MV2's choice for a commutative op over n ranks (red_scat_osu.c:1859-1893): the
+// ring from MV2_RED_SCAT_RING_ALGO_THRESHOLD (for node-major ranks the cyclic-hostfile test never
+// holds), else the default table (red_scat_tuning.c:214-287), its entry the first numproc >= n (the
+// last beyond), the function the first whose max >= nbytes.  MPIR_Reduce_scatter_ring_2lvl runs the
+// plain ring's order for the identity rank list (:1190-1300 against :1026-1180).
+int reduce_scatter_table(int n, long nbytes) {
+    if (knobs().red_scat_ring_thr <= nbytes) return ALG_RS_RING;
+    static const struct {
+        int numproc;
+        long basic, halving, pairwise;  // inclusive upper bounds; the ring beyond
+    } tab[] = {{8, 256, 16384, 65536},   {16, 64, 65536, 65536},   {32, 64, 131072, 131072},
+               {64, 1024, 262144, 262144}, {128, 128, 65536, 65536}, {256, 128, 65536, 65536},
+               {512, 256, 65536, 65536}};
+    const int last = (int)(sizeof(tab) / sizeof(tab[0])) - 1;
+    int r = 0;
+    while (r < last && n > tab[r].numproc) ++r;
+    if (nbytes <= tab[r].basic) return ALG_RS_BASIC;
+    if (nbytes <= tab[r].halving) return ALG_RS_REC_HALVING;
+    if (nbytes <= tab[r].pairwise) return ALG_RS_PAIRWISE;
+    return ALG_RS_RING;
+}
+
+int reduce_scatter_algo(int n, long nbytes) {
+    if (t_nbc == NBC_IREDUCE_SCATTER) return ALG_RS_PAIRWISE;
+    if (t_nbc == NBC_IREDUCE_SCATTER_BLOCK)
+        return nbytes < knobs().redscat_comm_long ? ALG_RS_REC_HALVING : ALG_RS_PAIRWISE;
+    return reduce_scatter_table(n, nbytes);
+}
+
 static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int tsize, int textent, Plan *p,
                                      int opk) {
     memset(p, 0, sizeof(*p));
@@ -879,15 +909,7 @@ static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int ts
         }
         return single_expr(s, e, p->ps) ? 0 : E_INTERN;
     }
-    const Knobs &K = knobs();
-    const long nbytes = (long)total * tsize;
-    // default table (red_scat_tuning.c:214-287), first entry (numproc 8) for n <= 8
-    int algo;
-    if (K.red_scat_ring_thr <= nbytes) algo = ALG_RS_RING;
-    else if (nbytes <= 256) algo = ALG_RS_BASIC;
-    else if (nbytes <= 16384) algo = ALG_RS_REC_HALVING;
-    else if (nbytes <= 65536) algo = ALG_RS_PAIRWISE;
-    else algo = ALG_RS_RING;
+    const int algo = reduce_scatter_table(n, (long)total * tsize);
     p->algo = algo;
     Sym s;
     switch (algo) {
@@ -916,7 +938,6 @@ static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int ts
 // Nonblocking collectives (one node, <= 8 ranks: the first row of each default
 // nonblocking table, i.e. the unlisted-architecture "RI" tables)
 // ---------------------------------------------------------------------------
-static thread_local int t_nbc = NBC_NONE;
 void nbc_set(int kind) { t_nbc = kind; }
 int nbc_kind() { return t_nbc; }
 

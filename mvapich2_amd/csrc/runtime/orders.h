@@ -140,6 +140,11 @@ int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, P
 // MPIR_Reduce_binomial_MV2 (reduce_osu.c:425) to `root`, whatever the selection (the leaders' step
 // of MPIR_Reduce_two_level_helper_MV2 across nodes)
 int plan_binomial(int n, int root, Plan *out, bool noncomm = false);
+// MPI_Reduce_scatter's algorithm for a commutative op over n ranks and nbytes in all (ALG_RS_*):
+// reduce_scatter_table = the blocking selection, reduce_scatter_algo = the one of the call being
+// initiated (nonblocking schedules while nbc_set names one)
+int reduce_scatter_table(int n, long nbytes);
+int reduce_scatter_algo(int n, long nbytes);
 // counts[n] per-rank block counts; elements are indexed over the whole operand
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *out,
                         int opk = OPK_BUILTIN);

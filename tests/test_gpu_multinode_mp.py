@@ -151,6 +151,38 @@ def expected_allreduce(sends, count, t, op, ppn, in_place=False):
     return two_level(sends, count, t, op, ppn)
 
 
+# MPIR_Reduce_scatter_MV2's default table (red_scat_tuning.c:214-287): numproc, then the inclusive
+# upper bounds of basic / recursive halving / pairwise; the ring beyond, and from
+# MV2_RED_SCAT_RING_ALGO_THRESHOLD (131072 B) whatever the entry (red_scat_osu.c:1859-1871)
+_RS_TABLE = [(8, 256, 16384, 65536), (16, 64, 65536, 65536), (32, 64, 131072, 131072), (64, 1024, 262144, 262144)]
+
+
+def rs_algo(n, nbytes, via=None):
+    if via == "inb":  # MPI_Ireduce_scatter: MPIR_Ireduce_scatter_pairwise
+        return "rs_pairwise"
+    if via in ("block", "iblock"):  # MPICH's MPIR_(I)reduce_scatter_block_intra (ired_scat_block.c:882-920)
+        return "rs_rec_halving" if nbytes < 524288 else "rs_pairwise"
+    if nbytes >= 131072:
+        return "rs_ring"
+    row = next((r for r in _RS_TABLE if n <= r[0]), _RS_TABLE[-1])
+    return "rs_basic" if nbytes <= row[1] else "rs_rec_halving" if nbytes <= row[2] else \
+        "rs_pairwise" if nbytes <= row[3] else "rs_ring"
+
+
+def expected_reduce_scatter(sends, counts, t, op, ppn, via=None):
+    """every rank's block of MPI_Reduce_scatter across nodes, concatenated: the algorithm of the
+    table over every rank; basic = MPIR_Reduce_MV2 to rank 0 over the whole job (the two-level
+    helper: each node's reduce to its local rank 0, binomial over the leaders) + scatter"""
+    n, total = len(sends), sum(counts)
+    algo = rs_algo(n, total * TYPES[t][2], via)
+    if algo == "rs_basic":
+        parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], total, TYPES[t][0], OPS[op], 0)
+                 for j in range(n // ppn)]
+        return binomial_leaders(parts, total, t, op, 0)
+    return oracle.reduce_scatter_ref([x.copy() for x in sends], counts, TYPES[t][0], OPS[op],
+                                     algo=oracle.ALGOS.index(algo))
+
+
 def node_step(xs, count, t, op, intra, knobs=None):
     """the leader's partial after a two-level entry's intra-node function over the node's ranks
     (MPIR_Allreduce_two_level_MV2 :1727-1745)"""
@@ -282,8 +314,7 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
         elif k == "reduce_scatter":  # MPIR_Reduce_scatter_MV2 flat over every rank
             counts = case["recvcounts"]
-            algo = oracle.ALGOS.index("rs_pairwise") if case.get("via") == "inb" else -1
-            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]], algo=algo)
+            full = expected_reduce_scatter(sends, counts, t, case["op"], ppn, case.get("via"))
             ext = TYPES[t][3]
             off = 0
             for r in range(n):
@@ -402,9 +433,17 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
             assert np.array_equal(res(cid, root).view(np.int32), want), (cid, root)
         else:
             counts = case["recvcounts"]
-            xs = [((np.arange(sum(counts)) + r) % 7).astype(np.int32) for r in range(n)]
-            want = ref_user.reduce_scatter(xs, _ufn, TYPES["MPI_INT"][0], counts) if commute else \
-                ref_user.reduce_scatter_noncomm(xs, _ufn, counts)
+            total = sum(counts)
+            xs = [((np.arange(total) + r) % 7).astype(np.int32) for r in range(n)]
+            if commute and rs_algo(n, total * 4) == "rs_basic":  # the multi-node reduce to 0 + scatter
+                parts = [ref_user.reduce(xs[j * ppn:(j + 1) * ppn], _ufn, True, TYPES["MPI_INT"][0], total, 0)
+                         for j in range(n // ppn)] if ppn > 1 else xs
+                full = ref_user.binomial(parts, _ufn, 0, True)
+                offs = np.cumsum([0] + counts)
+                want = [full[offs[r]:offs[r + 1]] for r in range(n)]
+            else:
+                want = ref_user.reduce_scatter(xs, _ufn, TYPES["MPI_INT"][0], counts) if commute else \
+                    ref_user.reduce_scatter_noncomm(xs, _ufn, counts)
             for r in range(n):
                 assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
 
@@ -486,7 +525,8 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
     pt2pt_rd the tables name over every rank, and the ring wrapper's pt2pt_rs remainder, run as
     the reference's message schedule over the point-to-point channels (coll.cpp sched_allreduce,
     RankChannels); the small-message shortcut's recursive doubling over more than 8 node leaders
-    (LeaderLinks); the tables' numproc 8 / 16 entries (10 and 12 ranks: comm_size_index of 8)."""
+    (LeaderLinks); the tables' numproc 8 / 16 entries (10 and 12 ranks: comm_size_index of 8);
+    MPI_Reduce_scatter's schedules over every rank (sched_rs_halving / _pairwise / _ring)."""
     cases, seed = [], 1300
     for t, op, count, ties in (("MPI_FLOAT", "MPI_SUM", 10, False), ("MPI_FLOAT", "MPI_SUM", 300, False),
                                ("MPI_FLOAT", "MPI_SUM", 700, False), ("MPI_FLOAT", "MPI_SUM", 1500, False),
@@ -512,6 +552,25 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
     cases.append({"id": f"m9{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": 3001,
                   "seed": seed})
     seed += 1
+    # reduce-scatter over every rank as message schedules: basic (<= 64 B at 9-16 ranks: the
+    # multi-node reduce + scatter), recursive halving (to 64 KiB), the ring, MPI_Ireduce_scatter's
+    # pairwise; ragged counts with empty blocks; signed zeros / NaN payloads under MAX
+    for t, op, counts, via, ties in (
+            ("MPI_FLOAT", "MPI_SUM", [1] * n, None, False),
+            ("MPI_FLOAT", "MPI_SUM", [100 + r for r in range(n)], None, False),
+            ("MPI_DOUBLE", "MPI_MAX", [300 + (r % 3) for r in range(n)], None, True),
+            ("MPI_FLOAT", "MPI_SUM", [0 if r % 3 == 0 else 500 + r for r in range(n)], None, False),
+            ("MPI_FLOAT", "MPI_SUM", [12000 + r for r in range(n)], None, False),
+            ("MPI_INT", "MPI_SUM", [0 if r % 2 else 9000 for r in range(n)], None, False),
+            ("MPI_FLOAT", "MPI_SUM", [700 + r for r in range(n)], "inb", False),
+            ("MPI_FLOAT", "MPI_SUM", [500] * n, "block", False),
+            ("MPI_FLOAT", "MPI_SUM", [12000] * n, "iblock", False)):
+        case = {"id": f"m9{seed}", "kind": "reduce_scatter", "type": t, "op": op, "recvcounts": counts,
+                "count": sum(counts), "seed": seed, "ties": ties}
+        if via:
+            case["via"] = via
+        cases.append(case)
+        seed += 1
     res = run_workers(n, cases, tmp_path, ppn=ppn)
     nodes = n // ppn
     for case in cases:
@@ -530,6 +589,12 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
             want = as_bytes(inputs(case, case["root"]))
             for r in range(n):
                 assert np.array_equal(res(cid, r), want), (cid, r)
+        elif k == "reduce_scatter":
+            counts, ext = case["recvcounts"], TYPES[t][3]
+            full = expected_reduce_scatter(sends, counts, t, case["op"], ppn, case.get("via"))
+            offs = np.cumsum([0] + counts) * ext
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), full[offs[r]:offs[r + 1]], t, counts[r], f"{cid} reduce_scatter rank {r}")
         else:
             want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
             for r in range(n):
