@@ -1648,27 +1648,32 @@ struct Xport {
         return shift(peer, sb, sbytes, peer, rb, rbytes);
     }
 };
+// redscat: the pre-step of MPIR_Reduce_redscat_gather_MV2 (reduce_osu.c:849-894) instead — the odd
+// ranks below 2 * rem hand their operand to rank - 1 — with the allgather standing for its gather
+// to the root and the broadcast after it (MPI_Iallreduce's naive schedule moves the blocks only).
 int sched_allreduce(Xport &x, int n, int rank, char *acc, char *tmp, size_t count, size_t ext, int dtype, int op,
-                    bool rd) {
+                    bool rd, bool redscat = false) {
     int pof2 = 1;
     while (pof2 * 2 <= n) pof2 *= 2;
     const int rem = n - pof2;
     const size_t S = count * ext;
     int rc = 0, newrank;
     auto uop = [&](size_t off, size_t cnt) { return mv2h_reduce_local(tmp + off, acc + off, cnt, dtype, op, nullptr); };
-    // non-power-of-two pre-step: even ranks below 2 * rem hand their operand to rank + 1
+    // non-power-of-two pre-step: even ranks below 2 * rem hand their operand to rank + 1 (redscat:
+    // the odd ones to rank - 1)
+    const int hand = redscat ? 1 : 0, keep = 1 - hand;
     if (rank < 2 * rem) {
-        if (rank % 2 == 0) {
-            if ((rc = x.xchg(rank + 1, acc, S, nullptr, 0))) return rc;
+        if (rank % 2 == hand) {
+            if ((rc = x.xchg(hand ? rank - 1 : rank + 1, acc, S, nullptr, 0))) return rc;
             newrank = -1;
         } else {
-            if ((rc = x.xchg(rank - 1, nullptr, 0, tmp, S)) || (rc = uop(0, count))) return rc;
+            if ((rc = x.xchg(hand ? rank + 1 : rank - 1, nullptr, 0, tmp, S)) || (rc = uop(0, count))) return rc;
             newrank = rank / 2;
         }
     } else {
         newrank = rank - rem;
     }
-    auto real = [&](int nr) { return nr < rem ? nr * 2 + 1 : nr + rem; };
+    auto real = [&](int nr) { return nr < rem ? nr * 2 + keep : nr + rem; };
     if (newrank != -1 && (rd || count < (size_t)pof2)) {
         for (int mask = 1; mask < pof2; mask <<= 1) {
             if ((rc = x.xchg(real(newrank ^ mask), acc, S, tmp, S)) || (rc = uop(0, count))) return rc;
@@ -1719,9 +1724,30 @@ int sched_allreduce(Xport &x, int n, int rank, char *acc, char *tmp, size_t coun
             if (newrank > newdst) send_idx = recv_idx;
         }
     }
-    // post-step: the odd ranks below 2 * rem return the result to rank - 1
-    if (rank < 2 * rem) rc = rank % 2 ? x.xchg(rank - 1, acc, S, nullptr, 0) : x.xchg(rank + 1, nullptr, 0, acc, S);
+    // post-step: the ranks that kept their place below 2 * rem return the result to the others
+    if (rank < 2 * rem) {
+        const int peer = rank % 2 ? rank - 1 : rank + 1;
+        rc = rank % 2 == keep ? x.xchg(peer, acc, S, nullptr, 0) : x.xchg(peer, nullptr, 0, acc, S);
+    }
     return rc;
+}
+
+// MPIR_Reduce_binomial_MV2's commutative schedule (reduce_osu.c:577-663; MPIR_Ireduce_binomial
+// reduces the same way): relative rank rel receives from rel | mask and reduces uop(tmp, acc)
+// until its bit `mask` is set, then sends its partial to rel & ~mask.  acc ends with the result
+// at the root.
+int sched_binomial_reduce(Xport &x, int n, int rank, int root, char *acc, char *tmp, size_t count, size_t ext,
+                          int dtype, int op) {
+    const int rel = (rank - root + n) % n;
+    const size_t S = count * ext;
+    int rc = 0;
+    for (int mask = 1; mask < n; mask <<= 1) {
+        if (rel & mask) return x.xchg(((rel & ~mask) + root) % n, acc, S, nullptr, 0);
+        if ((rel | mask) < n && ((rc = x.xchg(((rel | mask) + root) % n, nullptr, 0, tmp, S)) ||
+                                 (rc = mv2h_reduce_local(tmp, acc, count, dtype, op, nullptr))))
+            return rc;
+    }
+    return 0;
 }
 
 // the node leaders as ranks (node index), over their TCP links, staged through g_mn.h0 / h1
@@ -2062,6 +2088,39 @@ static int mn_sched_allreduce(const void *sendbuf, void *recvbuf, size_t count, 
     return acc == recvbuf || hipMemcpy(recvbuf, acc, S, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
 }
 
+// MVAPICH2's nonblocking schedules over more than kMaxRanks ranks, as messages: root >= 0
+// MPI_Ireduce = MPIR_Ireduce_binomial to the root (ireduce_osu.c -> ireduce_tuning.c first row);
+// root < 0 MPI_Iallreduce = MPIR_Iallreduce_naive (iallreduce.c:109-139): MPIR_Ireduce_intra to
+// rank 0 — redscat_gather for builtin ops above MPIR_CVAR_REDUCE_SHORT_MSG_SIZE with count >= pof2
+// (ireduce.c:700-731), else binomial — then MPIR_Ibcast, every rank taking rank 0's result.
+static int mn_bcast(void *buffer, size_t bytes, int root, void *stream);
+static int mn_sched_naive(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
+                          int root) {
+    World &w = world();
+    const DtypeInfo *dt = dtype_lookup(dtype);
+    const bool in_place = sendbuf == (const void *)-1;
+    const size_t ext = (size_t)dt->extent, S = count * ext;
+    const int n = w.gsize, me = w.grank;
+    int rc = mn_reserve_dev(S);
+    if (rc) return rc;
+    // the accumulator: recvbuf where it is significant and device memory, else device scratch
+    const bool mine = (root < 0 || me == root) && recvbuf && is_device(recvbuf);
+    char *acc = mine ? (char *)recvbuf : g_mn.d0;
+    const void *src = in_place ? recvbuf : sendbuf;
+    if (src != acc && hipMemcpy(acc, src, S, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+    RankChannels x;
+    int pof2 = 1;
+    while (pof2 * 2 <= n) pof2 *= 2;
+    if (root < 0 && (long)(count * (size_t)dt->size) > knobs().reduce_short_msg && count >= (size_t)pof2) {
+        rc = sched_allreduce(x, n, me, acc, g_mn.d1, count, ext, dtype, op, false, true);
+    } else {
+        rc = sched_binomial_reduce(x, n, me, root < 0 ? 0 : root, acc, g_mn.d1, count, ext, dtype, op);
+        if (!rc && root < 0) rc = mn_bcast(acc, S, 0, stream);
+    }
+    if (rc || (root >= 0 && me != root) || acc == recvbuf) return rc;
+    return hipMemcpy(recvbuf, acc, S, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+}
+
 // Flat pt2pt_rs / pt2pt_rd over every rank (allreduce_osu.c:633-1054, :360-630): every rank's operand reaches every rank
 // (node allgather into its global slot, a ring over the leaders, node broadcast), and each rank
 // evaluates the algorithm's per-element programs for its own rank — recursive doubling's results
@@ -2102,8 +2161,9 @@ static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dt
     // MPI_Iallreduce: MVAPICH2's nonblocking schedule is flat over the whole job
     // (MPIR_Iallreduce_intra_MV2 iallreduce_osu.c:257 -> MPIR_Iallreduce_naive: Ireduce to rank 0,
     // binomial or redscat_gather, then Ibcast), whatever the nodes
-    if (nbc_kind() == NBC_IALLREDUCE && gsize <= kMaxRanks)
-        return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0);
+    if (nbc_kind() == NBC_IALLREDUCE)
+        return gsize <= kMaxRanks ? mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0)
+                                  : mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, -1);
     int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD;
     const int sel = mn_select((long)(count * (size_t)dt->size), &intra, &inter);
     if (sel == 1) {
@@ -2248,8 +2308,9 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     // MPI_T: MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2039) with the leaders' binomial (:450)
     // MPI_Ireduce: MVAPICH2's nonblocking schedule (MPIR_Ireduce_binomial, ireduce_osu.c) is flat
     // over the whole job
-    if (nbc_kind() == NBC_IREDUCE && w.gsize <= kMaxRanks)
-        return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root);
+    if (nbc_kind() == NBC_IREDUCE)
+        return w.gsize <= kMaxRanks ? mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root)
+                                    : mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, root);
     const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
     pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
     if ((rc = mn_reserve_dev(bytes)) || (w.rank == 0 && (rc = mn_reserve_host(bytes)))) return rc;

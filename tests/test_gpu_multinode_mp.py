@@ -295,7 +295,7 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
         sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
-        if k == "iallreduce" and n <= 8:
+        if k == "iallreduce":
             want = oracle.iallreduce_ref(sends, count, TYPES[t][0], OPS[case["op"]])
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} iallreduce rank {r}")
@@ -526,7 +526,8 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
     the reference's message schedule over the point-to-point channels (coll.cpp sched_allreduce,
     RankChannels); the small-message shortcut's recursive doubling over more than 8 node leaders
     (LeaderLinks); the tables' numproc 8 / 16 entries (10 and 12 ranks: comm_size_index of 8);
-    MPI_Reduce_scatter's schedules over every rank (sched_rs_halving / _pairwise / _ring)."""
+    MPI_Reduce_scatter's schedules over every rank (sched_rs_halving / _pairwise / _ring); the
+    nonblocking Iallreduce / Ireduce schedules flat over every rank (mn_sched_naive)."""
     cases, seed = [], 1300
     for t, op, count, ties in (("MPI_FLOAT", "MPI_SUM", 10, False), ("MPI_FLOAT", "MPI_SUM", 300, False),
                                ("MPI_FLOAT", "MPI_SUM", 700, False), ("MPI_FLOAT", "MPI_SUM", 1500, False),
@@ -552,6 +553,18 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
     cases.append({"id": f"m9{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": 3001,
                   "seed": seed})
     seed += 1
+    # the nonblocking schedules, flat over the job: Iallreduce = Ireduce to 0 (redscat_gather above
+    # 2 KiB with count >= pof2, else binomial) + Ibcast; Ireduce = binomial
+    for t, op, count, ties in (("MPI_INT", "MPI_SUM", 5000, False), ("MPI_FLOAT", "MPI_SUM", 5000, False),
+                               ("MPI_FLOAT", "MPI_SUM", 70001, False), ("MPI_DOUBLE", "MPI_SUM", 30, False),
+                               ("MPI_DOUBLE", "MPI_MAX", 3000, True)):
+        cases.append({"id": f"m9{seed}", "kind": "iallreduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "ties": ties})
+        seed += 1
+    for count, root in ((1000, n - 1), (70001, 1), (7, 0)):
+        cases.append({"id": f"m9{seed}", "kind": "ireduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
     # reduce-scatter over every rank as message schedules: basic (<= 64 B at 9-16 ranks: the
     # multi-node reduce + scatter), recursive halving (to 64 KiB), the ring, MPI_Ireduce_scatter's
     # pairwise; ragged counts with empty blocks; signed zeros / NaN payloads under MAX
@@ -580,6 +593,13 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
             want = expected_allreduce(sends, count, t, case["op"], ppn, in_place=k == "allreduce_inplace")
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
+        elif k == "iallreduce":
+            want = oracle.iallreduce_ref(sends, count, TYPES[t][0], OPS[case["op"]])
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} iallreduce rank {r}")
+        elif k == "ireduce":
+            want = oracle.ireduce_ref(sends, count, TYPES[t][0], OPS[case["op"]], case["root"])
+            assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} ireduce root {case['root']}")
         elif k == "reduce":
             parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0],
                                        OPS[case["op"]], 0) for j in range(nodes)]
