@@ -2509,12 +2509,10 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         pvar_note(PV_COLL_ALLREDUCE, s->p, in_place, count, n);
         return 0;
     }
-    // two-level (also the fall-back of a flat choice over more than kMaxRanks ranks)
+    // a flat choice over more than kMaxRanks ranks: no program registers for it (the device path
+    // runs its message schedule; host-evaluated ops are refused rather than reordered)
+    if (sel != 0) return E_UNSUPPORTED;
     s->kind = MN_TWO_LEVEL;
-    if (sel != 0) {
-        intra = MN_INTRA_NODE;
-        inter = ALG_PT2PT_RD;
-    }
     const int chain[2] = {PV_AR_2LVL, inter == ALG_PT2PT_RS ? PV_AR_SHM_RS : PV_AR_SHM_RD};
     pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
     if (K > kMaxRanks) return E_UNSUPPORTED;
