@@ -332,7 +332,7 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n,ppn", [(6, 3), (8, 4), (4, 2)])
+@pytest.mark.parametrize("n,ppn", [(6, 3), (8, 4), (4, 2), (8, 2)])
 def test_two_level_table_entries_across_nodes(n, ppn, tmp_path):
     """With the small-message shortcuts off (MV2_ENABLE_TOPO_AWARE_COLLECTIVES=0,
     MV2_ENABLE_SKIP_TUNING_TABLE_SEARCH=0) small allreduces read the tables' two-level entries: at
@@ -344,7 +344,9 @@ def test_two_level_table_entries_across_nodes(n, ppn, tmp_path):
     cases, seed = [], 900
     for t, op, count, ties in (("MPI_FLOAT", "MPI_SUM", 100, False), ("MPI_DOUBLE", "MPI_MAX", 50, True),
                                ("MPI_FLOAT", "MPI_SUM", 60, False), ("MPI_FLOAT", "MPI_MIN", 60, True),
-                               ("MPI_INT", "MPI_SUM", 3, False), ("MPI_DOUBLE", "MPI_MAX", 1, True)):
+                               ("MPI_INT", "MPI_SUM", 3, False), ("MPI_DOUBLE", "MPI_MAX", 1, True),
+                               # 64-127 B: the 2-ppn numproc 8 entry's intra function is pt2pt_rs
+                               ("MPI_FLOAT", "MPI_MIN", 20, True), ("MPI_FLOAT", "MPI_SUM", 31, False)):
         cases.append({"id": f"mk{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed,
                       "ties": ties})
         seed += 1
