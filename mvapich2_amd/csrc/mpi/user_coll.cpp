@@ -267,6 +267,141 @@ int eval_into(const ProgSet &ps, long pbase, char *W, long rspan, long b, long e
     return 0;
 }
 
+// ---- more ranks (or leaders) than a program holds: the message schedules restated on the host ----
+// W holds `n` operands in the type's layout, rspan bytes apart, cnt elements each; every function
+// writes one rank's result (type layout, rspan bytes) to out and leaves W unchanged.
+struct BigEval {
+    const char *W;
+    long rspan;
+    int n, cnt;
+    const Typed *t;
+    MPI_User_function *fn;
+    bool comm;
+    std::vector<std::vector<char>> scratch;  // one operand-sized buffer per recursion level
+    char *level(int l) {
+        if ((int)scratch.size() <= l) scratch.resize((size_t)l + 1);
+        if (scratch[l].size() < (size_t)rspan + 1) scratch[l].resize((size_t)rspan + 1);
+        return scratch[l].data();
+    }
+    void uop(const char *in, char *inout) {
+        int c = cnt;
+        MPI_Datatype d = t->dt;
+        fn((void *)in, inout, &c, &d);
+    }
+    const char *x(int r) const { return W + (size_t)r * (size_t)rspan; }
+    void copy(char *dst, const char *src) const { memcpy(dst, src, (size_t)rspan); }
+
+    // MPIR_Allreduce_pt2pt_rd_MV2 (allreduce_osu.c:455-600; also pt2pt_rs for a user op, :802): the
+    // value newrank nr holds after `lev` doubling steps
+    void rd_value(int nr, int lev, char *out) {
+        int pof2 = 1;
+        while (pof2 * 2 <= n) pof2 *= 2;
+        const int rem = n - pof2;
+        auto real = [&](int q) { return q < rem ? q * 2 + 1 : q + rem; };
+        if (lev == 0) {
+            const int r = real(nr);
+            copy(out, x(r));
+            if (r < 2 * rem) uop(x(r - 1), out);  // the odd rank's pre-step: uop(tmp = x_{r-1}, recvbuf)
+            return;
+        }
+        const int mask = 1 << (lev - 1), pr = nr ^ mask;
+        char *other = level(lev);
+        rd_value(nr, lev - 1, out);
+        rd_value(pr, lev - 1, other);
+        if (comm || real(pr) < real(nr)) {
+            uop(other, out);  // uop(tmp_buf, recvbuf)
+        } else {
+            uop(out, other);  // uop(recvbuf, tmp_buf), then tmp_buf copied into recvbuf
+            copy(out, other);
+        }
+    }
+    // rank me's recursive-doubling result
+    void rd(int me, char *out) {
+        int pof2 = 1, lev = 0;
+        while (pof2 * 2 <= n) pof2 *= 2, ++lev;
+        const int rem = n - pof2;
+        // an even rank below 2 * rem takes rank + 1's result in the post-step
+        const int nr = me < 2 * rem ? me / 2 : me - rem;
+        rd_value(nr, lev, out);
+    }
+    // MPIR_Reduce_binomial_MV2 (reduce_osu.c:577-663): relative rank rel's value once the masks
+    // below m are done (a non-commutative op reduces towards rank 0, which forwards to the root)
+    void bin_value(int rel, int m, int lroot, int l, char *out) {
+        if (m == 1) {
+            copy(out, x((rel + lroot) % n));
+            return;
+        }
+        const int half = m / 2;
+        bin_value(rel, half, lroot, l + 1, out);
+        if ((rel | half) >= n) return;
+        char *child = level(l);
+        bin_value(rel | half, half, lroot, l + 1, child);
+        if (comm) {
+            uop(child, out);  // uop(tmp_buf, recvbuf)
+        } else {
+            uop(out, child);  // uop(recvbuf, tmp_buf), then tmp_buf copied into recvbuf
+            copy(out, child);
+        }
+    }
+    void binomial(int root, char *out) {
+        int m = 1;
+        while (m < n) m <<= 1;
+        bin_value(0, m, comm ? root : 0, 0, out);
+    }
+    // MPIR_Allreduce_pt2pt_ring_MV2's chunk c (allreduce_osu.c:3916-3968): x_c, then uop(x_{c+j},
+    // acc) for j = 1 .. n-1
+    void ring_chunk(int c, char *out) {
+        copy(out, x(c));
+        for (int j = 1; j < n; ++j) uop(x((c + j) % n), out);
+    }
+};
+
+// Big flat schedules over the job's operands (MnSched big, kind MN_FLAT); deliver: this rank
+// takes the result (MPI_Reduce: the root only)
+int run_big_flat(const Operands &o, int count, const MnSched &sc, const HostOp &op, void *recvbuf, bool deliver) {
+    const Typed &t = o.t;
+    const int n = o.n, me = job().me;
+    char *res_all = dev_scratch(DS_RES_ALL, (size_t)count * (size_t)t.tsize);
+    if (!res_all) return MPI_ERR_NO_MEM;
+    HostBuf W(HS_OPERANDS), R(HS_RESULT);
+    long rspan = 0;
+    int rc = 0;
+    auto eval = [&](long b, long e, auto &&body) -> int {
+        if (e <= b) return 0;
+        if ((rc = fetch(o, b, e, W, rspan))) return rc;
+        BigEval ev{W.data(), rspan, n, (int)(e - b), &t, op.fn, op.opk != OPK_USER_NONCOMM, {}};
+        std::vector<char> out((size_t)rspan + 1);
+        body(ev, out.data());
+        R.resize((size_t)(e - b) * (size_t)t.tsize + 1);
+        if (!R.data()) return MPI_ERR_NO_MEM;
+        return dtype_pack(out.data(), (int)(e - b), t.dt, R.data());
+    };
+    long U = 0;
+    if (sc.forced == ALG_RING) {
+        // rank r reduces ring chunk r (the reference's own split) and the chunks are allgathered
+        U = sc.U;
+        const long cc = U / n;
+        const size_t cb = (size_t)cc * (size_t)t.tsize;
+        char *res_mine = dev_scratch(DS_RES_MINE, cb);
+        if (!res_mine) return MPI_ERR_NO_MEM;
+        if ((rc = eval((long)me * cc, (long)(me + 1) * cc, [&](BigEval &ev, char *out) { ev.ring_chunk(me, out); })))
+            return rc;
+        if (cc && mv2h_memcpy_htod(res_mine, R.data(), cb)) return MPI_ERR_OTHER;
+        if ((rc = mv2h_allgather(res_mine, res_all, cb, nullptr))) return rc;
+    }
+    if (U < count) {
+        if (sc.forced == ALG_BINOMIAL && !deliver) return 0;
+        rc = eval(U, count, [&](BigEval &ev, char *out) {
+            if (sc.forced == ALG_BINOMIAL) ev.binomial(sc.root, out);
+            else ev.rd(me, out);
+        });
+        if (rc) return rc;
+        if (mv2h_memcpy_htod(res_all + (size_t)U * (size_t)t.tsize, R.data(), (size_t)(count - U) * (size_t)t.tsize))
+            return MPI_ERR_OTHER;
+    }
+    return deliver ? dtype_unpack(res_all, count, t.dt, recvbuf) : 0;
+}
+
 // A two-level schedule across nodes (MPIR_Allreduce_two_level_MV2 / the two-level reduce helper):
 // every node's partial from its ranks' operands (the node step's programs for local rank 0), then
 // the leaders' programs over the partials.  Result: packed type-map bytes of elements [0, count)
@@ -289,6 +424,12 @@ int run_two_level(const Operands &o, int count, const MnSched &sc, MPI_User_func
     }
     if (K == 1) {
         rc = dtype_pack(Pt.data(), count, t.dt, R.data());
+    } else if (sc.big) {  // more leaders than a program holds: the leaders' schedule itself
+        BigEval ev{Pt.data(), rspan, K, count, &t, fn, true, {}};
+        std::vector<char> out((size_t)rspan + 1);
+        if (sc.forced == ALG_BINOMIAL) ev.binomial(sc.root, out.data());
+        else ev.rd(w.node, out.data());
+        rc = dtype_pack(out.data(), count, t.dt, R.data());
     } else {
         rc = eval_range(sc.lead.ps, 0, Pt.data(), rspan, 0, count, t, fn, R.data());
     }
@@ -361,6 +502,7 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
             if ((rc = run_two_level(o, count, sc, op.fn, res))) return rc;
             return dtype_unpack(res, count, t.dt, recvbuf);
         }
+        if (sc.big) return run_big_flat(o, count, sc, op, recvbuf, true);
         p = sc.p;
         rem = sc.rem;
         forced = sc.forced;
@@ -420,6 +562,7 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
             if ((rc = run_two_level(o, count, sc, op.fn, res))) return rc;
             return dtype_unpack(res, count, t.dt, recvbuf);
         }
+        if (sc.big) return run_big_flat(o, count, sc, op, recvbuf, me == root);
         if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
         const Split sp{&pr.ps, count, &pr.ps, 0};
         return run_split(o, count, sp, op.fn, recvbuf, me == root);

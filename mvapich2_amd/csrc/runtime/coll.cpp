@@ -2453,18 +2453,27 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
 // pt2pt_rs or _rd / two-level with the entry's intra and inter functions).  Reduce: the flat
 // binomial for a non-commutative op (the two-level helper needs a commutative one,
 // reduce_osu.c:2628-2636) and for MPI_Ireduce, else the two-level helper (node reduce to local rank
-// 0, binomial over the leaders to the root's node).  Flat schedules need the job's ranks as
-// program registers (up to kMaxRanks).
+// 0, binomial over the leaders to the root's node).  Flat schedules take the job's ranks as
+// program registers up to kMaxRanks; above, `big` names the schedule the host evaluates itself.
 int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool in_place, int opk, int root, MnSched *s) {
     const World &w = world();
     const int n = w.gsize, me = w.grank, L = w.size, K = w.nnodes;
     memset(s, 0, sizeof(*s));
     s->kind = MN_FLAT;
+    s->coll = coll;
     s->U = 0;
+    const bool big = n > kMaxRanks;
     int rc = 0;
     if (coll == MN_COLL_REDUCE) {
         if (opk == OPK_USER_NONCOMM || nbc_kind() == NBC_IREDUCE) {
-            if (n > kMaxRanks) return E_UNSUPPORTED;
+            if (big) {  // the flat binomial (MPIR_Reduce_binomial_MV2 / MPIR_Ireduce_binomial)
+                const int id = PV_RED_BINOMIAL;
+                if (nbc_kind() == NBC_NONE) pvar_note_ids(&id, 1);
+                s->big = 1;
+                s->forced = ALG_BINOMIAL;
+                s->root = root;
+                return 0;
+            }
             rc = plan_reduce(n, me, root, count, tsize, textent, &s->p, opk);
             if (!rc) pvar_note(PV_COLL_REDUCE, s->p, in_place, count, n);
             return rc;
@@ -2473,16 +2482,55 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
         pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
         if ((rc = plan_reduce(L, 0, 0, count, tsize, textent, &s->node, opk))) return rc;
+        if (K > kMaxRanks) {
+            s->big = 1;
+            s->forced = ALG_BINOMIAL;
+            s->root = root / L;
+            return 0;
+        }
         return plan_binomial(K, root / L, &s->lead);
     }
-    if (opk == OPK_USER_NONCOMM || (nbc_kind() == NBC_IALLREDUCE && n <= kMaxRanks)) {
-        if (n > kMaxRanks) return E_UNSUPPORTED;
+    if (big && nbc_kind() == NBC_IALLREDUCE) {
+        // MPIR_Iallreduce_naive: Ireduce to rank 0 — binomial for a user op (redscat_gather needs a
+        // builtin one, ireduce.c:700-731) — and Ibcast: every rank takes rank 0's result
+        s->big = 1;
+        s->forced = ALG_BINOMIAL;
+        s->root = 0;
+        return 0;
+    }
+    if (big && opk == OPK_USER_NONCOMM) {  // every shortcut and two-level test fails: recursive doubling
+        const int id = PV_AR_SHM_RD;
+        pvar_note_ids(&id, 1);
+        s->big = 1;
+        s->forced = ALG_PT2PT_RD;
+        return 0;
+    }
+    if (opk == OPK_USER_NONCOMM || nbc_kind() == NBC_IALLREDUCE) {
         if ((rc = plan_allreduce(n, me, count, tsize, textent, in_place, 0, &s->p, opk))) return rc;
         pvar_note(PV_COLL_ALLREDUCE, s->p, in_place, count, n);
         return 0;
     }
     int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD;
     const int sel = mn_select((long)count * tsize, &intra, &inter);
+    if (big && sel != 0) {
+        // flat over more ranks than a program holds: the ring over (count / n) * n elements unless
+        // IN_PLACE or count < n, and pt2pt_rs — recursive doubling for a user op (:802) — elsewhere
+        s->big = 1;
+        s->forced = ALG_PT2PT_RD;
+        if (sel == 1 && !in_place && count >= (size_t)n) {
+            const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
+            pvar_note_ids(chain, count % (size_t)n ? 3 : 2);
+            s->forced = ALG_RING;
+            s->U = (long)(count / n) * n;
+        } else if (sel == 1) {
+            const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
+            pvar_note_ids(chain, 2);
+        } else {
+            const int id = PV_AR_SHM_RS;  // the tables' flat pt2pt_rs / _rd: recursive doubling either way
+            pvar_note_ids(&id, 1);
+        }
+        return 0;
+    }
     if (sel == 1 && n <= kMaxRanks) {  // the flat ring wrapper over every rank
         const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
         if (!in_place && count >= (size_t)n) {
@@ -2509,13 +2557,9 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         pvar_note(PV_COLL_ALLREDUCE, s->p, in_place, count, n);
         return 0;
     }
-    // a flat choice over more than kMaxRanks ranks: no program registers for it (the device path
-    // runs its message schedule; host-evaluated ops are refused rather than reordered)
-    if (sel != 0) return E_UNSUPPORTED;
     s->kind = MN_TWO_LEVEL;
     const int chain[2] = {PV_AR_2LVL, inter == ALG_PT2PT_RS ? PV_AR_SHM_RS : PV_AR_SHM_RD};
     pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
-    if (K > kMaxRanks) return E_UNSUPPORTED;
     switch (intra) {
     case MN_INTRA_P2P: rc = plan_reduce(L, 0, 0, count, tsize, textent, &s->node, opk); break;
     case MN_INTRA_SHMEM: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, ALG_SHMEM_LINEAR, &s->node, opk); break;
@@ -2524,6 +2568,11 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
     default: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, 0, &s->node, opk); break;
     }
     if (rc) return rc;
+    if (K > kMaxRanks) {  // the leaders' pt2pt_rs / _rd: recursive doubling for a user op
+        s->big = 1;
+        s->forced = ALG_PT2PT_RD;
+        return 0;
+    }
     return plan_allreduce(K, w.node, count, tsize, textent, true, inter, &s->lead, opk);
 }
 

@@ -173,13 +173,17 @@ int nbc_kind();
 // U; ranges split over the ranks when every rank's programs agree).  MN_TWO_LEVEL: `node` = the
 // node step's programs for local rank 0 over the node's ranks, `lead` = the leaders' programs over
 // the nodes' partials for the leader whose result this rank takes (its own node's, or for
-// MPI_Reduce the root's node).
+// MPI_Reduce the root's node).  big: more ranks (MN_FLAT) or nodes (MN_TWO_LEVEL's leaders) than
+// a program holds (kMaxRanks): the host evaluates the message schedule itself (mpi/user_coll.cpp):
+// forced ALG_PT2PT_RD = recursive doubling, ALG_RING = the ring over [0, U) and recursive doubling
+// on the rest, ALG_BINOMIAL = the binomial reduce to `root` (a node index for the leaders).
 enum : int { MN_FLAT = 0, MN_TWO_LEVEL = 1 };
 enum : int { MN_COLL_ALLREDUCE = 0, MN_COLL_REDUCE = 1 };
 struct MnSched {
     int kind;
     int forced;
     long U;
+    int coll, big, root, pad;
     Plan p, rem, node, lead;
 };
 int mn_host_schedule(int coll, size_t count, int tsize, int textent, bool in_place, int opk, int root, MnSched *s);

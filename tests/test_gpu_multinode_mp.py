@@ -377,6 +377,10 @@ def user_allreduce_across(xs, commute, count, ppn):
     if not commute:
         return ref_user.rd(xs, _ufn, False)
     nbytes = count * 4
+    if nbytes >= 2 << 20:  # the ring wrapper over every rank, recursive doubling on the remainder
+        main = (count // n) * n
+        rest = ref_user.rd([x[main:] for x in xs], _ufn, True)
+        return [np.concatenate([ref_user.ring_chunks(xs, _ufn, count), rest[r]]) for r in range(n)]
     if nbytes <= 2048 and ppn == 1:
         parts = [x.copy() for x in xs]
     elif nbytes <= 2048:
@@ -391,16 +395,19 @@ def user_allreduce_across(xs, commute, count, ppn):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 3), (8, 4), (3, 1)])
+@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 3), (8, 4), (3, 1), (12, 1), (10, 2)])
 def test_user_ops_across_nodes(n, ppn, tmp_path):
     """User MPI_Ops across nodes (host-evaluated, mpi/user_coll.cpp): the device path's schedule
     over the job's ranks — two-level (node step, leaders' step) or flat — with operands that travel
     packed over the leaders' links; MPI_Reduce: the two-level helper (node reduce to local rank 0,
     binomial over the leaders) for a commutative op, the flat binomial for a non-commutative one;
-    MPI_Reduce_scatter: MPIR_Reduce_scatter_MV2's flat selection (non_comm forms included)."""
+    MPI_Reduce_scatter: MPIR_Reduce_scatter_MV2's flat selection (non_comm forms included).  Above
+    8 ranks (12x1, 5x2) the host evaluates the message schedules themselves (user_coll.cpp
+    BigEval: recursive doubling, the ring's own chunk, the binomial; leaders' steps over more than
+    8 nodes); reduce-scatter there is not restated for host ops."""
     cases, seed = [], 700
     for commute in (1, 0):
-        for count in (100, 2000, 33):
+        for count in (100, 2000, 33) + ((600001,) if commute and n > 8 else ()):
             cases.append({"id": f"ua{seed}", "kind": "user_allreduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed})
             seed += 1
@@ -408,7 +415,7 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
             cases.append({"id": f"ur{seed}", "kind": "user_reduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed, "root": root})
             seed += 1
-        for per in (3, 400):
+        for per in ((3, 400) if n <= 8 else ()):
             counts = [per] * n if not commute else [per + (r % 2) for r in range(n)]
             cases.append({"id": f"us{seed}", "kind": "user_reduce_scatter", "commute": commute, "count": sum(counts),
                           "recvcounts": counts, "type": "MPI_INT", "seed": seed})
