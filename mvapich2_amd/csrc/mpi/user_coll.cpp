@@ -289,7 +289,8 @@ struct BigEval {
         fn((void *)in, inout, &c, &d);
     }
     const char *x(int r) const { return W + (size_t)r * (size_t)rspan; }
-    void copy(char *dst, const char *src) const { memcpy(dst, src, (size_t)rspan); }
+    // one operand's cnt elements (a sub-range's span, not the stride: W may start mid-operand)
+    void copy(char *dst, const char *src) const { memcpy(dst, src, (size_t)dtype_span(t->dt, cnt)); }
 
     // MPIR_Allreduce_pt2pt_rd_MV2 (allreduce_osu.c:455-600; also pt2pt_rs for a user op, :802): the
     // value newrank nr holds after `lev` doubling steps
@@ -313,6 +314,26 @@ struct BigEval {
         } else {
             uop(out, other);  // uop(recvbuf, tmp_buf), then tmp_buf copied into recvbuf
             copy(out, other);
+        }
+    }
+    // MPIR_Allreduce_pt2pt_rs_MV2's reduce-scatter + allgather (:852-1000; builtin ops, at least
+    // pof2 elements): block i of pof2 (count / pof2 elements, the last the remainder) is reduced
+    // at the newrank whose bits are i's reversed (each halving step keeps the lower half at the
+    // lower newrank), along the same doubling steps as recursive doubling at that newrank, and
+    // the allgather gives every rank every block
+    void rs(char *out) {
+        int pof2 = 1, lev = 0;
+        while (pof2 * 2 <= n) pof2 *= 2, ++lev;
+        const int whole = cnt;
+        const long per = whole / pof2;
+        for (int i = 0; i < pof2; ++i) {
+            const long b = (long)i * per, c = i < pof2 - 1 ? per : whole - per * (pof2 - 1);
+            int owner = 0;
+            for (int j = 0; j < lev; ++j) owner = (owner << 1) | ((i >> j) & 1);
+            BigEval sub{W + (size_t)b * (size_t)t->extent, rspan, n, (int)c, t, fn, comm, {}};
+            std::vector<char> part((size_t)rspan + 1);
+            sub.rd_value(owner, lev, part.data());
+            memcpy(out + (size_t)b * (size_t)t->extent, part.data(), (size_t)dtype_span(t->dt, (int)c));
         }
     }
     // rank me's recursive-doubling result
@@ -389,16 +410,30 @@ int run_big_flat(const Operands &o, int count, const MnSched &sc, const HostOp &
         if (cc && mv2h_memcpy_htod(res_mine, R.data(), cb)) return MPI_ERR_OTHER;
         if ((rc = mv2h_allgather(res_mine, res_all, cb, nullptr))) return rc;
     }
-    if (U < count) {
-        if (sc.forced == ALG_BINOMIAL && !deliver) return 0;
-        rc = eval(U, count, [&](BigEval &ev, char *out) {
-            if (sc.forced == ALG_BINOMIAL) ev.binomial(sc.root, out);
+    // pt2pt_rs on [b, e): its reduce-scatter for a builtin op over at least pof2 elements, else
+    // recursive doubling (:802)
+    int pof2 = 1;
+    while (pof2 * 2 <= n) pof2 *= 2;
+    auto segment = [&](long b, long e, int algo) -> int {
+        if (e <= b) return 0;
+        const int r = eval(b, e, [&](BigEval &ev, char *out) {
+            if (algo == ALG_BINOMIAL) ev.binomial(sc.root, out);
+            else if (algo == ALG_PT2PT_RS && op.opk == OPK_BUILTIN && e - b >= pof2) ev.rs(out);
             else ev.rd(me, out);
         });
-        if (rc) return rc;
-        if (mv2h_memcpy_htod(res_all + (size_t)U * (size_t)t.tsize, R.data(), (size_t)(count - U) * (size_t)t.tsize))
-            return MPI_ERR_OTHER;
+        if (r) return r;
+        return mv2h_memcpy_htod(res_all + (size_t)b * (size_t)t.tsize, R.data(), (size_t)(e - b) * (size_t)t.tsize)
+                   ? MPI_ERR_OTHER : 0;
+    };
+    if (sc.forced == ALG_BINOMIAL && !deliver) return 0;
+    if (sc.forced == ALG_RING) {
+        rc = segment(U, count, ALG_PT2PT_RS);  // the wrapper's pt2pt_rs on the remainder
+    } else if (sc.U > 0 && sc.U < count) {  // IN_PLACE: two pt2pt_rs calls
+        if (!(rc = segment(0, sc.U, sc.forced))) rc = segment(sc.U, count, sc.forced);
+    } else {
+        rc = segment(0, count, sc.forced);
     }
+    if (rc) return rc;
     return deliver ? dtype_unpack(res_all, count, t.dt, recvbuf) : 0;
 }
 

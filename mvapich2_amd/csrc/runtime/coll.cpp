@@ -2514,9 +2514,10 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
     const int sel = mn_select((long)count * tsize, &intra, &inter);
     if (big && sel != 0) {
         // flat over more ranks than a program holds: the ring over (count / n) * n elements unless
-        // IN_PLACE or count < n, and pt2pt_rs — recursive doubling for a user op (:802) — elsewhere
+        // IN_PLACE or count < n, then pt2pt_rs on the rest; IN_PLACE: two pt2pt_rs calls split
+        // at (count / n) * n (:4095, :3800); else the tables' pt2pt_rs / pt2pt_rd.  (pt2pt_rs is
+        // recursive doubling for a user op or fewer elements than pof2, :802.)
         s->big = 1;
-        s->forced = ALG_PT2PT_RD;
         if (sel == 1 && !in_place && count >= (size_t)n) {
             const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
             pvar_note_ids(chain, count % (size_t)n ? 3 : 2);
@@ -2525,9 +2526,13 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         } else if (sel == 1) {
             const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
             pvar_note_ids(chain, 2);
+            s->forced = ALG_PT2PT_RS;
+            s->U = in_place ? (long)(count / n) * n : 0;
+            if ((size_t)s->U == count) s->U = 0;
         } else {
-            const int id = PV_AR_SHM_RS;  // the tables' flat pt2pt_rs / _rd: recursive doubling either way
+            const int id = sel == ALG_PT2PT_RS || opk != OPK_BUILTIN ? PV_AR_SHM_RS : PV_AR_SHM_RD;
             pvar_note_ids(&id, 1);
+            s->forced = sel;
         }
         return 0;
     }

@@ -562,6 +562,17 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
     cases.append({"id": f"m9{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": 3001,
                   "seed": seed})
     seed += 1
+    # x87 long double (host-evaluated builtin ops): pt2pt_rs's reduce-scatter + allgather, the ring
+    # and its remainder, the IN_PLACE split, recursive doubling, MAX ties, the reduce
+    for kind, op, count in (("allreduce", "MPI_SUM", 100), ("allreduce", "MPI_SUM", 70001),
+                            ("allreduce", "MPI_MAX", 1000), ("allreduce", "MPI_SUM", 140005),
+                            ("allreduce_inplace", "MPI_SUM", 140005), ("allreduce", "MPI_SUM", 9)):
+        cases.append({"id": f"m9{seed}", "kind": kind, "type": "MPI_LONG_DOUBLE", "op": op, "count": count,
+                      "seed": seed})
+        seed += 1
+    cases.append({"id": f"m9{seed}", "kind": "reduce", "type": "MPI_LONG_DOUBLE", "op": "MPI_SUM", "count": 3001,
+                  "seed": seed, "root": n - 1})
+    seed += 1
     # the nonblocking schedules, flat over the job: Iallreduce = Ireduce to 0 (redscat_gather above
     # 2 KiB with count >= pof2, else binomial) + Ibcast; Ireduce = binomial
     for t, op, count, ties in (("MPI_INT", "MPI_SUM", 5000, False), ("MPI_FLOAT", "MPI_SUM", 5000, False),
