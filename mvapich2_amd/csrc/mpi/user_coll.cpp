@@ -292,19 +292,26 @@ struct BigEval {
     // one operand's cnt elements (a sub-range's span, not the stride: W may start mid-operand)
     void copy(char *dst, const char *src) const { memcpy(dst, src, (size_t)dtype_span(t->dt, cnt)); }
 
+    int pof2() const {
+        int p = 1;
+        while (p * 2 <= n) p *= 2;
+        return p;
+    }
+    int real(int q) const {
+        const int rem = n - pof2();
+        return q < rem ? q * 2 + 1 : q + rem;
+    }
+    // the non-power-of-two pre-step: newrank nr's starting value (an odd rank below 2 * rem has
+    // reduced uop(tmp = x_{r-1}, recvbuf))
+    void base(int nr, char *out) {
+        const int r = real(nr);
+        copy(out, x(r));
+        if (r < 2 * (n - pof2())) uop(x(r - 1), out);
+    }
     // MPIR_Allreduce_pt2pt_rd_MV2 (allreduce_osu.c:455-600; also pt2pt_rs for a user op, :802): the
     // value newrank nr holds after `lev` doubling steps
     void rd_value(int nr, int lev, char *out) {
-        int pof2 = 1;
-        while (pof2 * 2 <= n) pof2 *= 2;
-        const int rem = n - pof2;
-        auto real = [&](int q) { return q < rem ? q * 2 + 1 : q + rem; };
-        if (lev == 0) {
-            const int r = real(nr);
-            copy(out, x(r));
-            if (r < 2 * rem) uop(x(r - 1), out);  // the odd rank's pre-step: uop(tmp = x_{r-1}, recvbuf)
-            return;
-        }
+        if (lev == 0) return base(nr, out);
         const int mask = 1 << (lev - 1), pr = nr ^ mask;
         char *other = level(lev);
         rd_value(nr, lev - 1, out);
@@ -344,6 +351,41 @@ struct BigEval {
         // an even rank below 2 * rem takes rank + 1's result in the post-step
         const int nr = me < 2 * rem ? me / 2 : me - rem;
         rd_value(nr, lev, out);
+    }
+    // MPI_Reduce_scatter, this rank's block (W holds its elements of every operand; commutative
+    // ops).  MPIR_Reduce_scatter_Rec_Halving_MV2 (red_scat_osu.c:428-780): the pre-step, then
+    // halving steps with masks pof2/2, pof2/4, ... 1, each uop(tmp_recvbuf, tmp_results); newrank i
+    // ends with new block i, which holds rank i's block (and, below 2 * rem, its even neighbour's)
+    void rh_value(int nr, int k, int lev, char *out) {
+        if (k == 0) return base(nr, out);
+        const int mask = (1 << lev) >> k;
+        char *other = level(k);
+        rh_value(nr, k - 1, lev, out);
+        rh_value(nr ^ mask, k - 1, lev, other);
+        uop(other, out);
+    }
+    void rs_halving(int me, char *out) {
+        int p = 1, lev = 0;
+        while (p * 2 <= n) p *= 2, ++lev;
+        const int rem = n - p;
+        rh_value(me < 2 * rem ? me / 2 : me - rem, lev, lev, out);
+    }
+    // MPIR_Reduce_scatter_Pair_Wise_MV2 (:786-1020): own data, then uop(x_{me-i}, acc), i = 1 .. n-1
+    void rs_pairwise(int me, char *out) {
+        copy(out, x(me));
+        for (int i = 1; i < n; ++i) uop(x((me - i + n) % n), out);
+    }
+    // MPIR_Reduce_scatter_ring (:1026-1180): the block starts at rank me + 1; each next rank
+    // reduces the partial it receives into its own data, uop(tmp_recvbuf, tmp_sendbuf)
+    void rs_ring(int me, char *out) {
+        char *acc = level(0), *next = level(1);
+        copy(acc, x((me + 1) % n));
+        for (int j = 2; j <= n; ++j) {
+            copy(next, x((me + j) % n));
+            uop(acc, next);
+            std::swap(acc, next);
+        }
+        copy(out, acc);
     }
     // MPIR_Reduce_binomial_MV2 (reduce_osu.c:577-663): relative rank rel's value once the masks
     // below m are done (a non-commutative op reduces towards rank 0, which forwards to the root)
@@ -617,13 +659,15 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
 // MPIR_Reduce_scatter_non_comm_MV2 (mirror-permuted halving or recursive doubling) for
 // non-commutative ones.  The nonblocking non-commutative schedules are not restated: those take
 // the canonical rank order x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
-// associative op, applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block.
+// associative op, applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block (above
+// kMaxRanks ranks from the algorithm's message schedule, BigEval; commutative ops only there).
 int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, const HostOp &op) {
     const Job J = job();
     const Typed t = typed(dt);
     if (t.tsize < 0 || t.extent <= 0) return MPI_ERR_TYPE;
     const int n = J.n, me = J.me;
-    if (n > kMaxRanks) return MPI_ERR_UNSUPPORTED_OPERATION;  // programs over the job's ranks
+    // above kMaxRanks ranks the non-commutative forms are not restated (programs over the ranks)
+    if (n > kMaxRanks && op.opk == OPK_USER_NONCOMM) return MPI_ERR_UNSUPPORTED_OPERATION;
     long total = 0, disp = 0;
     std::vector<size_t> cz(n);
     for (int j = 0; j < n; ++j) {
@@ -634,7 +678,15 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     ProgSet ps{};
     Plan p;
     int rc;
-    if (op.opk != OPK_USER_NONCOMM || nbc_kind() == NBC_NONE) {
+    if (n > kMaxRanks) {
+        // more ranks than a program holds: the algorithm's schedule evaluated for this rank's block
+        const int algo = reduce_scatter_algo(n, total * t.tsize);
+        p.algo = algo;
+        const int id = algo == ALG_RS_RING ? PV_RS_RING : algo == ALG_RS_PAIRWISE ? PV_RS_PAIRWISE : PV_RS_REC_HALVING;
+        const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
+        if (algo == ALG_RS_BASIC) pvar_note_ids(chain, world().rank == 0 ? 3 : 2);
+        else pvar_note_ids(&id, 1);
+    } else if (op.opk != OPK_USER_NONCOMM || nbc_kind() == NBC_NONE) {
         if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)t.tsize, (int)t.extent, &p, op.opk))) return rc;
         if (J.multi && p.algo == ALG_RS_BASIC) {  // the reduce inside is the multi-node one
             const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
@@ -674,6 +726,15 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     if ((rc = fetch(o, disp, disp + c, W, rspan))) return rc;
     R.resize((size_t)c * (size_t)t.tsize + 1);
     if (!R.data()) return MPI_ERR_NO_MEM;
+    if (n > kMaxRanks) {
+        BigEval ev{W.data(), rspan, n, c, &t, op.fn, true, {}};
+        std::vector<char> out((size_t)rspan + 1);
+        if (p.algo == ALG_RS_RING) ev.rs_ring(me, out.data());
+        else if (p.algo == ALG_RS_PAIRWISE) ev.rs_pairwise(me, out.data());
+        else ev.rs_halving(me, out.data());
+        if ((rc = dtype_pack(out.data(), c, t.dt, R.data()))) return rc;
+        return dtype_unpack(R.data(), c, t.dt, recvbuf);
+    }
     if ((rc = eval_range(ps, 0, W.data(), rspan, disp, disp + c, t, op.fn, R.data()))) return rc;
     return dtype_unpack(R.data(), c, t.dt, recvbuf);
 }

@@ -165,11 +165,12 @@ def reduce(xs, fn, commute, dtype_handle, count, root):
     raise NotImplementedError(algo)
 
 
-def reduce_scatter(xs, fn, dtype_handle, counts):
-    """commutative user op: MPIR_Reduce_scatter_MV2's choice (red_scat_osu.c:1859-1896); every block"""
+def reduce_scatter(xs, fn, dtype_handle, counts, algo=None):
+    """commutative user op: MPIR_Reduce_scatter_MV2's choice (red_scat_osu.c:1859-1896; the
+    one-node table entry unless `algo` names it); every block"""
     n = len(xs)
     disps = np.concatenate([[0], np.cumsum(counts)]).astype(int)
-    algo = oracle.ALGOS[oracle.reduce_scatter_select(counts, dtype_handle)]
+    algo = algo or oracle.ALGOS[oracle.reduce_scatter_select(counts, dtype_handle)]
     blk = lambda x, b: x[disps[b]:disps[b + 1]]
     out = []
     if algo == "rs_ring":      # red_scat_osu.c:1290-1336

@@ -404,7 +404,8 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
     MPI_Reduce_scatter: MPIR_Reduce_scatter_MV2's flat selection (non_comm forms included).  Above
     8 ranks (12x1, 5x2) the host evaluates the message schedules themselves (user_coll.cpp
     BigEval: recursive doubling, the ring's own chunk, the binomial; leaders' steps over more than
-    8 nodes); reduce-scatter there is not restated for host ops."""
+    8 nodes; reduce-scatter's basic / recursive halving / ring for this rank's block); the
+    non-commutative reduce-scatter forms there are not restated."""
     cases, seed = [], 700
     for commute in (1, 0):
         for count in (100, 2000, 33) + ((600001,) if commute and n > 8 else ()):
@@ -415,7 +416,9 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
             cases.append({"id": f"ur{seed}", "kind": "user_reduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed, "root": root})
             seed += 1
-        for per in ((3, 400) if n <= 8 else ()):
+        # above 8 ranks: basic (a 24-byte operand, half the blocks empty), halving, ring; the
+        # non_comm forms only up to 8 ranks
+        for per in (3, 400) if n <= 8 else (0, 400, 12000) if commute else ():
             counts = [per] * n if not commute else [per + (r % 2) for r in range(n)]
             cases.append({"id": f"us{seed}", "kind": "user_reduce_scatter", "commute": commute, "count": sum(counts),
                           "recvcounts": counts, "type": "MPI_INT", "seed": seed})
@@ -451,8 +454,8 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
                 offs = np.cumsum([0] + counts)
                 want = [full[offs[r]:offs[r + 1]] for r in range(n)]
             else:
-                want = ref_user.reduce_scatter(xs, _ufn, TYPES["MPI_INT"][0], counts) if commute else \
-                    ref_user.reduce_scatter_noncomm(xs, _ufn, counts)
+                want = ref_user.reduce_scatter(xs, _ufn, TYPES["MPI_INT"][0], counts, algo=rs_algo(n, total * 4)) \
+                    if commute else ref_user.reduce_scatter_noncomm(xs, _ufn, counts)
             for r in range(n):
                 assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
 
