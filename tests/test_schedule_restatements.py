@@ -1,0 +1,103 @@
+"""CPU: the closed forms the host evaluator uses above 8 ranks (mpi/user_coll.cpp BigEval) against
+the oracle's step-by-step simulations of the reference's schedules, at 9-16 ranks, on operands
+made of signed zeros, ±1 and NaN payloads so that MAX exposes every operand order:
+
+* pt2pt_rs (allreduce_osu.c:852-1000): block i of pof2 is reduced at the newrank whose bits are
+  i's reversed, along recursive doubling's steps at that newrank;
+* Rec_Halving (red_scat_osu.c:428-780): newrank i's value after halving steps with masks
+  pof2/2 ... 1 holds rank i's block;
+* the reduce-scatter ring (:1026-1180) and pairwise (:786-1020) per block."""
+import numpy as np
+import pytest
+
+from mvapich2_amd.consts import OPS, TYPES
+from oracle import oracle
+
+H = TYPES["MPI_DOUBLE"][0]
+EXT = 8
+OP = OPS["MPI_MAX"]
+
+
+def uop(a_in, b_io, cnt):
+    out = b_io.copy()
+    assert oracle.reduce_local(a_in.copy(), out, cnt, H, OP) == 0
+    return out
+
+
+def operands(n, count, seed):
+    rng = np.random.default_rng(seed)
+    vals = np.array([0.0, -0.0, 1.0, -1.0, np.nan, -np.nan, 2.0])
+    return [rng.choice(vals, count).astype(np.float64).view(np.uint8).copy() for _ in range(n)]
+
+
+def geometry(n):
+    pof2, lev = 1, 0
+    while pof2 * 2 <= n:
+        pof2, lev = pof2 * 2, lev + 1
+    rem = n - pof2
+    return pof2, lev, rem, (lambda q: q * 2 + 1 if q < rem else q + rem)
+
+
+def base(xs, nr, b, e, rem, real):
+    r = real(nr)
+    out = xs[r][b * EXT:e * EXT].copy()
+    if r < 2 * rem:
+        out = uop(xs[r - 1][b * EXT:e * EXT], out, e - b)
+    return out
+
+
+@pytest.mark.parametrize("n", [9, 10, 12, 16])
+@pytest.mark.parametrize("count", [37, 40, 1000])
+def test_pt2pt_rs_blocks_are_bit_reversed_doubling(n, count):
+    xs = operands(n, count, n * count)
+    want = oracle.allreduce([x.copy() for x in xs], count, H, OP, algo=oracle.ALGOS.index("pt2pt_rs"))
+    pof2, lev, rem, real = geometry(n)
+
+    def rd(nr, k, b, e):
+        if k == 0:
+            return base(xs, nr, b, e, rem, real)
+        m = 1 << (k - 1)
+        return uop(rd(nr ^ m, k - 1, b, e), rd(nr, k - 1, b, e), e - b)
+
+    per = count // pof2
+    parts = []
+    for i in range(pof2):
+        b, c = i * per, per if i < pof2 - 1 else count - per * (pof2 - 1)
+        owner = int(format(i, f"0{lev}b")[::-1], 2)
+        parts.append(rd(owner, lev, b, b + c))
+    got = np.concatenate(parts)
+    for r in range(n):
+        assert np.array_equal(got, want[r]), (n, count, r)
+
+
+@pytest.mark.parametrize("n", [9, 10, 12, 16])
+def test_reduce_scatter_block_forms(n):
+    rng = np.random.default_rng(n)
+    counts = [int(rng.integers(0, 5)) + (r % 3) for r in range(n)]
+    total = sum(counts)
+    xs = operands(n, total, 7 * n)
+    disps = np.cumsum([0] + counts)
+    pof2, lev, rem, real = geometry(n)
+    for algo in ("rs_ring", "rs_rec_halving", "rs_pairwise"):
+        full = oracle.reduce_scatter_ref([x.copy() for x in xs], counts, H, OP, algo=oracle.ALGOS.index(algo))
+        for r in range(n):
+            b, e = int(disps[r]), int(disps[r + 1])
+            if e == b:
+                continue
+            X = lambda j: xs[j][b * EXT:e * EXT]
+            if algo == "rs_pairwise":
+                acc = X(r).copy()
+                for i in range(1, n):
+                    acc = uop(X((r - i) % n), acc, e - b)
+            elif algo == "rs_ring":
+                acc = X((r + 1) % n).copy()
+                for j in range(2, n + 1):
+                    acc = uop(acc, X((r + j) % n).copy(), e - b)
+            else:
+                def rh(nr, k):
+                    if k == 0:
+                        return base(xs, nr, b, e, rem, real)
+                    m = pof2 >> k
+                    return uop(rh(nr ^ m, k - 1), rh(nr, k - 1), e - b)
+                acc = rh(r // 2 if r < 2 * rem else r - rem, lev)
+            assert np.array_equal(acc, full[b * EXT:e * EXT]), (algo, n, r)
