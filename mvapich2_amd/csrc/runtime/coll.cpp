@@ -2075,6 +2075,7 @@ static int mn_sched_allreduce(const void *sendbuf, void *recvbuf, size_t count, 
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
     const size_t ext = (size_t)dt->extent, S = count * ext;
+    if (w.gsize > kMeshMaxRanks) return E_UNSUPPORTED;  // no rank mesh: every rank refuses alike
     const int id = algo == ALG_PT2PT_RS ? PV_AR_SHM_RS : PV_AR_SHM_RD;
     pvar_note_ids(&id, 1);
     int rc = mn_reserve_dev(S);
@@ -2101,6 +2102,7 @@ static int mn_sched_naive(const void *sendbuf, void *recvbuf, size_t count, int 
     const bool in_place = sendbuf == (const void *)-1;
     const size_t ext = (size_t)dt->extent, S = count * ext;
     const int n = w.gsize, me = w.grank;
+    if (n > kMeshMaxRanks) return E_UNSUPPORTED;  // no rank mesh: every rank refuses alike
     int rc = mn_reserve_dev(S);
     if (rc) return rc;
     // the accumulator: recvbuf where it is significant and device memory, else device scratch
@@ -2413,6 +2415,7 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
     }
     if (n > kMaxRanks) {
         // beyond the programs' registers: the algorithm's message schedule over the rank channels
+        if (n > kMeshMaxRanks) return E_UNSUPPORTED;  // no rank mesh: every rank refuses alike
         const int id = algo == ALG_RS_RING ? PV_RS_RING : algo == ALG_RS_PAIRWISE ? PV_RS_PAIRWISE : PV_RS_REC_HALVING;
         pvar_note_ids(&id, 1);
         std::vector<size_t> disps((size_t)n, 0);
