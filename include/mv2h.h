@@ -183,6 +183,10 @@ int mv2h_plan(int coll, int n, int rank, int root, size_t count, const size_t *c
  * 2 reduce_p2p, 3 pt2pt_rs, 4 pt2pt_rd; *inter: 2 pt2pt_rs, 3 pt2pt_rd), 2 / 3 for a flat
  * pt2pt_rs / pt2pt_rd over every rank. */
 int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter);
+/* MPIR_Reduce_scatter_MV2's blocking choice for a commutative op over n ranks and nbytes in all
+ * (red_scat_osu.c:1859-1893, the default table of red_scat_tuning.c): *algo codes of mv2h_plan
+ * (10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic). */
+int mv2h_reduce_scatter_table(int n, long nbytes);
 /* Nonblocking initiation: between mv2h_nbc_begin(kind) and mv2h_nbc_end() on this thread
  * the reducing collectives take the reference's nonblocking selection (MPIR_Iallreduce_MV2,
  * MPIR_Ireduce_MV2, MPIR_Ireduce_scatter_MV2, MPICH MPIR_Ireduce_scatter_block_intra) and

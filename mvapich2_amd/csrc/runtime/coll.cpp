@@ -970,6 +970,8 @@ int mv2h_reduce_n_prog(const void *const *srcs, int nsrc, void *dst, size_t coun
     return finish(st, world().timing);
 }
 
+int mv2h_reduce_scatter_table(int n, long nbytes) { return reduce_scatter_table(n, nbytes); }
+
 int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) {
     int in = -1, it = -1;
     const int t = mn_allreduce_table(ppn, gsize, nbytes, &in, &it);

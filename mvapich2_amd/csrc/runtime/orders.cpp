@@ -859,16 +859,19 @@ int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) 
 // MPIR_Reduce_scatter_MV2's choice for a commutative op over n ranks (red_scat_osu.c:1859-1893): the
 // ring from MV2_RED_SCAT_RING_ALGO_THRESHOLD (for node-major ranks the cyclic-hostfile test never
 // holds), else the default table (red_scat_tuning.c:214-287), its entry the first numproc >= n (the
-// last beyond), the function the first whose max >= nbytes.  MPIR_Reduce_scatter_ring_2lvl runs the
-// plain ring's order for the identity rank list (:1190-1300 against :1026-1180).
+// last beyond), the function the first whose max >= nbytes among the entry's declared
+// size_inter_table rows (:1877-1884: numproc 128 / 256 / 512 list a ring row but declare two rows,
+// so recursive halving runs up to the ring threshold there).  MPIR_Reduce_scatter_ring_2lvl runs
+// the plain ring's order for the identity rank list (:1190-1300 against :1026-1180).
 int reduce_scatter_table(int n, long nbytes) {
     if (knobs().red_scat_ring_thr <= nbytes) return ALG_RS_RING;
+    constexpr long kAll = 0x7fffffffffffffffL;
     static const struct {
         int numproc;
         long basic, halving, pairwise;  // inclusive upper bounds; the ring beyond
     } tab[] = {{8, 256, 16384, 65536},   {16, 64, 65536, 65536},   {32, 64, 131072, 131072},
-               {64, 1024, 262144, 262144}, {128, 128, 65536, 65536}, {256, 128, 65536, 65536},
-               {512, 256, 65536, 65536}};
+               {64, 1024, 262144, 262144}, {128, 128, kAll, kAll}, {256, 128, kAll, kAll},
+               {512, 256, kAll, kAll}};
     const int last = (int)(sizeof(tab) / sizeof(tab[0])) - 1;
     int r = 0;
     while (r < last && n > tab[r].numproc) ++r;

@@ -5,6 +5,8 @@ nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h by tests/golden/gen_mn_al
 tests/test_gpu_multinode_mp.py table_cell), every numproc entry, including each two-level entry's
 intra-node function (allreduce_osu.c:1727-1745)."""
 import ctypes
+import json
+from pathlib import Path
 
 import pytest
 
@@ -42,3 +44,29 @@ def test_table_matches_the_headers(ppn, gsize):
             assert t in FLAT and FLAT[t] == fn, tag
             continue
         assert t == 0 and FLAT[inter.value] == fn and INTRA[intra.value] == want_intra, tag
+
+
+# MPIR_Reduce_scatter_MV2's blocking table (tests/golden/red_scat_table.json, generated from
+# red_scat_tuning.c by tests/golden/gen_red_scat_table.py) read as the reference reads it
+# (red_scat_osu.c:1859-1893): the ring from the ring threshold; else the entry of the first
+# numproc >= n (the last beyond); the first of its size_inter_table rows whose max >= nbytes
+RS = json.loads((Path(__file__).parent / "golden" / "red_scat_table.json").read_text())
+RS_CODE = {"rs_ring": 10, "rs_rec_halving": 11, "rs_pairwise": 12, "rs_basic": 13}
+
+
+def rs_reference_choice(n, nbytes):
+    if nbytes >= RS["ring_threshold"]:
+        return "rs_ring"
+    ents = RS["entries"]
+    e = next((x for x in ents if n <= x["numproc"]), ents[-1])
+    rt = 0
+    while rt < e["size"] - 1 and nbytes > e["rows"][rt][1] and e["rows"][rt][1] != -1:
+        rt += 1
+    return e["rows"][rt][2]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8, 9, 12, 16, 17, 32, 33, 64, 65, 100, 128, 200, 512, 1000])
+def test_reduce_scatter_table_matches_the_reference_table(n):
+    L = m.lib()
+    for nbytes in SIZES + [64, 65, 1024, 1025, 65536, 65537, 100000, 131071, 131072, 262144, 262145]:
+        assert RS_CODE[rs_reference_choice(n, nbytes)] == L.mv2h_reduce_scatter_table(n, nbytes), (n, nbytes)
