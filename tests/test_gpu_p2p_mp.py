@@ -14,7 +14,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("n,ppn", [(2, 2), (3, 3), (8, 8), (4, 2), (3, 1), (6, 3), (10, 1)])
+# MV2AMD_TEST_P2P_EXTRA="12x4,..." adds shapes (a rehearsal of the case DESIGN §5 records)
+_EXTRA = [tuple(int(v) for v in s.split("x")) for s in os.environ.get("MV2AMD_TEST_P2P_EXTRA", "").split(",") if s]
+
+
+@pytest.mark.parametrize("n,ppn", [(2, 2), (3, 3), (8, 8), (4, 2), (3, 1), (6, 3), (10, 1)] + _EXTRA)
 def test_p2p_and_nonblocking_collectives(n, ppn):
     """ppn < n: emulated nodes (node-major ranks); messages between nodes travel the rank mesh
     (runtime/internode.cpp mesh_setup, runtime/p2p.cpp net_progress) under the same matching"""
