@@ -93,6 +93,20 @@ def cpu_baseline_host_allreduce(seconds=10.0, ranks=8):
                     f"{ranks} ranks pinned 1/core, OSU loop, sizes 8 B..64 MiB, <= {cap:.2f} s per size"}
 
 
+def cpu_baseline_nranks(seconds):
+    """The N > 1 line's cpu_baseline: configs[0]'s host allreduce at the largest size it covers
+    (64 MiB busbw, 8 ranks on 8 cores), with its 8-byte latency in the sample text."""
+    h = cpu_baseline_host_allreduce(seconds)
+    if "error" in h:
+        return {"value": None, "unit": "GB/s", "cores": 8, "kind": "port", "sample": h["error"]}
+    return {"value": h["busbw_64MiB_GBps"], "unit": "GB/s", "cores": h["cores"], "kind": "port",
+            "correct": h["all_ok"],
+            "sample": f"configs[0]: reference host-buffer ch3 shared-memory MPI_Allreduce fp32 SUM restated "
+                      f"(oracle/host_allreduce.c), 64 MiB busbw; 8 B latency {h['latency_8B_us']} us, 1 MiB busbw "
+                      f"{h['busbw_1MiB_GBps']} GB/s; {h['cores']} ranks pinned 1/core of '{h['cpu']}'; "
+                      f"{h['what']}"}
+
+
 def reduce_local_run(L, type_name, op_name, nbytes, steps, warmup):
     h, desc, size, ext = TYPES[type_name]
     count = nbytes // ext
@@ -387,6 +401,28 @@ def user_op_lines(L, world, sb, rb, size):
     return {"ok": ok, "lines": out}
 
 
+def pipe_traffic_for(size, nshare, alg):
+    """(traffic bytes, source file, note) for k_pipe PIPE_AR at this run's configuration: the
+    newest profiles/pmc_pipe_allreduce_*.json whose recorded configuration (ranks, ranks per GPU,
+    tiling knobs, remote-store flavour) equals this run's; else (None, None, why)."""
+    here = {"ranks": size, "nshare": nshare, "pipe_grid": m.info("pipe_grid"), "pipe_sub": m.info("pipe_sub"),
+            "pipe_rnt": m.info("pipe_rnt")}
+    best = None
+    for f in sorted(os.listdir(os.path.join(ROOT, "profiles"))):
+        if not f.startswith("pmc_pipe_allreduce_"):
+            continue
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", f)))
+        except Exception:
+            continue
+        cfg = d.get("config") or {}
+        if all(cfg.get(k) == v for k, v in here.items()) and d.get("traffic_over_algorithmic"):
+            best = (round(d["traffic_over_algorithmic"] * alg), os.path.join("profiles", f), None)
+    if best:
+        return best
+    return None, None, f"no committed PMC pass at this configuration {here}"
+
+
 def bench_nranks(args, L, rank, size):
     world = 0x44000000
     F32, F64, DINT = TYPES["MPI_FLOAT"][0], TYPES["MPI_DOUBLE"][0], TYPES["MPI_DOUBLE_INT"][0]
@@ -478,6 +514,7 @@ def bench_nranks(args, L, rank, size):
 
     # device point-to-point bandwidth, rank 0 -> rank 1 (osu_bw pattern: a window of
     # Isends, one Waitall; the receiver posts the matching Irecvs)
+    nshare = m.info("nshare")  # ranks sharing one GPU (test rehearsals): no xGMI byte moves then
     pbytes, win = 16 << 20, 8
     BYTE = TYPES["MPI_BYTE"][0]
     pb = m.DeviceBuffer(pbytes * win)
@@ -520,7 +557,6 @@ def bench_nranks(args, L, rank, size):
     busbw = 2.0 * f * S_BYTES / step_s / 1e9
     kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
     peak_all = (size - 1) * XGMI_LINK
-    nshare = m.info("nshare")  # ranks sharing one GPU (test rehearsals): no xGMI byte moves then
 
     def line4(t, k, bytes_bus):
         return {"busbw_GBps": round(bytes_bus / t / 1e9, 2), "kernel_busbw_GBps": round(bytes_bus / (k / 1e3) / 1e9, 2),
@@ -536,20 +572,14 @@ def bench_nranks(args, L, rank, size):
         "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
-    # HBM traffic of k_pipe (PIPE_AR) per launch on one rank: the PMC ratio of the newest committed
-    # pass (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE in separate passes, 2 ranks; tools/pmc_summary.py)
-    # times this call's per-rank algorithmic HBM bytes 2S(1 + 2(n-1)/n): reads of the operand, the
-    # RS and the AG slots; writes of the peers' RS pushes, the own segment, the peers' AG pushes and
-    # the gathered segments
+    # HBM traffic of k_pipe (PIPE_AR) per launch on one rank: the PMC ratio (rocprofv3 FETCH_SIZE x2 +
+    # WRITE_SIZE in separate passes, tools/pmc_summary.py) of a committed pass taken at THIS rank
+    # count, ranks per GPU and tiling knobs, times this call's per-rank algorithmic HBM bytes
+    # 2S(1 + 2(n-1)/n): reads of the operand, the RS and the AG slots; writes of the peers' RS
+    # pushes, the own segment, the peers' AG pushes and the gathered segments.  No matching pass:
+    # traffic is null and the nearest pass's configuration is named instead.
     pipe_alg = 2.0 * S_BYTES * (1.0 + 2.0 * (size - 1) / size)
-    pipe_traffic, pipe_tsrc = None, None
-    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.startswith("pmc_pipe_allreduce_"))
-    if cands:
-        pipe_tsrc = os.path.join("profiles", cands[-1])
-        try:
-            pipe_traffic = round(json.load(open(os.path.join(ROOT, pipe_tsrc)))["traffic_over_algorithmic"] * pipe_alg)
-        except Exception:
-            pipe_traffic, pipe_tsrc = None, None
+    pipe_traffic, pipe_tsrc, pipe_tnote = pipe_traffic_for(size, nshare, pipe_alg)
     tiling = {"grid": m.info("pipe_grid"), "bytes_per_workgroup_round": m.info("pipe_sub"),
               "remote_stores": "non-temporal" if m.info("pipe_rnt") else "plain",
               "autotuned_at_init": bool(m.info("pipe_tuned")),
@@ -587,11 +617,12 @@ def bench_nranks(args, L, rank, size):
                    "pipe_tiling": tiling},
         "roofline": ({"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
                       "frac": round(kbus / peak_all, 4), "traffic": pipe_traffic, "traffic_source": pipe_tsrc,
+                      "traffic_note": pipe_tnote,
                       "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg),
                       "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
                       "kernel_ms": round(kms, 4)} if nshare == 1 else
                      {"bound": "shared-gpu", "achieved": round(kbus, 1), "peak": None, "unit": "GB/s", "frac": None,
-                      "traffic": pipe_traffic, "traffic_source": pipe_tsrc,
+                      "traffic": pipe_traffic, "traffic_source": pipe_tsrc, "traffic_note": pipe_tnote,
                       "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)", "kernel_ms": round(kms, 4),
                       "note": f"{nshare} ranks share one GPU: every 'remote' store lands in the same HBM, no xGMI "
                               "link is used, so no xGMI roofline fraction applies"}),
@@ -625,6 +656,11 @@ def main():
     else:
         line = bench_nranks(args, L, rank, size)
     L.MPI_Finalize()
+    if rank == 0 and size > 1 and args.cpu_seconds > 0:
+        # configs[0], the reference's host-buffer shared-memory MPI_Allreduce with 8 ranks on this
+        # box's cores, in the same run (north_star): rank 0 after MPI_Finalize, when the GPU ranks
+        # have stopped spinning on the host, as a fresh child process with a time limit
+        line["cpu_baseline"] = cpu_baseline_nranks(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
 

@@ -187,6 +187,13 @@ int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *in
  * (red_scat_osu.c:1859-1893, the default table of red_scat_tuning.c): *algo codes of mv2h_plan
  * (10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic). */
 int mv2h_reduce_scatter_table(int n, long nbytes);
+/* Several nodes: the route a builtin-op call takes (coll 0 MPI_Allreduce, 1 MPI_Reduce, 2
+ * MPI_Reduce_scatter; nbc: enum mv2h_nbc): 0 two-level, 1 flat ring over every rank, 2 a flat
+ * algorithm as per-element programs (up to 8 ranks), 3 its message schedule over the rank channels
+ * (up to 64 ranks), 4 the two-level structure standing in above 64 ranks (fp order unpinned),
+ * 5 the basic reduce-scatter.  *rem_route: the ring wrapper's remainder's route, -1 for none.
+ * 12 (MPI_ERR_ARG's class) for a shape that is not ppn ranks on each of gsize / ppn nodes. */
+int mv2h_mn_route(int coll, int ppn, int gsize, long nbytes, size_t count, int in_place, int nbc, int *rem_route);
 /* Nonblocking initiation: between mv2h_nbc_begin(kind) and mv2h_nbc_end() on this thread
  * the reducing collectives take the reference's nonblocking selection (MPIR_Iallreduce_MV2,
  * MPIR_Ireduce_MV2, MPIR_Ireduce_scatter_MV2, MPICH MPIR_Ireduce_scatter_block_intra) and

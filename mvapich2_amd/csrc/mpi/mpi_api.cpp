@@ -81,6 +81,14 @@ int err_return(MPI_Comm comm, int code, const char *fn) {
         fflush(stderr);
         abort();
     }
+    static const int verbose = [] {
+        const char *v = getenv("MV2AMD_ERR_VERBOSE");  // tests: name every error a call returns
+        return v && *v && *v != '0';
+    }();
+    if (verbose) {
+        fprintf(stderr, "[mv2amd rank %d] %s returned %s\n", mv2h_rank(), fn, err_name(code));
+        fflush(stderr);
+    }
     return code;
 }
 

@@ -30,7 +30,7 @@
 
 namespace mv2 {
 
-int log_rank() { return world().rank; }
+int log_rank() { return world().grank; }  // the job's rank (a node's local rank 0 is not unique)
 bool log_debug_on() {
     static int on = -1;
     if (on < 0) {
@@ -393,6 +393,13 @@ static PipeGeom pipe_geom(size_t maxlen) {
     g.tseg = (size_t)g.grid * g.tsub;
     g.nrounds = (int)((maxlen + g.tseg - 1) / g.tseg);
     return g;
+}
+
+// the tiling a segment of seg_bytes runs with (MPI_Init's report)
+void pipe_tiling_for(size_t seg_bytes, int *grid, size_t *tsub) {
+    const PipeGeom g = pipe_geom(seg_bytes);
+    *grid = g.grid;
+    *tsub = g.tsub;
 }
 
 // n contiguous 16-byte-aligned segments of a `bytes` buffer (the last may be short or empty)
@@ -1771,9 +1778,17 @@ struct RankChannels : Xport {
         unsigned long long sq = 0, rq = 0;
         int rc = 0;
         if (rbytes && (rc = p2p_irecv(rb, rbytes, from, kCollTagBase - 3, &rq))) return rc;
-        if (sbytes && (rc = p2p_isend(sb, sbytes, to, kCollTagBase - 3, &sq))) return rc;
-        if (sbytes && (rc = mv2h_p2p_wait(sq, nullptr, nullptr, nullptr))) return rc;
-        return rbytes ? mv2h_p2p_wait(rq, nullptr, nullptr, nullptr) : 0;
+        if (sbytes && (rc = p2p_isend(sb, sbytes, to, kCollTagBase - 3, &sq))) {
+            if (rq) p2p_abandon(rq);  // withdrawn, or the context poisoned: never matched into later
+            return rc;
+        }
+        if (sbytes && (rc = mv2h_p2p_wait(sq, nullptr, nullptr, nullptr))) {
+            p2p_abandon(sq);
+            if (rq) p2p_abandon(rq);
+            return rc;
+        }
+        if (rbytes && (rc = mv2h_p2p_wait(rq, nullptr, nullptr, nullptr))) p2p_abandon(rq);
+        return rc;
     }
 };
 
@@ -1924,30 +1939,73 @@ static int mn_require_device_reduction(int dtype, int op) {
 // Returns 0 (two-level), 1 (flat ring wrapper), or ALG_PT2PT_RS / ALG_PT2PT_RD (flat over every
 // rank).  The small-message shortcuts (:118-160) keep the two-level structure; the skip-large gate
 // (:163-171) takes the ring wrapper; then the tuning tables (orders.cpp mn_allreduce_table).
-static int mn_select(long nbytes, int *intra, int *inter) {
-    const World &w = world();
+static int mn_select(int ppn, int gsize, long nbytes, int *intra, int *inter) {
     const Knobs &K = knobs();
     *intra = MN_INTRA_NODE;  // the shortcuts' node step is the node's own small-message order
     *inter = ALG_PT2PT_RD;   // and their leaders' step recursive doubling (:2215-2262, :147-153)
     bool tables = false;
     if (K.allred_skip_small) {
         if (nbytes <= K.topo_allred_max && nbytes >= K.topo_allred_min && K.enable_topo && K.use_topo_allreduce) {
-            if (w.size >= K.topo_allred_ppn) return 0;  // topology-aware hierarchical
-            tables = true;                              // goto use_tables
+            if (ppn >= K.topo_allred_ppn) return 0;  // topology-aware hierarchical
+            tables = true;                           // goto use_tables
         }
         if (!tables && K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr) return 0;
     }
     if (!tables && K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes &&
-        w.size <= K.allred_ring_ppn)
+        ppn <= K.allred_ring_ppn)
         return 1;
     int in = MN_INTRA_NODE, it = ALG_PT2PT_RD;
-    const int t = mn_allreduce_table(w.size, w.gsize, nbytes, &in, &it);
+    const int t = mn_allreduce_table(ppn, gsize, nbytes, &in, &it);
     if (t == 0) {
         *intra = in;
         *inter = it;
         return 0;
     }
     return t;
+}
+
+// How a multi-node call with a builtin op runs (a pure function of the job's shape and the call,
+// so every rank takes the same route; mv2h_mn_route exposes it to the CPU tests).  A flat
+// algorithm runs as per-element programs up to kMaxRanks ranks (MN_FLAT_PROG), as its message
+// schedule over the rank channels up to kMeshMaxRanks (MN_SCHED: the rank mesh exists up to
+// there), and above that the two-level structure stands in for it (MN_FALLBACK: Allreduce and
+// Iallreduce the two-level allreduce with the default node and leader steps, Ireduce the
+// two-level reduce helper, Reduce_scatter the basic algorithm) — correct for every builtin op,
+// its fp order not the reference's (unpinned; integer, bitwise, logical and LOC results exact).
+enum MnRoute { MN_TWO_LEVEL_R = 0, MN_RING_R = 1, MN_FLAT_PROG = 2, MN_SCHED = 3, MN_FALLBACK = 4, MN_BASIC_R = 5 };
+static int mn_flat_route(int gsize) {
+    return gsize <= kMaxRanks ? MN_FLAT_PROG : gsize <= kMeshMaxRanks ? MN_SCHED : MN_FALLBACK;
+}
+// MPI_Allreduce / MPI_Iallreduce (nbc = the call's mv2h_nbc kind).  *rem_route: the route of the
+// ring wrapper's count % gsize remainder (pt2pt_rs over every rank), -1 when there is none.
+static int mn_allreduce_route(int ppn, int gsize, long nbytes, size_t count, bool in_place, int nbc, int *intra,
+                              int *inter, int *sel_out, int *rem_route) {
+    *intra = MN_INTRA_NODE;
+    *inter = ALG_PT2PT_RD;
+    *sel_out = 0;
+    *rem_route = -1;
+    if (nbc == NBC_IALLREDUCE) return mn_flat_route(gsize);
+    const int sel = mn_select(ppn, gsize, nbytes, intra, inter);
+    *sel_out = sel;
+    if (sel == 1) {
+        if (!in_place && count >= (size_t)gsize) {
+            if (count % (size_t)gsize) *rem_route = mn_flat_route(gsize);
+            return MN_RING_R;
+        }
+        return mn_flat_route(gsize);
+    }
+    if (sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD) return mn_flat_route(gsize);
+    return MN_TWO_LEVEL_R;
+}
+// MPI_Reduce_scatter / MPI_Ireduce_scatter over gsize ranks, nbytes in all
+static int mn_reduce_scatter_route(int gsize, long nbytes) {
+    if (reduce_scatter_algo(gsize, nbytes) == ALG_RS_BASIC) return MN_BASIC_R;
+    const int r = mn_flat_route(gsize);
+    return r == MN_FALLBACK ? MN_BASIC_R : r;
+}
+// MPI_Reduce / MPI_Ireduce
+static int mn_reduce_route(int gsize, int nbc) {
+    return nbc == NBC_IREDUCE ? mn_flat_route(gsize) : MN_TWO_LEVEL_R;
 }
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
@@ -2140,7 +2198,8 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     const size_t S = count * (size_t)dt->extent;
     const int n = w.gsize;
     if (n > kMaxRanks && root < 0 && (algo == ALG_PT2PT_RS || algo == ALG_PT2PT_RD))
-        return mn_sched_allreduce(sendbuf, recvbuf, count, dtype, op, algo);
+        return mn_flat_route(n) == MN_SCHED ? mn_sched_allreduce(sendbuf, recvbuf, count, dtype, op, algo)
+                                            : mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
     Plan p;
     int rc = root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
                        : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
@@ -2159,24 +2218,27 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
 static int mn_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream) {
     int rc = mn_require_device_reduction(dtype, op);
     if (rc || count == 0) return rc;
+    const World &w = world();
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
-    const int gsize = world().gsize;
+    const int gsize = w.gsize;
+    int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD, sel = 0, rem = -1;
+    const int route = mn_allreduce_route(w.size, gsize, (long)(count * (size_t)dt->size), count, in_place, nbc_kind(),
+                                         &intra, &inter, &sel, &rem);
     // MPI_Iallreduce: MVAPICH2's nonblocking schedule is flat over the whole job
     // (MPIR_Iallreduce_intra_MV2 iallreduce_osu.c:257 -> MPIR_Iallreduce_naive: Ireduce to rank 0,
     // binomial or redscat_gather, then Ibcast), whatever the nodes
-    if (nbc_kind() == NBC_IALLREDUCE)
-        return gsize <= kMaxRanks ? mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0)
-                                  : mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, -1);
-    int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD;
-    const int sel = mn_select((long)(count * (size_t)dt->size), &intra, &inter);
+    if (nbc_kind() == NBC_IALLREDUCE) {
+        if (route == MN_FLAT_PROG) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0);
+        if (route == MN_SCHED) return mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, -1);
+        return mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
+    }
+    if (route == MN_RING_R) return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
     if (sel == 1) {
         // the wrapper's ring body needs count >= n and a separate sendbuf (:3893-3898); otherwise
         // it runs pt2pt_rs over every rank.  With
         // IN_PLACE the body's own fallback is pt2pt_rs over (count / n) * n elements (:4095-4100),
         // then the wrapper's pt2pt_rs on the remainder (:3800-3818): two calls, as on one node
-        if (!in_place && count >= (size_t)gsize)
-            return mn_ring_allreduce(sendbuf, recvbuf, count, dtype, op, stream);
         const int chain[2] = {PV_AR_RING_WRAPPER, PV_AR_SHM_RS};
         pvar_note_ids(chain, 2);
         const size_t main = in_place ? (count / (size_t)gsize) * (size_t)gsize : 0;
@@ -2312,9 +2374,10 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     // MPI_T: MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2039) with the leaders' binomial (:450)
     // MPI_Ireduce: MVAPICH2's nonblocking schedule (MPIR_Ireduce_binomial, ireduce_osu.c) is flat
     // over the whole job
-    if (nbc_kind() == NBC_IREDUCE)
-        return w.gsize <= kMaxRanks ? mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root)
-                                    : mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, root);
+    const int route = mn_reduce_route(w.gsize, nbc_kind());
+    if (route == MN_FLAT_PROG) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root);
+    if (route == MN_SCHED) return mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, root);
+    // MN_TWO_LEVEL_R, or MN_FALLBACK for an MPI_Ireduce above the rank mesh: the two-level helper
     const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
     pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
     if ((rc = mn_reserve_dev(bytes)) || (w.rank == 0 && (rc = mn_reserve_host(bytes)))) return rc;
@@ -2405,7 +2468,8 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
                    ? 0 : E_INTERN;
     }
     const int algo = reduce_scatter_algo(n, (long)(total * (size_t)dt->size));
-    if (algo == ALG_RS_BASIC) {
+    const int route = mn_reduce_scatter_route(n, (long)(total * (size_t)dt->size));
+    if (route == MN_BASIC_R) {
         // MPIR_Reduce_Scatter_Basic_MV2 (red_scat_osu.c:300-413): MPIR_Reduce_MV2 to rank 0 over
         // the whole communicator — the multi-node reduce (mn_reduce) — then the blocks scattered
         const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
@@ -2415,9 +2479,8 @@ static int mn_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *r
         if ((rc = mn_reduce(src, tmp, total, dtype, op, 0, stream)) || (rc = mn_bcast(tmp, S, 0, stream))) return rc;
         return !mine || hipMemcpy(recvbuf, tmp + off * ext, mine, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
     }
-    if (n > kMaxRanks) {
+    if (route == MN_SCHED) {
         // beyond the programs' registers: the algorithm's message schedule over the rank channels
-        if (n > kMeshMaxRanks) return E_UNSUPPORTED;  // no rank mesh: every rank refuses alike
         const int id = algo == ALG_RS_RING ? PV_RS_RING : algo == ALG_RS_PAIRWISE ? PV_RS_PAIRWISE : PV_RS_REC_HALVING;
         pvar_note_ids(&id, 1);
         std::vector<size_t> disps((size_t)n, 0);
@@ -2516,7 +2579,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         return 0;
     }
     int intra = MN_INTRA_NODE, inter = ALG_PT2PT_RD;
-    const int sel = mn_select((long)count * tsize, &intra, &inter);
+    const int sel = mn_select(L, n, (long)count * tsize, &intra, &inter);
     if (big && sel != 0) {
         // flat over more ranks than a program holds: the ring over (count / n) * n elements unless
         // IN_PLACE or count < n, then pt2pt_rs on the rest; IN_PLACE: two pt2pt_rs calls split
@@ -2587,6 +2650,20 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
 }
 
 extern "C" {
+
+int mv2h_mn_route(int coll, int ppn, int gsize, long nbytes, size_t count, int in_place, int nbc, int *rem_route) {
+    if (ppn < 1 || gsize < ppn || gsize % ppn) return E_ARG;
+    int intra = 0, inter = 0, sel = 0, rem = -1;
+    int r;
+    switch (coll) {
+    case 0: r = mn_allreduce_route(ppn, gsize, nbytes, count, in_place != 0, nbc, &intra, &inter, &sel, &rem); break;
+    case 1: r = mn_reduce_route(gsize, nbc); break;
+    case 2: r = mn_reduce_scatter_route(gsize, nbytes); break;
+    default: return E_ARG;
+    }
+    if (rem_route) *rem_route = rem;
+    return r;
+}
 
 int mv2h_allgather(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
     if (world().nnodes > 1) {

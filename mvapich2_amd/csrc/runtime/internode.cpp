@@ -141,6 +141,19 @@ int connect_retry(const char *host, int port) {
     return fd;
 }
 
+// a host name or address as dotted IPv4 (the form every node's ranks connect to, and what fits the
+// control segment's node_ip); "" when it does not resolve
+std::string numeric_ipv4(const std::string &host) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host.c_str(), nullptr, &hints, &res) != 0 || !res) return "";
+    char buf[INET_ADDRSTRLEN] = {};
+    inet_ntop(AF_INET, &((const sockaddr_in *)res->ai_addr)->sin_addr, buf, sizeof(buf));
+    freeaddrinfo(res);
+    return buf;
+}
+
 int accept_timed(int lfd) {
     pollfd p{lfd, POLLIN, 0};
     const int ms = (int)(timeout_s() * 1000.0);
@@ -150,8 +163,10 @@ int accept_timed(int lfd) {
     return fd;
 }
 
-// full-duplex transfer on one socket: send sn bytes and receive rn bytes, interleaved
-int xfer(int fd, const char *sb, size_t sn, char *rb, size_t rn) {
+// full-duplex transfer on one socket: send sn bytes and receive rn bytes, interleaved.  `peer`
+// names the other end in the diagnostics (a node index on the leaders' links, -1: bootstrap);
+// every failure path says what failed, with errno, before the caller closes anything.
+int xfer(int fd, const char *sb, size_t sn, char *rb, size_t rn, int peer = -1) {
     size_t so = 0, ro = 0;
     const int ms = (int)(timeout_s() * 1000.0);
     while (so < sn || ro < rn) {
@@ -159,25 +174,35 @@ int xfer(int fd, const char *sb, size_t sn, char *rb, size_t rn) {
         const int r = poll(&p, 1, ms);
         if (r <= 0) {
             if (r < 0 && errno == EINTR) continue;
-            MV2_ERR("inter-node transfer timed out (MV2AMD_TIMEOUT_S)");
+            if (r < 0) MV2_ERR("inter-node link to node %d: poll failed: %s", peer, strerror(errno));
+            else MV2_ERR("inter-node link to node %d: no progress for %.0f s (MV2AMD_TIMEOUT_S; sent %zu of %zu, "
+                         "received %zu of %zu bytes)", peer, timeout_s(), so, sn, ro, rn);
             return E_OTHER;
         }
         if (p.revents & (POLLERR | POLLHUP | POLLNVAL) && !(p.revents & POLLIN)) {
-            MV2_ERR("inter-node connection lost");
+            MV2_ERR("inter-node link to node %d lost (poll revents 0x%x; sent %zu of %zu, received %zu of %zu bytes)",
+                    peer, (unsigned)p.revents, so, sn, ro, rn);
             return E_OTHER;
         }
         if ((p.revents & POLLIN) && ro < rn) {
             const ssize_t k = recv(fd, rb + ro, rn - ro, 0);
             if (k == 0) {
-                MV2_ERR("inter-node connection closed by the peer");
+                MV2_ERR("inter-node link to node %d closed by the peer (received %zu of %zu bytes): that node's "
+                        "leader has exited", peer, ro, rn);
                 return E_OTHER;
             }
-            if (k < 0 && errno != EINTR && errno != EAGAIN) return E_OTHER;
+            if (k < 0 && errno != EINTR && errno != EAGAIN) {
+                MV2_ERR("inter-node link to node %d: recv failed: %s", peer, strerror(errno));
+                return E_OTHER;
+            }
             if (k > 0) ro += (size_t)k;
         }
         if ((p.revents & POLLOUT) && so < sn) {
             const ssize_t k = send(fd, sb + so, sn - so, MSG_NOSIGNAL | MSG_DONTWAIT);
-            if (k < 0 && errno != EINTR && errno != EAGAIN && errno != EWOULDBLOCK) return E_OTHER;
+            if (k < 0 && errno != EINTR && errno != EAGAIN && errno != EWOULDBLOCK) {
+                MV2_ERR("inter-node link to node %d: send failed: %s", peer, strerror(errno));
+                return E_OTHER;
+            }
             if (k > 0) so += (size_t)k;
         }
     }
@@ -186,7 +211,7 @@ int xfer(int fd, const char *sb, size_t sn, char *rb, size_t rn) {
 
 // send sn bytes on fd_out while receiving rn bytes on fd_in (a ring step: different peers),
 // interleaved so that neither side's socket buffers can fill up and stall the ring
-int xfer2(int fd_out, const char *sb, size_t sn, int fd_in, char *rb, size_t rn) {
+int xfer2(int fd_out, const char *sb, size_t sn, int fd_in, char *rb, size_t rn, int to, int from) {
     size_t so = 0, ro = 0;
     const int ms = (int)(timeout_s() * 1000.0);
     while (so < sn || ro < rn) {
@@ -194,27 +219,36 @@ int xfer2(int fd_out, const char *sb, size_t sn, int fd_in, char *rb, size_t rn)
         const int r = poll(p, 2, ms);
         if (r <= 0) {
             if (r < 0 && errno == EINTR) continue;
-            MV2_ERR("inter-node transfer timed out (MV2AMD_TIMEOUT_S)");
+            if (r < 0) MV2_ERR("inter-node ring step (to node %d, from node %d): poll failed: %s", to, from, strerror(errno));
+            else MV2_ERR("inter-node ring step (to node %d, from node %d): no progress for %.0f s (MV2AMD_TIMEOUT_S; "
+                         "sent %zu of %zu, received %zu of %zu bytes)", to, from, timeout_s(), so, sn, ro, rn);
             return E_OTHER;
         }
         if ((p[1].revents & POLLIN) && ro < rn) {
             const ssize_t k = recv(fd_in, rb + ro, rn - ro, 0);
             if (k == 0) {
-                MV2_ERR("inter-node connection closed by the peer");
+                MV2_ERR("inter-node link from node %d closed by the peer (received %zu of %zu bytes): that node's "
+                        "leader has exited", from, ro, rn);
                 return E_OTHER;
             }
-            if (k < 0 && errno != EINTR && errno != EAGAIN) return E_OTHER;
+            if (k < 0 && errno != EINTR && errno != EAGAIN) {
+                MV2_ERR("inter-node link from node %d: recv failed: %s", from, strerror(errno));
+                return E_OTHER;
+            }
             if (k > 0) ro += (size_t)k;
         } else if (p[1].revents & (POLLERR | POLLHUP | POLLNVAL)) {
-            MV2_ERR("inter-node connection lost");
+            MV2_ERR("inter-node link from node %d lost (poll revents 0x%x)", from, (unsigned)p[1].revents);
             return E_OTHER;
         }
         if ((p[0].revents & POLLOUT) && so < sn) {
             const ssize_t k = send(fd_out, sb + so, sn - so, MSG_NOSIGNAL | MSG_DONTWAIT);
-            if (k < 0 && errno != EINTR && errno != EAGAIN && errno != EWOULDBLOCK) return E_OTHER;
+            if (k < 0 && errno != EINTR && errno != EAGAIN && errno != EWOULDBLOCK) {
+                MV2_ERR("inter-node link to node %d: send failed: %s", to, strerror(errno));
+                return E_OTHER;
+            }
             if (k > 0) so += (size_t)k;
         } else if (p[0].revents & (POLLERR | POLLHUP | POLLNVAL)) {
-            MV2_ERR("inter-node connection lost");
+            MV2_ERR("inter-node link to node %d lost (poll revents 0x%x)", to, (unsigned)p[0].revents);
             return E_OTHER;
         }
     }
@@ -233,21 +267,21 @@ int link_fd(int peer) {
 
 int net_send(int peer, const void *buf, size_t bytes) {
     const int fd = link_fd(peer);
-    return fd < 0 ? E_INTERN : xfer(fd, (const char *)buf, bytes, nullptr, 0);
+    return fd < 0 ? E_INTERN : xfer(fd, (const char *)buf, bytes, nullptr, 0, peer);
 }
 int net_recv(int peer, void *buf, size_t bytes) {
     const int fd = link_fd(peer);
-    return fd < 0 ? E_INTERN : xfer(fd, nullptr, 0, (char *)buf, bytes);
+    return fd < 0 ? E_INTERN : xfer(fd, nullptr, 0, (char *)buf, bytes, peer);
 }
 int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes) {
     const int fd = link_fd(peer);
-    return fd < 0 ? E_INTERN : xfer(fd, (const char *)sbuf, sbytes, (char *)rbuf, rbytes);
+    return fd < 0 ? E_INTERN : xfer(fd, (const char *)sbuf, sbytes, (char *)rbuf, rbytes, peer);
 }
 
 int net_shift(int to, const void *sbuf, size_t sbytes, int from, void *rbuf, size_t rbytes) {
     if (to == from) return net_sendrecv(to, sbuf, sbytes, rbuf, rbytes);
     const int fo = link_fd(to), fi = link_fd(from);
-    return fo < 0 || fi < 0 ? E_INTERN : xfer2(fo, (const char *)sbuf, sbytes, fi, (char *)rbuf, rbytes);
+    return fo < 0 || fi < 0 ? E_INTERN : xfer2(fo, (const char *)sbuf, sbytes, fi, (char *)rbuf, rbytes, to, from);
 }
 
 int net_init() {
@@ -256,7 +290,13 @@ int net_init() {
     g_net.fd.assign((size_t)nn, -1);
     const char *ba = getenv("MV2AMD_BOOT_ADDR");
     const char *ma = getenv("MASTER_ADDR");
-    const std::string host = ba && *ba ? ba : (ma && *ma ? ma : "127.0.0.1");
+    const std::string name = ba && *ba ? ba : (ma && *ma ? ma : "127.0.0.1");
+    const std::string host = numeric_ipv4(name);
+    if (host.empty()) {
+        MV2_ERR("multi-node job: the leaders' rendezvous host '%s' (MV2AMD_BOOT_ADDR / MASTER_ADDR) does not resolve "
+                "to an IPv4 address", name.c_str());
+        return E_OTHER;
+    }
     const char *bp = getenv("MV2AMD_BOOT_PORT");
     const char *mp = getenv("MASTER_PORT");
     const int port = bp && *bp ? atoi(bp) : (mp && *mp ? atoi(mp) + 1 : 0);
@@ -304,7 +344,10 @@ int net_init() {
     } else {
         int myport = 0;
         g_net.listen_fd = open_listener(nullptr, 0, &myport);
-        if (g_net.listen_fd < 0) return E_OTHER;
+        if (g_net.listen_fd < 0) {
+            MV2_ERR("leader of node %d: cannot open its mesh listener: %s", me, strerror(errno));
+            return E_OTHER;
+        }
         const int fd = connect_retry(host.c_str(), port);
         if (fd < 0) {
             MV2_ERR("leader of node %d: cannot reach the rendezvous %s:%d", me, host.c_str(), port);
@@ -361,7 +404,11 @@ int net_barrier() {
         char t = 1, r = 0;
         int rc = net_send(to, &t, 1);  // one byte never blocks in the socket buffer
         if (!rc) rc = net_recv(from, &r, 1);
-        if (rc) return rc;
+        if (rc) {
+            MV2_ERR("leaders' barrier (node %d of %d): step %d (token to node %d, from node %d) failed", me, nn, d,
+                    to, from);
+            return rc;
+        }
     }
     return 0;
 }
@@ -390,7 +437,13 @@ int mesh_setup() {
             if (all[g] < 0) rc = E_OTHER;
         if (w.shm) {
             for (int g = 0; g < n; ++g) w.shm->mesh_port[g] = all[g];
-            for (int j = 0; j < K; ++j) snprintf(w.shm->node_ip[j], sizeof(w.shm->node_ip[j]), "%s", g_net.ip[j].c_str());
+            for (int j = 0; j < K; ++j) {
+                if (g_net.ip[j].size() >= sizeof(w.shm->node_ip[j])) {  // dotted IPv4 always fits
+                    MV2_ERR("rank mesh: node %d's address '%s' does not fit the control segment", j, g_net.ip[j].c_str());
+                    rc = E_OTHER;
+                }
+                snprintf(w.shm->node_ip[j], sizeof(w.shm->node_ip[j]), "%s", g_net.ip[j].c_str());
+            }
             w.shm->net_rc.store(rc);
         }
         for (int j = 0; j < K; ++j) ip[j] = g_net.ip[j];

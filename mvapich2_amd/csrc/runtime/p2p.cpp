@@ -203,7 +203,7 @@ int net_progress(bool *moved) {
             const ssize_t k = send(fd, o.buf.data() + o.off, o.buf.size() - o.off, MSG_DONTWAIT | MSG_NOSIGNAL);
             if (k < 0) {
                 if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
-                MV2_ERR("point-to-point to rank %d: connection lost", g);
+                MV2_ERR("point-to-point to rank %d (rank mesh): send failed: %s", g, strerror(errno));
                 return E_OTHER;
             }
             o.off += (size_t)k;
@@ -226,12 +226,13 @@ int net_progress(bool *moved) {
             if (want) {
                 const ssize_t k = recv(fd, dst, want, MSG_DONTWAIT);
                 if (k == 0) {
-                    MV2_ERR("point-to-point from rank %d: connection closed", g);
+                    MV2_ERR("point-to-point from rank %d (rank mesh): connection closed by the peer (%s): that rank "
+                            "has exited", g, in.body ? "inside a message" : "between messages");
                     return E_OTHER;
                 }
                 if (k < 0) {
                     if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
-                    MV2_ERR("point-to-point from rank %d: connection lost", g);
+                    MV2_ERR("point-to-point from rank %d (rank mesh): recv failed: %s", g, strerror(errno));
                     return E_OTHER;
                 }
                 *moved = true;
@@ -389,6 +390,17 @@ int progress(bool *moved) {
     return 0;
 }
 
+bool g_coll_poisoned = false;  // a collective gave up a request mid-flight (p2p_abandon)
+
+int coll_context_check(int tag) {
+    if (tag <= kCollTagBase && g_coll_poisoned) {
+        MV2_ERR("an earlier collective failed with a message in flight: the library's collective context is "
+                "unusable (MPI_ERR_OTHER for every later collective that sends or receives)");
+        return E_OTHER;
+    }
+    return 0;
+}
+
 uint64_t add_req(Req *r) {
     const uint64_t id = g_next_id++;
     g_reqs[id] = r;
@@ -402,7 +414,7 @@ using namespace mv2;
 
 int mv2::p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req) {
     int rc = ready();
-    if (rc) return rc;
+    if (rc || (rc = coll_context_check(tag))) return rc;
     World &w = world();
     if (dest < 0 || dest >= w.gsize) return E_RANK;
     if (bytes && !buf) return E_BUFFER;
@@ -455,7 +467,7 @@ int mv2::p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned lo
 
 int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req) {
     int rc = ready();
-    if (rc) return rc;
+    if (rc || (rc = coll_context_check(tag))) return rc;
     World &w = world();
     if (source != MV2H_ANY_SOURCE && (source < 0 || source >= w.gsize)) return E_RANK;
     if (cap && !buf) return E_BUFFER;
@@ -497,6 +509,22 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
     g_posted.push_back(r);
     bool moved;
     return progress(&moved);
+}
+
+void mv2::p2p_abandon(unsigned long long id) {
+    auto it = g_reqs.find(id);
+    if (it == g_reqs.end()) return;
+    Req *r = it->second;
+    const auto pit = std::find(g_posted.begin(), g_posted.end(), r);
+    if (pit != g_posted.end() || r->done) {  // never matched (or finished): nothing refers to it
+        if (pit != g_posted.end()) g_posted.erase(pit);
+        g_reqs.erase(it);
+        delete r;
+        return;
+    }
+    // matched and still arriving, or a send still queued: the transport keeps referring to it, so
+    // it stays allocated, and later collectives refuse to run rather than match what follows
+    g_coll_poisoned = true;
 }
 
 extern "C" {

@@ -552,6 +552,25 @@ int world_init() {
         }
     }
     w.init_ms = ms_since(t_init);
+    // one line on the job's rank 0 (stderr) naming what MPI_Init decided for this node's
+    // device collectives, so a run's log explains itself even without its result line
+    // (MV2AMD_INIT_REPORT=0: silent; =1: also for a single-rank job)
+    const long rep = env_long("MV2AMD_INIT_REPORT", -1);
+    if (w.grank == 0 && (rep > 0 || (rep < 0 && w.gsize > 1))) {
+        const bool ran = w.size > 1 && w.size <= kMaxRanks && env_long("MV2AMD_SELFTEST", 1) != 0;
+        int g256 = 0;
+        size_t t256 = 0;
+        pipe_tiling_for(((size_t)256 << 20) / (size_t)w.size, &g256, &t256);  // a 256 MiB allreduce's segment
+        fprintf(stderr,
+                "[mv2amd] MPI_Init: %d ranks (%d per node, %d node%s, %d per GPU); self-test %s; tiling %s, %s stores "
+                "(256 MiB allreduce: %d workgroups x %zu KiB per round); one-shot up to %zu KiB; init %.1f ms "
+                "(self-test %.1f, autotune %.1f)\n",
+                w.gsize, w.size, w.nnodes, w.nnodes > 1 ? "s" : "", w.nshare,
+                !ran ? "not run" : w.light_release ? "passed, light release" : "passed, full system-scope release",
+                w.pipe_tuned ? "autotuned" : "default", w.pipe_rnt ? "non-temporal" : "plain", g256, t256 >> 10,
+                w.oneshot_max >> 10, w.init_ms, w.selftest_ms, w.tune_ms);
+        fflush(stderr);
+    }
     MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d): %.1f ms (self-test %.1f, autotune %.1f)",
               w.grank, w.gsize, w.rank, w.device, w.nshare, w.node, w.nnodes, w.init_ms, w.selftest_ms, w.tune_ms);
     return 0;

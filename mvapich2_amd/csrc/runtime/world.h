@@ -188,6 +188,7 @@ int global_barrier();  // node barrier, leaders' barrier across nodes, node barr
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
+void pipe_tiling_for(size_t seg_bytes, int *grid, size_t *tsub);  // coll.cpp: a segment's grid and bytes per round
 int pipe_autotune();  // coll.cpp: init-time choice of the pipelined kernels' tiling
 void host_prof_report();  // coll.cpp: MV2AMD_HOST_PROFILE summary
 // The library's own messages on the node's point-to-point channels (the steps of the multi-node
@@ -196,5 +197,9 @@ void host_prof_report();  // coll.cpp: MV2AMD_HOST_PROFILE summary
 constexpr int kCollTagBase = -0x100;
 int p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned long long *req);  // runtime/p2p.cpp
 int p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long long *req);
+// a collective's request given up after an error: an unmatched receive is withdrawn; one whose data
+// is still arriving (or a send still in flight) poisons the collective context, so every later
+// library collective fails instead of matching stale messages (runtime/p2p.cpp)
+void p2p_abandon(unsigned long long req);
 
 }  // namespace mv2

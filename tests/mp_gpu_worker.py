@@ -160,6 +160,36 @@ def big_case(L, case, rank, n):
             full = oracle.reduce_scatter_ref([x.view(np.uint8) for x in xs], counts, F, OPS["MPI_SUM"]).view(np.uint32)
             want = full[off:off + counts[rank]]
         return np.array([np.count_nonzero(got != want)])
+    if k == "gib_allreduce":
+        # configs[2]'s upper end at any n: 1 GiB fp32 SUM.  (a) the exact pattern, every element on
+        # every rank; (b) random N(0,1) operands drawn per 4 MiB block from (seed, rank, block), so
+        # rank 0 can regenerate any slice of any rank: it checks a slice of `slice` floats inside
+        # each ring chunk bit-exactly against the oracle's ring (oracle.allreduce algo 4 over the
+        # n slices laid out as the chunks of a smaller call: chunk c keeps its rotation x_c, x_c+1 ..)
+        cnt, sl = case["count"], case["slice"]
+        B = 1 << 20
+        per = np.resize(np.arange(1, 101, dtype=np.float32), cnt)
+        sb, rb = m.DeviceBuffer.from_array(per * np.float32(rank + 1)), m.DeviceBuffer(cnt * 4)
+        assert L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, F, OPS["MPI_SUM"], WORLD) == 0
+        bad = np.count_nonzero(rb.download(np.float32, count=cnt) != per * np.float32(n * (n + 1) // 2))
+        del per
+
+        def blocks(r, b0, nb):
+            return np.concatenate([np.random.default_rng([case["seed"], r, b]).standard_normal(B, dtype=np.float32)
+                                   for b in range(b0, b0 + nb)])
+        sb.upload(blocks(rank, 0, cnt // B))
+        assert L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, F, OPS["MPI_SUM"], WORLD) == 0
+        bad_rand = 0
+        if rank == 0:
+            from oracle import oracle
+            chunk = cnt // n
+            assert cnt % (n * B) == 0 and sl % B == 0 and chunk % B == 0
+            offs = [c * chunk + ((c * 7 + 3) * B) % (chunk - sl + B) // B * B for c in range(n)]
+            xs = [np.concatenate([blocks(r, o // B, sl // B) for o in offs]) for r in range(n)]
+            want = oracle.allreduce([x.view(np.uint8) for x in xs], n * sl, F, OPS["MPI_SUM"], algo=4)[0].view(np.uint32)
+            got = rb.download(np.uint32, count=cnt)
+            bad_rand = sum(np.count_nonzero(got[o:o + sl] != want[c * sl:(c + 1) * sl]) for c, o in enumerate(offs))
+        return np.array([bad, bad_rand])
     if k == "huge":  # operands above 4 GiB: 64-bit byte offsets through every kernel and copy
         cnt = case["count"]
         D = TYPES["MPI_DOUBLE"][0]
@@ -473,7 +503,7 @@ def main():
             res = rb.download(np.uint8, count=cnt * ext_f * 4)
             L.MPI_Op_free(ctypes.byref(op))
             L.MPI_Type_free(ctypes.byref(vt))
-        elif k.startswith("big_") or k == "huge":
+        elif k.startswith("big_") or k in ("huge", "gib_allreduce"):
             res = big_case(L, case, rank, n)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)

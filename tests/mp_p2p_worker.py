@@ -35,6 +35,11 @@ def get_count(L, st, dt):
     return c.value
 
 
+def step(k):
+    # where each rank was: a failed run prints every failed rank's tail (test_gpu_p2p_mp.py)
+    print(f"rank {os.environ['RANK']} step {k}", flush=True)
+
+
 def main():
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     L = m.lib()
@@ -42,6 +47,7 @@ def main():
     L.MPI_Comm_set_errhandler(WORLD, 0x54000001)
     right, left = (rank + 1) % n, (rank - 1) % n
 
+    step(1)
     # 1. ring exchange with Sendrecv at sizes below, at and above the 32 MiB channel ring (8 MiB chunks)
     for nbytes in (0, 1, 4093, 8 << 20, (8 << 20) + 17, 40 << 20):
         sb = m.DeviceBuffer.from_array(pattern(nbytes, rank, right, 5)) if nbytes else m.DeviceBuffer(1)
@@ -54,6 +60,7 @@ def main():
             got = rb.download(np.uint8, count=nbytes)
             assert np.array_equal(got, pattern(nbytes, left, rank, 5)), ("sendrecv data", nbytes)
 
+    step(2)
     # 2. tag matching out of order + ANY_SOURCE/ANY_TAG: rank 0 receives from every
     #    other rank, tags posted in reverse of the send order (unexpected queue)
     if rank != 0:
@@ -84,6 +91,7 @@ def main():
             seen.add(st.MPI_SOURCE)
         assert seen == set(range(1, n))
 
+    step(3)
     # 3. Isend/Irecv both directions with Waitall (must not deadlock above the ring size)
     nbytes = 48 << 20
     sb = m.DeviceBuffer.from_array(pattern(nbytes, rank, right, 9))
@@ -95,6 +103,7 @@ def main():
     assert L.MPI_Waitall(2, reqs, None) == 0 and reqs[0] == reqs[1] == 0x2c000000
     assert np.array_equal(rb.download(np.uint8, count=nbytes), pattern(nbytes, left, rank, 9))
 
+    step(4)
     # 4. truncation: 100 bytes into a 60-byte receive -> MPI_ERR_TRUNCATE (14), first 60 delivered
     sb = m.DeviceBuffer.from_array(pattern(100, rank, right, 11))
     rb = m.DeviceBuffer(60)
@@ -105,10 +114,12 @@ def main():
     assert np.array_equal(rb.download(np.uint8, count=60), pattern(100, left, rank, 11)[:60])
     assert L.MPI_Wait(ctypes.byref(rq), None) == 0
 
+    step(5)
     # 5. MPI_PROC_NULL
     st = Status()
     assert L.MPI_Recv(rb.ptr, 60, BYTE, PROC_NULL, 0, WORLD, ctypes.byref(st)) == 0 and st.MPI_SOURCE == PROC_NULL
 
+    step(6)
     # 6. derived type: MPI_Type_vector(64, 4, 8, MPI_FLOAT) send -> contiguous receive
     vt = ctypes.c_int()
     assert L.MPI_Type_vector(64, 4, 8, FLOAT, ctypes.byref(vt)) == 0 and L.MPI_Type_commit(ctypes.byref(vt)) == 0
@@ -121,6 +132,7 @@ def main():
     assert np.array_equal(rb.download(np.float32, count=256), want) and get_count(L, st, FLOAT) == 256
     L.MPI_Type_free(ctypes.byref(vt))
 
+    step(7)
     # 7. nonblocking collectives: two Iallreduce in flight (pipelined + one-shot sizes), Ibcast, Wait/Test
     cnt = 3 << 20
     a = m.DeviceBuffer.from_array(np.arange(cnt, dtype=np.int32) * (rank + 1))
@@ -142,9 +154,11 @@ def main():
     assert np.array_equal(ra.download(np.int32), (np.arange(cnt, dtype=np.int64) * tri).astype(np.int32))
     assert np.all(rbb.download(np.int32) == n)
     assert np.all(c.download(np.int32) == 77)
+    step("7b")
     rq = ctypes.c_int()
     assert L.MPI_Ibarrier(WORLD, ctypes.byref(rq)) == 0 and L.MPI_Wait(ctypes.byref(rq), None) == 0
 
+    step(8)
     # 8. MPI_Testall is all-or-nothing (MPI-3.1 §3.7.5): with one receive finished and one
     #    pending it returns flag = 0 and leaves both handles (and the finished one) intact
     if rank == 1:
@@ -179,9 +193,9 @@ def main():
             assert L.MPI_Testall(1, rest, ctypes.byref(flag), None) == 0
         assert rest[0] == 0x2c000000
         assert np.array_equal(r21.download(np.uint8, count=999), pattern(999, 1, 0, 21))
-    L.MPI_Barrier(WORLD)
-
-    L.MPI_Finalize()
+    step(9)
+    assert L.MPI_Barrier(WORLD) == 0
+    assert L.MPI_Finalize() == 0
     print(f"rank {rank} p2p ok", flush=True)
 
 

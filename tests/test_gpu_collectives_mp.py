@@ -391,7 +391,7 @@ def test_user_op_on_strided_vector_operand(n, tmp_path):
 
 
 @pytest.mark.timeout(480)
-@pytest.mark.parametrize("n", [2, 8])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_full_size_baseline_configs(n, tmp_path):
     """BASELINE configs[2]-[4] at their full sizes: 256 MiB fp32 SUM allreduce, 256 MiB
     reduce_scatter / allgather / bcast, 16 Mi-record MAXLOC on MPI_DOUBLE_INT; each rank checks
@@ -422,6 +422,19 @@ def test_allreduce_1gib_bit_exact(tmp_path):
     res = run_workers(n, cases, tmp_path, timeout=360)
     for r in range(n):
         assert int(res("gb1", r)[0]) == 0, (r, int(res("gb1", r)[0]))
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("n", [4, 8])
+def test_allreduce_1gib_n4_n8(n, tmp_path):
+    """configs[2]'s 1 GiB point at 4 and 8 ranks (osu_allreduce.c:98-163 sweeps to -M): an exact
+    integer-valued pattern checked over every element on every rank, then random N(0,1) operands
+    whose result rank 0 checks bit-exactly against the oracle's ring on a 64 MiB slice (one slice
+    inside each ring chunk; every rank regenerating 8 x 1 GiB of inputs would not fit the host)."""
+    cases = [{"id": "gn1", "kind": "gib_allreduce", "count": 1 << 28, "slice": (16 << 20) // n, "seed": 13}]
+    res = run_workers(n, cases, tmp_path, timeout=360)
+    for r in range(n):
+        assert [int(v) for v in res("gn1", r)] == [0, 0], (r, res("gn1", r))
 
 
 @pytest.mark.timeout(600)

@@ -70,3 +70,37 @@ def test_reduce_scatter_table_matches_the_reference_table(n):
     L = m.lib()
     for nbytes in SIZES + [64, 65, 1024, 1025, 65536, 65537, 100000, 131071, 131072, 262144, 262145]:
         assert RS_CODE[rs_reference_choice(n, nbytes)] == L.mv2h_reduce_scatter_table(n, nbytes), (n, nbytes)
+
+
+ROUTES = {0: "two-level", 1: "flat ring", 2: "flat programs", 3: "message schedule", 4: "two-level stand-in",
+          5: "basic reduce-scatter"}
+E_UNSUPPORTED = 44
+
+
+@pytest.mark.parametrize("ppn,gsize", [(1, 2), (2, 8), (4, 12), (8, 16), (8, 64), (1, 65), (8, 72), (9, 72),
+                                       (16, 128), (8, 128), (16, 1024)])
+def test_every_builtin_route_is_supported(ppn, gsize):
+    """above 64 ranks (no rank mesh) a flat algorithm's message schedule cannot
+    run; the multi-node dispatch (coll.cpp mn_*_route) must then take the two-level stand-in, never
+    refuse a builtin op.  Every size from 4 B to 1 GiB, blocking and nonblocking, IN_PLACE or not."""
+    L = m.lib()
+    rem = ctypes.c_int()
+    for k in range(2, 31):
+        for nbytes in (1 << k, (1 << k) + 4 * (gsize + 1)):
+            count = nbytes // 4
+            for coll, nbcs in ((0, (0, 1)), (1, (0, 2)), (2, (0, 3))):
+                for nbc in nbcs:
+                    for ip in (0, 1):
+                        r = L.mv2h_mn_route(coll, ppn, gsize, nbytes, count, ip, nbc, ctypes.byref(rem))
+                        where = (coll, nbytes, nbc, ip, r)
+                        assert r in ROUTES and r != E_UNSUPPORTED, where
+                        for route in (r, rem.value):
+                            if route == 3:
+                                assert 8 < gsize <= 64, where
+                            if route == 2:
+                                assert gsize <= 8, where
+                            if route == 4:
+                                assert gsize > 64, where
+                        if coll == 2 and gsize > 64:
+                            assert r == 5, where
+    assert L.mv2h_mn_route(0, 3, 8, 64, 16, 0, 0, None) == 12  # 8 ranks are not 3 per node

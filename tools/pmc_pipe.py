@@ -21,5 +21,11 @@ a.upload(np.random.default_rng(rank).uniform(-1, 1, n).astype(np.float32))
 for _ in range(6):
     m.check(L.MPI_Allreduce(a.ptr, b.ptr, n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], 0x44000000), "MPI_Allreduce")
 L.MPI_Barrier(0x44000000)
+cfg_out = os.environ.get("PMC_CONFIG_OUT")
+if cfg_out and rank == 0:  # the configuration bench.py matches a pass against (pipe_traffic_for)
+    import json
+    json.dump({"ranks": int(os.environ.get("WORLD_SIZE", "1")), "nshare": m.info("nshare"),
+               "pipe_grid": m.info("pipe_grid"), "pipe_sub": m.info("pipe_sub"), "pipe_rnt": m.info("pipe_rnt"),
+               "bytes": nbytes}, open(cfg_out, "w"))
 L.MPI_Finalize()
 print("done", rank)

@@ -20,6 +20,7 @@ def main():
     fetch_csv, write_csv, match, out = sys.argv[1:5]
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
     last = int(sys.argv[6]) if len(sys.argv) > 6 else 0  # keep only the last N launches (skip init self-tests)
+    cfg = json.load(open(sys.argv[7])) if len(sys.argv) > 7 else None  # the measured run's configuration
     f = per_kernel(fetch_csv, "FETCH_SIZE", match)
     w = per_kernel(write_csv, "WRITE_SIZE", match)
     if last:
@@ -33,6 +34,8 @@ def main():
            "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB -> bytes"}
     if alg:
         res["traffic_over_algorithmic"] = (fetch_b + write_b) / alg
+    if cfg:
+        res["config"] = cfg
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
