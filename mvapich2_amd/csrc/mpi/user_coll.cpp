@@ -1,9 +1,11 @@
 // user_coll.cpp — host-evaluated reductions (user MPI_Op, x87 builtin ops; see user_coll.h).
 //
 // Data path.  Operands travel packed: each rank packs its operand on the device (the strided
-// / run-table pack kernels; a host operand is packed on the host and uploaded) and the packed
-// operands are allgathered device to device.  The host then fetches only the element slices it
-// evaluates, unpacks them into the type's layout — the user function is called on the derived
+// / run-table pack kernels; a host operand is packed on the host and uploaded) and each rank
+// receives, device to device, only the packed element ranges it evaluates: an all-to-all of
+// ranges over the point-to-point channels where the work is split by ranges (below), the whole
+// operands (an allgather) where every rank evaluates every element.  The host then fetches only
+// the element slices it evaluates, unpacks them into the type's layout — the user function is called on the derived
 // type's layout, as the reference calls it on (char *)buf + disp * extent — runs the plan's
 // programs (one uop(in, inout) call per program step and element block, the calls the
 // reference's algorithm makes), packs the result's type-map bytes and returns them to the
@@ -16,7 +18,11 @@
 // local rank 0 and broadcast) and MPI_Reduce (only the root's result counts).  Those elements
 // are split in n ranges, rank r evaluates range r (in the ring: its own chunk, as in the
 // reference) and the packed results are allgathered, so each rank makes uop calls over (n-1)/n
-// of the operand instead of n-1 whole operands.  Where the programs differ between ranks
+// of the operand instead of n-1 whole operands, and receives (n-1)/n of one operand's bytes
+// (the reference's ring moves 2(n-1)/n of it per rank, allreduce_osu.c:3925-4005: the reduce-
+// scatter half here, the results' allgather the other).  MPI_Reduce gathers the results at the
+// root only; MPI_Reduce_scatter moves each rank only its own block of every operand.  Where the
+// programs differ between ranks
 // (recursive doubling, :360-630: each rank's own bracketing) every rank evaluates its own
 // result over every element, from the packed operands.
 //
@@ -69,7 +75,7 @@ void HostBuf::resize(size_t n) {
 namespace {
 
 // device scratch kept between calls, grown on demand
-enum DevSlot { DS_MINE, DS_ALL, DS_RES_MINE, DS_RES_ALL, DS_COUNT };
+enum DevSlot { DS_MINE, DS_ALL, DS_RES_MINE, DS_RES_ALL, DS_REM, DS_COUNT };
 char *dev_scratch(int slot, size_t bytes) {
     static void *p[DS_COUNT];
     static size_t cap[DS_COUNT];
@@ -106,34 +112,114 @@ Typed typed(MPI_Datatype dt) {
     return t;
 }
 
-// every rank's operand, packed, on the device: rank j's at all + j * P
+// every rank's operand, packed, on the device, for elements [lo, hi): rank j's element e at
+// all + j * stride + (e - lo) * tsize
 struct Operands {
     Typed t;
     int n;
-    size_t P;
+    size_t P;  // one whole packed operand
     const char *all;
+    size_t stride;
+    long lo, hi;
 };
 
-int stage_operands(const void *src, int count, const Typed &t, Operands &o) {
-    o.t = t;
-    o.n = job().n;
-    o.P = (size_t)count * (size_t)t.tsize;
-    char *mine = dev_scratch(DS_MINE, o.P);
-    char *all = dev_scratch(DS_ALL, o.P * (size_t)o.n);
-    if (!mine || !all) return MPI_ERR_NO_MEM;
+constexpr int kTagRanges = kCollTagBase - 4;  // the library's collective context (runtime/world.h)
+
+// this rank's operand packed on the device (DS_MINE)
+int pack_mine(const void *src, int count, const Typed &t, char **out) {
+    const size_t P = (size_t)count * (size_t)t.tsize;
+    char *mine = dev_scratch(DS_MINE, P);
+    if (!mine) return MPI_ERR_NO_MEM;
     int rc;
     if (mv2h_is_device_ptr(src)) {
         rc = dtype_pack(src, count, t.dt, mine);
     } else {
         HostBuf h(HS_PACKED);
-        h.resize(o.P + 1);
+        h.resize(P + 1);
         if (!h.data()) return MPI_ERR_NO_MEM;
         rc = dtype_pack(src, count, t.dt, h.data());
-        if (!rc && mv2h_memcpy_htod(mine, h.data(), o.P)) rc = MPI_ERR_OTHER;
+        if (!rc && mv2h_memcpy_htod(mine, h.data(), P)) rc = MPI_ERR_OTHER;
     }
-    if (!rc) rc = o.n > 1 ? mv2h_allgather(mine, all, o.P, nullptr) : (mv2h_memcpy_dtod(all, mine, o.P) ? MPI_ERR_OTHER : 0);
-    o.all = all;
+    *out = mine;
     return rc;
+}
+
+// every rank's whole packed operand on every rank (the device allgather)
+int gather_whole(const char *mine, int count, const Typed &t, int slot, Operands &o) {
+    o.t = t;
+    o.n = job().n;
+    o.P = (size_t)count * (size_t)t.tsize;
+    char *all = dev_scratch(slot, o.P * (size_t)o.n);
+    if (!all) return MPI_ERR_NO_MEM;
+    o.all = all;
+    o.stride = o.P;
+    o.lo = 0;
+    o.hi = count;
+    if (o.n == 1) return mv2h_memcpy_dtod(all, mine, o.P) ? MPI_ERR_OTHER : 0;
+    return mv2h_allgather(mine, all, o.P, nullptr);
+}
+
+// the point-to-point channels reach every rank of the job (every node's ranks up to the rank mesh)
+bool channels_reach_all() {
+    const World &w = world();
+    return w.nnodes == 1 || w.gsize <= kMeshMaxRanks;
+}
+
+// Elements [lo[me], hi[me]) of every rank's packed operand onto this rank (rank j's at
+// all + j * stride): an all-to-all of ranges over the point-to-point channels, each rank sent
+// only the range it evaluates.  Beyond the channels' reach: the whole operands, windowed.
+int exchange_ranges(const char *mine, int count, const Typed &t, const std::vector<long> &lo,
+                    const std::vector<long> &hi, Operands &o) {
+    const Job J = job();
+    const int n = J.n, me = J.me;
+    if (!channels_reach_all()) {
+        const int rc = gather_whole(mine, count, t, DS_ALL, o);
+        if (rc) return rc;
+        o.all += (size_t)lo[me] * (size_t)t.tsize;
+        o.lo = lo[me];
+        o.hi = hi[me];
+        return 0;
+    }
+    const size_t ts = (size_t)t.tsize, mb = (size_t)(hi[me] - lo[me]) * ts;
+    char *all = dev_scratch(DS_ALL, mb * (size_t)n);
+    if (!all) return MPI_ERR_NO_MEM;
+    o.t = t;
+    o.n = n;
+    o.P = (size_t)count * ts;
+    o.all = all;
+    o.stride = mb;
+    o.lo = lo[me];
+    o.hi = hi[me];
+    std::vector<unsigned long long> reqs;
+    reqs.reserve(2 * (size_t)n);
+    int rc = 0;
+    for (int j = 0; j < n && !rc; ++j) {
+        if (j == me || !mb) continue;
+        unsigned long long q = 0;
+        if (!(rc = p2p_irecv(all + (size_t)j * mb, mb, j, kTagRanges, &q))) reqs.push_back(q);
+    }
+    for (int j = 0; j < n && !rc; ++j) {
+        const size_t jb = (size_t)(hi[j] - lo[j]) * ts;
+        if (j == me || !jb) continue;
+        unsigned long long q = 0;
+        if (!(rc = p2p_isend(mine + (size_t)lo[j] * ts, jb, j, kTagRanges, &q))) reqs.push_back(q);
+    }
+    if (!rc && mb && mv2h_memcpy_dtod(all + (size_t)me * mb, mine + (size_t)lo[me] * ts, mb)) rc = MPI_ERR_OTHER;
+    for (unsigned long long q : reqs) {
+        if (rc) {
+            p2p_abandon(q);
+            continue;
+        }
+        if ((rc = mv2h_p2p_wait(q, nullptr, nullptr, nullptr))) p2p_abandon(q);
+    }
+    return rc ? MPI_ERR_OTHER : 0;
+}
+
+// the whole packed operands on every rank (every element evaluated by every rank)
+int stage_operands(const void *src, int count, const Typed &t, Operands &o) {
+    char *mine = nullptr;
+    const int rc = pack_mine(src, count, t, &mine);
+    return rc ? rc : gather_whole(mine, count, t, DS_ALL, o);
 }
 
 // Elements [b, e) of every rank's operand in the type's layout (element b at offset 0),
@@ -141,18 +227,20 @@ int stage_operands(const void *src, int count, const Typed &t, Operands &o) {
 int fetch(const Operands &o, long b, long e, HostBuf &W, long &rspan) {
     const Typed &t = o.t;
     const int cnt = (int)(e - b);
+    if (b < o.lo || e > o.hi) return MPI_ERR_INTERN;  // outside what this rank received
     rspan = dtype_span(t.dt, cnt);
     const size_t rb = (size_t)cnt * (size_t)t.tsize;
     W.resize((size_t)rspan * (size_t)o.n + 1);
     if (!W.data()) return MPI_ERR_NO_MEM;
-    const char *src = o.all + (size_t)b * (size_t)t.tsize;
+    if (!cnt) return 0;
+    const char *src = o.all + (size_t)(b - o.lo) * (size_t)t.tsize;
     if (t.contig)  // the slices land in place: one strided copy
-        return hipMemcpy2D(W.data(), (size_t)rspan, src, o.P, rb, (size_t)o.n, hipMemcpyDeviceToHost) == hipSuccess
+        return hipMemcpy2D(W.data(), (size_t)rspan, src, o.stride, rb, (size_t)o.n, hipMemcpyDeviceToHost) == hipSuccess
                    ? 0 : MPI_ERR_OTHER;
     HostBuf pk(HS_PACKED);
     pk.resize(rb * (size_t)o.n + 1);
     if (!pk.data()) return MPI_ERR_NO_MEM;
-    if (hipMemcpy2D(pk.data(), rb, src, o.P, rb, (size_t)o.n, hipMemcpyDeviceToHost) != hipSuccess) return MPI_ERR_OTHER;
+    if (hipMemcpy2D(pk.data(), rb, src, o.stride, rb, (size_t)o.n, hipMemcpyDeviceToHost) != hipSuccess) return MPI_ERR_OTHER;
     for (int j = 0; j < o.n; ++j) {
         const int rc = dtype_unpack(pk.data() + (size_t)j * rb, cnt, t.dt, W.data() + (size_t)j * (size_t)rspan);
         if (rc) return rc;
@@ -206,33 +294,96 @@ struct Split {
     long own_base;
 };
 
-int run_split(const Operands &o, int count, const Split &sp, MPI_User_function *fn, void *recvbuf, bool deliver) {
-    const Typed &t = o.t;
-    const int n = o.n, me = job().me;
+// The operands a split needs, staged: the uniform part [0, U) by ranges (rank r gets range r of
+// every operand, ou), the own part [U, count) whole on every rank (oo; an allgather of those
+// elements only).  U = 0: every rank's whole operand (recursive doubling: each rank's own tree).
+int stage_split(const void *src, int count, const Typed &t, const Split &sp, Operands &ou, Operands &oo) {
+    char *mine = nullptr;
+    int rc = pack_mine(src, count, t, &mine);
+    if (rc) return rc;
+    if (sp.U == 0) return gather_whole(mine, count, t, DS_ALL, oo);
+    const int n = job().n;
+    const long chunk = (sp.U + n - 1) / n;
+    std::vector<long> lo((size_t)n), hi((size_t)n);
+    for (int j = 0; j < n; ++j) {
+        lo[j] = std::min<long>(sp.U, (long)j * chunk);
+        hi[j] = std::min<long>(sp.U, lo[j] + chunk);
+    }
+    if ((rc = exchange_ranges(mine, count, t, lo, hi, ou))) return rc;
+    if (sp.U < count) {  // the own part: those elements of every operand
+        const size_t rb = (size_t)(count - sp.U) * (size_t)t.tsize;
+        char *rem = dev_scratch(DS_REM, rb * (size_t)n);
+        if (!rem) return MPI_ERR_NO_MEM;
+        if ((rc = mv2h_allgather(mine + (size_t)sp.U * (size_t)t.tsize, rem, rb, nullptr))) return rc;
+        oo = Operands{t, n, (size_t)count * (size_t)t.tsize, rem, rb, sp.U, count};
+    }
+    return 0;
+}
+
+// Every rank's range of results (packed; range j of `chunk` elements, the last ones short or empty)
+// into res_all at j * chunk: allgathered (root < 0), or gathered at the root over the point-to-point
+// channels (MPI_Reduce: only the root's result counts)
+int collect_results(const char *res_mine, char *res_all, long U, long chunk, size_t tsize, int root) {
+    const Job J = job();
+    const int n = J.n, me = J.me;
+    const size_t cb = (size_t)chunk * tsize;
+    if (root < 0 || !channels_reach_all()) return mv2h_allgather(res_mine, res_all, cb, nullptr);
+    auto bytes_of = [&](int j) { return (size_t)(std::min<long>(U, (long)(j + 1) * chunk) - std::min<long>(U, (long)j * chunk)) * tsize; };
+    int rc = 0;
+    unsigned long long q = 0;
+    if (me != root) {
+        if (!bytes_of(me)) return 0;
+        if ((rc = p2p_isend(res_mine, bytes_of(me), root, kTagRanges, &q))) return MPI_ERR_OTHER;
+        if ((rc = mv2h_p2p_wait(q, nullptr, nullptr, nullptr))) p2p_abandon(q);
+        return rc ? MPI_ERR_OTHER : 0;
+    }
+    std::vector<unsigned long long> reqs;
+    for (int j = 0; j < n && !rc; ++j) {
+        if (j == me || !bytes_of(j)) continue;
+        if (!(rc = p2p_irecv(res_all + (size_t)j * cb, bytes_of(j), j, kTagRanges, &q))) reqs.push_back(q);
+    }
+    if (!rc && bytes_of(me) && mv2h_memcpy_dtod(res_all + (size_t)me * cb, res_mine, bytes_of(me))) rc = MPI_ERR_OTHER;
+    for (unsigned long long r : reqs) {
+        if (rc) {
+            p2p_abandon(r);
+            continue;
+        }
+        if ((rc = mv2h_p2p_wait(r, nullptr, nullptr, nullptr))) p2p_abandon(r);
+    }
+    return rc ? MPI_ERR_OTHER : 0;
+}
+
+// root < 0: every rank delivers the result; root >= 0: the root only
+int run_split(const void *src, int count, const Typed &t, const Split &sp, MPI_User_function *fn, void *recvbuf,
+              int root) {
+    const int n = job().n, me = job().me;
+    const bool deliver = root < 0 || me == root;
+    Operands ou{}, oo{};
+    int rc = stage_split(src, count, t, sp, ou, oo);
+    if (rc) return rc;
     const long chunk = sp.U ? (sp.U + n - 1) / n : 0;
     const long mb = std::min<long>(sp.U, (long)me * chunk), me_e = std::min<long>(sp.U, mb + chunk);
     char *res_all = dev_scratch(DS_RES_ALL, (size_t)std::max<long>((long)n * chunk, count) * (size_t)t.tsize);
     if (!res_all) return MPI_ERR_NO_MEM;
     HostBuf W(HS_OPERANDS), R(HS_RESULT);
     long rspan = 0;
-    int rc = 0;
     if (sp.U > 0) {
         const size_t cb = (size_t)chunk * (size_t)t.tsize;
         char *res_mine = dev_scratch(DS_RES_MINE, cb);
         R.resize(cb + 1);
         if (!res_mine || !R.data()) return MPI_ERR_NO_MEM;
         if (me_e > mb) {
-            if ((rc = fetch(o, mb, me_e, W, rspan))) return rc;
+            if ((rc = fetch(ou, mb, me_e, W, rspan))) return rc;
             if ((rc = eval_range(*sp.uni, 0, W.data(), rspan, mb, me_e, t, fn, R.data()))) return rc;
             if (mv2h_memcpy_htod(res_mine, R.data(), (size_t)(me_e - mb) * t.tsize)) return MPI_ERR_OTHER;
         }
         // a short (or empty) last range leaves its padding at or after element U, where the
         // own part below (or nothing) lands
-        if ((rc = mv2h_allgather(res_mine, res_all, cb, nullptr))) return rc;
+        if ((rc = collect_results(res_mine, res_all, sp.U, chunk, (size_t)t.tsize, root))) return rc;
     }
-    if (sp.U < count) {
+    if (sp.U < count && deliver) {
         const size_t ob = (size_t)(count - sp.U) * (size_t)t.tsize;
-        if ((rc = fetch(o, sp.U, count, W, rspan))) return rc;
+        if ((rc = fetch(oo, sp.U, count, W, rspan))) return rc;
         R.resize(ob + 1);
         if (!R.data()) return MPI_ERR_NO_MEM;
         if ((rc = eval_range(*sp.own, sp.own_base, W.data(), rspan, sp.U, count, t, fn, R.data()))) return rc;
@@ -571,8 +722,9 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
         if ((rc = mn_host_schedule(MN_COLL_ALLREDUCE, (size_t)count, (int)t.tsize, (int)t.extent, in_place, op.opk, -1,
                                    &sc)))
             return rc == E_UNSUPPORTED ? MPI_ERR_UNSUPPORTED_OPERATION : MPI_ERR_INTERN;
+        const bool whole = sc.kind == MN_TWO_LEVEL || sc.big || (sc.forced != ALG_RING && sc.U && sc.U < count);
         Operands o;
-        if ((rc = stage_operands(src, count, t, o))) return rc;
+        if (whole && (rc = stage_operands(src, count, t, o))) return rc;
         if (sc.kind == MN_TWO_LEVEL) {
             char *res = dev_scratch(DS_RES_ALL, (size_t)count * (size_t)t.tsize);
             if (!res) return MPI_ERR_NO_MEM;
@@ -590,7 +742,7 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
         } else {
             sp = Split{&p.ps, uniform_over_ranks(n, me, count, t, in_place, forced, op.opk, p.ps) ? count : 0, &p.ps, 0};
         }
-        return run_split(o, count, sp, op.fn, recvbuf, true);
+        return run_split(src, count, t, sp, op.fn, recvbuf, -1);
     }
     rc = plan_allreduce(n, me, (size_t)count, (int)t.tsize, (int)t.extent, in_place, 0, &p, op.opk);
     if (rc) return rc;
@@ -609,9 +761,7 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
     } else {
         sp.U = uniform_over_ranks(n, me, count, t, in_place, 0, op.opk, p.ps) ? count : 0;
     }
-    Operands o;
-    if ((rc = stage_operands(src, count, t, o))) return rc;
-    return run_split(o, count, sp, op.fn, recvbuf, true);
+    return run_split(src, count, t, sp, op.fn, recvbuf, -1);
 }
 
 // MPI_Reduce: the root's programs (MPIR_Reduce_index_tuned_intra_MV2's choice, binomial /
@@ -630,28 +780,26 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
         if ((rc = mn_host_schedule(MN_COLL_REDUCE, (size_t)count, (int)t.tsize, (int)t.extent, sendbuf == MPI_IN_PLACE,
                                    op.opk, root, &sc)))
             return rc == E_UNSUPPORTED ? MPI_ERR_UNSUPPORTED_OPERATION : MPI_ERR_INTERN;
-        Operands o;
-        if ((rc = stage_operands(src, count, t, o))) return rc;
-        if (sc.kind == MN_TWO_LEVEL) {  // only the root's result counts: the root evaluates it
-            if (me != root) return MPI_SUCCESS;
+        if (sc.kind == MN_TWO_LEVEL || sc.big) {
+            Operands o;
+            if ((rc = stage_operands(src, count, t, o))) return rc;
+            if (sc.big) return run_big_flat(o, count, sc, op, recvbuf, me == root);
+            if (me != root) return MPI_SUCCESS;  // only the root's result counts: the root evaluates it
             char *res = dev_scratch(DS_RES_ALL, (size_t)count * (size_t)t.tsize);
             if (!res) return MPI_ERR_NO_MEM;
             if ((rc = run_two_level(o, count, sc, op.fn, res))) return rc;
             return dtype_unpack(res, count, t.dt, recvbuf);
         }
-        if (sc.big) return run_big_flat(o, count, sc, op, recvbuf, me == root);
         if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
         const Split sp{&pr.ps, count, &pr.ps, 0};
-        return run_split(o, count, sp, op.fn, recvbuf, me == root);
+        return run_split(src, count, t, sp, op.fn, recvbuf, root);
     }
     rc = plan_reduce(n, me, root, (size_t)count, (int)t.tsize, (int)t.extent, &p, op.opk);
     if (rc) return rc;
     pvar_note(PV_COLL_REDUCE, p, sendbuf == MPI_IN_PLACE, (size_t)count, n);  // every rank runs the algorithm
     if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
-    Operands o;
-    if ((rc = stage_operands(src, count, t, o))) return rc;
     const Split sp{&pr.ps, count, &pr.ps, 0};
-    return run_split(o, count, sp, op.fn, recvbuf, me == root);
+    return run_split(src, count, t, sp, op.fn, recvbuf, root);
 }
 
 // Reduce_scatter: the order of MPIR_Reduce_scatter_MV2's choice for this rank's block — ring,
@@ -704,10 +852,27 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
             ps.p[0].src[s] = (uint8_t)(n - 2 - s);
         }
     }
+    // each rank receives only its own block of every operand (an all-to-all of blocks), except the
+    // multi-node basic algorithm, whose reduce every rank evaluates whole
+    const bool basic_mn = J.multi && op.opk != OPK_USER_NONCOMM && p.algo == ALG_RS_BASIC;
     Operands o;
-    if ((rc = stage_operands(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, (int)total, t, o))) return rc;
+    {
+        const void *src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+        if (basic_mn) {
+            rc = stage_operands(src, (int)total, t, o);
+        } else {
+            char *mine = nullptr;
+            std::vector<long> lo((size_t)n), hi((size_t)n);
+            for (long j = 0, d = 0; j < n; d += counts[j], ++j) {
+                lo[j] = d;
+                hi[j] = d + counts[j];
+            }
+            if (!(rc = pack_mine(src, (int)total, t, &mine))) rc = exchange_ranges(mine, (int)total, t, lo, hi, o);
+        }
+        if (rc) return rc;
+    }
     const int c = counts[me];
-    if (J.multi && op.opk != OPK_USER_NONCOMM && p.algo == ALG_RS_BASIC) {
+    if (basic_mn) {
         // MPIR_Reduce_Scatter_Basic_MV2 (red_scat_osu.c:300-413): MPIR_Reduce_MV2 to rank 0 over the
         // whole job — the two-level reduce helper for a commutative op — then the scatter: every
         // rank evaluates that reduce's result (a basic operand is at most a few hundred bytes)
