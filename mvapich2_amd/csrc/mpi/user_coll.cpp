@@ -155,6 +155,8 @@ int gather_whole(const char *mine, int count, const Typed &t, int slot, Operands
     o.stride = o.P;
     o.lo = 0;
     o.hi = count;
+    world().uop_in_bytes = o.P * (size_t)(o.n - 1);
+    world().uop_area_bytes = o.P * (size_t)o.n;
     if (o.n == 1) return mv2h_memcpy_dtod(all, mine, o.P) ? MPI_ERR_OTHER : 0;
     return mv2h_allgather(mine, all, o.P, nullptr);
 }
@@ -190,6 +192,8 @@ int exchange_ranges(const char *mine, int count, const Typed &t, const std::vect
     o.stride = mb;
     o.lo = lo[me];
     o.hi = hi[me];
+    world().uop_in_bytes = mb * (size_t)(n - 1);
+    world().uop_area_bytes = mb * (size_t)n;
     std::vector<unsigned long long> reqs;
     reqs.reserve(2 * (size_t)n);
     int rc = 0;

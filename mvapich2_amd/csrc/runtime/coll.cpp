@@ -786,6 +786,8 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "init_us")) *value = (long)(w.init_ms * 1e3 + 0.5);
     else if (!strcmp(key, "selftest_us")) *value = (long)(w.selftest_ms * 1e3 + 0.5);
     else if (!strcmp(key, "autotune_us")) *value = (long)(w.tune_ms * 1e3 + 0.5);
+    else if (!strcmp(key, "uop_in_bytes")) *value = (long)w.uop_in_bytes;
+    else if (!strcmp(key, "uop_area_bytes")) *value = (long)w.uop_area_bytes;
     else if (!strncmp(key, "os_tune_one_", 12) || !strncmp(key, "os_tune_pipe_", 13)) {
         const long i = strtol(strrchr(key, '_') + 1, nullptr, 10);
         if (i < 0 || i >= w.os_tune_n) return E_ARG;

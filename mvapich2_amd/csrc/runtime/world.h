@@ -157,7 +157,8 @@ struct World {
     int tune_grid[kTuneMax] = {};
     size_t tune_sub[kTuneMax] = {};
     double tune_us[kTuneMax] = {};                // max over ranks per candidate
-    double init_ms = 0, selftest_ms = 0, tune_ms = 0;  // MPI_Init wall time and its self-test / autotune parts
+    double init_ms = 0, selftest_ms = 0, tune_ms = 0;
+    size_t uop_in_bytes = 0, uop_area_bytes = 0;  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)

@@ -501,6 +501,9 @@ def main():
             rc = L.MPI_Allreduce(sb.ptr, rb.ptr, cnt, vt.value, op.value, WORLD)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=cnt * ext_f * 4)
+            # the operand bytes this rank received, and its receive area (mpi/user_coll.cpp staging)
+            np.save(os.path.join(out, f"{case['id']}_staged_r{rank}.npy"),
+                    np.array([m.info("uop_in_bytes"), m.info("uop_area_bytes")], dtype=np.int64))
             L.MPI_Op_free(ctypes.byref(op))
             L.MPI_Type_free(ctypes.byref(vt))
         elif k.startswith("big_") or k in ("huge", "gib_allreduce"):

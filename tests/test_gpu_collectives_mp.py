@@ -388,6 +388,19 @@ def test_user_op_on_strided_vector_operand(n, tmp_path):
             assert np.array_equal(typemap(got).reshape(cnt, nb * 4).view(np.uint32),
                                   want[r].reshape(cnt, nb * 4).view(np.uint32)), (case["id"], r)
             assert np.all(gaps(got) == -7.0), f"{case['id']} rank {r}: gap bytes of the vector type were written"
+            # operands move reduce-scatter-shaped where the ring splits the work (count >= n): each
+            # rank receives (n-1)/n of one packed operand (P) into a P-byte area; recursive doubling
+            # (count < n) needs every operand whole
+            inb, area = (int(v) for v in res(case["id"] + "_staged", r))
+            P = cnt * nb * 16
+            ring = cnt * nb * 16 >= (2 << 20) and cnt >= n  # the ring wrapper (2 MiB and up, n <= 8)
+            if ring:
+                chunk = cnt // n
+                assert inb == (n - 1) * chunk * nb * 16 and area == n * chunk * nb * 16 <= P, \
+                    (case["id"], r, inb, area, P)
+            else:  # smaller: a tree order (split by ranges) or recursive doubling (whole operands)
+                assert inb <= (n - 1) * P and (inb == (n - 1) * P or inb <= (n - 1) * -(-cnt // n) * nb * 16), \
+                    (case["id"], r, inb, P)
 
 
 @pytest.mark.timeout(480)
