@@ -95,6 +95,7 @@ static inline bool hp_on() {
 static bool g_call_start = true;  // tmark0: record ev0 at the first launch of this API call
 static inline void hp_entry() {
     g_call_start = true;
+    beacon(BC_ENTRY, true);
     if (hp_on()) g_hp.t_entry = now_ns();
 }
 static inline void hp_done() {
@@ -178,6 +179,18 @@ static int check_err_word() {
             "%llu from ranks 0x%x; flags seen:%s; host epoch %llu, round %llu, one-shot calls %llu, call %llu",
             e[1], (unsigned long long)ep, (unsigned)e[4], seen, (unsigned long long)w.epoch, (unsigned long long)w.round,
             (unsigned long long)w.os_calls, (unsigned long long)w.done_seq);
+    // where each late peer's host is now (its beacon in the control segment), next to this rank's
+    if (w.shm) {
+        const uint64_t t = now_ns();
+        for (int j = 0; j < w.size && j < kMaxRanks; ++j) {
+            const uint64_t v = (uint64_t)(uint32_t)e[8 + 2 * j] | ((uint64_t)(uint32_t)e[9 + 2 * j] << 32);
+            if (j != w.rank && !((((unsigned)e[4] >> j) & 1u) && v < ep)) continue;
+            const uint64_t b = w.shm->r[j].beacon.load(std::memory_order_relaxed);
+            const uint64_t bt = w.shm->r[j].beacon_ns.load(std::memory_order_relaxed);
+            MV2_ERR("  %s local rank %d: library call %llu, %s, for %.1f ms", j == w.rank ? "this is" : "late peer:", j,
+                    (unsigned long long)(b >> 8), beacon_name((int)(b & 0xff)), bt && t > bt ? (t - bt) / 1e6 : 0.0);
+        }
+    }
     memset(e + 1, 0, (kErrWords - 1) * sizeof(int));
     __atomic_store_n(e, 0, __ATOMIC_RELEASE);
     return E_OTHER;
@@ -195,6 +208,7 @@ static int finish(hipStream_t st, bool timed) {
         return 0;
     }
     if (w.defer) w.deferred = 0;
+    beacon(BC_WAIT);
     if (want) {
         e = wait_done(st, want);
         if (e == hipSuccess && timed) e = hipEventSynchronize(w.ev1);
@@ -211,6 +225,7 @@ static int finish(hipStream_t st, bool timed) {
         w.last_ms = ms;
     }
     if (check_err_word()) return E_OTHER;
+    beacon(BC_DONE);
     hp_done();
     return 0;
 }
@@ -218,6 +233,7 @@ static int finish(hipStream_t st, bool timed) {
 // kernel-time events bracket the call's first launch to its last (calls made of several
 // launches: ring main part + remainder, staged copies)
 static inline void tmark0(hipStream_t st) {
+    if (g_call_start) beacon(BC_LAUNCH);
     if (world().timing && g_call_start) hipEventRecord(world().ev0, st);
     g_call_start = false;
     if (hp_on() && g_hp.t_entry && !g_hp.t_l0) g_hp.t_l0 = now_ns();

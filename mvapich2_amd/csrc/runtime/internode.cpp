@@ -266,19 +266,23 @@ int link_fd(int peer) {
 }  // namespace
 
 int net_send(int peer, const void *buf, size_t bytes) {
+    beacon(BC_NET);
     const int fd = link_fd(peer);
     return fd < 0 ? E_INTERN : xfer(fd, (const char *)buf, bytes, nullptr, 0, peer);
 }
 int net_recv(int peer, void *buf, size_t bytes) {
+    beacon(BC_NET);
     const int fd = link_fd(peer);
     return fd < 0 ? E_INTERN : xfer(fd, nullptr, 0, (char *)buf, bytes, peer);
 }
 int net_sendrecv(int peer, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes) {
+    beacon(BC_NET);
     const int fd = link_fd(peer);
     return fd < 0 ? E_INTERN : xfer(fd, (const char *)sbuf, sbytes, (char *)rbuf, rbytes, peer);
 }
 
 int net_shift(int to, const void *sbuf, size_t sbytes, int from, void *rbuf, size_t rbytes) {
+    beacon(BC_NET);
     if (to == from) return net_sendrecv(to, sbuf, sbytes, rbuf, rbytes);
     const int fo = link_fd(to), fi = link_fd(from);
     return fo < 0 || fi < 0 ? E_INTERN : xfer2(fo, (const char *)sbuf, sbytes, fi, (char *)rbuf, rbytes, to, from);

@@ -575,6 +575,7 @@ int mv2h_p2p_peek(unsigned long long id, int *done) {
 
 int mv2h_p2p_wait(unsigned long long id, int *source, int *tag, size_t *bytes) {
     if (g_reqs.find(id) == g_reqs.end()) return E_REQUEST;
+    beacon(BC_P2P_WAIT);
     const auto t0 = std::chrono::steady_clock::now();
     const char *tv = getenv("MV2AMD_TIMEOUT_S");
     const double limit = (tv && *tv) ? atof(tv) : 120.0;

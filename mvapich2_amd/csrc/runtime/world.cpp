@@ -79,9 +79,38 @@ static std::string job_key() {
     return std::string(buf);
 }
 
+static uint64_t mono_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+void beacon(int phase, bool new_call) {
+    World &w = g_world;
+    if (new_call) ++w.api_calls;
+    if (w.size == 1 || !w.shm) return;
+    ShmRank &r = w.shm->r[w.rank];
+    r.beacon.store((w.api_calls << 8) | (uint64_t)phase, std::memory_order_relaxed);
+    r.beacon_ns.store(mono_ns(), std::memory_order_relaxed);
+}
+
+const char *beacon_name(int phase) {
+    switch (phase) {
+    case BC_ENTRY: return "entered a call, before its first kernel launch (planning / staging copies)";
+    case BC_LAUNCH: return "launching the call's kernel";
+    case BC_WAIT: return "waiting for its kernel to complete";
+    case BC_DONE: return "between calls (the last one completed)";
+    case BC_BARRIER: return "in a host barrier";
+    case BC_P2P_WAIT: return "waiting for a point-to-point request";
+    case BC_NET: return "on the leaders' inter-node links";
+    default: return "not yet in a call";
+    }
+}
+
 void host_barrier() {
     World &w = g_world;
     if (w.size == 1 || !w.shm) return;
+    beacon(BC_BARRIER);
     const uint64_t g = ++w.bar_gen;
     w.shm->r[w.rank].arrive.store(g, std::memory_order_release);
     const auto t0 = std::chrono::steady_clock::now();

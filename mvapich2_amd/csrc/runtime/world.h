@@ -76,6 +76,10 @@ struct alignas(64) ShmRank {
     int topo_nlevels;               // this rank's topology levels (world.cpp my_topology)
     int topo_color[kTopoLevels];    // its cluster id per level
     int mesh_port;                  // this rank's rank-mesh listener (internode.cpp mesh_setup)
+    // where this rank's host is (world.cpp beacon): (API call number << 8) | Beacon phase, and
+    // when it got there; a peer whose device wait runs out prints every late rank's beacon
+    std::atomic<uint64_t> beacon;
+    std::atomic<uint64_t> beacon_ns;
 };
 
 constexpr int kMeshMaxRanks = 64;  // jobs up to this many ranks get the rank mesh (p2p across nodes)
@@ -158,7 +162,8 @@ struct World {
     size_t tune_sub[kTuneMax] = {};
     double tune_us[kTuneMax] = {};                // max over ranks per candidate
     double init_ms = 0, selftest_ms = 0, tune_ms = 0;
-    size_t uop_in_bytes = 0, uop_area_bytes = 0;  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
+    size_t uop_in_bytes = 0, uop_area_bytes = 0;
+    uint64_t api_calls = 0;  // library calls entered (the beacon's call number)  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
@@ -185,6 +190,10 @@ World &world();
 int world_init();
 int world_finalize();
 void host_barrier();
+// beacon phases (ShmRank::beacon)
+enum Beacon { BC_ENTRY = 1, BC_LAUNCH = 2, BC_WAIT = 3, BC_DONE = 4, BC_BARRIER = 5, BC_P2P_WAIT = 6, BC_NET = 7 };
+void beacon(int phase, bool new_call = false);
+const char *beacon_name(int phase);
 int global_barrier();  // node barrier, leaders' barrier across nodes, node barrier
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
