@@ -126,6 +126,7 @@ static Done arm_done(hipStream_t st) {
 }
 
 static inline hipError_t enq_copy(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    beacon(BC_COPY_OUT);
     world().pending = 0;
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
 }
@@ -189,6 +190,7 @@ static int check_err_word() {
             const uint64_t bt = w.shm->r[j].beacon_ns.load(std::memory_order_relaxed);
             MV2_ERR("  %s local rank %d: library call %llu, %s, for %.1f ms", j == w.rank ? "this is" : "late peer:", j,
                     (unsigned long long)(b >> 8), beacon_name((int)(b & 0xff)), bt && t > bt ? (t - bt) / 1e6 : 0.0);
+            beacon_report(j, t);
         }
     }
     memset(e + 1, 0, (kErrWords - 1) * sizeof(int));
@@ -239,6 +241,7 @@ static inline void tmark0(hipStream_t st) {
     if (hp_on() && g_hp.t_entry && !g_hp.t_l0) g_hp.t_l0 = now_ns();
 }
 static inline void tmark1(hipStream_t st) {
+    beacon(BC_LAUNCHED);
     if (world().timing) hipEventRecord(world().ev1, st);
     if (hp_on() && g_hp.t_entry) g_hp.t_l1 = now_ns();
 }
@@ -1119,6 +1122,7 @@ static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, 
     s.user_recv = recv;
     s.bytes = rbytes;
     const bool recv_ok = is_device(recv) && ((uintptr_t)recv % 16 == 0);
+    beacon(BC_STAGE);
     if (recv_ok) {
         s.recv = (char *)recv;
     } else {
@@ -1469,6 +1473,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     } else {
         char *t = (char *)get_scratch(0, padded);
         if (!t) return E_NO_MEM;
+        beacon(BC_STAGE);
         size_t o = 0, po = 0;
         for (int j = 0; j < n; ++j) {
             const size_t len = recvcounts[j] * ext;

@@ -90,8 +90,29 @@ void beacon(int phase, bool new_call) {
     if (new_call) ++w.api_calls;
     if (w.size == 1 || !w.shm) return;
     ShmRank &r = w.shm->r[w.rank];
-    r.beacon.store((w.api_calls << 8) | (uint64_t)phase, std::memory_order_relaxed);
-    r.beacon_ns.store(mono_ns(), std::memory_order_relaxed);
+    const uint64_t code = (w.api_calls << 8) | (uint64_t)phase, t = mono_ns();
+    r.beacon.store(code, std::memory_order_relaxed);
+    r.beacon_ns.store(t, std::memory_order_relaxed);
+    const uint32_t k = r.bh_pos.load(std::memory_order_relaxed);
+    r.bh_code[k % 16].store(code, std::memory_order_relaxed);
+    r.bh_ns[k % 16].store(t, std::memory_order_relaxed);
+    r.bh_pos.store(k + 1, std::memory_order_relaxed);
+}
+
+void beacon_report(int j, uint64_t now) {
+    World &w = g_world;
+    if (!w.shm || j < 0 || j >= w.size) return;
+    ShmRank &r = w.shm->r[j];
+    const uint32_t pos = r.bh_pos.load(std::memory_order_relaxed);
+    char line[1024];
+    int o = 0;
+    for (uint32_t i = pos > 16 ? pos - 16 : 0; i < pos && o < (int)sizeof(line) - 64; ++i) {
+        const uint64_t c = r.bh_code[i % 16].load(std::memory_order_relaxed), t = r.bh_ns[i % 16].load(std::memory_order_relaxed);
+        o += snprintf(line + o, sizeof(line) - o, " %llu:%d@-%.1fms", (unsigned long long)(c >> 8), (int)(c & 0xff),
+                      t && now > t ? (now - t) / 1e6 : 0.0);
+    }
+    line[o] = 0;
+    MV2_ERR("    local rank %d beacon history (call:phase@age):%s", j, line);
 }
 
 const char *beacon_name(int phase) {
@@ -103,6 +124,10 @@ const char *beacon_name(int phase) {
     case BC_BARRIER: return "in a host barrier";
     case BC_P2P_WAIT: return "waiting for a point-to-point request";
     case BC_NET: return "on the leaders' inter-node links";
+    case BC_SCRATCH: return "growing device scratch (hipFree + hipMalloc)";
+    case BC_STAGE: return "staging operands to the device";
+    case BC_COPY_OUT: return "copying a result out";
+    case BC_LAUNCHED: return "after the kernel launch";
     default: return "not yet in a call";
     }
 }
@@ -132,6 +157,7 @@ void host_barrier() {
 void *get_scratch(int idx, size_t bytes) {
     World &w = g_world;
     if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];
+    beacon(BC_SCRATCH);
     if (w.scratch[idx]) {
         hipStreamSynchronize(w.stream);
         hipFree(w.scratch[idx]);
@@ -142,6 +168,49 @@ void *get_scratch(int idx, size_t bytes) {
     if (hipMalloc(&w.scratch[idx], sz) != hipSuccess) return nullptr;
     w.scratch_bytes[idx] = sz;
     return w.scratch[idx];
+}
+
+// GPUs this process can see, counted without initialising HIP: the KFD topology's GPU nodes,
+// narrowed by a visibility list if one is set (every entry counts as one device)
+static int gpus_visible_before_hip() {
+    int n = 0;
+    for (int i = 0; i < 256; ++i) {
+        char path[96];
+        snprintf(path, sizeof(path), "/sys/class/kfd/kfd/topology/nodes/%d/gpu_id", i);
+        FILE *f = fopen(path, "r");
+        if (!f) break;
+        long id = 0;
+        if (fscanf(f, "%ld", &id) == 1 && id != 0) ++n;
+        fclose(f);
+    }
+    for (const char *v : {"ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"}) {
+        const char *e = getenv(v);
+        if (!e || !*e) continue;
+        int k = 1;
+        for (const char *c = e; *c; ++c) k += *c == ',';
+        if (n == 0 || k < n) n = k;
+    }
+    return n;
+}
+
+// Several ranks on one GPU (tests, the one-GPU box, mv2run --share-gpu): every collective
+// kernel needs its peers' kernels resident at the same time, and with HIP's default 4 hardware
+// queues per process five ranks' queues starve each other — one rank's kernel was not dispatched
+// for 30 s while the others' kernels spun (profiles/r04f_queue_starvation.txt; 3 ms with 2 queues
+// per process).  So before HIP starts, a process that will share its GPU asks for 2 hardware queues
+// unless GPU_MAX_HW_QUEUES is set (MV2AMD_HW_QUEUES=0 leaves it alone, =k asks for k).  One rank
+// per GPU is not touched.  Returns the value set, or 0.
+static int limit_hw_queues_if_shared(int local_size) {
+    const long want = env_long("MV2AMD_HW_QUEUES", 2);
+    if (want <= 0 || getenv("GPU_MAX_HW_QUEUES")) return 0;
+    const int ndev = gpus_visible_before_hip();
+    const bool shared = env_long("MV2AMD_NSHARE", 1) > 1 || (getenv("MV2AMD_DEVICE") && local_size > 1) ||
+                        (ndev > 0 && local_size > ndev);
+    if (!shared) return 0;
+    char v[24];
+    snprintf(v, sizeof(v), "%ld", want);
+    setenv("GPU_MAX_HW_QUEUES", v, 0);
+    return (int)want;
 }
 
 static int setup_device_common() {
@@ -362,6 +431,7 @@ int world_init() {
     const char *cpo = getenv("MV2AMD_CONTROL_PLANE_ONLY");
     const bool control_only = cpo && *cpo == '1';
     if (!w.stream && !control_only) {
+        w.hw_queues_set = limit_hw_queues_if_shared(w.size);
         int rc = setup_device_common();
         if (rc) return rc;
     }
@@ -593,11 +663,12 @@ int world_init() {
         fprintf(stderr,
                 "[mv2amd] MPI_Init: %d ranks (%d per node, %d node%s, %d per GPU); self-test %s; tiling %s, %s stores "
                 "(256 MiB allreduce: %d workgroups x %zu KiB per round); one-shot up to %zu KiB; init %.1f ms "
-                "(self-test %.1f, autotune %.1f)\n",
+                "(self-test %.1f, autotune %.1f)%s\n",
                 w.gsize, w.size, w.nnodes, w.nnodes > 1 ? "s" : "", w.nshare,
                 !ran ? "not run" : w.light_release ? "passed, light release" : "passed, full system-scope release",
                 w.pipe_tuned ? "autotuned" : "default", w.pipe_rnt ? "non-temporal" : "plain", g256, t256 >> 10,
-                w.oneshot_max >> 10, w.init_ms, w.selftest_ms, w.tune_ms);
+                w.oneshot_max >> 10, w.init_ms, w.selftest_ms, w.tune_ms,
+                w.hw_queues_set ? "; 2 HW queues per process (GPU shared)" : "");
         fflush(stderr);
     }
     MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d): %.1f ms (self-test %.1f, autotune %.1f)",

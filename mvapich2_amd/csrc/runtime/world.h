@@ -80,6 +80,8 @@ struct alignas(64) ShmRank {
     // when it got there; a peer whose device wait runs out prints every late rank's beacon
     std::atomic<uint64_t> beacon;
     std::atomic<uint64_t> beacon_ns;
+    std::atomic<uint64_t> bh_code[16], bh_ns[16];  // the last 16 beacons (history ring)
+    std::atomic<uint32_t> bh_pos;
 };
 
 constexpr int kMeshMaxRanks = 64;  // jobs up to this many ranks get the rank mesh (p2p across nodes)
@@ -163,7 +165,8 @@ struct World {
     double tune_us[kTuneMax] = {};                // max over ranks per candidate
     double init_ms = 0, selftest_ms = 0, tune_ms = 0;
     size_t uop_in_bytes = 0, uop_area_bytes = 0;
-    uint64_t api_calls = 0;  // library calls entered (the beacon's call number)  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
+    uint64_t api_calls = 0;  // library calls entered (the beacon's call number)
+    int hw_queues_set = 0;   // GPU_MAX_HW_QUEUES this library set before HIP started (ranks sharing a GPU)  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
@@ -191,7 +194,9 @@ int world_init();
 int world_finalize();
 void host_barrier();
 // beacon phases (ShmRank::beacon)
-enum Beacon { BC_ENTRY = 1, BC_LAUNCH = 2, BC_WAIT = 3, BC_DONE = 4, BC_BARRIER = 5, BC_P2P_WAIT = 6, BC_NET = 7 };
+enum Beacon { BC_ENTRY = 1, BC_LAUNCH = 2, BC_WAIT = 3, BC_DONE = 4, BC_BARRIER = 5, BC_P2P_WAIT = 6, BC_NET = 7,
+              BC_SCRATCH = 8, BC_STAGE = 9, BC_COPY_OUT = 10, BC_LAUNCHED = 11 };
+void beacon_report(int j, uint64_t now);  // print local rank j's beacon history (stderr)
 void beacon(int phase, bool new_call = false);
 const char *beacon_name(int phase);
 int global_barrier();  // node barrier, leaders' barrier across nodes, node barrier
