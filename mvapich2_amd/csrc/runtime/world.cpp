@@ -197,19 +197,20 @@ static int gpus_visible_before_hip() {
 // kernel needs its peers' kernels resident at the same time, and with HIP's default 4 hardware
 // queues per process five ranks' queues starve each other — one rank's kernel was not dispatched
 // for 30 s while the others' kernels spun (profiles/r04f_queue_starvation.txt; 3 ms with 2 queues
-// per process).  So before HIP starts, a process that will share its GPU asks for 2 hardware queues
-// unless GPU_MAX_HW_QUEUES is set (MV2AMD_HW_QUEUES=0 leaves it alone, =k asks for k).  One rank
-// per GPU is not touched.  Returns the value set, or 0.
+// per process).  So before HIP starts, a process that will share its GPU lowers GPU_MAX_HW_QUEUES
+// to 2 (unset, or set higher — the one-GPU box exports HIP's default 4); MV2AMD_HW_QUEUES=0 leaves
+// it alone, =k asks for k.  One rank per GPU is not touched.  Returns the value set, or 0.
 static int limit_hw_queues_if_shared(int local_size) {
     const long want = env_long("MV2AMD_HW_QUEUES", 2);
-    if (want <= 0 || getenv("GPU_MAX_HW_QUEUES")) return 0;
+    const long have = env_long("GPU_MAX_HW_QUEUES", 0);
+    if (want <= 0 || (have > 0 && have <= want)) return 0;
     const int ndev = gpus_visible_before_hip();
     const bool shared = env_long("MV2AMD_NSHARE", 1) > 1 || (getenv("MV2AMD_DEVICE") && local_size > 1) ||
                         (ndev > 0 && local_size > ndev);
     if (!shared) return 0;
     char v[24];
     snprintf(v, sizeof(v), "%ld", want);
-    setenv("GPU_MAX_HW_QUEUES", v, 0);
+    setenv("GPU_MAX_HW_QUEUES", v, 1);
     return (int)want;
 }
 
@@ -663,12 +664,12 @@ int world_init() {
         fprintf(stderr,
                 "[mv2amd] MPI_Init: %d ranks (%d per node, %d node%s, %d per GPU); self-test %s; tiling %s, %s stores "
                 "(256 MiB allreduce: %d workgroups x %zu KiB per round); one-shot up to %zu KiB; init %.1f ms "
-                "(self-test %.1f, autotune %.1f)%s\n",
+                "(self-test %.1f, autotune %.1f)%s%s\n",
                 w.gsize, w.size, w.nnodes, w.nnodes > 1 ? "s" : "", w.nshare,
                 !ran ? "not run" : w.light_release ? "passed, light release" : "passed, full system-scope release",
                 w.pipe_tuned ? "autotuned" : "default", w.pipe_rnt ? "non-temporal" : "plain", g256, t256 >> 10,
                 w.oneshot_max >> 10, w.init_ms, w.selftest_ms, w.tune_ms,
-                w.hw_queues_set ? "; 2 HW queues per process (GPU shared)" : "");
+                w.hw_queues_set ? "; GPU shared: GPU_MAX_HW_QUEUES lowered to " : "", w.hw_queues_set ? getenv("GPU_MAX_HW_QUEUES") : "");
         fflush(stderr);
     }
     MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d): %.1f ms (self-test %.1f, autotune %.1f)",
