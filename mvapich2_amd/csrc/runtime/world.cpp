@@ -250,12 +250,8 @@ static int setup_device_common() {
     w.light_release = (int)env_long("MV2AMD_LIGHT_RELEASE", w.light_release);
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
     knobs_reload();  // MV2_* algorithm-selection knobs (orders.cpp)
-    // kernel-time events (mv2h_timing_enable): timing only — completion and visibility come from the
-    // completion word or the stream — so no system-scope fence: the default event's end-of-kernel
-    // L2 writeback added 2-9 us to a kernel's measured duration against rocprofv3's timestamps
-    // (unpack of the configs[4] vector: 83.4 us by default events, 77.8 us in rocprofv3, r04c)
-    hipEventCreateWithFlags(&w.ev0, hipEventDisableSystemFence);
-    hipEventCreateWithFlags(&w.ev1, hipEventDisableSystemFence);
+    hipEventCreate(&w.ev0);
+    hipEventCreate(&w.ev1);
     return 0;
 }
 
