@@ -187,6 +187,12 @@ int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *in
  * (red_scat_osu.c:1859-1893, the default table of red_scat_tuning.c): *algo codes of mv2h_plan
  * (10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic). */
 int mv2h_reduce_scatter_table(int n, long nbytes);
+/* Several nodes: MPI_Reduce's tuning-table cell (reduce_osu.c:2516-2620, the default tables of
+ * reduce_tuning.c:1563-1649, CMA or not as MV2_SMP_USE_CMA says): *two_level = 1 for
+ * MPIR_Reduce_two_level_helper_MV2, *inter the leaders' (or flat) algorithm and *intra the node step
+ * (mv2h_plan algo codes: 1 shmem, 7 binomial, 8 knomial, 9 redscat_gather), *k the knomial factor.
+ * Returns the table entry index (comm_size_index), or an error class. */
+int mv2h_mn_reduce_table(int ppn, int gsize, long nbytes, int *two_level, int *inter, int *intra, int *k);
 /* Several nodes: the route a builtin-op call takes (coll 0 MPI_Allreduce, 1 MPI_Reduce, 2
  * MPI_Reduce_scatter; nbc: enum mv2h_nbc): 0 two-level, 1 flat ring over every rank, 2 a flat
  * algorithm as per-element programs (up to 8 ranks), 3 its message schedule over the rank channels

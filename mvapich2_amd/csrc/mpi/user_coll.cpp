@@ -433,6 +433,9 @@ struct BigEval {
     MPI_User_function *fn;
     bool comm;
     std::vector<std::vector<char>> scratch;  // one operand-sized buffer per recursion level
+    // MPIR_Reduce_redscat_gather_MV2's pre-step (reduce_osu.c:849-894: odd ranks below 2 * rem hand
+    // their operand to rank - 1, the even ones keep their place) instead of the allreduce's
+    bool redscat = false;
     char *level(int l) {
         if ((int)scratch.size() <= l) scratch.resize((size_t)l + 1);
         if (scratch[l].size() < (size_t)rspan + 1) scratch[l].resize((size_t)rspan + 1);
@@ -454,14 +457,14 @@ struct BigEval {
     }
     int real(int q) const {
         const int rem = n - pof2();
-        return q < rem ? q * 2 + 1 : q + rem;
+        return q < rem ? q * 2 + (redscat ? 0 : 1) : q + rem;
     }
     // the non-power-of-two pre-step: newrank nr's starting value (an odd rank below 2 * rem has
-    // reduced uop(tmp = x_{r-1}, recvbuf))
+    // reduced uop(tmp = x_{r-1}, recvbuf); redscat_gather: an even one uop(tmp = x_{r+1}, recvbuf))
     void base(int nr, char *out) {
         const int r = real(nr);
         copy(out, x(r));
-        if (r < 2 * (n - pof2())) uop(x(r - 1), out);
+        if (r < 2 * (n - pof2())) uop(x(redscat ? r + 1 : r - 1), out);
     }
     // MPIR_Allreduce_pt2pt_rd_MV2 (allreduce_osu.c:455-600; also pt2pt_rs for a user op, :802): the
     // value newrank nr holds after `lev` doubling steps
@@ -566,6 +569,32 @@ struct BigEval {
         while (m < n) m <<= 1;
         bin_value(0, m, comm ? root : 0, 0, out);
     }
+    // MPIR_Reduce_knomial_MV2 (reduce_osu.c:1639-1837) to `root`: relative rank rel's value is its
+    // own operand reduced with its children's values (MPIR_Reduce_knomial_trace :1568-1633), the
+    // trace's last child first (request-index order), uop(tmp, recvbuf)
+    void knom_value(int rel, int root, int k, int l, char *out) {
+        copy(out, x((rel + root) % n));
+        int mask = 1;
+        while (mask < n && !(rel % (k * mask))) mask *= k;
+        mask /= k;
+        std::vector<int> kids;
+        for (int m = mask; m > 0; m /= k)
+            for (int j = 1; j < k; ++j)
+                if (rel + m * j < n) kids.push_back(rel + m * j);
+        char *child = level(l);
+        for (size_t i = kids.size(); i-- > 0;) {
+            knom_value(kids[i], root, k, l + 1, child);
+            uop(child, out);
+        }
+    }
+    void knomial(int root, int k, char *out) { knom_value(0, root, k < 2 ? 2 : k, 0, out); }
+    // MPIR_Reduce_redscat_gather_MV2 (reduce_osu.c:718-1100): its reduce-scatter (the recursive
+    // halving of pt2pt_rs after its own pre-step), the gather to the root
+    void redscat_gather(char *out) {
+        redscat = true;
+        rs(out);
+        redscat = false;
+    }
     // MPIR_Allreduce_pt2pt_ring_MV2's chunk c (allreduce_osu.c:3916-3968): x_c, then uop(x_{c+j},
     // acc) for j = 1 .. n-1
     void ring_chunk(int c, char *out) {
@@ -615,6 +644,8 @@ int run_big_flat(const Operands &o, int count, const MnSched &sc, const HostOp &
         if (e <= b) return 0;
         const int r = eval(b, e, [&](BigEval &ev, char *out) {
             if (algo == ALG_BINOMIAL) ev.binomial(sc.root, out);
+            else if (algo == ALG_KNOMIAL) ev.knomial(sc.root, sc.k, out);
+            else if (algo == ALG_REDSCAT_GATHER) ev.redscat_gather(out);
             else if (algo == ALG_PT2PT_RS && op.opk == OPK_BUILTIN && e - b >= pof2) ev.rs(out);
             else ev.rd(me, out);
         });
@@ -622,7 +653,7 @@ int run_big_flat(const Operands &o, int count, const MnSched &sc, const HostOp &
         return mv2h_memcpy_htod(res_all + (size_t)b * (size_t)t.tsize, R.data(), (size_t)(e - b) * (size_t)t.tsize)
                    ? MPI_ERR_OTHER : 0;
     };
-    if (sc.forced == ALG_BINOMIAL && !deliver) return 0;
+    if ((sc.forced == ALG_BINOMIAL || sc.forced == ALG_KNOMIAL || sc.forced == ALG_REDSCAT_GATHER) && !deliver) return 0;
     if (sc.forced == ALG_RING) {
         rc = segment(U, count, ALG_PT2PT_RS);  // the wrapper's pt2pt_rs on the remainder
     } else if (sc.U > 0 && sc.U < count) {  // IN_PLACE: two pt2pt_rs calls
@@ -660,6 +691,8 @@ int run_two_level(const Operands &o, int count, const MnSched &sc, MPI_User_func
         BigEval ev{Pt.data(), rspan, K, count, &t, fn, true, {}};
         std::vector<char> out((size_t)rspan + 1);
         if (sc.forced == ALG_BINOMIAL) ev.binomial(sc.root, out.data());
+        else if (sc.forced == ALG_KNOMIAL) ev.knomial(sc.root, sc.k, out.data());
+        else if (sc.forced == ALG_REDSCAT_GATHER) ev.redscat_gather(out.data());
         else ev.rd(w.node, out.data());
         rc = dtype_pack(out.data(), count, t.dt, R.data());
     } else {
@@ -794,7 +827,7 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
             if ((rc = run_two_level(o, count, sc, op.fn, res))) return rc;
             return dtype_unpack(res, count, t.dt, recvbuf);
         }
-        if ((rc = plan_reduce(n, root, root, (size_t)count, (int)t.tsize, (int)t.extent, &pr, op.opk))) return rc;
+        pr = sc.p;  // the root's programs of the flat algorithm over the job's ranks
         const Split sp{&pr.ps, count, &pr.ps, 0};
         return run_split(src, count, t, sp, op.fn, recvbuf, root);
     }

@@ -1350,7 +1350,10 @@ int mv2h_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, 
     return rc;
 }
 
-static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
+// forced: the programs to run instead of the one-node selection's (a node step of
+// MPIR_Reduce_two_level_helper_MV2 across nodes, whose function the multi-node table names)
+static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream,
+                        const Plan *forced = nullptr) {
     hp_entry();
     const DtypeInfo *dt = nullptr;
     int rc = check_op_dtype(op, dtype, &dt);
@@ -1367,7 +1370,8 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
     const bool in_place = sendbuf == (const void *)-1 || (is_root && sendbuf == recvbuf);
     // MPIR_Reduce_index_tuned_intra_MV2's one-node choice (orders.cpp plan_reduce)
     Plan p;
-    if ((rc = plan_reduce(w.size, w.rank, root, count, dt->size, dt->extent, &p))) return rc;
+    if (forced) p = *forced;
+    else if ((rc = plan_reduce(w.size, w.rank, root, count, dt->size, dt->extent, &p))) return rc;
     log_plan("reduce", p, count);
     pvar_note(PV_COLL_REDUCE, p, in_place, count, w.size);
     const TreeParams tp = tree_from_plan(p, w.size, count, w.rank);
@@ -1782,6 +1786,37 @@ int sched_binomial_reduce(Xport &x, int n, int rank, int root, char *acc, char *
     return 0;
 }
 
+// MPIR_Reduce_knomial_MV2 (reduce_osu.c:1639-1837) as messages: the children of
+// MPIR_Reduce_knomial_trace (:1568-1633: k - 1 per mask, masks from the largest down) send their
+// partials; the receives are posted from the trace's last child to its first (:1735-1741) and
+// reduced uop(tmp, acc) in request-index order (the Waitany order restated), then the
+// partial goes to the parent.  acc ends with the result at the root (commutative ops only, as in
+// the reference's dispatch, :2637-2644).
+int sched_knomial_reduce(Xport &x, int n, int rank, int root, int k, char *acc, char *tmp, size_t count, size_t ext,
+                         int dtype, int op) {
+    const int rel = (rank - root + n) % n;
+    const size_t S = count * ext;
+    int mask = 1, dst = -1;
+    while (mask < n) {
+        if (rel % (k * mask)) {
+            dst = rel / (k * mask) * (k * mask) + root;
+            if (dst >= n) dst -= n;
+            break;
+        }
+        mask *= k;
+    }
+    mask /= k;
+    std::vector<int> src;
+    for (int m = mask; m > 0; m /= k)
+        for (int j = 1; j < k; ++j)
+            if (rel + m * j < n) src.push_back(rank + m * j >= n ? rank + m * j - n : rank + m * j);
+    int rc = 0;
+    for (size_t i = src.size(); i-- > 0;)
+        if ((rc = x.xchg(src[i], nullptr, 0, tmp, S)) || (rc = mv2h_reduce_local(tmp, acc, count, dtype, op, nullptr)))
+            return rc;
+    return dst >= 0 ? x.xchg(dst, acc, S, nullptr, 0) : 0;
+}
+
 // the node leaders as ranks (node index), over their TCP links, staged through g_mn.h0 / h1
 struct LeaderLinks : Xport {
     int shift(int to, const char *sb, size_t sbytes, int from, char *rb, size_t rbytes) override {
@@ -2026,15 +2061,56 @@ static int mn_reduce_scatter_route(int gsize, long nbytes) {
     const int r = mn_flat_route(gsize);
     return r == MN_FALLBACK ? MN_BASIC_R : r;
 }
-// MPI_Reduce / MPI_Ireduce
-static int mn_reduce_route(int gsize, int nbc) {
-    return nbc == NBC_IREDUCE ? mn_flat_route(gsize) : MN_TWO_LEVEL_R;
+// MPIR_Reduce_index_tuned_intra_MV2 across nodes (reduce_osu.c:2498-2660) for a commutative op
+// (opk: builtin or commutative user op; a non-commutative one always takes the flat binomial,
+// :2628-2636): two_level = MPIR_Reduce_two_level_helper_MV2 with the node step `intra` to local rank
+// 0 and `algo` over the leaders to the root's node; else `algo` flat over every rank.  The
+// small-message shortcut (:2508-2514: up to MV2_COLL_SKIP_TABLE_THRESHOLD, shmem + binomial) and the
+// tables (orders.cpp mn_reduce_table).  The helper's MPIR_Reduce_shmem_MV2 node step becomes the intra
+// knomial wrapper from the shmem slot size on (:2240-2251); the flat knomial needs a commutative op and
+// the flat redscat_gather a builtin op with count >= pof2 (:2637-2652), else binomial.  The
+// topology-aware reduce (:2498-2506, off by default) is not restated across nodes.
+struct MnRedSel {
+    bool two_level;
+    int intra, algo, k;
+};
+static int floor_pof2(int n) {
+    int p = 1;
+    while (p * 2 <= n) p *= 2;
+    return p;
+}
+static MnRedSel mn_reduce_select(int ppn, int gsize, size_t count, int tsize, int textent, int opk) {
+    const Knobs &K = knobs();
+    const long nbytes = (long)count * tsize;
+    MnReduceCell c{};
+    MnRedSel r{true, ALG_SHMEM_LINEAR, ALG_BINOMIAL, 4};
+    if (opk == OPK_USER_NONCOMM) return MnRedSel{false, 0, ALG_BINOMIAL, 4};
+    if (!(K.enable_shmem_reduce && K.enable_skip_search && nbytes <= K.coll_skip_thr)) {
+        mn_reduce_table(ppn, gsize, nbytes, &c);
+        r = MnRedSel{c.two_level != 0, c.intra, c.inter, c.k};
+    } else {
+        mn_reduce_table(ppn, gsize, nbytes, &c);  // the knomial factor only
+        r.k = c.k;
+    }
+    if (r.two_level) {
+        if (r.intra == ALG_SHMEM_LINEAR && !(K.enable_shmem_reduce && (long)count * textent < K.shmem_coll_max_msg))
+            r.intra = ALG_KNOMIAL;
+        return r;
+    }
+    if (r.algo == ALG_REDSCAT_GATHER && !(opk == OPK_BUILTIN && count >= (size_t)floor_pof2(gsize))) r.algo = ALG_BINOMIAL;
+    return r;
+}
+// MPI_Reduce / MPI_Ireduce: MN_TWO_LEVEL_R (the helper), or a flat algorithm's route
+static int mn_reduce_route(int ppn, int gsize, size_t count, int tsize, int nbc) {
+    if (nbc == NBC_IREDUCE) return mn_flat_route(gsize);
+    const MnRedSel sel = mn_reduce_select(ppn, gsize, count, tsize, tsize, OPK_BUILTIN);
+    return sel.two_level ? MN_TWO_LEVEL_R : mn_flat_route(gsize);
 }
 
 static int mn_allreduce_2lvl(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
                              int intra = MN_INTRA_NODE, int inter = ALG_PT2PT_RD);
 static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
-                             int algo, int root = -1);
+                             int algo, int root = -1, const Plan *forced = nullptr);
 
 // The node's S-byte operands at its leader only (G: L * S bytes, local rank order; unused on the
 // other ranks), over the node's device point-to-point channels in the library's collective context
@@ -2214,7 +2290,7 @@ static int mn_sched_naive(const void *sendbuf, void *recvbuf, size_t count, int 
 // call's: MPIR_Iallreduce_naive = Ireduce to rank 0 + Ibcast, every rank takes rank 0's result).
 // root >= 0 (MPI_Ireduce): only the root evaluates, the plan of MPIR_Ireduce_binomial.
 static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, void *stream,
-                             int algo, int root) {
+                             int algo, int root, const Plan *forced) {
     World &w = world();
     const DtypeInfo *dt = dtype_lookup(dtype);
     const bool in_place = sendbuf == (const void *)-1;
@@ -2224,8 +2300,9 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
         return mn_flat_route(n) == MN_SCHED ? mn_sched_allreduce(sendbuf, recvbuf, count, dtype, op, algo)
                                             : mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
     Plan p;
-    int rc = root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
-                       : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
+    int rc = forced ? (p = *forced, 0)
+             : root >= 0 ? plan_reduce(n, w.grank, root, count, dt->size, dt->extent, &p)
+                         : plan_allreduce(n, w.grank, count, dt->size, dt->extent, in_place, algo, &p);
     if (rc) return rc;
     pvar_note(root >= 0 ? PV_COLL_REDUCE : PV_COLL_ALLREDUCE, p, in_place, count, n);
     char *W = nullptr;  // every rank's operand, global rank order
@@ -2384,6 +2461,59 @@ static int mn_bcast(void *buffer, size_t bytes, int root, void *stream) {
     return rc;
 }
 
+// MPI_Reduce across nodes: the nonblocking schedule (MPI_Ireduce), else MPIR_Reduce_index_tuned_intra_MV2's
+// choice (mn_reduce_select): MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2030-2330: the node step
+// to local rank 0, the leaders' algorithm to the root's node, the leader to the root) or a flat
+// algorithm over every rank (programs up to kMaxRanks, its message schedule up to the rank mesh,
+// the two-level helper with the shortcut's steps beyond).
+static int mn_reduce_flat_sched(const void *src, void *recvbuf, size_t count, const DtypeInfo *dt, int dtype, int op,
+                                int root, int algo, int k) {
+    World &w = world();
+    const size_t ext = (size_t)dt->extent, S = count * ext;
+    const int n = w.gsize, me = w.grank;
+    int rc = mn_reserve_dev(S);
+    if (rc) return rc;
+    const bool mine = me == root && recvbuf && is_device(recvbuf);
+    char *acc = mine ? (char *)recvbuf : g_mn.d0;
+    if (src != acc && hipMemcpy(acc, src, S, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+    RankChannels x;
+    if (algo == ALG_KNOMIAL) rc = sched_knomial_reduce(x, n, me, root, k, acc, g_mn.d1, count, ext, dtype, op);
+    else if (algo == ALG_REDSCAT_GATHER) rc = sched_allreduce(x, n, me, acc, g_mn.d1, count, ext, dtype, op, false, true);
+    else rc = sched_binomial_reduce(x, n, me, root, acc, g_mn.d1, count, ext, dtype, op);
+    if (rc || me != root || acc == recvbuf) return rc;
+    return hipMemcpy(recvbuf, acc, S, hipMemcpyDefault) == hipSuccess ? 0 : E_INTERN;
+}
+
+// the leaders' step of the two-level helper: every leader's partial in g_mn.d0, the result in the
+// root node's leader's g_mn.d0.  Up to kMaxRanks nodes the partials travel to that leader, which
+// evaluates the algorithm's programs for the root node; above, the message schedule runs.
+static int mn_reduce_leaders(size_t count, const DtypeInfo *dt, int dtype, int op, int rnode, int algo, int k) {
+    World &w = world();
+    const int K = w.nnodes, me = w.node;
+    const size_t ext = (size_t)dt->extent, bytes = count * ext;
+    int rc = 0;
+    if (K > kMaxRanks) {
+        LeaderLinks x;
+        if (algo == ALG_KNOMIAL) return sched_knomial_reduce(x, K, me, rnode, k, g_mn.d0, g_mn.d1, count, ext, dtype, op);
+        if (algo == ALG_REDSCAT_GATHER)
+            return sched_allreduce(x, K, me, g_mn.d0, g_mn.d1, count, ext, dtype, op, false, true);
+        return sched_binomial_reduce(x, K, me, rnode, g_mn.d0, g_mn.d1, count, ext, dtype, op);
+    }
+    if (me != rnode) return (rc = mn_d2h(g_mn.h0, g_mn.d0, bytes)) ? rc : net_send(rnode, g_mn.h0, bytes);
+    Plan pl;
+    if ((rc = plan_reduce_forced(K, rnode, count, algo, k, &pl))) return rc;
+    char *W = (char *)get_scratch(6, (size_t)K * bytes);
+    if (!W) return E_NO_MEM;
+    for (int j = 0; j < K; ++j) {
+        if (j == me) rc = hipMemcpy(W + (size_t)j * bytes, g_mn.d0, bytes, hipMemcpyDeviceToDevice) == hipSuccess ? 0 : E_INTERN;
+        else if (!(rc = net_recv(j, g_mn.h1, bytes))) rc = mn_h2d(W + (size_t)j * bytes, g_mn.h1, bytes);
+        if (rc) return rc;
+    }
+    const void *srcs[kMaxRanks];
+    for (int j = 0; j < K; ++j) srcs[j] = W + (size_t)j * bytes;
+    return mv2h_reduce_n_prog(srcs, K, g_mn.d0, count, dtype, op, (const mv2h_progset *)&pl.ps, nullptr);
+}
+
 static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
     World &w = world();
     if (root < 0 || root >= w.gsize) return E_ROOT;
@@ -2394,35 +2524,44 @@ static int mn_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype
     const int rnode = root / w.size, rlocal = root % w.size;
     const bool me_root = w.grank == root;
     const void *src = sendbuf == (const void *)-1 ? recvbuf : sendbuf;  // IN_PLACE: at the root only
-    // MPI_T: MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2039) with the leaders' binomial (:450)
     // MPI_Ireduce: MVAPICH2's nonblocking schedule (MPIR_Ireduce_binomial, ireduce_osu.c) is flat
     // over the whole job
-    const int route = mn_reduce_route(w.gsize, nbc_kind());
-    if (route == MN_FLAT_PROG) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root);
-    if (route == MN_SCHED) return mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, root);
-    // MN_TWO_LEVEL_R, or MN_FALLBACK for an MPI_Ireduce above the rank mesh: the two-level helper
-    const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
-    pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
-    if ((rc = mn_reserve_dev(bytes)) || (w.rank == 0 && (rc = mn_reserve_host(bytes)))) return rc;
-    // node step: the leader's partial lands in g_mn.d0 (a non-root's recvbuf is not significant)
-    if ((rc = reduce_entry(src, w.rank == 0 ? g_mn.d0 : nullptr, count, dtype, op, 0, stream))) return rc;
-    if (w.rank == 0) {
-        // binomial over the leaders to the root's node, commutative form (reduce_osu.c:425-681)
-        const int n = w.nnodes, rel = (w.node - rnode + n) % n;
-        for (int mask = 1; mask < n; mask <<= 1) {
-            if (rel & mask) {
-                const int dst = ((rel & ~mask) + rnode) % n;
-                if ((rc = mn_d2h(g_mn.h0, g_mn.d0, bytes)) || (rc = net_send(dst, g_mn.h0, bytes))) return rc;
-                break;
-            }
-            if ((rel | mask) < n) {
-                const int srcn = ((rel | mask) + rnode) % n;
-                if ((rc = net_recv(srcn, g_mn.h1, bytes)) || (rc = mn_h2d(g_mn.d1, g_mn.h1, bytes)) ||
-                    (rc = mv2h_reduce_local(g_mn.d1, g_mn.d0, count, dtype, op, nullptr)))
-                    return rc;
-            }
-        }
+    if (nbc_kind() == NBC_IREDUCE) {
+        const int route = mn_flat_route(w.gsize);
+        if (route == MN_FLAT_PROG) return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root);
+        if (route == MN_SCHED) return mn_sched_naive(sendbuf, recvbuf, count, dtype, op, stream, root);
     }
+    MnRedSel sel = mn_reduce_select(w.size, w.gsize, count, dt->size, dt->extent, OPK_BUILTIN);
+    if (nbc_kind() == NBC_IREDUCE || (!sel.two_level && mn_flat_route(w.gsize) == MN_FALLBACK))
+        sel = MnRedSel{true, ALG_SHMEM_LINEAR, ALG_BINOMIAL, sel.k};  // beyond the rank mesh (unpinned)
+    if (!sel.two_level) {
+        const int ids[3] = {sel.algo == ALG_KNOMIAL ? PV_RED_KNOMIAL : sel.algo == ALG_REDSCAT_GATHER ? PV_RED_REDSCAT_GATHER
+                                                                                                       : PV_RED_BINOMIAL};
+        pvar_note_ids(ids, 1);
+        if (mn_flat_route(w.gsize) == MN_FLAT_PROG) {
+            Plan p;
+            if ((rc = plan_reduce_forced(w.gsize, root, count, sel.algo, sel.k, &p))) return rc;
+            return mn_flat_allreduce(sendbuf, recvbuf, count, dtype, op, stream, 0, root, &p);
+        }
+        return mn_reduce_flat_sched(src, recvbuf, count, dt, dtype, op, root, sel.algo, sel.k);
+    }
+    // MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:2039) with the leaders' function
+    const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, sel.algo == ALG_KNOMIAL ? PV_RED_KNOMIAL
+                                                   : sel.algo == ALG_REDSCAT_GATHER ? PV_RED_REDSCAT_GATHER
+                                                                                    : PV_RED_BINOMIAL};
+    pvar_note_ids(chain, w.rank == 0 && w.nnodes > 1 ? 2 : 1);
+    if ((rc = mn_reserve_dev(bytes)) || (w.rank == 0 && (rc = mn_reserve_host(bytes)))) return rc;
+    // node step to local rank 0: the leader's partial lands in g_mn.d0 (a non-root's recvbuf is not
+    // significant)
+    if (w.size > 1) {
+        Plan pn;
+        if ((rc = plan_reduce_forced(w.size, 0, count, sel.intra, sel.k, &pn)) ||
+            (rc = reduce_entry(src, w.rank == 0 ? g_mn.d0 : nullptr, count, dtype, op, 0, stream, &pn)))
+            return rc;
+    } else if (hipMemcpy(g_mn.d0, src, bytes, hipMemcpyDefault) != hipSuccess) {
+        return E_INTERN;
+    }
+    if (w.rank == 0 && (rc = mn_reduce_leaders(count, dt, dtype, op, rnode, sel.algo, sel.k))) return rc;
     if (w.node != rnode) return 0;
     if (rlocal == 0) return me_root ? mn_d2h(recvbuf, g_mn.d0, bytes) : 0;
     // the root is not the leader: the node's device point-to-point channel carries the result
@@ -2569,17 +2708,33 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
             if (!rc) pvar_note(PV_COLL_REDUCE, s->p, in_place, count, n);
             return rc;
         }
+        // MPIR_Reduce_index_tuned_intra_MV2's choice across nodes, as on the device path (mn_reduce)
+        const MnRedSel sel = mn_reduce_select(L, n, count, tsize, textent, opk);
+        const int fid = sel.algo == ALG_KNOMIAL ? PV_RED_KNOMIAL : sel.algo == ALG_REDSCAT_GATHER ? PV_RED_REDSCAT_GATHER
+                                                                                                 : PV_RED_BINOMIAL;
+        s->k = sel.k;
+        if (!sel.two_level) {
+            pvar_note_ids(&fid, 1);
+            if (big) {  // the flat algorithm's schedule, evaluated on the host
+                s->big = 1;
+                s->forced = sel.algo;
+                s->root = root;
+                return 0;
+            }
+            s->forced = sel.algo;
+            return plan_reduce_forced(n, root, count, sel.algo, sel.k, &s->p);
+        }
         s->kind = MN_TWO_LEVEL;
-        const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
+        const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, fid};
         pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
-        if ((rc = plan_reduce(L, 0, 0, count, tsize, textent, &s->node, opk))) return rc;
+        if ((rc = plan_reduce_forced(L, 0, count, sel.intra, sel.k, &s->node))) return rc;
         if (K > kMaxRanks) {
             s->big = 1;
-            s->forced = ALG_BINOMIAL;
+            s->forced = sel.algo;
             s->root = root / L;
             return 0;
         }
-        return plan_binomial(K, root / L, &s->lead);
+        return plan_reduce_forced(K, root / L, count, sel.algo, sel.k, &s->lead);
     }
     if (big && nbc_kind() == NBC_IALLREDUCE) {
         // MPIR_Iallreduce_naive: Ireduce to rank 0 — binomial for a user op (redscat_gather needs a
@@ -2674,13 +2829,24 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
 
 extern "C" {
 
+int mv2h_mn_reduce_table(int ppn, int gsize, long nbytes, int *two_level, int *inter, int *intra, int *k) {
+    if (ppn < 1 || gsize < 1) return E_ARG;
+    MnReduceCell c{};
+    const int rc = mn_reduce_table(ppn, gsize, nbytes, &c);
+    if (two_level) *two_level = c.two_level;
+    if (inter) *inter = c.inter;
+    if (intra) *intra = c.intra;
+    if (k) *k = c.k;
+    return rc ? rc : c.entry;
+}
+
 int mv2h_mn_route(int coll, int ppn, int gsize, long nbytes, size_t count, int in_place, int nbc, int *rem_route) {
     if (ppn < 1 || gsize < ppn || gsize % ppn) return E_ARG;
     int intra = 0, inter = 0, sel = 0, rem = -1;
     int r;
     switch (coll) {
     case 0: r = mn_allreduce_route(ppn, gsize, nbytes, count, in_place != 0, nbc, &intra, &inter, &sel, &rem); break;
-    case 1: r = mn_reduce_route(gsize, nbc); break;
+    case 1: r = mn_reduce_route(ppn, gsize, count, nbytes > 0 && count ? (int)(nbytes / (long)count) : 4, nbc); break;
     case 2: r = mn_reduce_scatter_route(gsize, nbytes); break;
     default: return E_ARG;
     }

@@ -853,6 +853,113 @@ int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *inter) 
     return 0;
 }
 
+// Several nodes: MPIR_Reduce_index_tuned_intra_MV2's table step (reduce_osu.c:2516-2620) over the
+// tables MVAPICH2 falls back to for an unlisted architecture (reduce_tuning.c:1563-1649, the
+// "Stampede" branch): tuning/reduce/gen2{_cma}_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h, the
+// first 5 / 6 / 6 numproc entries, as tests/golden/gen_mn_reduce_tables.py reads them.  Per entry:
+// numproc, inter_k_degree, intra_k_degree, is_two_level_reduce per inter size index, the
+// inter-leader list (smallest size, function per index: b binomial, k inter-knomial wrapper,
+// r redscat_gather) and the intra-node list (h MPIR_Reduce_shmem_MV2, b binomial, i intra-knomial
+// wrapper).  The lists hold size_inter_table / size_intra_table entries (the headers carry one more).
+namespace {
+struct MnRedEntry {
+    int numproc, k, intra_k;
+    const char *two_level;
+    int inter_min;
+    const char *inter;
+    int intra_min;
+    const char *intra;
+};
+const MnRedEntry kMnRedCma1[] = {
+    {2, 4, 4, "111111111111111010", 1, "bbrkkbkkbbbkbrbbbb", 1, "bhbhbhhihiibiiihih"},
+    {4, 4, 4, "111111111111010000", 1, "kkkbrbrkbrkbkrbbbb", 1, "bhihbiibhibhhihhhh"},
+    {8, 4, 4, "111111111111011111", 1, "brrrrrrkbbkkkrkbbr", 1, "bbbbbbbbiihbhbbbib"},
+    {16, 4, 4, "111111111111000111", 1, "bkkkkbkkkrbkkkbbbb", 1, "ibbhbbbbbbbihhhbhi"},
+    {32, 4, 4, "111111111111000101", 1, "kkrbkrbrbbrrkbbbbr", 1, "bbhbibbiiihbhhhhhi"},
+};
+const MnRedEntry kMnRedCma2[] = {
+    {2, 4, 4, "0111111111000111111", 4, "rbkkrbbkkbbrbrkkbbb", 4, "hhhiibihhhhhhbhbhh"},
+    {2, 4, 4, "111111111100110111", 1, "rbbkbrkrbkbrrrkrrr", 1, "hihhbhbhhihhhhhhhh"},
+    {4, 4, 4, "111111111111111100", 1, "rrbbrbbkbrbkkrkbbb", 1, "bihihihhihiihhhhhh"},
+    {8, 4, 4, "111111111111111111", 1, "bkbbbrbbbbkkkrbbbb", 1, "biihibihhibhhhhhbb"},
+    {16, 4, 4, "111111111111111111", 1, "brrrrrkkkrkkkkbbbb", 1, "ihihhhibihbhhhhhbb"},
+    {32, 4, 4, "111111111111111101", 1, "rkkkkbkkkrrkkrbbbb", 1, "iiiibhiibihhhhhhhb"},
+};
+const MnRedEntry kMnRedCma16[] = {
+    {16, 4, 4, "1111111111001100000", 4, "krbrrbbkrrkrbbkrrrr", 4, "ihhbbhbhihhhiiihhh"},
+    {16, 4, 4, "111111111100000000", 1, "bkkbkkbrkkkbbbbbrr", 1, "ihbhhhhbibhhhhhhhh"},
+    {32, 4, 4, "111111111111111111", 1, "kbkrrrkbkrkrkrkkkb", 1, "bhihbbhihbbbhhhhhb"},
+    {64, 4, 4, "111111111111111111", 1, "rbbkrrrrkkbkkkbbbb", 1, "bihbbbiihbhhhhhhhb"},
+    {128, 4, 4, "111111111111111111", 1, "rkbbbkkbbbrbkkkbbb", 1, "bbihhihibbiihhhhhb"},
+    {256, 4, 4, "111111111111111100", 1, "brbrkkkkbkrbkkbbbb", 1, "hihiiihhbhbihhhhhh"},
+};
+const MnRedEntry kMnRed1[] = {
+    {2, 4, 4, "111111111111110000", 1, "kkkbrkbbkkrrbrbbbk", 1, "iiiiiibhbhbihihhhh"},
+    {4, 4, 4, "111111111111010010", 1, "kkrkbkrbbkrkkrbbbb", 1, "iihiihihiiihhbhhbh"},
+    {8, 4, 4, "111111111111111110", 1, "bkrbbbbkkbkkkrkbbb", 1, "hihhhhhbhhbbbibbbh"},
+    {16, 4, 4, "111111111111000011", 1, "kkkkbkkkkkrkkkbbbb", 1, "hhhhihhhhbbbhhhhbi"},
+    {32, 4, 4, "111111111111000001", 1, "krrbkrbkkkrkkbbbbr", 1, "ihbbbhhbbbbbhhhhhb"},
+};
+const MnRedEntry kMnRed2[] = {
+    {2, 4, 4, "111111111100000000", 1, "rkkbbbbkbrbbbbbbbb", 1, "bihihbhhhhhhhhhhhh"},
+    {4, 4, 4, "111111111111111100", 1, "kbrrrrrkrbrrbrbbbb", 1, "bhiihbibhiiihhhhhh"},
+    {8, 4, 4, "111111111111111100", 1, "brrrbrkkkbbrkrbbbb", 1, "iihiibhhihhihhhhhh"},
+    {16, 4, 4, "111111111111011100", 1, "rrkrkrrkkkkkkrbkbb", 1, "iibihiiiibhhhhhhhh"},
+    {32, 4, 4, "111111111111111100", 1, "rrrkkkrrrbbrkbbbbb", 1, "ibbbiibiibihhhhhhh"},
+    {64, 4, 4, "111111111111011100", 1, "kbkkkkkbbrrkkkbbbb", 1, "bihibbiihhibhhhhhh"},
+};
+const MnRedEntry kMnRed16[] = {
+    {16, 4, 4, "111111111100000010", 1, "bkbbrrrrrrkkkkkkkb", 1, "hiihbiihhihhhhhhhh"},
+    {32, 4, 4, "111111111111011000", 1, "kkrbrrrkbkrkkbbkkb", 1, "bhbiibiihhbhhhihhh"},
+    {64, 4, 4, "111111111111010010", 1, "kbkrrkkkbkbbkkkkbb", 1, "iihihhbbhhhhhhhhih"},
+    {128, 4, 4, "111111111111010110", 1, "kkrrkrrkkkkkkkkbbb", 1, "hibihbbihiihhhhiih"},
+    {256, 4, 4, "111111111111010110", 1, "kkkrbkkkkbbkkkkbrb", 1, "bihbhibhbbbhhhhiih"},
+    {512, 4, 4, "111111111111111111", 1, "kbrkkkkrkbkbkkbbbb", 1, "iihhhhhhhhibihiiib"},
+};
+}  // namespace
+
+int mn_reduce_table(int ppn, int gsize, long nbytes, MnReduceCell *c) {
+    const Knobs &K = knobs();
+    // FIND_PPN_INDEX over {1, 2, 16} (reduce_osu.c:2517, common_tuning.h:91-115)
+    const int conf = ppn_conf(ppn);
+    const MnRedEntry *tab = conf == 0 ? (K.smp_use_cma ? kMnRedCma1 : kMnRed1)
+                          : conf == 1 ? (K.smp_use_cma ? kMnRedCma2 : kMnRed2)
+                                      : (K.smp_use_cma ? kMnRedCma16 : kMnRed16);
+    const int ntab = conf == 0 ? 5 : 6;
+    // comm_size_index (:2528-2546): clamped to the table's ends, else log2 of floor_pof2(size) over
+    // floor_pof2(the first entry's numproc) — an index, not a numproc match (the CMA 2- and 16-ppn
+    // tables list their first numproc twice, so e.g. 32 ranks at 16 ppn read the second "16" entry)
+    int ci;
+    if (gsize < tab[0].numproc) {
+        ci = 0;
+    } else if (gsize > tab[ntab - 1].numproc) {
+        ci = ntab - 1;
+    } else {
+        const int lmin = pof2_of(tab[0].numproc), l = pof2_of(gsize);
+        ci = 0;
+        for (int v = l; v > lmin; v >>= 1) ++ci;
+        if (l < lmin) ci = 0;
+    }
+    const MnRedEntry &e = tab[ci];
+    const int ni = (int)strlen(e.inter), nj = (int)strlen(e.intra);
+    const int ii = table_index(nbytes, e.inter_min, ni), ij = table_index(nbytes, e.intra_min, nj);
+    c->entry = ci;
+    c->two_level = e.two_level[ii] == '1';
+    c->inter = e.inter[ii] == 'k' ? ALG_KNOMIAL : e.inter[ii] == 'r' ? ALG_REDSCAT_GATHER : ALG_BINOMIAL;
+    c->intra = e.intra[ij] == 'h' ? ALG_SHMEM_LINEAR : e.intra[ij] == 'i' ? ALG_KNOMIAL : ALG_BINOMIAL;
+    // mv2_reduce_inter_knomial_factor (:2600-2607): MV2_USE_INTER_KNOMIAL_REDUCE_FACTOR, else the
+    // entry's inter_k_degree; both knomial wrappers use it (:1841-1890)
+    const int k = K.reduce_inter_k >= 0 ? K.reduce_inter_k : e.k;
+    c->k = k < 2 ? 2 : k;  // factors 0 and 1 never terminate the reference's trace loop
+    return 0;
+}
+
+int plan_reduce_forced(int n, int root, size_t count, int algo, int k, Plan *p, bool noncomm) {
+    memset(p, 0, sizeof(*p));
+    if (n <= 1) return 0;
+    return reduce_fill(p, algo, n, root, count, k < 2 ? 2 : k, noncomm);
+}
+
 // ---------------------------------------------------------------------------
 // MPI_Reduce_scatter (commutative ops; red_scat_osu.c:1859-1896)
 // ---------------------------------------------------------------------------

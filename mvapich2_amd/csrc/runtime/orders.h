@@ -137,6 +137,18 @@ enum MnIntra : int {
 };
 int mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra = nullptr, int *inter = nullptr);
 int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, Plan *out, int opk = OPK_BUILTIN);
+// several nodes: MPI_Reduce's tuning-table cell (reduce_osu.c:2516-2620) for ppn ranks per node,
+// gsize ranks and nbytes: two_level (MPIR_Reduce_two_level_helper_MV2) with the node step `intra`
+// (ALG_SHMEM_LINEAR / ALG_BINOMIAL / ALG_KNOMIAL to local rank 0) and the leaders' `inter`
+// (ALG_BINOMIAL / ALG_KNOMIAL / ALG_REDSCAT_GATHER), or `inter` flat over every rank; k = the
+// knomial factor; entry = comm_size_index
+struct MnReduceCell {
+    int two_level, inter, intra, k, entry;
+};
+int mn_reduce_table(int ppn, int gsize, long nbytes, MnReduceCell *c);
+// the programs of one reduce algorithm to `root` over n ranks (the steps of the two-level helper
+// and the flat algorithms across nodes)
+int plan_reduce_forced(int n, int root, size_t count, int algo, int k, Plan *out, bool noncomm = false);
 // MPIR_Reduce_binomial_MV2 (reduce_osu.c:425) to `root`, whatever the selection (the leaders' step
 // of MPIR_Reduce_two_level_helper_MV2 across nodes)
 int plan_binomial(int n, int root, Plan *out, bool noncomm = false);
@@ -176,14 +188,15 @@ int nbc_kind();
 // MPI_Reduce the root's node).  big: more ranks (MN_FLAT) or nodes (MN_TWO_LEVEL's leaders) than
 // a program holds (kMaxRanks): the host evaluates the message schedule itself (mpi/user_coll.cpp):
 // forced ALG_PT2PT_RD = recursive doubling, ALG_RING = the ring over [0, U) and recursive doubling
-// on the rest, ALG_BINOMIAL = the binomial reduce to `root` (a node index for the leaders).
+// on the rest, ALG_BINOMIAL / ALG_KNOMIAL (factor k) / ALG_REDSCAT_GATHER = that reduce to `root` (a
+// node index for the leaders).
 enum : int { MN_FLAT = 0, MN_TWO_LEVEL = 1 };
 enum : int { MN_COLL_ALLREDUCE = 0, MN_COLL_REDUCE = 1 };
 struct MnSched {
     int kind;
     int forced;
     long U;
-    int coll, big, root, pad;
+    int coll, big, root, k;  // k: the knomial factor (forced ALG_KNOMIAL)
     Plan p, rem, node, lead;
 };
 int mn_host_schedule(int coll, size_t count, int tsize, int textent, bool in_place, int opk, int root, MnSched *s);

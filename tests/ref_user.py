@@ -150,6 +150,51 @@ def knomial(xs, fn, root, k):
     return node(root)
 
 
+def redscat_gather(xs, fn, count):
+    """MPIR_Reduce_redscat_gather_MV2 (reduce_osu.c:718-1100) for a commutative op: the pre-step (odd
+    ranks below 2 * rem hand their operand to rank - 1, which computes uop(tmp, recvbuf)), recursive
+    halving over pof2 blocks (the last takes the remainder; each step uop(tmp, recvbuf) on the kept
+    half), then the gather: the result every rank's blocks make up"""
+    n = len(xs)
+    pof2 = pof2_of(n)
+    rem = n - pof2
+    rb = [x.copy() for x in xs]
+    for r in range(0, 2 * rem, 2):
+        rb[r] = fn(xs[r + 1], rb[r])
+    real = [2 * nr if nr < rem else nr + rem for nr in range(pof2)]
+    cnts = [count // pof2] * (pof2 - 1) + [count - (count // pof2) * (pof2 - 1)]
+    disps = [sum(cnts[:i]) for i in range(pof2)] + [count]
+    send_idx, recv_idx, last_idx, own = [0] * pof2, [0] * pof2, [pof2] * pof2, [0] * pof2
+    mask = 1
+    while mask < pof2:
+        snap = [rb[real[nr]].copy() for nr in range(pof2)]
+        for nr in range(pof2):
+            nd = nr ^ mask
+            if nr < nd:
+                send_idx[nr] = recv_idx[nr] + pof2 // (mask * 2)
+                lo, hi = recv_idx[nr], send_idx[nr]
+            else:
+                recv_idx[nr] = send_idx[nr] + pof2 // (mask * 2)
+                lo, hi = recv_idx[nr], last_idx[nr]
+            a, b = disps[lo], disps[hi]
+            if b > a:
+                rb[real[nr]][a:b] = fn(snap[nd][a:b], snap[nr][a:b])
+            own[nr] = lo
+            send_idx[nr] = recv_idx[nr]
+        mask <<= 1
+        if mask < pof2:
+            for nr in range(pof2):
+                last_idx[nr] = recv_idx[nr] + pof2 // mask
+    out = xs[0].copy() if pof2 == 1 else np.empty_like(xs[0])
+    if pof2 > 1:
+        for nr in range(pof2):
+            i = own[nr]
+            out[disps[i]:disps[i + 1]] = rb[real[nr]][disps[i]:disps[i + 1]]
+    else:
+        out = rb[0]
+    return out
+
+
 def reduce(xs, fn, commute, dtype_handle, count, root):
     n = len(xs)
     a, kf, root0 = oracle.reduce_select(n, count, dtype_handle, 1 if commute else 2)

@@ -183,6 +183,65 @@ def expected_reduce_scatter(sends, counts, t, op, ppn, via=None):
                                      algo=oracle.ALGOS.index(algo))
 
 
+# the multi-node reduce tables (reduce_tuning.c:1563-1649, tuning/reduce/
+# gen2{_cma}_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h), generated from the headers by
+# tests/golden/gen_mn_reduce_tables.py
+_RTABLES = json.loads((Path(__file__).parent / "golden" / "mn_reduce_tables.json").read_text())
+_RALGO = {"b": "binomial", "k": "knomial", "r": "redscat_gather", "i": "knomial", "h": "shmem_linear"}
+
+
+def _pof2(n):
+    return 1 << (n.bit_length() - 1)
+
+
+def _tindex(nbytes, minsz, size):
+    """the message-size index (reduce_osu.c:2556-2586): floor(log2(nbytes / smallest)), clamped"""
+    if nbytes < minsz:
+        return 0
+    if nbytes > minsz << (size - 1):
+        return size - 1
+    return (nbytes // minsz).bit_length() - 1
+
+
+def reduce_cell(ppn, n, nbytes, cma=True):
+    """MPIR_Reduce_index_tuned_intra_MV2's table step (reduce_osu.c:2516-2620): (two_level, inter
+    letter, intra letter, knomial factor).  comm_size_index = log2(floor_pof2(n) / floor_pof2(first
+    numproc)) clamped to the table's ends — an index, not a numproc match."""
+    tab = _RTABLES[("cma_" if cma else "nocma_") + ("1ppn" if ppn <= 1 else "2ppn" if ppn == 2 else "16ppn")]
+    if n < tab[0]["numproc"]:
+        ci = 0
+    elif n > tab[-1]["numproc"]:
+        ci = len(tab) - 1
+    else:
+        ci = max(0, (_pof2(n) // _pof2(tab[0]["numproc"])).bit_length() - 1)
+    e = tab[ci]
+    ii, ij = _tindex(nbytes, e["inter_min"], len(e["inter"])), _tindex(nbytes, e["intra_min"], len(e["intra"]))
+    return e["two_level"][ii] == "1", e["inter"][ii], e["intra"][ij], e["inter_k"]
+
+
+def expected_reduce(sends, count, t, op, ppn, root):
+    """the root's result of MPI_Reduce across nodes (builtin op): up to 1 KiB the small-message
+    shortcut (reduce_osu.c:2508-2514: the two-level helper with MPIR_Reduce_shmem_MV2 in the node and
+    binomial over the leaders), else the tables: MPIR_Reduce_two_level_helper_MV2 (reduce_osu.c:
+    2030-2330: the node's intra function to local rank 0 — shmem becomes the intra knomial from the
+    32 KiB shmem slot on — then the inter function over the node leaders to the root's node) or the
+    inter function flat over every rank (redscat_gather needs count >= pof2, else binomial).  Every
+    step is the oracle's forced algorithm."""
+    n, nbytes, ext = len(sends), count * TYPES[t][2], TYPES[t][3]
+    nodes, rnode = n // ppn, root // ppn
+    two, inter, intra, _k = (True, "b", "h", 4) if nbytes <= 1024 else reduce_cell(ppn, n, nbytes)
+
+    def run(xs, algo, r):
+        return oracle.reduce_ref([x.copy() for x in xs], count, TYPES[t][0], OPS[op], r,
+                                 algo=oracle.ALGOS.index(_RALGO[algo]))
+    if two:
+        ia = "k" if intra == "h" and count * ext >= 32768 else intra
+        parts = [run(sends[j * ppn:(j + 1) * ppn], ia, 0) if ppn > 1 else sends[j].copy() for j in range(nodes)]
+        return run(parts, inter, rnode) if nodes > 1 else parts[0]
+    algo = "b" if inter == "r" and count < _pof2(n) else inter
+    return run(sends, algo, root)
+
+
 def node_step(xs, count, t, op, intra, knobs=None):
     """the leader's partial after a two-level entry's intra-node function over the node's ranks
     (MPIR_Allreduce_two_level_MV2 :1727-1745)"""
@@ -241,6 +300,17 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
                                ("MPI_DOUBLE", "MPI_MIN", 300, 0)):
         cases.append({"id": f"mr{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
                       "root": root})
+        seed += 1
+    # above 1 KiB the multi-node reduce tables (reduce_osu.c:2516-2660): per size the two-level helper
+    # with its intra (shmem / binomial / intra knomial) and inter (binomial / knomial / redscat_gather)
+    # functions, or one of them flat over every rank (reduce_cell); fp SUM and tie-laden MAX make the
+    # operand order visible
+    for t, op, count, root, ties in (("MPI_FLOAT", "MPI_SUM", 520, 0, False), ("MPI_FLOAT", "MPI_SUM", 1030, n - 1, False),
+                                     ("MPI_FLOAT", "MPI_SUM", 2050, 1 % n, False), ("MPI_DOUBLE", "MPI_SUM", 2049, n - 1, False),
+                                     ("MPI_FLOAT", "MPI_SUM", 16400, 0, False), ("MPI_DOUBLE", "MPI_MAX", 1025, n // 2, True),
+                                     ("MPI_FLOAT", "MPI_SUM", 40000, n - 1, False)):
+        cases.append({"id": f"mq{seed}", "kind": "reduce", "type": t, "op": op, "count": count, "seed": seed,
+                      "root": root, "ties": ties})
         seed += 1
     for count, root in ((70001, n - 1), (1000, 1 % n), (5, 0)):
         cases.append({"id": f"mb{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
@@ -307,10 +377,7 @@ def test_two_level_collectives_across_nodes(n, ppn, tmp_path):
             for r in range(n):
                 assert_bytes_equal(res(cid, r), want[r], t, count, f"{cid} {t} {case['op']} rank {r}")
         elif k == "reduce":
-            rnode = case["root"] // ppn
-            parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0],
-                                       OPS[case["op"]], 0) for j in range(nodes)]
-            want = binomial_leaders(parts, count, t, case["op"], rnode)
+            want = expected_reduce(sends, count, t, case["op"], ppn, case["root"])
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
         elif k == "reduce_scatter":  # MPIR_Reduce_scatter_MV2 flat over every rank
             counts = case["recvcounts"]
@@ -394,6 +461,32 @@ def user_allreduce_across(xs, commute, count, ppn):
     return [lead[r // ppn] for r in range(n)]
 
 
+def user_reduce_across(xs, commute, count, ppn, root):
+    """MPI_Reduce with a user op across nodes (coll.cpp mn_host_schedule): non-commutative -> the
+    flat binomial; commutative -> the device path's selection (expected_reduce), with a user op's
+    flat redscat_gather falling back to binomial (it needs a builtin op, reduce_osu.c:2645-2652) while
+    the two-level helper's leaders run the table's function as it is (:2315)"""
+    n = len(xs)
+    if not commute:
+        return ref_user.reduce(xs, _ufn, False, TYPES["MPI_INT"][0], count, root)
+    nbytes, nodes = count * 4, n // ppn
+    two, inter, intra, k = (True, "b", "h", 4) if nbytes <= 1024 else reduce_cell(ppn, n, nbytes)
+
+    def run(ys, a, r):
+        if a == "b":
+            return ref_user.binomial(ys, _ufn, r, True)
+        if a in "ki":
+            return ref_user.knomial(ys, _ufn, r, k)
+        if a == "h":
+            return ref_user.linear(ys, _ufn)
+        return ref_user.redscat_gather(ys, _ufn, count)
+    if two:
+        ia = "k" if intra == "h" and count * 4 >= 32768 else intra
+        parts = [run(xs[j * ppn:(j + 1) * ppn], ia, 0) if ppn > 1 else xs[j].copy() for j in range(nodes)]
+        return run(parts, inter, root // ppn) if nodes > 1 else parts[0]
+    return run(xs, "b" if inter == "r" else inter, root)
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("n,ppn", [(4, 2), (6, 3), (8, 4), (3, 1), (12, 1), (10, 2)])
 def test_user_ops_across_nodes(n, ppn, tmp_path):
@@ -412,7 +505,7 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
             cases.append({"id": f"ua{seed}", "kind": "user_allreduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed})
             seed += 1
-        for count, root in ((100, n - 1), (3000, 1 % n)):
+        for count, root in ((100, n - 1), (3000, 1 % n), (1030, 0), (4100, n - 1), (16400, n // 2)):
             cases.append({"id": f"ur{seed}", "kind": "user_reduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed, "root": root})
             seed += 1
@@ -434,14 +527,7 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
         elif k == "user_reduce":
             xs = [(np.arange(count, dtype=np.int32) + r) % 7 for r in range(n)]
             root = case["root"]
-            if commute and ppn == 1:
-                want = ref_user.binomial(xs, _ufn, root, True)
-            elif commute:
-                parts = [ref_user.reduce(xs[j * ppn:(j + 1) * ppn], _ufn, True, TYPES["MPI_INT"][0], count, 0)
-                         for j in range(n // ppn)]
-                want = ref_user.binomial(parts, _ufn, root // ppn, True)
-            else:
-                want = ref_user.reduce(xs, _ufn, False, TYPES["MPI_INT"][0], count, root)
+            want = user_reduce_across(xs, commute, count, ppn, root)
             assert np.array_equal(res(cid, root).view(np.int32), want), (cid, root)
         else:
             counts = case["recvcounts"]
@@ -509,7 +595,7 @@ def test_stream_ordered_across_nodes(n, ppn, tmp_path):
 def test_mpit_counts_across_nodes(tmp_path):
     """MPI_T across nodes: Allreduce counts MPIR_Allreduce_two_level_MV2 (allreduce_osu.c:1693) and,
     on the node leaders, the leaders' recursive doubling (pt2pt_rd :366); Reduce counts the
-    two-level helper (reduce_osu.c:2039) and the leaders' binomial (:450); a 2.4 MB Allreduce the
+    two-level helper (reduce_osu.c:2039) and the leaders' function of the table entry; a 2.4 MB Allreduce the
     flat ring wrapper and ring (:3761, :3898); Reduce_scatter (400 floats over 4 ranks) its flat
     recursive halving (red_scat_osu.c:449)."""
     import json
@@ -520,12 +606,17 @@ def test_mpit_counts_across_nodes(tmp_path):
              {"coll": "allreduce", "type": "MPI_FLOAT", "count": 600000},  # the flat ring (wrapper, :3761)
              {"coll": "allreduce", "type": "MPI_FLOAT", "count": 70001}]  # 2-ppn table: flat pt2pt_rs
     res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path, ppn=ppn)
+    # the 4000-byte reduce reads the 2-ppn table: the two-level helper, its leaders' function counted
+    # on the leaders (reduce_osu.c:2315 calls it there)
+    two, inter, _intra, _k = reduce_cell(ppn, n, 4000)
+    assert two
+    lead = {"b": "mv2_coll_reduce_binomial", "k": "mv2_coll_reduce_knomial", "r": "mv2_coll_reduce_redscat_gather"}[inter]
     for r in range(n):
         want = {"mv2_coll_allreduce_2lvl": 1, "mv2_coll_reduce_two_level_helper": 1,
                 "mv2_coll_reduce_scatter_rec_halving": 1, "mv2_coll_allreduce_pt2pt_ring_wrapper": 1, "mv2_coll_allreduce_pt2pt_ring": 1,
                 "mv2_coll_allreduce_shm_rs": 1}
         if r % ppn == 0:
-            want.update({"mv2_coll_allreduce_shm_rd": 1, "mv2_coll_reduce_binomial": 1})
+            want.update({"mv2_coll_allreduce_shm_rd": 1, lead: 1})
         got = json.loads(res("mpit", r).tobytes().decode())
         assert {k: v for k, v in got.items() if v} == want, (r, got)
 
@@ -555,7 +646,9 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
         cases.append({"id": f"m9{seed}", "kind": "allreduce_inplace", "type": "MPI_FLOAT", "op": "MPI_SUM",
                       "count": count, "seed": seed})
         seed += 1
-    for count, root in ((1000, n - 1), (70001, 1)):
+    # MPI_Reduce: the shortcut, then the tables' helper / flat algorithms (knomial and redscat_gather
+    # flat over every rank run their message schedules above 8 ranks, the leaders' above 8 nodes)
+    for count, root in ((1000, n - 1), (70001, 1), (1030, 0), (2050, n - 1), (4100, 2), (16400, n - 1), (40000, 0)):
         cases.append({"id": f"m9{seed}", "kind": "reduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
                       "seed": seed, "root": root})
         seed += 1
@@ -624,9 +717,7 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
             want = oracle.ireduce_ref(sends, count, TYPES[t][0], OPS[case["op"]], case["root"])
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} ireduce root {case['root']}")
         elif k == "reduce":
-            parts = [oracle.reduce_ref([x.copy() for x in sends[j * ppn:(j + 1) * ppn]], count, TYPES[t][0],
-                                       OPS[case["op"]], 0) for j in range(nodes)]
-            want = binomial_leaders(parts, count, t, case["op"], case["root"] // ppn)
+            want = expected_reduce(sends, count, t, case["op"], ppn, case["root"])
             assert_bytes_equal(res(cid, case["root"]), want, t, count, f"{cid} reduce root {case['root']}")
         elif k == "bcast":
             want = as_bytes(inputs(case, case["root"]))

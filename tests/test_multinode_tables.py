@@ -104,3 +104,40 @@ def test_every_builtin_route_is_supported(ppn, gsize):
                         if coll == 2 and gsize > 64:
                             assert r == 5, where
     assert L.mv2h_mn_route(0, 3, 8, 64, 16, 0, 0, None) == 12  # 8 ranks are not 3 per node
+
+
+RED_CODE = {"b": 7, "k": 8, "r": 9, "h": 1, "i": 8}
+
+
+@pytest.mark.parametrize("cma", [1, 0])
+def test_reduce_table_matches_the_headers(cma, monkeypatch):
+    """orders.cpp mn_reduce_table (the multi-node MPI_Reduce selection, reduce_osu.c:2516-2620)
+    against the tests' reading of tests/golden/mn_reduce_tables.json (generated from the reference's
+    gen2{_cma}_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h): every job shape, every size, the CMA
+    and the plain tables (MV2_SMP_USE_CMA)"""
+    from tests.test_gpu_multinode_mp import reduce_cell
+    L = m.lib()
+    monkeypatch.setenv("MV2_SMP_USE_CMA", str(cma))
+    assert L.mv2h_knobs_reload() == 0
+    try:
+        tl, inter, intra, k = (ctypes.c_int() for _ in range(4))
+        for ppn, gsize in JOBS + [(16, 32), (2, 4), (16, 48), (1, 3)]:
+            for nbytes in SIZES + [1 << 19, 1 << 20, (1 << 21) + 5]:
+                L.mv2h_mn_reduce_table(ppn, gsize, nbytes, ctypes.byref(tl), ctypes.byref(inter), ctypes.byref(intra),
+                                       ctypes.byref(k))
+                want = reduce_cell(ppn, gsize, nbytes, cma=bool(cma))
+                assert (bool(tl.value), inter.value, intra.value, k.value) == \
+                    (want[0], RED_CODE[want[1]], RED_CODE[want[2]], want[3]), (ppn, gsize, nbytes, cma)
+    finally:
+        monkeypatch.delenv("MV2_SMP_USE_CMA")
+        L.mv2h_knobs_reload()
+
+
+def test_reduce_table_reads_duplicate_first_entries_by_index():
+    """the CMA 2- and 16-ppn tables list their first numproc twice; comm_size_index is arithmetic
+    (reduce_osu.c:2537-2546), so 4 ranks at 2 ppn read the second "2" entry and 32 ranks at 16 ppn
+    the second "16" entry, as the reference does"""
+    L = m.lib()
+    assert L.mv2h_mn_reduce_table(2, 4, 4096, None, None, None, None) == 1
+    assert L.mv2h_mn_reduce_table(16, 32, 4096, None, None, None, None) == 1
+    assert L.mv2h_mn_reduce_table(16, 64, 4096, None, None, None, None) == 2
