@@ -187,6 +187,11 @@ int mv2h_mn_allreduce_table(int ppn, int gsize, long nbytes, int *intra, int *in
  * (red_scat_osu.c:1859-1893, the default table of red_scat_tuning.c): *algo codes of mv2h_plan
  * (10 rs_ring, 11 rs_rec_halving, 12 rs_pairwise, 13 rs_basic). */
 int mv2h_reduce_scatter_table(int n, long nbytes);
+/* The expression of rank me's block of the non-commutative reduce-scatter over n ranks (the host
+ * evaluates it above 8 ranks): node i is rank leaf[i]'s operand when leaf[i] >= 0, else
+ * uop(in = node b[i], inout = node a[i]); *root the result's node.  Returns the node count, or minus
+ * the count needed when cap is too small. */
+int mv2h_rs_noncomm_expr(int n, int me, int pof2_equal, int *leaf, int *a, int *b, int cap, int *root);
 /* Several nodes: MPI_Reduce's tuning-table cell (reduce_osu.c:2516-2620, the default tables of
  * reduce_tuning.c:1563-1649, CMA or not as MV2_SMP_USE_CMA says): *two_level = 1 for
  * MPIR_Reduce_two_level_helper_MV2, *inter the leaders' (or flat) algorithm and *intra the node step

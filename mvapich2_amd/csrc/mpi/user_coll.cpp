@@ -595,6 +595,18 @@ struct BigEval {
         rs(out);
         redscat = false;
     }
+    // an expression tree (orders.h ExprNode) over the n operands: node e's value into out
+    void expr(const std::vector<ExprNode> &nodes, int e, int l, char *out) {
+        const ExprNode &nd = nodes[(size_t)e];
+        if (nd.leaf >= 0) {
+            copy(out, x(nd.leaf));
+            return;
+        }
+        expr(nodes, nd.a, l + 1, out);  // the inout operand
+        char *in = level(l);
+        expr(nodes, nd.b, l + 1, in);
+        uop(in, out);
+    }
     // MPIR_Allreduce_pt2pt_ring_MV2's chunk c (allreduce_osu.c:3916-3968): x_c, then uop(x_{c+j},
     // acc) for j = 1 .. n-1
     void ring_chunk(int c, char *out) {
@@ -845,14 +857,12 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
 // non-commutative ones.  The nonblocking non-commutative schedules are not restated: those take
 // the canonical rank order x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
 // associative op, applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block (above
-// kMaxRanks ranks from the algorithm's message schedule, BigEval; commutative ops only there).
+// kMaxRanks ranks from the algorithm's message schedule or expression tree, BigEval).
 int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, const HostOp &op) {
     const Job J = job();
     const Typed t = typed(dt);
     if (t.tsize < 0 || t.extent <= 0) return MPI_ERR_TYPE;
     const int n = J.n, me = J.me;
-    // above kMaxRanks ranks the non-commutative forms are not restated (programs over the ranks)
-    if (n > kMaxRanks && op.opk == OPK_USER_NONCOMM) return MPI_ERR_UNSUPPORTED_OPERATION;
     long total = 0, disp = 0;
     std::vector<size_t> cz(n);
     for (int j = 0; j < n; ++j) {
@@ -863,7 +873,17 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     ProgSet ps{};
     Plan p;
     int rc;
-    if (n > kMaxRanks) {
+    const bool noncomm = op.opk == OPK_USER_NONCOMM;
+    if (n > kMaxRanks && noncomm) {
+        // MPIR_Reduce_scatter_non_comm_MV2 (red_scat_osu.c:1367-1760) beyond a program's registers:
+        // this rank's block evaluated from the algorithm's expression (or, for MPI_Ireduce_scatter,
+        // the canonical order, as below); a power-of-two size with equal counts takes the
+        // mirror-permuted halving, else recursive doubling
+        bool equal = true;
+        for (int j = 1; j < n; ++j) equal = equal && counts[j] == counts[0];
+        p.algo = (n & (n - 1)) == 0 && equal ? ALG_RS_NONCOMM_POF2 : ALG_RS_NONCOMM_RD;
+        if (nbc_kind() == NBC_NONE) pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
+    } else if (n > kMaxRanks) {
         // more ranks than a program holds: the algorithm's schedule evaluated for this rank's block
         const int algo = reduce_scatter_algo(n, total * t.tsize);
         p.algo = algo;
@@ -871,7 +891,7 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
         const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
         if (algo == ALG_RS_BASIC) pvar_note_ids(chain, world().rank == 0 ? 3 : 2);
         else pvar_note_ids(&id, 1);
-    } else if (op.opk != OPK_USER_NONCOMM || nbc_kind() == NBC_NONE) {
+    } else if (!noncomm || nbc_kind() == NBC_NONE) {
         if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)t.tsize, (int)t.extent, &p, op.opk))) return rc;
         if (J.multi && p.algo == ALG_RS_BASIC) {  // the reduce inside is the multi-node one
             const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
@@ -928,6 +948,28 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     if ((rc = fetch(o, disp, disp + c, W, rspan))) return rc;
     R.resize((size_t)c * (size_t)t.tsize + 1);
     if (!R.data()) return MPI_ERR_NO_MEM;
+    if (n > kMaxRanks && noncomm) {
+        // the expression's tree over the n operands' block, uop(in = b, inout = a) per node; the
+        // nonblocking canonical order x_0 op (x_1 op (... op x_{n-1}))
+        std::vector<ExprNode> nodes;
+        int root = -1;
+        if (nbc_kind() == NBC_NONE) {
+            root = rs_noncomm_expr(n, me, p.algo == ALG_RS_NONCOMM_POF2, nodes);
+        } else {
+            root = (int)nodes.size();
+            nodes.push_back(ExprNode{n - 1, -1, -1});
+            for (int j = n - 2; j >= 0; --j) {
+                nodes.push_back(ExprNode{j, -1, -1});
+                nodes.push_back(ExprNode{-1, root, (int)nodes.size() - 1});
+                root = (int)nodes.size() - 1;
+            }
+        }
+        BigEval ev{W.data(), rspan, n, c, &t, op.fn, false, {}};
+        std::vector<char> out((size_t)rspan + 1);
+        ev.expr(nodes, root, 0, out.data());
+        if ((rc = dtype_pack(out.data(), c, t.dt, R.data()))) return rc;
+        return dtype_unpack(R.data(), c, t.dt, recvbuf);
+    }
     if (n > kMaxRanks) {
         BigEval ev{W.data(), rspan, n, c, &t, op.fn, true, {}};
         std::vector<char> out((size_t)rspan + 1);

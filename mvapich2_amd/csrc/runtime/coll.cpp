@@ -2829,6 +2829,19 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
 
 extern "C" {
 
+int mv2h_rs_noncomm_expr(int n, int me, int pof2_equal, int *leaf, int *a, int *b, int cap, int *root) {
+    if (n < 1 || me < 0 || me >= n || !root) return E_ARG;
+    std::vector<ExprNode> nodes;
+    *root = rs_noncomm_expr(n, me, pof2_equal != 0, nodes);
+    if ((int)nodes.size() > cap || !leaf || !a || !b) return -(int)nodes.size();
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        leaf[i] = nodes[i].leaf;
+        a[i] = nodes[i].a;
+        b[i] = nodes[i].b;
+    }
+    return (int)nodes.size();
+}
+
 int mv2h_mn_reduce_table(int ppn, int gsize, long nbytes, int *two_level, int *inter, int *intra, int *k) {
     if (ppn < 1 || gsize < 1) return E_ARG;
     MnReduceCell c{};

@@ -1171,6 +1171,15 @@ int plan_reduce(int n, int me, int root, size_t count, int tsize, int textent, P
                   [&] { return plan_reduce_build(n, me, root, count, tsize, textent, p, opk); });
 }
 
+int rs_noncomm_expr(int n, int me, bool pof2_equal, std::vector<ExprNode> &nodes) {
+    Sym s;
+    const int e = pof2_equal ? rs_noncomm_pof2_expr(s, n, me) : rs_noncomm_rd_expr(s, n, me);
+    nodes.clear();
+    nodes.reserve(s.nodes.size());
+    for (const Sym::Node &nd : s.nodes) nodes.push_back(ExprNode{nd.leaf, nd.a, nd.b});
+    return e;
+}
+
 int plan_binomial(int n, int root, Plan *p, bool noncomm) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;

@@ -14,6 +14,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../coll/kernels.h"
 
 namespace mv2 {
@@ -160,6 +162,15 @@ int reduce_scatter_algo(int n, long nbytes);
 // counts[n] per-rank block counts; elements are indexed over the whole operand
 int plan_reduce_scatter(int n, int me, const size_t *counts, int tsize, int textent, Plan *out,
                         int opk = OPK_BUILTIN);
+// The expression of rank me's block of MPIR_Reduce_scatter_non_comm_MV2 over any number of ranks
+// (more than a program's registers: the host evaluates it, mpi/user_coll.cpp): pof2_equal selects
+// MPIR_Reduce_scatter_noncomm_MV2's mirror-permuted halving (red_scat_osu.c:132-290), else the
+// recursive doubling (:1478-1722).  nodes[i].leaf >= 0: that rank's operand; else
+// uop(in = value of nodes[i].b, inout = value of nodes[i].a).  Returns the root node's index.
+struct ExprNode {
+    int leaf, a, b;
+};
+int rs_noncomm_expr(int n, int me, bool pof2_equal, std::vector<ExprNode> &nodes);
 
 // Nonblocking collectives.  While a nonblocking call is being initiated
 // (nbc_set(kind) on this thread), plan_allreduce / plan_reduce /

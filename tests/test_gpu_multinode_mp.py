@@ -497,8 +497,8 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
     MPI_Reduce_scatter: MPIR_Reduce_scatter_MV2's flat selection (non_comm forms included).  Above
     8 ranks (12x1, 5x2) the host evaluates the message schedules themselves (user_coll.cpp
     BigEval: recursive doubling, the ring's own chunk, the binomial; leaders' steps over more than
-    8 nodes; reduce-scatter's basic / recursive halving / ring for this rank's block); the
-    non-commutative reduce-scatter forms there are not restated."""
+    8 nodes; reduce-scatter's basic / recursive halving / ring for this rank's block, and the
+    non-commutative reduce-scatter's recursive doubling as an expression tree)."""
     cases, seed = [], 700
     for commute in (1, 0):
         for count in (100, 2000, 33) + ((600001,) if commute and n > 8 else ()):
@@ -510,8 +510,8 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
                           "type": "MPI_INT", "seed": seed, "root": root})
             seed += 1
         # above 8 ranks: basic (a 24-byte operand, half the blocks empty), halving, ring; the
-        # non_comm forms only up to 8 ranks
-        for per in (3, 400) if n <= 8 else (0, 400, 12000) if commute else ():
+        # non_comm recursive doubling from its expression tree (user_coll.cpp BigEval::expr)
+        for per in (3, 400) if n <= 8 else (0, 400, 12000) if commute else (5, 300):
             counts = [per] * n if not commute else [per + (r % 2) for r in range(n)]
             cases.append({"id": f"us{seed}", "kind": "user_reduce_scatter", "commute": commute, "count": sum(counts),
                           "recvcounts": counts, "type": "MPI_INT", "seed": seed})

@@ -101,3 +101,34 @@ def test_reduce_scatter_block_forms(n):
                     return uop(rh(nr ^ m, k - 1), rh(nr, k - 1), e - b)
                 acc = rh(r // 2 if r < 2 * rem else r - rem, lev)
             assert np.array_equal(acc, full[b * EXT:e * EXT]), (algo, n, r)
+
+
+@pytest.mark.parametrize("n", [9, 12, 13, 16])
+def test_noncomm_reduce_scatter_expression_above_eight_ranks(n):
+    """The non-commutative reduce-scatter above 8 ranks is evaluated on the host from the library's
+    expression of each rank's block (orders.cpp rs_noncomm_expr, red_scat_osu.c:132-290 / :1478-1722);
+    evaluated here with a non-commutative, non-associative function it equals tests/ref_user.py's
+    rank-by-rank restatement for every rank (equal counts: the mirror-permuted halving at n = 16,
+    recursive doubling otherwise)"""
+    import ctypes
+    import numpy as np
+    import mvapich2_amd as m
+    from tests import ref_user
+    L = m.lib()
+    fn = lambda a, b: (a.astype(np.int64) * 2 + b.astype(np.int64) * 3).astype(np.int32)  # noqa: E731
+    counts = [3] * n
+    xs = [((np.arange(3 * n) * 5 + r * 11) % 13).astype(np.int32) for r in range(n)]
+    want = ref_user.reduce_scatter_noncomm(xs, fn, counts)
+    pof2_equal = n & (n - 1) == 0
+    cap = 1 << 16
+    leaf, a, b = ((ctypes.c_int * cap)() for _ in range(3))
+    root = ctypes.c_int()
+    for me in range(n):
+        cnt = L.mv2h_rs_noncomm_expr(n, me, int(pof2_equal), leaf, a, b, cap, ctypes.byref(root))
+        assert cnt > 0
+
+        def ev(e):
+            if leaf[e] >= 0:
+                return xs[leaf[e]][3 * me:3 * me + 3].copy()
+            return fn(ev(b[e]), ev(a[e]))
+        assert np.array_equal(ev(root.value), want[me]), (n, me)
