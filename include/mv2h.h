@@ -192,6 +192,26 @@ int mv2h_reduce_scatter_table(int n, long nbytes);
  * uop(in = node b[i], inout = node a[i]); *root the result's node.  Returns the node count, or minus
  * the count needed when cap is too small. */
 int mv2h_rs_noncomm_expr(int n, int me, int pof2_equal, int *leaf, int *a, int *b, int cap, int *root);
+/* The message schedules the host evaluates for a user op above 8 ranks (mpi/user_coll.cpp BigEval),
+ * run on n int32 operands of count elements each (ops: operand r at ops + r * count) with the fixed
+ * function inout = 2 in + 3 inout; commute as the op's flag.  Writes rank me's (MPI_Reduce: the
+ * root's) result to out: recursive doubling (allreduce_osu.c:455-600), pt2pt_rs (:852-1000),
+ * binomial (reduce_osu.c:577-663), knomial with factor k (:1639-1837), redscat_gather (:718-1100),
+ * the reduce-scatter's recursive halving / pairwise / ring over one block (red_scat_osu.c:428-1180),
+ * and the allreduce ring's chunk me (allreduce_osu.c:3916-3968).  Needs no GPU.  Test hook. */
+enum mv2h_sched_form {
+    MV2H_SCHED_RD = 0,
+    MV2H_SCHED_PT2PT_RS = 1,
+    MV2H_SCHED_BINOMIAL = 2,
+    MV2H_SCHED_KNOMIAL = 3,
+    MV2H_SCHED_REDSCAT_GATHER = 4,
+    MV2H_SCHED_RS_HALVING = 5,
+    MV2H_SCHED_RS_PAIRWISE = 6,
+    MV2H_SCHED_RS_RING = 7,
+    MV2H_SCHED_RING_CHUNK = 8
+};
+int mv2h_host_sched_eval(int form, int n, int me, int root, int k, int count, int commute, const int32_t *ops,
+                         int32_t *out);
 /* Several nodes: MPI_Reduce's tuning-table cell (reduce_osu.c:2516-2620, the default tables of
  * reduce_tuning.c:1563-1649, CMA or not as MV2_SMP_USE_CMA says): *two_level = 1 for
  * MPIR_Reduce_two_level_helper_MV2, *inter the leaders' (or flat) algorithm and *intra the node step

@@ -73,7 +73,8 @@ def lib():
         "mv2h_mn_allreduce_table": ([c_int, c_int, ctypes.c_long, ctypes.POINTER(c_int), ctypes.POINTER(c_int)], c_int),
         "mv2h_reduce_scatter_table": ([c_int, ctypes.c_long], c_int),
         "mv2h_rs_noncomm_expr": ([c_int, c_int, c_int] + [ctypes.POINTER(c_int)] * 3 + [c_int, ctypes.POINTER(c_int)], c_int),
-        "mv2h_mn_reduce_table": ([c_int, c_int, ctypes.c_long] + [ctypes.POINTER(c_int)] * 4, c_int),
+        "mv2h_host_sched_eval": ([c_int] * 7 + [ctypes.c_void_p, ctypes.c_void_p], c_int),
+        "mv2h_mn_reduce_table":([c_int, c_int, ctypes.c_long] + [ctypes.POINTER(c_int)] * 4, c_int),
         "mv2h_mn_route": ([c_int, c_int, c_int, ctypes.c_long, ctypes.c_size_t, c_int, c_int, ctypes.POINTER(c_int)], c_int),
         "mv2h_nbc_begin": ([c_int], c_int),
         "mv2h_nbc_end": ([], c_int),

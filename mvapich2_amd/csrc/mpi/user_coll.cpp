@@ -496,6 +496,7 @@ struct BigEval {
             int owner = 0;
             for (int j = 0; j < lev; ++j) owner = (owner << 1) | ((i >> j) & 1);
             BigEval sub{W + (size_t)b * (size_t)t->extent, rspan, n, (int)c, t, fn, comm, {}};
+            sub.redscat = redscat;  // the block keeps redscat_gather's pre-step
             std::vector<char> part((size_t)rspan + 1);
             sub.rd_value(owner, lev, part.data());
             memcpy(out + (size_t)b * (size_t)t->extent, part.data(), (size_t)dtype_span(t->dt, (int)c));
@@ -984,3 +985,35 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
 }
 
 }  // namespace mv2
+
+namespace {
+// the hook's user function: inout = 2 in + 3 inout, int32 wrapping (neither commutative nor
+// associative, so every operand order shows)
+void hook_fn(void *in, void *inout, int *len, MPI_Datatype *) {
+    const int32_t *a = (const int32_t *)in;
+    int32_t *b = (int32_t *)inout;
+    for (int i = 0; i < *len; ++i) b[i] = (int32_t)((uint32_t)a[i] * 2u + (uint32_t)b[i] * 3u);
+}
+}  // namespace
+
+extern "C" int mv2h_host_sched_eval(int form, int n, int me, int root, int k, int count, int commute,
+                                    const int32_t *ops, int32_t *out) {
+    using namespace mv2;
+    if (n < 1 || count < 1 || me < 0 || me >= n || root < 0 || root >= n || !ops || !out) return MPI_ERR_ARG;
+    const Typed t = typed(MPI_INT);
+    BigEval ev{(const char *)ops, (long)count * 4, n, count, &t, hook_fn, commute != 0, {}};
+    char *o = (char *)out;
+    switch (form) {
+        case MV2H_SCHED_RD: ev.rd(me, o); break;
+        case MV2H_SCHED_PT2PT_RS: ev.rs(o); break;
+        case MV2H_SCHED_BINOMIAL: ev.binomial(root, o); break;
+        case MV2H_SCHED_KNOMIAL: ev.knomial(root, k, o); break;
+        case MV2H_SCHED_REDSCAT_GATHER: ev.redscat_gather(o); break;
+        case MV2H_SCHED_RS_HALVING: ev.rs_halving(me, o); break;
+        case MV2H_SCHED_RS_PAIRWISE: ev.rs_pairwise(me, o); break;
+        case MV2H_SCHED_RS_RING: ev.rs_ring(me, o); break;
+        case MV2H_SCHED_RING_CHUNK: ev.ring_chunk(me, o); break;
+        default: return MPI_ERR_ARG;
+    }
+    return 0;
+}

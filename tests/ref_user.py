@@ -150,18 +150,23 @@ def knomial(xs, fn, root, k):
     return node(root)
 
 
-def redscat_gather(xs, fn, count):
+def redscat_gather(xs, fn, count, allreduce_pre=False):
     """MPIR_Reduce_redscat_gather_MV2 (reduce_osu.c:718-1100) for a commutative op: the pre-step (odd
     ranks below 2 * rem hand their operand to rank - 1, which computes uop(tmp, recvbuf)), recursive
     halving over pof2 blocks (the last takes the remainder; each step uop(tmp, recvbuf) on the kept
-    half), then the gather: the result every rank's blocks make up"""
+    half), then the gather: the result every rank's blocks make up.  allreduce_pre: the pre-step of
+    MPIR_Allreduce_pt2pt_rs_MV2 instead (allreduce_osu.c:852-1000: even ranks hand theirs to rank + 1),
+    whose reduce-scatter + allgather is otherwise the same"""
     n = len(xs)
     pof2 = pof2_of(n)
     rem = n - pof2
     rb = [x.copy() for x in xs]
     for r in range(0, 2 * rem, 2):
-        rb[r] = fn(xs[r + 1], rb[r])
-    real = [2 * nr if nr < rem else nr + rem for nr in range(pof2)]
+        if allreduce_pre:
+            rb[r + 1] = fn(xs[r], rb[r + 1])
+        else:
+            rb[r] = fn(xs[r + 1], rb[r])
+    real = [2 * nr + int(allreduce_pre) if nr < rem else nr + rem for nr in range(pof2)]
     cnts = [count // pof2] * (pof2 - 1) + [count - (count // pof2) * (pof2 - 1)]
     disps = [sum(cnts[:i]) for i in range(pof2)] + [count]
     send_idx, recv_idx, last_idx, own = [0] * pof2, [0] * pof2, [pof2] * pof2, [0] * pof2

@@ -601,14 +601,14 @@ def test_mpit_counts_across_nodes(tmp_path):
     import json
     n, ppn = 4, 2
     calls = [{"coll": "allreduce", "type": "MPI_FLOAT", "count": 300},
-             {"coll": "reduce", "type": "MPI_INT", "count": 1000, "root": n - 1},
+             {"coll": "reduce", "type": "MPI_INT", "count": 2000, "root": n - 1},
              {"coll": "reduce_scatter", "type": "MPI_FLOAT", "count": 100},
              {"coll": "allreduce", "type": "MPI_FLOAT", "count": 600000},  # the flat ring (wrapper, :3761)
              {"coll": "allreduce", "type": "MPI_FLOAT", "count": 70001}]  # 2-ppn table: flat pt2pt_rs
     res = run_workers(n, [{"id": "mpit", "kind": "mpit_counts", "calls": calls}], tmp_path, ppn=ppn)
-    # the 4000-byte reduce reads the 2-ppn table: the two-level helper, its leaders' function counted
+    # the 8000-byte reduce reads the 2-ppn table: the two-level helper, its leaders' function counted
     # on the leaders (reduce_osu.c:2315 calls it there)
-    two, inter, _intra, _k = reduce_cell(ppn, n, 4000)
+    two, inter, _intra, _k = reduce_cell(ppn, n, 8000)
     assert two
     lead = {"b": "mv2_coll_reduce_binomial", "k": "mv2_coll_reduce_knomial", "r": "mv2_coll_reduce_redscat_gather"}[inter]
     for r in range(n):
