@@ -855,10 +855,9 @@ int host_reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, 
 // Reduce_scatter: the order of MPIR_Reduce_scatter_MV2's choice for this rank's block — ring,
 // recursive halving, pairwise or reduce + scatter for commutative ops,
 // MPIR_Reduce_scatter_non_comm_MV2 (mirror-permuted halving or recursive doubling) for
-// non-commutative ones.  The nonblocking non-commutative schedules are not restated: those take
-// the canonical rank order x_0 op (x_1 op (... op x_{n-1})) that MPI-3.1 §5.9.1 requires of an
-// associative op, applied as fn(in = x_i, inout = acc).  Each rank evaluates its own block (above
-// kMaxRanks ranks from the algorithm's message schedule or expression tree, BigEval).
+// non-commutative ones, which MPI_Ireduce_scatter and both block forms choose alike
+// (orders.cpp plan_rs_noncomm).  Each rank evaluates its own block (above kMaxRanks ranks from
+// the algorithm's message schedule or expression tree, BigEval).
 int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, MPI_Datatype dt, const HostOp &op) {
     const Job J = job();
     const Typed t = typed(dt);
@@ -876,10 +875,10 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     int rc;
     const bool noncomm = op.opk == OPK_USER_NONCOMM;
     if (n > kMaxRanks && noncomm) {
-        // MPIR_Reduce_scatter_non_comm_MV2 (red_scat_osu.c:1367-1760) beyond a program's registers:
-        // this rank's block evaluated from the algorithm's expression (or, for MPI_Ireduce_scatter,
-        // the canonical order, as below); a power-of-two size with equal counts takes the
-        // mirror-permuted halving, else recursive doubling
+        // MPIR_Reduce_scatter_non_comm_MV2 (red_scat_osu.c:1367-1760) and the nonblocking / block
+        // forms' same choice (orders.cpp plan_rs_noncomm) beyond a program's registers: this rank's
+        // block evaluated from the algorithm's expression; a power-of-two size with equal counts
+        // takes the mirror-permuted halving, else recursive doubling
         bool equal = true;
         for (int j = 1; j < n; ++j) equal = equal && counts[j] == counts[0];
         p.algo = (n & (n - 1)) == 0 && equal ? ALG_RS_NONCOMM_POF2 : ALG_RS_NONCOMM_RD;
@@ -892,7 +891,7 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
         const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
         if (algo == ALG_RS_BASIC) pvar_note_ids(chain, world().rank == 0 ? 3 : 2);
         else pvar_note_ids(&id, 1);
-    } else if (!noncomm || nbc_kind() == NBC_NONE) {
+    } else {
         if ((rc = plan_reduce_scatter(n, me, cz.data(), (int)t.tsize, (int)t.extent, &p, op.opk))) return rc;
         if (J.multi && p.algo == ALG_RS_BASIC) {  // the reduce inside is the multi-node one
             const int chain[3] = {PV_RS_BASIC, PV_RED_TWO_LEVEL_HELPER, PV_RED_BINOMIAL};
@@ -901,14 +900,6 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
             pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
         }
         ps = p.ps;
-    } else {
-        ps.nprog = 1;
-        ps.p[0].nsteps = (uint8_t)(n - 1);
-        ps.p[0].res = (uint8_t)(n - 1);
-        for (int s = 0; s < n - 1; ++s) {
-            ps.p[0].dst[s] = (uint8_t)(n - 1);
-            ps.p[0].src[s] = (uint8_t)(n - 2 - s);
-        }
     }
     // each rank receives only its own block of every operand (an all-to-all of blocks), except the
     // multi-node basic algorithm, whose reduce every rank evaluates whole
@@ -950,21 +941,9 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     R.resize((size_t)c * (size_t)t.tsize + 1);
     if (!R.data()) return MPI_ERR_NO_MEM;
     if (n > kMaxRanks && noncomm) {
-        // the expression's tree over the n operands' block, uop(in = b, inout = a) per node; the
-        // nonblocking canonical order x_0 op (x_1 op (... op x_{n-1}))
+        // the expression's tree over the n operands' block, uop(in = b, inout = a) per node
         std::vector<ExprNode> nodes;
-        int root = -1;
-        if (nbc_kind() == NBC_NONE) {
-            root = rs_noncomm_expr(n, me, p.algo == ALG_RS_NONCOMM_POF2, nodes);
-        } else {
-            root = (int)nodes.size();
-            nodes.push_back(ExprNode{n - 1, -1, -1});
-            for (int j = n - 2; j >= 0; --j) {
-                nodes.push_back(ExprNode{j, -1, -1});
-                nodes.push_back(ExprNode{-1, root, (int)nodes.size() - 1});
-                root = (int)nodes.size() - 1;
-            }
-        }
+        const int root = rs_noncomm_expr(n, me, p.algo == ALG_RS_NONCOMM_POF2, nodes);
         BigEval ev{W.data(), rspan, n, c, &t, op.fn, false, {}};
         std::vector<char> out((size_t)rspan + 1);
         ev.expr(nodes, root, 0, out.data());

@@ -995,30 +995,40 @@ int reduce_scatter_algo(int n, long nbytes) {
     return reduce_scatter_table(n, nbytes);
 }
 
+// A non-commutative op's reduce-scatter: the power-of-two / equal-count special case (the mirror-
+// permuted recursive halving) or recursive doubling.  The blocking MPIR_Reduce_scatter_non_comm_MV2
+// (red_scat_osu.c:1367-1760), MPI_Ireduce_scatter's MPIR_Ireduce_scatter_tune_helper_MV2
+// (ired_scat_osu.c:191-209: MPIR_Ireduce_scatter_noncomm :29-151 / MPIR_Ireduce_scatter_rec_dbl,
+// ired_scat.c:496-752), MPIR_Reduce_scatter_block_intra (red_scat_block.c:614-640) and
+// MPIR_Ireduce_scatter_block_intra (ired_scat_block.c:910-920; block counts are always equal) all
+// make this choice, and their schedules reduce in the same order (op(received, mine) on the
+// higher rank, op(mine, received) on the lower; the rec_dbl non-power-of-two hand-off inside subtrees)
+static int plan_rs_noncomm(int n, int me, const size_t *counts, Plan *p) {
+    int pof2 = 1;
+    while (pof2 < n) pof2 <<= 1;
+    bool regular = true;
+    for (int j = 0; j + 1 < n; ++j) regular = regular && counts[j] == counts[j + 1];
+    Sym s;
+    int e;
+    if (pof2 == n && regular) {
+        p->algo = ALG_RS_NONCOMM_POF2;
+        e = rs_noncomm_pof2_expr(s, n, me);
+    } else {
+        p->algo = ALG_RS_NONCOMM_RD;
+        e = rs_noncomm_rd_expr(s, n, me);
+    }
+    return single_expr(s, e, p->ps) ? 0 : E_INTERN;
+}
+
 static int plan_reduce_scatter_build(int n, int me, const size_t *counts, int tsize, int textent, Plan *p,
                                      int opk) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
     size_t total = 0;
     for (int j = 0; j < n; ++j) total += counts[j];
-    if (opk == OPK_USER_NONCOMM) {
-        // MPIR_Reduce_scatter_MV2 sends every non-commutative op to MPIR_Reduce_scatter_non_comm_MV2
-        // (red_scat_osu.c:1895-1898): the pof2 / equal-count special case or recursive doubling
-        int pof2 = 1;
-        while (pof2 < n) pof2 <<= 1;
-        bool regular = true;
-        for (int j = 0; j + 1 < n; ++j) regular = regular && counts[j] == counts[j + 1];
-        Sym s;
-        int e;
-        if (pof2 == n && regular) {
-            p->algo = ALG_RS_NONCOMM_POF2;
-            e = rs_noncomm_pof2_expr(s, n, me);
-        } else {
-            p->algo = ALG_RS_NONCOMM_RD;
-            e = rs_noncomm_rd_expr(s, n, me);
-        }
-        return single_expr(s, e, p->ps) ? 0 : E_INTERN;
-    }
+    // MPIR_Reduce_scatter_MV2 sends every non-commutative op to MPIR_Reduce_scatter_non_comm_MV2
+    // (red_scat_osu.c:1895-1898)
+    if (opk == OPK_USER_NONCOMM) return plan_rs_noncomm(n, me, counts, p);
     const int algo = reduce_scatter_table(n, (long)total * tsize);
     p->algo = algo;
     Sym s;
@@ -1085,7 +1095,7 @@ static int plan_ireduce_build(int n, int root, size_t count, Plan *p, int opk) {
 static int plan_ireduce_scatter_build(int n, int me, const size_t *counts, int tsize, bool block, Plan *p, int opk) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
-    if (opk == OPK_USER_NONCOMM) return E_INTERN;  // noncomm / rec_dbl schedules: not restated
+    if (opk == OPK_USER_NONCOMM) return plan_rs_noncomm(n, me, counts, p);
     size_t total = 0;
     for (int j = 0; j < n; ++j) total += counts[j];
     const long nbytes = (long)total * tsize;

@@ -469,7 +469,17 @@ def main():
             sb = m.DeviceBuffer.from_array(x)
             rb = m.DeviceBuffer(max(1, counts[rank]) * 4)
             arr = (ctypes.c_int * n)(*counts)
-            rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, TYPES["MPI_INT"][0], op.value, WORLD)
+            via, req, H = case.get("via"), ctypes.c_int(), TYPES["MPI_INT"][0]
+            if via == "block":
+                rc = L.MPI_Reduce_scatter_block(sb.ptr, rb.ptr, counts[0], H, op.value, WORLD)
+            elif via == "iblock":
+                rc = L.MPI_Ireduce_scatter_block(sb.ptr, rb.ptr, counts[0], H, op.value, WORLD, ctypes.byref(req))
+            elif via == "inb":
+                rc = L.MPI_Ireduce_scatter(sb.ptr, rb.ptr, arr, H, op.value, WORLD, ctypes.byref(req))
+            else:
+                rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, H, op.value, WORLD)
+            if rc == 0 and via in ("iblock", "inb"):
+                rc = L.MPI_Wait(ctypes.byref(req), None)
             assert rc == 0, (case["id"], rc)
             res = rb.download(np.uint8, count=counts[rank] * 4)
             L.MPI_Op_free(ctypes.byref(op))

@@ -211,6 +211,12 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             cases.append({"id": f"ur{seed}", "kind": "user_reduce_scatter", "recvcounts": counts, "count": sum(counts),
                           "commute": commute, "seed": seed, "type": "MPI_INT", "op": "MPI_SUM"})
             seed += 1
+        # the nonblocking and block forms (a non-commutative op: the same noncomm / rec_dbl choice)
+        for via, counts in (("inb", [7 + (r % 3) for r in range(n)]), ("inb", [9] * n), ("block", [6] * n),
+                            ("iblock", [6] * n), ("iblock", [3000] * n)):
+            cases.append({"id": f"ur{seed}", "kind": "user_reduce_scatter", "recvcounts": counts, "count": sum(counts),
+                          "commute": commute, "seed": seed, "type": "MPI_INT", "op": "MPI_SUM", "via": via})
+            seed += 1
     cases.append({"id": f"vb{seed}", "kind": "vector_bcast", "nblocks": 1000, "root": 0, "count": 8000,
                   "seed": seed, "type": "MPI_FLOAT", "op": "MPI_SUM"})
     seed += 1
@@ -266,7 +272,7 @@ def test_collectives_multiprocess(n, geom, tmp_path, golden):
             for r in range(n):
                 assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
         elif k == "user_reduce_scatter":
-            want = user_reduce_scatter_expected(n, case["recvcounts"], case["commute"])
+            want = user_reduce_scatter_expected(n, case["recvcounts"], case["commute"], case.get("via"))
             for r in range(n):
                 assert np.array_equal(res(cid, r).view(np.int32), want[r]), (cid, r)
         elif k == "vector_bcast":
@@ -289,14 +295,21 @@ def user_allreduce_expected(n, count, commute):
     return ref_user.allreduce(xs, ufn, commute, TYPES["MPI_INT"][0], count)
 
 
-def user_reduce_scatter_expected(n, counts, commute):
-    """commutative: MPIR_Reduce_scatter_MV2's choice (ref_user.reduce_scatter); non-commutative:
-    MPIR_Reduce_scatter_non_comm_MV2 (ref_user.reduce_scatter_noncomm)"""
+def user_reduce_scatter_expected(n, counts, commute, via=None):
+    """commutative: MPIR_Reduce_scatter_MV2's choice (ref_user.reduce_scatter), MPI_Ireduce_scatter's
+    pairwise, the block forms' MPICH selection; non-commutative: MPIR_Reduce_scatter_non_comm_MV2
+    (ref_user.reduce_scatter_noncomm), which the nonblocking and block forms choose alike
+    (ired_scat_osu.c:191-209, red_scat_block.c:614-640, ired_scat_block.c:910-920)"""
     total = sum(counts)
     xs = [((np.arange(total) + r) % 7).astype(np.int32) for r in range(n)]
-    if commute:
-        return ref_user.reduce_scatter(xs, ufn, TYPES["MPI_INT"][0], counts)
-    return ref_user.reduce_scatter_noncomm(xs, ufn, counts)
+    h = TYPES["MPI_INT"][0]
+    if not commute:
+        return ref_user.reduce_scatter_noncomm(xs, ufn, counts)
+    if via == "inb":
+        return ref_user.reduce_scatter(xs, ufn, h, counts, algo="rs_pairwise")
+    if via in ("block", "iblock"):
+        return ref_user.reduce_scatter(xs, ufn, h, counts, algo=oracle.ALGOS[oracle.reduce_scatter_block_select(n, counts[0], h)])
+    return ref_user.reduce_scatter(xs, ufn, h, counts)
 
 
 KNOB_RUNS = [

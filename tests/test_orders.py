@@ -323,14 +323,21 @@ def test_noncommutative_reduce_scatter_matches_reference(n):
         total = sum(counts)
         xs = [((np.arange(total) * (r + 3) + r) % 13).astype(np.int64) for r in range(n)]
         want = ref_user.reduce_scatter_noncomm(xs, fn, counts)
-        off = 0
-        for r in range(n):
-            algo, _, _, progs, blk = m.plan("reduce_scatter", n, r, h, counts=counts, opkind=2)
-            regular = len(set(counts)) == 1
-            assert oracle.ALGOS[algo] == ("rs_noncomm_pof2" if pof2 == n and regular else "rs_noncomm_rd")
-            got = eval_progs_fn(xs, progs, blk, off, off + counts[r], fn)
-            assert np.array_equal(got, want[r]), (n, counts, r, oracle.ALGOS[algo])
-            off += counts[r]
+        regular = len(set(counts)) == 1
+        # the blocking call, then MPI_Ireduce_scatter (ired_scat_osu.c:191-209) and, for equal
+        # counts, the block forms (red_scat_block.c:614-640, ired_scat_block.c:910-920): one choice
+        for kind in (None, "ireduce_scatter") + (("reduce_scatter_block",) if regular else ()):
+            off = 0
+            for r in range(n):
+                if kind:
+                    with m.nbc(kind):
+                        algo, _, _, progs, blk = m.plan("reduce_scatter", n, r, h, counts=counts, opkind=2)
+                else:
+                    algo, _, _, progs, blk = m.plan("reduce_scatter", n, r, h, counts=counts, opkind=2)
+                assert oracle.ALGOS[algo] == ("rs_noncomm_pof2" if pof2 == n and regular else "rs_noncomm_rd")
+                got = eval_progs_fn(xs, progs, blk, off, off + counts[r], fn)
+                assert np.array_equal(got, want[r]), (kind, n, counts, r, oracle.ALGOS[algo])
+                off += counts[r]
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 7, 8])
