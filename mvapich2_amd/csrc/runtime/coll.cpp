@@ -348,11 +348,13 @@ static TreeParams tree_from_plan(const Plan &p, int n, size_t count, int me) {
     switch (p.algo) {
     case ALG_PT2PT_RS: return tree_rs(n, count, me, false);
     case ALG_PT2PT_RD: return tree_rs(n, count, me, true);
-    case ALG_SHMEM_LINEAR: {
-        TreeParams tp = tree_base(n);
-        tp.linear = 1;
-        return tp;
-    }
+    case ALG_SHMEM_LINEAR:
+        if (!p.inner) {
+            TreeParams tp = tree_base(n);
+            tp.linear = 1;
+            return tp;
+        }
+        [[fallthrough]];  // reduce_shmem from the shmem slot on: the inner reduce's programs
     default: {
         TreeParams tp = tree_base(n);
         tp.linear = 4;

@@ -722,12 +722,31 @@ static int allreduce_fill(Plan *p, int algo, int n, int me, size_t count, int op
     return ok ? 0 : E_INTERN;
 }
 
+// MPIR_Allreduce_reduce_shmem_MV2 (allreduce_osu.c:1486-1610): below the shmem slot the leader's
+// linear reduction; from the slot size on (count x extent >= MV2_SHMEM_COLL_MAX_MSG_SIZE, :1521-1526)
+// it calls MPICH's MPIR_Reduce_intra to local rank 0 on the node's shmem communicator (not node
+// aware, so flat; reduce.c:865-894): redscat_gather for a builtin op above
+// MPIR_CVAR_REDUCE_SHORT_MSG_SIZE with count >= pof2, else binomial (reduce.c:92-265 and :298-,
+// which reduce in MVAPICH2's binomial / redscat_gather order).  The shmem broadcast then gives every
+// rank local rank 0's result; the plan keeps algo = shmem (its counters) with the reduce in inner.
+static int reduce_shmem_fill(Plan *p, int n, int me, size_t count, int tsize, int textent, int opk) {
+    const Knobs &K = knobs();
+    if ((long)count * textent < K.shmem_coll_max_msg) return allreduce_fill(p, ALG_SHMEM_LINEAR, n, me, count, opk);
+    const long nbytes = (long)count * tsize;
+    const bool rsg = nbytes > K.reduce_short_msg && opk == OPK_BUILTIN && count >= (size_t)pof2_of(n);
+    const int rc = reduce_fill(p, rsg ? ALG_REDSCAT_GATHER : ALG_BINOMIAL, n, 0, count, 0, opk == OPK_USER_NONCOMM);
+    p->inner = p->algo;
+    p->algo = ALG_SHMEM_LINEAR;
+    return rc;
+}
+
 static int plan_allreduce_build(int n, int me, size_t count, int tsize, int textent, bool in_place, int forced,
                                 Plan *p, int opk) {
     memset(p, 0, sizeof(*p));
     if (n <= 1) return 0;
     const Knobs &K = knobs();
-    if (forced == ALG_PT2PT_RS || forced == ALG_PT2PT_RD || forced == ALG_RING || forced == ALG_SHMEM_LINEAR)
+    if (forced == ALG_SHMEM_LINEAR) return reduce_shmem_fill(p, n, me, count, tsize, textent, opk);
+    if (forced == ALG_PT2PT_RS || forced == ALG_PT2PT_RD || forced == ALG_RING)
         return allreduce_fill(p, forced, n, me, count, opk);
     // a non-commutative op fails every shortcut's is_commutative test and ends in
     // recursive doubling whatever the size (allreduce_osu.c:3359-3368, :3893-3898, :802)
@@ -746,7 +765,7 @@ static int plan_allreduce_build(int n, int me, size_t count, int tsize, int text
             }
         }
         if (!tables && K.enable_shmem_allreduce && K.enable_skip_search && nbytes <= K.coll_skip_thr)
-            return allreduce_fill(p, ALG_SHMEM_LINEAR, n, me, count, opk);
+            return reduce_shmem_fill(p, n, me, count, tsize, textent, opk);
     }
     // ALLREDUCE_SKIP_LARGE_MESSAGE_TUNING_TABLES (:163-188): the flat ring wrapper at low ppn
     if (!tables && K.allred_skip_large && K.allred_use_ring == 1 && K.allred_ring_thr <= nbytes &&
@@ -763,13 +782,7 @@ static int plan_allreduce_build(int n, int me, size_t count, int tsize, int text
         if (!(K.enable_shmem_allreduce && K.enable_shmem_collectives))
             return allreduce_fill(p, ALG_PT2PT_RD, n, me, count, opk);
         const int iidx = table_index(nbytes, 1, 18);
-        if (e.intra[iidx] == I_SHMEM) {
-            const int rc = allreduce_fill(p, ALG_SHMEM_LINEAR, n, me, count, opk);
-            // from the shmem slot size on reduce_shmem runs MPICH's MPIR_Reduce_intra (:1521-1526),
-            // whose order is not restated; only reachable through raised thresholds
-            if ((long)count * textent >= K.shmem_coll_max_msg) p->unpinned = 1;
-            return rc;
-        }
+        if (e.intra[iidx] == I_SHMEM) return reduce_shmem_fill(p, n, me, count, tsize, textent, opk);
         // reduce_p2p (:1616-1684): MPIR_Reduce_MV2 to local rank 0, then the shmem bcast
         Plan r;
         const int rc = plan_reduce_build(n, me, 0, count, tsize, textent, &r, opk);

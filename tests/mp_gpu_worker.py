@@ -471,11 +471,12 @@ def main():
             arr = (ctypes.c_int * n)(*counts)
             via, req, H = case.get("via"), ctypes.c_int(), TYPES["MPI_INT"][0]
             if via == "block":
-                rc = L.MPI_Reduce_scatter_block(sb.ptr, rb.ptr, counts[0], H, op.value, WORLD)
+                rc = L.MPI_Reduce_scatter_block(P(sb.ptr), P(rb.ptr), counts[0], H, op.value, WORLD)
             elif via == "iblock":
-                rc = L.MPI_Ireduce_scatter_block(sb.ptr, rb.ptr, counts[0], H, op.value, WORLD, ctypes.byref(req))
+                rc = L.MPI_Ireduce_scatter_block(P(sb.ptr), P(rb.ptr), counts[0], H, op.value, WORLD,
+                                                 ctypes.byref(req))
             elif via == "inb":
-                rc = L.MPI_Ireduce_scatter(sb.ptr, rb.ptr, arr, H, op.value, WORLD, ctypes.byref(req))
+                rc = L.MPI_Ireduce_scatter(P(sb.ptr), P(rb.ptr), arr, H, op.value, WORLD, ctypes.byref(req))
             else:
                 rc = L.MPI_Reduce_scatter(sb.ptr, rb.ptr, arr, H, op.value, WORLD)
             if rc == 0 and via in ("iblock", "inb"):

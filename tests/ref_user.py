@@ -83,9 +83,11 @@ def ring_chunks(xs, fn, count):
     return np.concatenate(out) if out else xs[0][:0].copy()
 
 
-def allreduce(xs, fn, commute, dtype_handle, count, in_place=False, nbytes=None):
+def allreduce(xs, fn, commute, dtype_handle, count, in_place=False, nbytes=None, stride=0, slot=32768):
     """nbytes: the call's count * type size when the elements are of a derived type
-    (the selection depends on it; the algorithms on the element count)"""
+    (the selection depends on it; the algorithms on the element count).  stride: count x extent;
+    reduce_shmem from the shmem slot on (allreduce_osu.c:1521-1526) runs MPICH's MPIR_Reduce_intra
+    to rank 0 — binomial for a user op (reduce.c:874-894) — and broadcasts rank 0's result"""
     n = len(xs)
     if nbytes is None:
         sel = oracle.allreduce_select(n, count, dtype_handle, in_place, 1 if commute else 2)
@@ -95,6 +97,8 @@ def allreduce(xs, fn, commute, dtype_handle, count, in_place=False, nbytes=None)
     if algo == "topo_tree":
         return [tree(xs, fn)] * n
     if algo == "shmem_linear":
+        if stride >= slot:
+            return [binomial(xs, fn, 0, commute)] * n
         return [linear(xs, fn)] * n
     if algo == "ring_wrapper":
         main = 0 if (in_place or count < n) else (count // n) * n

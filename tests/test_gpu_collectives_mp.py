@@ -329,6 +329,12 @@ KNOB_RUNS = [
     # MV2_COLL_SKIP_TABLE_THRESHOLD=0 and no tree: small calls take the tables (pt2pt_rs / RD / two-level)
     ({"MV2_COLL_SKIP_TABLE_THRESHOLD": "0", "MV2_USE_TOPO_AWARE_ALLREDUCE": "0"},
      {"coll_skip_thr": 0, "use_topo_allreduce": 0}, [("MPI_FLOAT", "MPI_SUM", 10), ("MPI_FLOAT", "MPI_SUM", 1)]),
+    # a lowered shmem slot (MV2_SHMEM_COLL_MAX_MSG_SIZE): reduce_shmem runs MPICH's MPIR_Reduce_intra
+    # from it on (allreduce_osu.c:1521-1526: binomial to 2 KiB, redscat_gather above)
+    ({"MV2_SHMEM_COLL_MAX_MSG_SIZE": "1024", "MV2_COLL_SKIP_TABLE_THRESHOLD": "8192",
+      "MV2_TOPO_AWARE_ALLREDUCE_MAX_MSG": "64"},
+     {"shmem_coll_max_msg": 1024, "coll_skip_thr": 8192, "topo_allred_max": 64},
+     [("MPI_DOUBLE", "MPI_SUM", 200), ("MPI_DOUBLE", "MPI_SUM", 301), ("MPI_FLOAT", "MPI_MAX", 1500)]),
 ]
 
 

@@ -183,6 +183,11 @@ KNOB_CASES = [
      {"allred_use_ring": 0, "red_scat_ring_thr": 1024}),
     ({"MV2_COLL_SKIP_TABLE_THRESHOLD": "4096", "MV2_TOPO_AWARE_ALLREDUCE_MAX_MSG": "64"},
      {"coll_skip_thr": 4096, "topo_allred_max": 64}),
+    # reduce_shmem from a lowered shmem slot on: MPICH's MPIR_Reduce_intra (binomial to 2 KiB,
+    # redscat_gather above, allreduce_osu.c:1521-1526); the reduce helper's knomial from the slot
+    ({"MV2_SHMEM_COLL_MAX_MSG_SIZE": "1024", "MV2_COLL_SKIP_TABLE_THRESHOLD": "8192",
+      "MV2_TOPO_AWARE_ALLREDUCE_MAX_MSG": "64"},
+     {"shmem_coll_max_msg": 1024, "coll_skip_thr": 8192, "topo_allred_max": 64}),
 ]
 
 
