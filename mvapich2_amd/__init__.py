@@ -15,7 +15,8 @@ from . import consts
 from .consts import OPS, TYPES
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmpi.so")
+# MV2AMD_LIBMPI: another build of the same library (the host-sanitizer build the CPU tests can run)
+LIB_PATH = os.environ.get("MV2AMD_LIBMPI") or os.path.join(_HERE, "lib", "libmpi.so")
 _lib = None
 
 
@@ -74,7 +75,7 @@ def lib():
         "mv2h_reduce_scatter_table": ([c_int, ctypes.c_long], c_int),
         "mv2h_rs_noncomm_expr": ([c_int, c_int, c_int] + [ctypes.POINTER(c_int)] * 3 + [c_int, ctypes.POINTER(c_int)], c_int),
         "mv2h_host_sched_eval": ([c_int] * 7 + [ctypes.c_void_p, ctypes.c_void_p], c_int),
-        "mv2h_mn_reduce_table":([c_int, c_int, ctypes.c_long] + [ctypes.POINTER(c_int)] * 4, c_int),
+        "mv2h_mn_reduce_table": ([c_int, c_int, ctypes.c_long] + [ctypes.POINTER(c_int)] * 4, c_int),
         "mv2h_mn_route": ([c_int, c_int, c_int, ctypes.c_long, ctypes.c_size_t, c_int, c_int, ctypes.POINTER(c_int)], c_int),
         "mv2h_nbc_begin": ([c_int], c_int),
         "mv2h_nbc_end": ([], c_int),
