@@ -539,6 +539,73 @@ def test_pipe_autotune_agrees_and_keeps_results(n, tmp_path):
             assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"], f"{case['id']} rank {r}")
 
 
+PROTOCOL_VARIANTS = [
+    # the full system-scope release MPI_Init's self-test falls back to when the light release fails
+    # on a topology (coll.cpp coll_selftest) — never taken on a shared GPU by itself
+    {"MV2AMD_LIGHT_RELEASE": "0"},
+    # tilings the init-time autotune can adopt over xGMI (coll.cpp kGrid / kSub), with the
+    # one-shot path narrowed so the pipelined kernel carries the small sizes too
+    {"MV2AMD_PIPE_GRID": "64", "MV2AMD_PIPE_SUB": str(512 << 10)},
+    {"MV2AMD_PIPE_GRID": "256", "MV2AMD_PIPE_SUB": str(16 << 10), "MV2AMD_ONESHOT_MAX": str(16 << 10)},
+]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("vi", range(len(PROTOCOL_VARIANTS)))
+def test_release_and_tiling_variants(n, vi, tmp_path):
+    """The cross-process protocol under the settings a one-rank-per-GPU node may adopt at
+    MPI_Init: the full-release fallback and non-default tilings.  Every collective stays
+    bit-exact with the oracle (the tiling and the release never change a reduction order)."""
+    env = PROTOCOL_VARIANTS[vi]
+    cases, seed = [], 4000
+    for t, op, count in (("MPI_FLOAT", "MPI_SUM", 1000), ("MPI_FLOAT", "MPI_SUM", 70001),
+                         ("MPI_DOUBLE", "MPI_MAX", 300007), ("MPI_FLOAT", "MPI_SUM", (1 << 20) + 3),
+                         ("MPI_FLOAT", "MPI_SUM", 524291), ("MPI_DOUBLE_INT", "MPI_MAXLOC", 70001)):
+        cases.append({"id": f"pv{seed}", "kind": "allreduce", "type": t, "op": op, "count": count, "seed": seed})
+        seed += 1
+    for count, root in ((4096, 1 % n), (300007, n - 1)):
+        cases.append({"id": f"pv{seed}", "kind": "reduce", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": count,
+                      "seed": seed, "root": root})
+        seed += 1
+    for counts in ([70001] * n, [1000 + r for r in range(n)]):
+        cases.append({"id": f"pv{seed}", "kind": "reduce_scatter", "type": "MPI_FLOAT", "op": "MPI_SUM",
+                      "recvcounts": counts, "count": sum(counts), "seed": seed})
+        seed += 1
+    cases.append({"id": f"pv{seed}", "kind": "allgather", "type": "MPI_CHAR", "op": "MPI_SUM", "count": 1 << 20,
+                  "seed": seed})
+    seed += 1
+    cases.append({"id": f"pv{seed}", "kind": "bcast", "type": "MPI_FLOAT", "op": "MPI_SUM", "count": 300007,
+                  "seed": seed, "root": n - 1})
+    res = run_workers(n, cases, tmp_path, extra_env=env)
+    for case in cases:
+        k, cid, t = case["kind"], case["id"], case["type"]
+        if k == "allreduce":
+            want = expected_allreduce(case, n)
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {env} rank {r}")
+        elif k == "reduce":
+            want = expected_reduce(case, n)
+            assert_bytes_equal(res(cid, case["root"]), want, t, case["count"], f"{cid} {env}")
+        elif k == "reduce_scatter":
+            counts = case["recvcounts"]
+            sends = [as_bytes(inputs(dict(case, count=sum(counts)), r)).copy() for r in range(n)]
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
+            off, ext = 0, TYPES[t][3]
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), full[off * ext:(off + counts[r]) * ext], t, counts[r],
+                                   f"{cid} {env} rank {r}")
+                off += counts[r]
+        elif k == "allgather":
+            want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        else:
+            want = as_bytes(inputs(case, case["root"]))
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+
+
 @pytest.mark.parametrize("n", [2, 3])
 def test_stream_ordered_collectives(n, tmp_path):
     """MPIX_*_enqueue (mv2h.h stream-ordered collectives): a chain of calls on one HIP stream,
