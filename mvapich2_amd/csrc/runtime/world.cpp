@@ -456,6 +456,7 @@ int world_init() {
         me.pid = getpid();
         me.device = w.device;
         if (!control_only) {
+            hipDeviceGetAttribute(&me.pci_domain, hipDeviceAttributePciDomainId, w.device);
             hipDeviceGetAttribute(&me.pci_bus, hipDeviceAttributePciBusId, w.device);
             hipDeviceGetAttribute(&me.pci_device, hipDeviceAttributePciDeviceId, w.device);
         }
@@ -490,7 +491,9 @@ int world_init() {
         for (int i = 0; i < w.size; ++i) {
             int c = 0;
             for (int j = 0; j < w.size; ++j)
-                if (w.shm->r[j].pci_bus == w.shm->r[i].pci_bus && w.shm->r[j].pci_device == w.shm->r[i].pci_device) ++c;
+                if (w.shm->r[j].pci_domain == w.shm->r[i].pci_domain && w.shm->r[j].pci_bus == w.shm->r[i].pci_bus &&
+                    w.shm->r[j].pci_device == w.shm->r[i].pci_device)
+                    ++c;
             if (c > w.nshare) w.nshare = c;
         }
         // emulated nodes on one GPU (tests, mv2run --nodes --share-gpu): the GPU is shared with

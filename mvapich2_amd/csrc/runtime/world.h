@@ -59,6 +59,7 @@ struct alignas(64) ShmRank {
     char pad0[56];
     int pid;
     int device;
+    int pci_domain;  // with bus and device: the GPU's identity (segments may reuse bus numbers)
     int pci_bus;
     int pci_device;
     hipIpcMemHandle_t sig_handle;
