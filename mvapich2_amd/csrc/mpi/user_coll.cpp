@@ -746,6 +746,99 @@ int run_split2(const Operands &o, int count, const ProgSet &a, long U, const Pro
     return dtype_unpack(res, count, t.dt, recvbuf);
 }
 
+// MPIR_Allreduce_pt2pt_rd_MV2 (allreduce_osu.c:455-600) with its messages, on one node: each
+// rank keeps its own accumulator in its host window and exchanges it with the step's partner
+// through host shared memory, as the reference's ranks do through their shared-memory channel —
+// the pre-step (an odd rank below 2 * rem reduces uop(tmp = x_{r-1}, acc)), log2(pof2) doubling
+// steps (uop(tmp, acc) if commutative or the partner is lower, else uop(acc, tmp) copied back),
+// the post-step (the even rank takes its partner's result).  The same operand order as the
+// rank's own tree over every operand (the programs), with log2(pof2) uop calls instead of n - 1
+// and one operand fetched instead of n.  Returns with *taken = false (and nothing done) when some
+// rank's window or partner view could not be set up (a small /dev/shm): the caller takes the
+// programs' path, on every rank alike.
+int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op, void *recvbuf, bool *taken) {
+    World &w = world();
+    const int n = w.size, me = w.rank;
+    // MV2AMD_UOP_EXCHANGE: 1 always, 0 never; default from 4 ranks on, where it saves uop calls
+    // (log2(pof2) against n - 1) and operand fetches (one against n); at 2 ranks both make one
+    // call and the programs' path, whose operands never leave pinned memory, measured faster
+    static const long mode = [] {
+        const char *e = getenv("MV2AMD_UOP_EXCHANGE");
+        return e && *e ? atol(e) : -1L;
+    }();
+    *taken = false;
+    if (mode == 0 || (mode < 0 && n < 4)) return 0;
+    const bool comm = op.opk != OPK_USER_NONCOMM;
+    const size_t rspan = (size_t)dtype_span(t.dt, count), P = (size_t)count * (size_t)t.tsize;
+    int pof2 = 1;
+    while (pof2 * 2 <= n) pof2 *= 2;
+    const int rem = n - pof2;
+    const int newrank = me < 2 * rem ? ((me & 1) ? me / 2 : -1) : me - rem;
+    auto real = [&](int q) { return q < rem ? 2 * q + 1 : q + rem; };
+    char *acc = host_window(rspan + 1);
+    bool ok = acc != nullptr;
+    host_barrier();  // every window reserved before any peer view is taken
+    if (me < 2 * rem) ok = ok && host_peer_window((me & 1) ? me - 1 : me + 1, rspan + 1);
+    if (newrank >= 0)
+        for (int mask = 1; mask < pof2; mask <<= 1) ok = ok && host_peer_window(real(newrank ^ mask), rspan + 1);
+    *taken = host_window_vote(ok);
+    if (!*taken) return 0;
+    auto peer = [&](int r) { return host_peer_window(r, rspan + 1); };
+    auto uop = [&](const char *in, char *io) {
+        int c = count;
+        MPI_Datatype d = t.dt;
+        op.fn((void *)in, io, &c, &d);
+    };
+    // this rank's operand into its window, in the type's layout
+    HostBuf pk(HS_PACKED), T(HS_OPERANDS);
+    pk.resize(P + 1);
+    T.resize(rspan + 1);
+    if (!pk.data() || !T.data()) return MPI_ERR_NO_MEM;
+    char *tmp = T.data();
+    int rc;
+    if (mv2h_is_device_ptr(src)) {
+        char *d = dev_scratch(DS_MINE, P);
+        if (!d) return MPI_ERR_NO_MEM;
+        if ((rc = dtype_pack(src, count, t.dt, d))) return rc;
+        if (P && mv2h_memcpy_dtoh(pk.data(), d, P)) return MPI_ERR_OTHER;
+    } else if ((rc = dtype_pack(src, count, t.dt, pk.data()))) {
+        return rc;
+    }
+    if ((rc = dtype_unpack(pk.data(), count, t.dt, acc))) return rc;
+    // pre-step (:455-505)
+    host_barrier();  // every accumulator in place
+    if (me < 2 * rem && (me & 1)) memcpy(tmp, peer(me - 1), rspan);
+    host_barrier();  // every read done before any accumulator changes
+    if (me < 2 * rem && (me & 1)) uop(tmp, acc);
+    // doubling steps (:507-584)
+    for (int mask = 1; mask < pof2; mask <<= 1) {
+        const int dst = newrank >= 0 ? real(newrank ^ mask) : -1;
+        host_barrier();
+        if (dst >= 0) memcpy(tmp, peer(dst), rspan);
+        host_barrier();
+        if (dst < 0) continue;
+        if (comm || dst < me) {
+            uop(tmp, acc);
+        } else {
+            uop(acc, tmp);
+            memcpy(acc, tmp, rspan);
+        }
+    }
+    // post-step (:585-600): the even rank below 2 * rem takes rank + 1's result
+    host_barrier();
+    if (me < 2 * rem && !(me & 1)) memcpy(tmp, peer(me + 1), rspan);
+    const char *res_h = me < 2 * rem && !(me & 1) ? tmp : acc;
+    if ((rc = dtype_pack(res_h, count, t.dt, pk.data()))) return rc;
+    host_barrier();  // the post-step's reads are done before any window is reused
+    char *res = dev_scratch(DS_RES_ALL, P);
+    if (!res) return MPI_ERR_NO_MEM;
+    if (P && mv2h_memcpy_htod(res, pk.data(), P)) return MPI_ERR_OTHER;
+    // operand bytes this rank received (packed measure): pre- or post-step, and one per doubling step
+    world().uop_in_bytes = P * (size_t)((me < 2 * rem) + (newrank >= 0 ? __builtin_ctz((unsigned)pof2) : 0));
+    world().uop_area_bytes = rspan;
+    return dtype_unpack(res, count, t.dt, recvbuf);
+}
+
 // one rank: recvbuf's type map <- src's
 int copy_typemap(const void *src, void *recvbuf, int count, const Typed &t) {
     char *tmp = dev_scratch(DS_MINE, (size_t)count * (size_t)t.tsize);
@@ -807,9 +900,19 @@ int host_allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype d
             if (rc) return rc;
             sp.own = &rem.ps;
             sp.own_base = sp.U;
+            if (sp.U == 0 && rem.algo == ALG_PT2PT_RD) {  // the wrapper's pt2pt_rs is recursive doubling
+                bool taken = false;
+                rc = run_rd_exchange(src, count, t, op, recvbuf, &taken);
+                if (taken) return rc;
+            }
         }
     } else {
         sp.U = uniform_over_ranks(n, me, count, t, in_place, 0, op.opk, p.ps) ? count : 0;
+        if (sp.U == 0 && p.algo == ALG_PT2PT_RD && count > 0) {  // every rank its own tree: the exchanges
+            bool taken = false;
+            rc = run_rd_exchange(src, count, t, op, recvbuf, &taken);
+            if (taken) return rc;
+        }
     }
     return run_split(src, count, t, sp, op.fn, recvbuf, -1);
 }

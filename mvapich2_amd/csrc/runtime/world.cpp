@@ -154,6 +154,98 @@ void host_barrier() {
     }
 }
 
+namespace {
+struct HostWin {
+    char *p = nullptr;
+    size_t cap = 0;
+    int fd = -1;
+};
+HostWin g_own_win;
+HostWin g_peer_win[kMaxRanks];
+std::string window_name(int r) { return g_world.shm_name + ".ux" + std::to_string(r); }
+}  // namespace
+
+char *host_window(size_t bytes) {
+    World &w = g_world;
+    if (!w.shm || w.size <= 1) return nullptr;
+    HostWin &o = g_own_win;
+    if (bytes <= o.cap) return o.p;
+    if (o.fd < 0 && (o.fd = shm_open(window_name(w.rank).c_str(), O_CREAT | O_RDWR, 0600)) < 0) {
+        MV2_DEBUG("host window: shm_open failed");
+        return nullptr;
+    }
+    const size_t page = 1 << 21;
+    size_t want = std::max(bytes, 2 * o.cap);
+    want = (want + page - 1) / page * page;
+    if (posix_fallocate(o.fd, 0, (off_t)want) != 0) {  // a small /dev/shm: the exact size, or nothing
+        want = (bytes + 4095) / 4096 * 4096;
+        if (posix_fallocate(o.fd, 0, (off_t)want) != 0) {
+            MV2_DEBUG("host window: /dev/shm has no room for %zu bytes", bytes);
+            return nullptr;
+        }
+    }
+    if (o.p) munmap(o.p, o.cap);
+    void *q = mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_SHARED, o.fd, 0);
+    if (q == MAP_FAILED) {
+        o.p = nullptr;
+        o.cap = 0;
+        return nullptr;
+    }
+    o.p = (char *)q;
+    o.cap = want;
+    return o.p;
+}
+
+const char *host_peer_window(int r, size_t bytes) {
+    if (r < 0 || r >= kMaxRanks) return nullptr;
+    HostWin &v = g_peer_win[r];
+    if (v.p && v.cap >= bytes) return v.p;
+    const int fd = shm_open(window_name(r).c_str(), O_RDONLY, 0);
+    if (fd < 0) return nullptr;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || (size_t)st.st_size < bytes) {
+        close(fd);
+        return nullptr;
+    }
+    if (v.p) munmap(v.p, v.cap);
+    void *q = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);
+    close(fd);
+    if (q == MAP_FAILED) {
+        v.p = nullptr;
+        v.cap = 0;
+        return nullptr;
+    }
+    v.p = (char *)q;
+    v.cap = (size_t)st.st_size;
+    return v.p;
+}
+
+bool host_window_vote(bool ok) {
+    World &w = g_world;
+    if (w.size == 1 || !w.shm) return ok;
+    host_barrier();  // every window reserved (or not)
+    w.shm->r[w.rank].window_ok = ok ? 1 : 0;
+    host_barrier();
+    bool all = true;
+    for (int j = 0; j < w.size; ++j) all = all && w.shm->r[j].window_ok;
+    host_barrier();  // every vote read before the next vote overwrites it
+    return all;
+}
+
+static void host_windows_release() {
+    World &w = g_world;
+    for (HostWin &v : g_peer_win) {
+        if (v.p) munmap(v.p, v.cap);
+        v = HostWin{};
+    }
+    if (g_own_win.p) munmap(g_own_win.p, g_own_win.cap);
+    if (g_own_win.fd >= 0) {
+        close(g_own_win.fd);
+        shm_unlink(window_name(w.rank).c_str());
+    }
+    g_own_win = HostWin{};
+}
+
 void *get_scratch(int idx, size_t bytes) {
     World &w = g_world;
     if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];
@@ -700,6 +792,7 @@ int world_finalize() {
     }
     if (w.size > 1 && w.shm) {
         host_barrier();
+        host_windows_release();
         for (int j = 0; j < kMaxRanks; ++j) {
             if (j != w.rank && j < w.size && w.size <= kMaxRanks) {
                 if (w.peer_sig.p[j]) hipIpcCloseMemHandle(w.peer_sig.p[j]);

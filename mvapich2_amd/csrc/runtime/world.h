@@ -72,6 +72,7 @@ struct alignas(64) ShmRank {
     hipIpcMemHandle_t g_sig_handle, g_arena_handle, g_rs_handle, g_ag_handle;  // graph lane
     int graph_lane;   // 1: this rank allocated the graph lane
     int selftest_ok;  // coll_selftest verdict of this rank (agreed through host_barrier)
+    int window_ok;    // host_window_vote: this rank's window and its partners' views are in place
     double tune_us[kTuneMax];  // pipe_autotune: this rank's time per candidate tiling
     Knobs knobs;      // MV2_* selection knobs as this rank parsed them (must agree)
     int topo_nlevels;               // this rank's topology levels (world.cpp my_topology)
@@ -194,6 +195,16 @@ World &world();
 int world_init();
 int world_finalize();
 void host_barrier();
+// Host shared-memory windows between the ranks of a node, for host-evaluated reductions that
+// exchange partial results the way the reference's point-to-point algorithms do: this rank's
+// window (grown on demand, backed by /dev/shm space reserved up front so a full tmpfs is an
+// error here and not a SIGBUS later), and a read-only view of a node peer's window of at least
+// `bytes` (nullptr when the peer's window is smaller or absent).  Released by world_finalize.
+char *host_window(size_t bytes);
+const char *host_peer_window(int rank, size_t bytes);
+// Every rank of the node votes `ok`; returns true on every rank iff all voted true (three host
+// barriers: windows reserved before the vote, votes read by everyone before the next one).
+bool host_window_vote(bool ok);
 // beacon phases (ShmRank::beacon)
 enum Beacon { BC_ENTRY = 1, BC_LAUNCH = 2, BC_WAIT = 3, BC_DONE = 4, BC_BARRIER = 5, BC_P2P_WAIT = 6, BC_NET = 7,
               BC_SCRATCH = 8, BC_STAGE = 9, BC_COPY_OUT = 10, BC_LAUNCHED = 11 };

@@ -368,8 +368,8 @@ def test_mv2_selection_knobs(n, tmp_path):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("n", [2, 3, 8])
-def test_user_op_on_strided_vector_operand(n, tmp_path):
+@pytest.mark.parametrize("n,xchg", [(2, None), (3, None), (8, None), (5, None), (3, "1")])
+def test_user_op_on_strided_vector_operand(n, xchg, tmp_path):
     """configs[4]: MPI_Allreduce with a commutative user op on MPI_Type_vector(N, 4, 8, MPI_FLOAT)
     operands (the reference rejects predefined ops on derived types).  The result follows the
     reference's order for the call and only type-map bytes of recvbuf are written (gap bytes keep
@@ -384,7 +384,7 @@ def test_user_op_on_strided_vector_operand(n, tmp_path):
     for seed, (nb, cnt) in enumerate(sizes, start=700):
         cases.append({"id": f"uv{seed}", "kind": "user_vector_allreduce", "nblocks": nb, "count": cnt,
                       "seed": seed})
-    res = run_workers(n, cases, tmp_path, timeout=360)
+    res = run_workers(n, cases, tmp_path, timeout=360, extra_env={"MV2AMD_UOP_EXCHANGE": xchg} if xchg else None)
     fn = lambda a, b: (a * np.float32(0.5) + b * np.float32(1.5)).astype(np.float32)
     for case in cases:
         nb, cnt = case["nblocks"], case["count"]
@@ -413,7 +413,15 @@ def test_user_op_on_strided_vector_operand(n, tmp_path):
             inb, area = (int(v) for v in res(case["id"] + "_staged", r))
             P = cnt * nb * 16
             ring = cnt * nb * 16 >= (2 << 20) and cnt >= n  # the ring wrapper (2 MiB and up, n <= 8)
-            if ring:
+            algo = oracle.ALGOS[oracle.allreduce_select(n, P, 0x4c00010d, False, 1)]  # MPI_BYTE sizing
+            if (algo == "pt2pt_rd" or (algo == "ring_wrapper" and cnt < n)) and (n >= 4 or xchg == "1"):
+                # recursive doubling with its exchanges (user_coll.cpp run_rd_exchange, from 4
+                # ranks on): one operand per step received, the pre- or post-step's included
+                pof2 = ref_user.pof2_of(n)
+                rem = n - pof2
+                recvs = (1 if r < 2 * rem else 0) + (0 if (r < 2 * rem and r % 2 == 0) else pof2.bit_length() - 1)
+                assert inb == recvs * P, (case["id"], r, inb, recvs, P)
+            elif ring:
                 chunk = cnt // n
                 assert inb == (n - 1) * chunk * nb * 16 and area == n * chunk * nb * 16 <= P, \
                     (case["id"], r, inb, area, P)
