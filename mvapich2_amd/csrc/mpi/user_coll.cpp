@@ -775,8 +775,16 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     const int rem = n - pof2;
     const int newrank = me < 2 * rem ? ((me & 1) ? me / 2 : -1) : me - rem;
     auto real = [&](int q) { return q < rem ? 2 * q + 1 : q + rem; };
+    // everything this rank needs is allocated before the vote, so that nothing after it can fail
+    // short of a copy error (a rank leaving after the vote would stall the others' barriers)
+    const bool dev_src = mv2h_is_device_ptr(src);
+    HostBuf pk(HS_PACKED), T(HS_OPERANDS);
+    pk.resize(P + 1);
+    T.resize(rspan + 1);
+    char *d = dev_src ? dev_scratch(DS_MINE, P) : nullptr;
+    char *res = dev_scratch(DS_RES_ALL, P);
     char *acc = host_window(rspan + 1);
-    bool ok = acc != nullptr;
+    bool ok = acc && pk.data() && T.data() && res && (d || !dev_src);
     host_barrier();  // every window reserved before any peer view is taken
     if (me < 2 * rem) ok = ok && host_peer_window((me & 1) ? me - 1 : me + 1, rspan + 1);
     if (newrank >= 0)
@@ -786,19 +794,13 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     auto peer = [&](int r) { return host_peer_window(r, rspan + 1); };
     auto uop = [&](const char *in, char *io) {
         int c = count;
-        MPI_Datatype d = t.dt;
-        op.fn((void *)in, io, &c, &d);
+        MPI_Datatype dd = t.dt;
+        op.fn((void *)in, io, &c, &dd);
     };
     // this rank's operand into its window, in the type's layout
-    HostBuf pk(HS_PACKED), T(HS_OPERANDS);
-    pk.resize(P + 1);
-    T.resize(rspan + 1);
-    if (!pk.data() || !T.data()) return MPI_ERR_NO_MEM;
     char *tmp = T.data();
     int rc;
-    if (mv2h_is_device_ptr(src)) {
-        char *d = dev_scratch(DS_MINE, P);
-        if (!d) return MPI_ERR_NO_MEM;
+    if (dev_src) {
         if ((rc = dtype_pack(src, count, t.dt, d))) return rc;
         if (P && mv2h_memcpy_dtoh(pk.data(), d, P)) return MPI_ERR_OTHER;
     } else if ((rc = dtype_pack(src, count, t.dt, pk.data()))) {
@@ -830,8 +832,6 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     const char *res_h = me < 2 * rem && !(me & 1) ? tmp : acc;
     if ((rc = dtype_pack(res_h, count, t.dt, pk.data()))) return rc;
     host_barrier();  // the post-step's reads are done before any window is reused
-    char *res = dev_scratch(DS_RES_ALL, P);
-    if (!res) return MPI_ERR_NO_MEM;
     if (P && mv2h_memcpy_htod(res, pk.data(), P)) return MPI_ERR_OTHER;
     // operand bytes this rank received (packed measure): pre- or post-step, and one per doubling step
     world().uop_in_bytes = P * (size_t)((me < 2 * rem) + (newrank >= 0 ? __builtin_ctz((unsigned)pof2) : 0));
