@@ -385,7 +385,10 @@ def user_op_lines(L, world, sb, rb, size):
         span = count * ext
         sb.upload(((np.arange(span, dtype=np.int64) % 61) + L.mv2h_rank()).astype(np.float32))
         call = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, count, vt.value, uop.value, world)  # noqa: E731
-        s_, _ = _timed(L, world, call, 3, 1)
+        phases = ("stage", "fetch", "eval", "deliver")
+        ph0 = [m.info(f"uop_{p}_us") for p in phases]
+        s_, _ = _timed(L, world, call, 3, 1)  # 1 + 3 + 3 calls (warmup, timed, kernel-timing loop)
+        ph = {p: round((m.info(f"uop_{p}_us") - a) / 7 / 1e3, 3) for p, a in zip(phases, ph0)}
         got = rb.download(np.float32, count=min(span, 1 << 20))
         k = np.arange(len(got), dtype=np.int64)
         onmap = (k % ext) % 8 < 4
@@ -395,7 +398,7 @@ def user_op_lines(L, world, sb, rb, size):
         L.MPI_Type_free(ctypes.byref(vt))
         del keep
         algo = "ring (own chunk per rank)" if count >= size else "recursive doubling (every rank its own tree)"
-        out.append({"name": name, "s": s_, "payload": count * nb * 16,
+        out.append({"name": name, "s": s_, "payload": count * nb * 16, "phases_ms_rank0": ph,
                     "what": f"configs[4]: commutative user op ({'C' if kind == 'c' else 'numpy via ctypes'}) on "
                             f"{count} x MPI_Type_vector({nb},4,8,MPI_FLOAT), {count * nb * 16 >> 20} MiB payload, {algo}"})
     return {"ok": ok, "lines": out}
@@ -568,7 +571,7 @@ def bench_nranks(args, L, rank, size):
         "bcast_char": line4(bc_s, bc_k, S_BYTES),
         "allreduce_maxloc_double_int": line4(ml_s, ml_k, 2.0 * f * nrec * 12),
         **{u["name"]: {"payload_busbw_GBps": round(2.0 * f * u["payload"] / u["s"] / 1e9, 2), "ms": round(u["s"] * 1e3, 3),
-                       "what": u["what"]} for u in uops["lines"]},
+                       "phases_ms_rank0": u["phases_ms_rank0"], "what": u["what"]} for u in uops["lines"]},
         "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }

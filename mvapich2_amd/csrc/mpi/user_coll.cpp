@@ -38,6 +38,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "../../../include/mv2h.h"
@@ -75,7 +76,7 @@ void HostBuf::resize(size_t n) {
 namespace {
 
 // device scratch kept between calls, grown on demand
-enum DevSlot { DS_MINE, DS_ALL, DS_RES_MINE, DS_RES_ALL, DS_REM, DS_COUNT };
+enum DevSlot { DS_MINE, DS_ALL, DS_RES_MINE, DS_RES_ALL, DS_REM, DS_SPAN, DS_COUNT };
 char *dev_scratch(int slot, size_t bytes) {
     static void *p[DS_COUNT];
     static size_t cap[DS_COUNT];
@@ -99,6 +100,18 @@ Job job() {
     const World &w = world();
     return w.nnodes > 1 ? Job{w.gsize, w.grank, true} : Job{w.size, w.rank, false};
 }
+
+// Phase accounting of a host-evaluated call (World::uop_ns, mv2h_get_info "uop_*_us"): mark(p)
+// charges the time since the previous mark to phase p.
+enum UopPhase { UP_STAGE, UP_FETCH, UP_EVAL, UP_DELIVER };
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(int phase) {
+        const auto now = std::chrono::steady_clock::now();
+        world().uop_ns[phase] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+        t = now;
+    }
+};
 
 struct Typed {
     MPI_Datatype dt;
@@ -241,6 +254,17 @@ int fetch(const Operands &o, long b, long e, HostBuf &W, long &rspan) {
     if (t.contig)  // the slices land in place: one strided copy
         return hipMemcpy2D(W.data(), (size_t)rspan, src, o.stride, rb, (size_t)o.n, hipMemcpyDeviceToHost) == hipSuccess
                    ? 0 : MPI_ERR_OTHER;
+    // a derived layout: unpacked on the device (one kernel per operand), then one copy of the
+    // n spans — the host's own block loop over a sparse layout reads-for-ownership every line
+    // it half-writes, several times slower than moving the gaps over PCIe (r04r: 3.7 ms of a
+    // 4.4 ms call at 2 ranks)
+    if (char *sp = dev_scratch(DS_SPAN, (size_t)rspan * (size_t)o.n)) {
+        for (int j = 0; j < o.n; ++j) {
+            const int rc = dtype_unpack(src + (size_t)j * o.stride, cnt, t.dt, sp + (size_t)j * (size_t)rspan);
+            if (rc) return rc;
+        }
+        return mv2h_memcpy_dtoh(W.data(), sp, (size_t)rspan * (size_t)o.n) ? MPI_ERR_OTHER : 0;
+    }
     HostBuf pk(HS_PACKED);
     pk.resize(rb * (size_t)o.n + 1);
     if (!pk.data()) return MPI_ERR_NO_MEM;
@@ -276,6 +300,44 @@ int eval_range(const ProgSet &ps, long pbase, char *W, long rspan, long b, long 
         x = xe;
     }
     return 0;
+}
+
+int eval_into(const ProgSet &ps, long pbase, char *W, long rspan, long b, long e, const Typed &t,
+              MPI_User_function *fn, char *dst);
+
+// eval_range with the packed result on the device at dev_out: a derived layout's result goes up
+// in the type's layout and is packed there (the host's pack loop is the slow part, see fetch)
+int eval_to_device(const ProgSet &ps, long pbase, char *W, long rspan, long b, long e, const Typed &t,
+                   MPI_User_function *fn, char *dev_out) {
+    const size_t pb = (size_t)(e - b) * (size_t)t.tsize;
+    if (e <= b) return 0;
+    int rc;
+    if (!t.contig) {
+        const long span = dtype_span(t.dt, (int)(e - b));
+        char *sp = dev_scratch(DS_SPAN, (size_t)span);
+        if (sp && ps.nprog == 1) {  // one program: its steps in place, the result register goes up as it is
+            const Prog &p = ps.p[0];
+            for (int s = 0; s < p.nsteps; ++s) {
+                int cnt = (int)(e - b);
+                MPI_Datatype d = t.dt;
+                fn(W + (size_t)p.src[s] * rspan, W + (size_t)p.dst[s] * rspan, &cnt, &d);
+            }
+            if (mv2h_memcpy_htod(sp, W + (size_t)p.res * rspan, (size_t)span)) return MPI_ERR_OTHER;
+            return dtype_pack(sp, (int)(e - b), t.dt, dev_out);
+        }
+        HostBuf R(HS_RESULT);
+        R.resize((size_t)span + 1);
+        if (R.data() && sp) {
+            if ((rc = eval_into(ps, pbase, W, rspan, b, e, t, fn, R.data()))) return rc;
+            if (mv2h_memcpy_htod(sp, R.data(), (size_t)span)) return MPI_ERR_OTHER;
+            return dtype_pack(sp, (int)(e - b), t.dt, dev_out);
+        }
+    }
+    HostBuf R(HS_RESULT);
+    R.resize(pb + 1);
+    if (!R.data()) return MPI_ERR_NO_MEM;
+    if ((rc = eval_range(ps, pbase, W, rspan, b, e, t, fn, R.data()))) return rc;
+    return mv2h_memcpy_htod(dev_out, R.data(), pb) ? MPI_ERR_OTHER : 0;
 }
 
 bool same_progs(const ProgSet &a, const ProgSet &b) {
@@ -362,9 +424,11 @@ int run_split(const void *src, int count, const Typed &t, const Split &sp, MPI_U
               int root) {
     const int n = job().n, me = job().me;
     const bool deliver = root < 0 || me == root;
+    PhaseClock pc;
     Operands ou{}, oo{};
     int rc = stage_split(src, count, t, sp, ou, oo);
     if (rc) return rc;
+    pc.mark(UP_STAGE);
     const long chunk = sp.U ? (sp.U + n - 1) / n : 0;
     const long mb = std::min<long>(sp.U, (long)me * chunk), me_e = std::min<long>(sp.U, mb + chunk);
     char *res_all = dev_scratch(DS_RES_ALL, (size_t)std::max<long>((long)n * chunk, count) * (size_t)t.tsize);
@@ -378,22 +442,26 @@ int run_split(const void *src, int count, const Typed &t, const Split &sp, MPI_U
         if (!res_mine || !R.data()) return MPI_ERR_NO_MEM;
         if (me_e > mb) {
             if ((rc = fetch(ou, mb, me_e, W, rspan))) return rc;
-            if ((rc = eval_range(*sp.uni, 0, W.data(), rspan, mb, me_e, t, fn, R.data()))) return rc;
-            if (mv2h_memcpy_htod(res_mine, R.data(), (size_t)(me_e - mb) * t.tsize)) return MPI_ERR_OTHER;
+            pc.mark(UP_FETCH);
+            if ((rc = eval_to_device(*sp.uni, 0, W.data(), rspan, mb, me_e, t, fn, res_mine))) return rc;
+            pc.mark(UP_EVAL);
         }
         // a short (or empty) last range leaves its padding at or after element U, where the
         // own part below (or nothing) lands
         if ((rc = collect_results(res_mine, res_all, sp.U, chunk, (size_t)t.tsize, root))) return rc;
+        pc.mark(UP_DELIVER);
     }
     if (sp.U < count && deliver) {
-        const size_t ob = (size_t)(count - sp.U) * (size_t)t.tsize;
         if ((rc = fetch(oo, sp.U, count, W, rspan))) return rc;
-        R.resize(ob + 1);
-        if (!R.data()) return MPI_ERR_NO_MEM;
-        if ((rc = eval_range(*sp.own, sp.own_base, W.data(), rspan, sp.U, count, t, fn, R.data()))) return rc;
-        if (mv2h_memcpy_htod(res_all + (size_t)sp.U * t.tsize, R.data(), ob)) return MPI_ERR_OTHER;
+        pc.mark(UP_FETCH);
+        if ((rc = eval_to_device(*sp.own, sp.own_base, W.data(), rspan, sp.U, count, t, fn,
+                                 res_all + (size_t)sp.U * t.tsize)))
+            return rc;
+        pc.mark(UP_EVAL);
     }
-    return deliver ? dtype_unpack(res_all, count, t.dt, recvbuf) : 0;
+    rc = deliver ? dtype_unpack(res_all, count, t.dt, recvbuf) : 0;
+    pc.mark(UP_DELIVER);
+    return rc;
 }
 
 // Run ps over elements [b, e) of the nreg operands at W (rspan bytes apart, element b at offset 0),
@@ -798,6 +866,7 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
         op.fn((void *)in, io, &c, &dd);
     };
     // this rank's operand into its window, in the type's layout
+    PhaseClock pc;
     char *tmp = T.data();
     int rc;
     if (dev_src) {
@@ -807,6 +876,7 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
         return rc;
     }
     if ((rc = dtype_unpack(pk.data(), count, t.dt, acc))) return rc;
+    pc.mark(UP_FETCH);
     // pre-step (:455-505)
     host_barrier();  // every accumulator in place
     if (me < 2 * rem && (me & 1)) memcpy(tmp, peer(me - 1), rspan);
@@ -832,11 +902,14 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     const char *res_h = me < 2 * rem && !(me & 1) ? tmp : acc;
     if ((rc = dtype_pack(res_h, count, t.dt, pk.data()))) return rc;
     host_barrier();  // the post-step's reads are done before any window is reused
+    pc.mark(UP_EVAL);  // the exchanges and the uop calls
     if (P && mv2h_memcpy_htod(res, pk.data(), P)) return MPI_ERR_OTHER;
     // operand bytes this rank received (packed measure): pre- or post-step, and one per doubling step
     world().uop_in_bytes = P * (size_t)((me < 2 * rem) + (newrank >= 0 ? __builtin_ctz((unsigned)pof2) : 0));
     world().uop_area_bytes = rspan;
-    return dtype_unpack(res, count, t.dt, recvbuf);
+    rc = dtype_unpack(res, count, t.dt, recvbuf);
+    pc.mark(UP_DELIVER);
+    return rc;
 }
 
 // one rank: recvbuf's type map <- src's

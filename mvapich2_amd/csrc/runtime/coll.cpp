@@ -809,6 +809,10 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "autotune_us")) *value = (long)(w.tune_ms * 1e3 + 0.5);
     else if (!strcmp(key, "uop_in_bytes")) *value = (long)w.uop_in_bytes;
     else if (!strcmp(key, "uop_area_bytes")) *value = (long)w.uop_area_bytes;
+    else if (!strcmp(key, "uop_stage_us")) *value = (long)(w.uop_ns[0] / 1000);
+    else if (!strcmp(key, "uop_fetch_us")) *value = (long)(w.uop_ns[1] / 1000);
+    else if (!strcmp(key, "uop_eval_us")) *value = (long)(w.uop_ns[2] / 1000);
+    else if (!strcmp(key, "uop_deliver_us")) *value = (long)(w.uop_ns[3] / 1000);
     else if (!strncmp(key, "os_tune_one_", 12) || !strncmp(key, "os_tune_pipe_", 13)) {
         const long i = strtol(strrchr(key, '_') + 1, nullptr, 10);
         if (i < 0 || i >= w.os_tune_n) return E_ARG;

@@ -167,6 +167,10 @@ struct World {
     double tune_us[kTuneMax] = {};                // max over ranks per candidate
     double init_ms = 0, selftest_ms = 0, tune_ms = 0;
     size_t uop_in_bytes = 0, uop_area_bytes = 0;
+    // host-evaluated reductions, cumulative ns per phase (mpi/user_coll.cpp UopPhase): staging the
+    // operands (device pack + exchange), fetching them to the host (D2H + unpack), evaluating (uop
+    // calls + result pack), delivering (H2D + results' exchange + device unpack)
+    uint64_t uop_ns[4] = {0, 0, 0, 0};
     uint64_t api_calls = 0;  // library calls entered (the beacon's call number)
     int hw_queues_set = 0;   // GPU_MAX_HW_QUEUES this library set before HIP started (ranks sharing a GPU)  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
