@@ -104,6 +104,15 @@ Job job() {
 // Phase accounting of a host-evaluated call (World::uop_ns, mv2h_get_info "uop_*_us"): mark(p)
 // charges the time since the previous mark to phase p.
 enum UopPhase { UP_STAGE, UP_FETCH, UP_EVAL, UP_DELIVER };
+
+// Where a derived layout's gaps are handled: on the device (spans cross PCIe, gaps included) or
+// on the host (packed bytes cross PCIe, the host's block loop writes the spans).  A sparse span
+// costs the device route its gap bytes on the link, the host route a read-for-ownership pass over
+// the span; the link is the GPU's, shared by the ranks on it, the host loop is each rank's own
+// core.  Measured on the configs[4] vector (half gaps): the device route wins with the link to
+// itself or shared by 2 (4.4 -> 3.6 ms per call), the host route with 8 ranks on one link
+// (7.5 -> 10 ms); the crossover of the two costs is at a few ranks per link.
+bool layout_on_device() { return world().nshare <= 4; }
 struct PhaseClock {
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     void mark(int phase) {
@@ -258,7 +267,7 @@ int fetch(const Operands &o, long b, long e, HostBuf &W, long &rspan) {
     // n spans — the host's own block loop over a sparse layout reads-for-ownership every line
     // it half-writes, several times slower than moving the gaps over PCIe (r04r: 3.7 ms of a
     // 4.4 ms call at 2 ranks)
-    if (char *sp = dev_scratch(DS_SPAN, (size_t)rspan * (size_t)o.n)) {
+    if (char *sp = layout_on_device() ? dev_scratch(DS_SPAN, (size_t)rspan * (size_t)o.n) : nullptr) {
         for (int j = 0; j < o.n; ++j) {
             const int rc = dtype_unpack(src + (size_t)j * o.stride, cnt, t.dt, sp + (size_t)j * (size_t)rspan);
             if (rc) return rc;
@@ -312,7 +321,7 @@ int eval_to_device(const ProgSet &ps, long pbase, char *W, long rspan, long b, l
     const size_t pb = (size_t)(e - b) * (size_t)t.tsize;
     if (e <= b) return 0;
     int rc;
-    if (!t.contig) {
+    if (!t.contig && layout_on_device()) {
         const long span = dtype_span(t.dt, (int)(e - b));
         char *sp = dev_scratch(DS_SPAN, (size_t)span);
         if (sp && ps.nprog == 1) {  // one program: its steps in place, the result register goes up as it is
@@ -845,14 +854,21 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     auto real = [&](int q) { return q < rem ? 2 * q + 1 : q + rem; };
     // everything this rank needs is allocated before the vote, so that nothing after it can fail
     // short of a copy error (a rank leaving after the vote would stall the others' barriers)
-    const bool dev_src = mv2h_is_device_ptr(src);
+    const bool dev_src = mv2h_is_device_ptr(src), dev_dst = mv2h_is_device_ptr(recvbuf);
+    // the operand's bytes from its true lower bound on (the layout is copied as it is, gaps
+    // included: no pack / unpack on the host, whose block loop over a sparse span is slow)
+    MPI_Aint tlb = 0, text = 0;
+    PMPI_Type_get_true_extent(t.dt, &tlb, &text);
+    const bool direct = tlb >= 0 && (t.contig || layout_on_device());
+    const size_t dlen = direct ? rspan - (size_t)tlb : 0;
     HostBuf pk(HS_PACKED), T(HS_OPERANDS);
     pk.resize(P + 1);
     T.resize(rspan + 1);
-    char *d = dev_src ? dev_scratch(DS_MINE, P) : nullptr;
+    char *d = dev_src && !direct ? dev_scratch(DS_MINE, P) : nullptr;
     char *res = dev_scratch(DS_RES_ALL, P);
+    char *sp = dev_dst && direct ? dev_scratch(DS_SPAN, rspan) : nullptr;
     char *acc = host_window(rspan + 1);
-    bool ok = acc && pk.data() && T.data() && res && (d || !dev_src);
+    bool ok = acc && pk.data() && T.data() && res && (d || !(dev_src && !direct)) && (sp || !(dev_dst && direct));
     host_barrier();  // every window reserved before any peer view is taken
     if (me < 2 * rem) ok = ok && host_peer_window((me & 1) ? me - 1 : me + 1, rspan + 1);
     if (newrank >= 0)
@@ -869,13 +885,21 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     PhaseClock pc;
     char *tmp = T.data();
     int rc;
-    if (dev_src) {
-        if ((rc = dtype_pack(src, count, t.dt, d))) return rc;
-        if (P && mv2h_memcpy_dtoh(pk.data(), d, P)) return MPI_ERR_OTHER;
-    } else if ((rc = dtype_pack(src, count, t.dt, pk.data()))) {
-        return rc;
+    if (direct) {
+        if (dev_src) {
+            if (dlen && mv2h_memcpy_dtoh(acc + tlb, (const char *)src + tlb, dlen)) return MPI_ERR_OTHER;
+        } else {
+            memcpy(acc + tlb, (const char *)src + tlb, dlen);
+        }
+    } else {
+        if (dev_src) {
+            if ((rc = dtype_pack(src, count, t.dt, d))) return rc;
+            if (P && mv2h_memcpy_dtoh(pk.data(), d, P)) return MPI_ERR_OTHER;
+        } else if ((rc = dtype_pack(src, count, t.dt, pk.data()))) {
+            return rc;
+        }
+        if ((rc = dtype_unpack(pk.data(), count, t.dt, acc))) return rc;
     }
-    if ((rc = dtype_unpack(pk.data(), count, t.dt, acc))) return rc;
     pc.mark(UP_FETCH);
     // pre-step (:455-505)
     host_barrier();  // every accumulator in place
@@ -900,14 +924,21 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     host_barrier();
     if (me < 2 * rem && !(me & 1)) memcpy(tmp, peer(me + 1), rspan);
     const char *res_h = me < 2 * rem && !(me & 1) ? tmp : acc;
-    if ((rc = dtype_pack(res_h, count, t.dt, pk.data()))) return rc;
+    if (direct && dev_dst) {  // the result's span up, its type map packed on the device
+        if (dlen && mv2h_memcpy_htod(sp + tlb, res_h + tlb, dlen)) return MPI_ERR_OTHER;
+        if ((rc = dtype_pack(sp, count, t.dt, res))) return rc;
+    } else if (direct) {  // a host receive buffer: its type map from the result's
+        dtype_merge_typemap((char *)recvbuf, res_h, t.dt, count);
+    } else if ((rc = dtype_pack(res_h, count, t.dt, pk.data()))) {
+        return rc;
+    }
     host_barrier();  // the post-step's reads are done before any window is reused
     pc.mark(UP_EVAL);  // the exchanges and the uop calls
-    if (P && mv2h_memcpy_htod(res, pk.data(), P)) return MPI_ERR_OTHER;
+    if (!direct && P && mv2h_memcpy_htod(res, pk.data(), P)) return MPI_ERR_OTHER;
     // operand bytes this rank received (packed measure): pre- or post-step, and one per doubling step
     world().uop_in_bytes = P * (size_t)((me < 2 * rem) + (newrank >= 0 ? __builtin_ctz((unsigned)pof2) : 0));
     world().uop_area_bytes = rspan;
-    rc = dtype_unpack(res, count, t.dt, recvbuf);
+    rc = direct && !dev_dst ? 0 : dtype_unpack(res, count, t.dt, recvbuf);
     pc.mark(UP_DELIVER);
     return rc;
 }

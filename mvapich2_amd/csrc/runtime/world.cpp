@@ -159,6 +159,7 @@ struct HostWin {
     char *p = nullptr;
     size_t cap = 0;
     int fd = -1;
+    bool pinned = false;  // own window: registered with HIP, so device copies to and from it are DMA
 };
 HostWin g_own_win;
 HostWin g_peer_win[kMaxRanks];
@@ -184,15 +185,21 @@ char *host_window(size_t bytes) {
             return nullptr;
         }
     }
-    if (o.p) munmap(o.p, o.cap);
+    if (o.p) {
+        if (o.pinned) hipHostUnregister(o.p);
+        munmap(o.p, o.cap);
+    }
     void *q = mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_SHARED, o.fd, 0);
     if (q == MAP_FAILED) {
         o.p = nullptr;
         o.cap = 0;
+        o.pinned = false;
         return nullptr;
     }
     o.p = (char *)q;
     o.cap = want;
+    o.pinned = hipHostRegister(o.p, o.cap, hipHostRegisterDefault) == hipSuccess;
+    if (!o.pinned) (void)hipGetLastError();  // still usable, through staged copies
     return o.p;
 }
 
@@ -238,7 +245,10 @@ static void host_windows_release() {
         if (v.p) munmap(v.p, v.cap);
         v = HostWin{};
     }
-    if (g_own_win.p) munmap(g_own_win.p, g_own_win.cap);
+    if (g_own_win.p) {
+        if (g_own_win.pinned) hipHostUnregister(g_own_win.p);
+        munmap(g_own_win.p, g_own_win.cap);
+    }
     if (g_own_win.fd >= 0) {
         close(g_own_win.fd);
         shm_unlink(window_name(w.rank).c_str());
