@@ -213,7 +213,13 @@ __device__ __forceinline__ void block_done(const Done &d) {
             return;
         if (__hip_atomic_fetch_add(c + (kDoneSub + x) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != subs)
             return;
+        // this XCD's L2 written back before its group counts as done.  The wait is explicit: after a
+        // returned atomic the compiler drops the s_waitcnt behind buffer_wbl2 (MI355X_MICROARCH.md,
+        // compiler hazard), and the next add then overtook the write-back — the host saw the word
+        // while another XCD's dirty lines were still in its L2, and a copy engine reading the result
+        // (point-to-point copies of a host-driven schedule) read stale bytes (r04x, 12-rank Iallreduce)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (__hip_atomic_fetch_add(c + (kDoneSub + 8) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups)
             return;
         for (int k = 0; k < kDoneCtrs; ++k)
