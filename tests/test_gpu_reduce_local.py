@@ -166,3 +166,32 @@ def test_op_table_entries_on_device_buffers():
     assert L.MPIR_Op_errno() == 9
     assert L.MPIR_Op_errno() == 0
     assert np.all(b.download(np.float32) == 5)
+
+
+def test_result_visible_to_a_copy_engine_at_return():
+    """A blocking call returns on the kernel-written completion word, before the kernel's own
+    end-of-kernel release; the result must nevertheless be in memory for any reader at that point
+    (device_util.h block_done: every XCD's L2 written back before its group counts, r04y).  A copy
+    on a non-blocking stream issued right at return — not ordered behind the kernel — reads it;
+    SUM of integers with a fresh pattern per round, so a stale line shows as the previous round's
+    value.  A guard of the contract, not a reproducer: one run against the pre-fix word passed
+    (the race is rare; r04x's failure came from a 12-rank schedule under load)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(st), 1) == 0  # hipStreamNonBlocking
+    L = m.lib()
+    count = 16 << 20  # 64 MiB of int32: every XCD's L2 holds dirty lines of the result
+    I32, SUM = TYPES["MPI_INT"][0], OPS["MPI_SUM"]
+    a, b, c = m.DeviceBuffer(count * 4), m.DeviceBuffer(count * 4), m.DeviceBuffer(count * 4)
+    a.upload(np.ones(count, dtype=np.int32))
+    for rnd in range(12):
+        b.upload(np.full(count, rnd * 1000, dtype=np.int32))
+        L.mv2h_device_synchronize()
+        assert L.MPI_Reduce_local(a.ptr, b.ptr, count, I32, SUM) == 0
+        assert hip.hipMemcpyAsync(ctypes.c_void_p(c.ptr), ctypes.c_void_p(b.ptr), ctypes.c_size_t(count * 4), 3, st) == 0
+        assert hip.hipStreamSynchronize(st) == 0
+        got = c.download(np.int32, count=count)
+        bad = np.flatnonzero(got != rnd * 1000 + 1)
+        assert bad.size == 0, (rnd, bad.size, bad[:4], got[bad[:4]])
+    hip.hipStreamDestroy(st)
