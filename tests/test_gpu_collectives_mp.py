@@ -547,6 +547,116 @@ def test_pipe_autotune_agrees_and_keeps_results(n, tmp_path):
             assert_bytes_equal(res(case["id"], r), want[r], case["type"], case["count"], f"{case['id']} rank {r}")
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,seed0", [(3, 5000), (4, 6000), (8, 7000)])
+def test_random_sequence_of_collectives(n, seed0, tmp_path):
+    """A seeded random sequence of 48 blocking and nonblocking collectives back to back — every
+    kind, one-shot and pipelined sizes, ragged tails, several roots, types and ops — so that the
+    arenas, epochs, completion words and plan cache are reused across kinds and sizes in orders no
+    other test takes; every result bit-exact with the oracle."""
+    rng = np.random.default_rng(seed0)
+    kinds = ["allreduce", "allreduce_inplace", "iallreduce", "reduce", "ireduce", "reduce_scatter", "allgather",
+             "bcast"]
+    cases = []
+    for i in range(48):
+        k = kinds[int(rng.integers(len(kinds)))]
+        op, t = BASIC[int(rng.integers(len(BASIC)))]
+        if k in ("allgather", "bcast"):
+            t, op = "MPI_CHAR" if k == "allgather" else "MPI_FLOAT", "MPI_SUM"
+        count = int(rng.choice([1, 5, 777, 4099, 33333, 70001, 200003]))
+        if t in ("MPI_SHORT_INT", "MPI_C_FLOAT_COMPLEX"):
+            count = min(count, 4099)
+        case = {"id": f"rq{seed0 + i}", "kind": k, "type": t, "op": op, "count": count, "seed": seed0 + i,
+                "small": op == "MPI_PROD", "root": int(rng.integers(n))}
+        if k == "reduce_scatter":
+            counts = [count // n + int(rng.integers(0, 3)) for _ in range(n)]
+            case.update(recvcounts=counts, count=sum(counts))
+        cases.append(case)
+    res = run_workers(n, cases, tmp_path)
+    for case in cases:
+        k, cid, t = case["kind"], case["id"], case["type"]
+        if k in ("allreduce", "allreduce_inplace", "iallreduce"):
+            want = expected_allreduce(case, n)
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {k} {t} {case['op']} rank {r}")
+        elif k in ("reduce", "ireduce"):
+            want = expected_reduce(case, n)
+            assert_bytes_equal(res(cid, case["root"]), want, t, case["count"], f"{cid} {k} {t} {case['op']}")
+        elif k == "reduce_scatter":
+            counts = case["recvcounts"]
+            sends = [as_bytes(inputs(dict(case, count=sum(counts)), r)).copy() for r in range(n)]
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
+            off, ext = 0, TYPES[t][3]
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), full[off * ext:(off + counts[r]) * ext], t, counts[r], f"{cid} rank {r}")
+                off += counts[r]
+        elif k == "allgather":
+            want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        else:
+            want = as_bytes(inputs(case, case["root"]))
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+
+
+# (op, type) pairs whose result does not depend on the reduction order (wrapping integer arithmetic,
+# bitwise and logical ops, integer MAX / MAXLOC): any algorithm's bits equal the one-node oracle's
+ORDER_FREE = [("MPI_SUM", "MPI_INT"), ("MPI_PROD", "MPI_INT"), ("MPI_BXOR", "MPI_UNSIGNED_CHAR"),
+              ("MPI_LAND", "MPI_C_BOOL"), ("MPI_MAX", "MPI_INT"), ("MPI_MAXLOC", "MPI_2INT"), ("MPI_BOR", "MPI_LONG")]
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("n,ppn,seed0", [(6, 3, 8000), (12, 4, 9000)])
+def test_random_sequence_across_nodes(n, ppn, seed0, tmp_path):
+    """The random sequence on emulated nodes (node-major ranks, leaders over TCP; 12 ranks take the
+    message schedules over the point-to-point channels), with order-free (op, type) pairs so that
+    every multi-node algorithm must reproduce the one-node oracle's bits exactly."""
+    rng = np.random.default_rng(seed0)
+    kinds = ["allreduce", "iallreduce", "reduce", "ireduce", "reduce_scatter", "allgather", "bcast"]
+    cases = []
+    for i in range(36):
+        k = kinds[int(rng.integers(len(kinds)))]
+        op, t = ORDER_FREE[int(rng.integers(len(ORDER_FREE)))]
+        if k in ("allgather", "bcast"):
+            t, op = "MPI_CHAR" if k == "allgather" else "MPI_INT", "MPI_SUM"
+        count = int(rng.choice([1, 5, 777, 4099, 33333, 70001, 700003]))
+        case = {"id": f"rn{seed0 + i}", "kind": k, "type": t, "op": op, "count": count, "seed": seed0 + i,
+                "small": op == "MPI_PROD", "root": int(rng.integers(n))}
+        if k == "reduce_scatter":
+            counts = [count // n + int(rng.integers(0, 3)) for _ in range(n)]
+            case.update(recvcounts=counts, count=sum(counts))
+        cases.append(case)
+    res = run_workers(n, cases, tmp_path, ppn=ppn, timeout=300)
+    for case in cases:
+        k, cid, t = case["kind"], case["id"], case["type"]
+        if k in ("allreduce", "iallreduce"):
+            sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+            want = oracle.allreduce_ref(sends, case["count"], TYPES[t][0], OPS[case["op"]])
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), want[r], t, case["count"], f"{cid} {k} {t} {case['op']} rank {r}")
+        elif k in ("reduce", "ireduce"):
+            sends = [inputs(case, r).view(np.uint8).ravel().copy() for r in range(n)]
+            want = oracle.reduce_ref(sends, case["count"], TYPES[t][0], OPS[case["op"]], case["root"])
+            assert_bytes_equal(res(cid, case["root"]), want, t, case["count"], f"{cid} {k} {t} {case['op']}")
+        elif k == "reduce_scatter":
+            counts = case["recvcounts"]
+            sends = [as_bytes(inputs(dict(case, count=sum(counts)), r)).copy() for r in range(n)]
+            full = oracle.reduce_scatter_ref(sends, counts, TYPES[t][0], OPS[case["op"]])
+            off, ext = 0, TYPES[t][3]
+            for r in range(n):
+                assert_bytes_equal(res(cid, r), full[off * ext:(off + counts[r]) * ext], t, counts[r], f"{cid} rank {r}")
+                off += counts[r]
+        elif k == "allgather":
+            want = np.concatenate([as_bytes(inputs(case, r)) for r in range(n)])
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+        else:
+            want = as_bytes(inputs(case, case["root"]))
+            for r in range(n):
+                assert np.array_equal(res(cid, r), want), (cid, r)
+
+
 PROTOCOL_VARIANTS = [
     # the full system-scope release MPI_Init's self-test falls back to when the light release fails
     # on a topology (coll.cpp coll_selftest) — never taken on a shared GPU by itself
