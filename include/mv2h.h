@@ -198,7 +198,9 @@ int mv2h_rs_noncomm_expr(int n, int me, int pof2_equal, int *leaf, int *a, int *
  * root's) result to out: recursive doubling (allreduce_osu.c:455-600), pt2pt_rs (:852-1000),
  * binomial (reduce_osu.c:577-663), knomial with factor k (:1639-1837), redscat_gather (:718-1100),
  * the reduce-scatter's recursive halving / pairwise / ring over one block (red_scat_osu.c:428-1180),
- * and the allreduce ring's chunk me (allreduce_osu.c:3916-3968).  Needs no GPU.  Test hook. */
+ * the allreduce ring's chunk me (allreduce_osu.c:3916-3968), and the non-commutative reduce-scatter's
+ * expression for block me with equal counts (red_scat_osu.c:132-290 / :1478-1722).  Needs no GPU.
+ * Test hook. */
 enum mv2h_sched_form {
     MV2H_SCHED_RD = 0,
     MV2H_SCHED_PT2PT_RS = 1,
@@ -208,7 +210,8 @@ enum mv2h_sched_form {
     MV2H_SCHED_RS_HALVING = 5,
     MV2H_SCHED_RS_PAIRWISE = 6,
     MV2H_SCHED_RS_RING = 7,
-    MV2H_SCHED_RING_CHUNK = 8
+    MV2H_SCHED_RING_CHUNK = 8,
+    MV2H_SCHED_RS_NONCOMM = 9  /* the non-commutative reduce-scatter's expression for rank me's block */
 };
 int mv2h_host_sched_eval(int form, int n, int me, int root, int k, int count, int commute, const int32_t *ops,
                          int32_t *out);

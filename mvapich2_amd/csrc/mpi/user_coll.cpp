@@ -1199,6 +1199,13 @@ extern "C" int mv2h_host_sched_eval(int form, int n, int me, int root, int k, in
         case MV2H_SCHED_RS_PAIRWISE: ev.rs_pairwise(me, o); break;
         case MV2H_SCHED_RS_RING: ev.rs_ring(me, o); break;
         case MV2H_SCHED_RING_CHUNK: ev.ring_chunk(me, o); break;
+        case MV2H_SCHED_RS_NONCOMM: {  // equal blocks: the mirror-permuted halving at a power of two
+            std::vector<ExprNode> nodes;
+            const int e = rs_noncomm_expr(n, me, (n & (n - 1)) == 0, nodes);
+            if (e < 0) return MPI_ERR_INTERN;
+            ev.expr(nodes, e, 0, o);
+            break;
+        }
         default: return MPI_ERR_ARG;
     }
     return 0;

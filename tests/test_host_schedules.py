@@ -13,7 +13,7 @@ from mvapich2_amd.consts import OPS, TYPES
 from oracle import oracle
 from tests import ref_user
 
-RD, PT2PT_RS, BINOMIAL, KNOMIAL, REDSCAT, RS_HALVING, RS_PAIRWISE, RS_RING, RING_CHUNK = range(9)
+RD, PT2PT_RS, BINOMIAL, KNOMIAL, REDSCAT, RS_HALVING, RS_PAIRWISE, RS_RING, RING_CHUNK, RS_NONCOMM = range(10)
 NS = [1, 2, 3, 5, 8, 9, 12, 13, 16, 17]
 
 
@@ -76,6 +76,17 @@ def test_reduce_scatter_block(n, algo, form):
     for me in range(n):
         blocks = [x[me * c:(me + 1) * c].copy() for x in xs]
         assert np.array_equal(hook(form, blocks, me=me), want[me]), (algo, n, me)
+
+
+@pytest.mark.parametrize("n", NS)
+def test_noncomm_reduce_scatter_block(n):
+    """the host tree walk (BigEval::expr) of the non-commutative reduce-scatter's expression"""
+    c = 2
+    xs = operands(n, c * n, 13 * n)
+    want = ref_user.reduce_scatter_noncomm(xs, fn, [c] * n)
+    for me in range(n):
+        blocks = [x[me * c:(me + 1) * c].copy() for x in xs]
+        assert np.array_equal(hook(RS_NONCOMM, blocks, me=me, commute=False), want[me]), (n, me)
 
 
 @pytest.mark.parametrize("n", NS)
