@@ -853,7 +853,8 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     const int newrank = me < 2 * rem ? ((me & 1) ? me / 2 : -1) : me - rem;
     auto real = [&](int q) { return q < rem ? 2 * q + 1 : q + rem; };
     // everything this rank needs is allocated before the vote, so that nothing after it can fail
-    // short of a copy error (a rank leaving after the vote would stall the others' barriers)
+    // short of a copy error (and that one still keeps the barriers: a rank leaving after the vote
+    // would stall the others')
     const bool dev_src = mv2h_is_device_ptr(src), dev_dst = mv2h_is_device_ptr(recvbuf);
     // the operand's bytes from its true lower bound on (the layout is copied as it is, gaps
     // included: no pack / unpack on the host, whose block loop over a sparse span is slow)
@@ -881,24 +882,23 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
         MPI_Datatype dd = t.dt;
         op.fn((void *)in, io, &c, &dd);
     };
-    // this rank's operand into its window, in the type's layout
+    // this rank's operand into its window, in the type's layout.  From the vote on, a failing
+    // copy or pack leaves rc set but the rank still takes part in every barrier below, so that
+    // the other ranks finish the call (with this rank's stale window) instead of stalling
     PhaseClock pc;
     char *tmp = T.data();
-    int rc;
+    int rc = 0;
     if (direct) {
         if (dev_src) {
-            if (dlen && mv2h_memcpy_dtoh(acc + tlb, (const char *)src + tlb, dlen)) return MPI_ERR_OTHER;
+            if (dlen && mv2h_memcpy_dtoh(acc + tlb, (const char *)src + tlb, dlen)) rc = MPI_ERR_OTHER;
         } else {
             memcpy(acc + tlb, (const char *)src + tlb, dlen);
         }
-    } else {
-        if (dev_src) {
-            if ((rc = dtype_pack(src, count, t.dt, d))) return rc;
-            if (P && mv2h_memcpy_dtoh(pk.data(), d, P)) return MPI_ERR_OTHER;
-        } else if ((rc = dtype_pack(src, count, t.dt, pk.data()))) {
-            return rc;
-        }
-        if ((rc = dtype_unpack(pk.data(), count, t.dt, acc))) return rc;
+    } else if (dev_src) {
+        if (!(rc = dtype_pack(src, count, t.dt, d)) && P && mv2h_memcpy_dtoh(pk.data(), d, P)) rc = MPI_ERR_OTHER;
+        if (!rc) rc = dtype_unpack(pk.data(), count, t.dt, acc);
+    } else if (!(rc = dtype_pack(src, count, t.dt, pk.data()))) {
+        rc = dtype_unpack(pk.data(), count, t.dt, acc);
     }
     pc.mark(UP_FETCH);
     // pre-step (:455-505)
@@ -924,16 +924,17 @@ int run_rd_exchange(const void *src, int count, const Typed &t, const HostOp &op
     host_barrier();
     if (me < 2 * rem && !(me & 1)) memcpy(tmp, peer(me + 1), rspan);
     const char *res_h = me < 2 * rem && !(me & 1) ? tmp : acc;
-    if (direct && dev_dst) {  // the result's span up, its type map packed on the device
-        if (dlen && mv2h_memcpy_htod(sp + tlb, res_h + tlb, dlen)) return MPI_ERR_OTHER;
-        if ((rc = dtype_pack(sp, count, t.dt, res))) return rc;
-    } else if (direct) {  // a host receive buffer: its type map from the result's
+    if (!rc && direct && dev_dst) {  // the result's span up, its type map packed on the device
+        if (dlen && mv2h_memcpy_htod(sp + tlb, res_h + tlb, dlen)) rc = MPI_ERR_OTHER;
+        if (!rc) rc = dtype_pack(sp, count, t.dt, res);
+    } else if (!rc && direct) {  // a host receive buffer: its type map from the result's
         dtype_merge_typemap((char *)recvbuf, res_h, t.dt, count);
-    } else if ((rc = dtype_pack(res_h, count, t.dt, pk.data()))) {
-        return rc;
+    } else if (!rc) {
+        rc = dtype_pack(res_h, count, t.dt, pk.data());
     }
     host_barrier();  // the post-step's reads are done before any window is reused
     pc.mark(UP_EVAL);  // the exchanges and the uop calls
+    if (rc) return rc;
     if (!direct && P && mv2h_memcpy_htod(res, pk.data(), P)) return MPI_ERR_OTHER;
     // operand bytes this rank received (packed measure): pre- or post-step, and one per doubling step
     world().uop_in_bytes = P * (size_t)((me < 2 * rem) + (newrank >= 0 ? __builtin_ctz((unsigned)pof2) : 0));
