@@ -399,11 +399,13 @@ struct PipeGeom {
 // Grid and per-block range of a pipelined call.  A pure function of the
 // message geometry and of values every rank shares (CU count, ranks per GPU,
 // tuning knobs), so block b of every rank handles the same bytes.
+static long env_long_coll(const char *name, long dflt);
 static PipeGeom pipe_geom(size_t maxlen) {
     World &w = world();
     int cap = std::min(kPipeMaxGrid, xcd_fair_cap(1, w.cus, w.nshare));  // k_pipe: one block per CU
     cap = std::min(cap, std::max(1, w.pipe_grid));
-    const size_t kMinSub = (size_t)16 << 10;
+    // the smallest per-workgroup tile (MV2AMD_PIPE_MIN_SUB, default 16 KiB)
+    static const size_t kMinSub = (size_t)std::max(4096L, env_long_coll("MV2AMD_PIPE_MIN_SUB", 16 << 10)) & ~(size_t)4095;
     PipeGeom g{};
     g.grid = (int)std::min<size_t>((size_t)cap, std::max<size_t>(1, (maxlen + kMinSub - 1) / kMinSub));
     size_t tsub = (maxlen + g.grid - 1) / g.grid;
@@ -1223,8 +1225,13 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.timeout = w.timeout_ticks;
         a.light = w.light_release;
         a.done = arm_done(st);
-        int g = (int)((nvec + 511) / 512);
-        g = std::max(1, std::min(g, std::min(gcap, 32)));
+        // one 16-B vector per thread of a 256-thread workgroup, up to 64 workgroups (256 KiB):
+        // the kernel is latency-bound, and each further vector a thread owns costs it another
+        // dependent memory round trip (MV2AMD_ONESHOT_VECS_PER_WG / _MAX_WG override)
+        static const long vpw = std::max(64L, env_long_coll("MV2AMD_ONESHOT_VECS_PER_WG", 256));
+        static const int wmax = (int)std::min(1024L, std::max(1L, env_long_coll("MV2AMD_ONESHOT_MAX_WG", 64)));
+        int g = (int)((nvec + vpw - 1) / vpw);
+        g = std::max(1, std::min(g, std::min(gcap, wmax)));
         LaunchCfg cfg = coll_cfg(g, st);
         tmark0(st);
         rc = launch_oneshot(oi, dt->kind, a, dt->extent, cfg);
