@@ -3,6 +3,7 @@ set -o pipefail
 O=gpurun_out/r04pt
 mkdir -p $O
 export TMPDIR=/tmp
+export MV2AMD_PIPE_MIN_SUB=4096  # the candidate default, under every step
 timeout -k 10 1000 python -u -m pytest -x -v -m gpu --timeout 480 --timeout-method thread tests > $O/pytest.log 2>&1 || { echo "tests failed"; tail -120 $O/pytest.log; exit 1; }
 tail -n 2 $O/pytest.log
 for nr in 2 4; do
