@@ -257,6 +257,21 @@ static int is_device(const void *p) {
     return a.type == hipMemoryTypeDevice ? 1 : 0;
 }
 
+// The call's last copy, device to device, as a copy kernel that raises the completion word:
+// a hipMemcpyAsync cannot raise it, and without it finish() falls back to a stream
+// synchronisation (several us at small sizes).  Other copies keep enq_copy.
+static hipError_t enq_copy_last(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    constexpr size_t kKernelCopyMax = (size_t)4 << 20;
+    if (bytes && bytes <= kKernelCopyMax && is_device(dst) && is_device(src)) {
+        const Done d = arm_done(st);
+        if (d.flag) {
+            beacon(BC_COPY_OUT);
+            return launch_pack_strided(src, dst, 1, bytes, bytes, 0, st, d) == 0 ? hipSuccess : hipErrorLaunchFailure;
+        }
+    }
+    return enq_copy(dst, src, bytes, st);
+}
+
 static int kind_supported(const DtypeInfo *dt) {
     if (!dt) return E_TYPE;
     if (dt->kind == K_LDOUBLE) {
@@ -1158,7 +1173,7 @@ static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, 
 }
 
 static void stage_out(const Staged &s, hipStream_t st) {
-    if (s.copy_back) enq_copy(s.user_recv, s.recv, s.bytes, st);
+    if (s.copy_back) enq_copy_last(s.user_recv, s.recv, s.bytes, st);
 }
 
 // One allreduce over `count` elements in the order `tp` (ring = true: the flat
@@ -1533,7 +1548,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     }
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
-    if (!direct && mycnt) enq_copy(recvbuf, dst, mycnt * ext, st);
+    if (!direct && mycnt) enq_copy_last(recvbuf, dst, mycnt * ext, st);
     return finish(st, w.timing);
 }
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
@@ -1623,7 +1638,7 @@ static int bcast_node(void *buffer, size_t bytes, int root, void *stream) {
     a.esize = 1;
     even_segments(a, bytes, w.size);
     if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
-    if (!direct && w.rank != root) enq_copy(buffer, buf, bytes, st);
+    if (!direct && w.rank != root) enq_copy_last(buffer, buf, bytes, st);
     return finish(st, w.timing);
 }
 
