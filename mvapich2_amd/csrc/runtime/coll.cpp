@@ -88,7 +88,7 @@ static inline uint64_t now_ns() {
 static inline bool hp_on() {
     if (g_hp.on < 0) {
         const char *v = getenv("MV2AMD_HOST_PROFILE");
-        g_hp.on = v && atoi(v) > 0;
+        g_hp.on = v && atoi(v) > 0 ? atoi(v) : 0;
     }
     return g_hp.on;
 }
@@ -101,6 +101,13 @@ static inline void hp_entry() {
 static inline void hp_done() {
     if (!hp_on() || !g_hp.t_entry || !g_hp.t_l1) return;
     const uint64_t t = now_ns();
+    // MV2AMD_HOST_PROFILE=k > 1: the first k - 1 calls (warm-up, first-launch code loading) are
+    // left out of the means
+    static uint64_t seen = 0;
+    if (++seen < (uint64_t)g_hp.on) {
+        g_hp.t_entry = g_hp.t_l0 = g_hp.t_l1 = 0;
+        return;
+    }
     ++g_hp.calls;
     g_hp.pre_ns += g_hp.t_l0 - g_hp.t_entry;
     g_hp.launch_ns += g_hp.t_l1 - g_hp.t_l0;

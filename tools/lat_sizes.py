@@ -1,4 +1,4 @@
-"""Small-message allreduce latency probe (fp32 SUM, device buffers): per size, the algorithm the
+"""Small-message collective latency probe (LAT_COLL = allreduce | reduce_scatter_block | bcast) (fp32 SUM, device buffers): per size, the algorithm the
 selection picks, the OSU-loop wall time per call (barrier before every call, as osu_coll does)
 and the kernel time from HIP events on the library's stream.  Run under mv2run, e.g.
     python -m mvapich2_amd.mv2run -n 2 --share-gpu python tools/lat_sizes.py
@@ -27,8 +27,21 @@ def main():
     for sz in sizes:
         count = max(1, sz // 4)
         sb.upload(np.full(count, 1.0 + rank, np.float32))
-        algo, inner, _, progs, blk = m.plan("allreduce", size, rank, F32, count)
-        call = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, count, F32, SUM, world)  # noqa: E731
+        coll = os.environ.get("LAT_COLL", "allreduce")
+        if coll == "allreduce":
+            algo, inner, _, progs, blk = m.plan("allreduce", size, rank, F32, count)
+            call = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, count, F32, SUM, world)  # noqa: E731
+        elif coll == "reduce_scatter_block":
+            count = max(size, count - count % size)
+            sb.upload(np.full(count, 1.0 + rank, np.float32))
+            algo, inner, progs = -1, 0, []
+            call = lambda: L.MPI_Reduce_scatter_block(sb.ptr, rb.ptr, count // size, F32, SUM, world)  # noqa: E731
+        else:
+            sb.upload(np.full(count, 1.0 + size * (size + 1) / 2 - 1.0, np.float32))
+            algo, inner, progs = -1, 0, []
+            call = lambda: L.MPI_Bcast(sb.ptr if rank == 0 else rb.ptr, count, F32, 0, world)  # noqa: E731
+            if rank == 0:
+                rb.upload(np.full(count, size * (size + 1) / 2, np.float32))
         for _ in range(200):
             m.check(call(), "warmup")
         tot = 0.0
@@ -44,7 +57,7 @@ def main():
             m.check(call(), "call")
             kms.append(L.mv2h_last_kernel_ms())
         L.mv2h_timing_enable(0)
-        got = rb.download(np.float32, count=count)
+        got = rb.download(np.float32, count=count if coll == "allreduce" or coll == "bcast" else count // size)
         ok = bool(np.all(got == np.float32(size * (size + 1) / 2)))
         if rank == 0:
             print(f"{sz:>8} B  algo {algo} inner {inner} nprog {len(progs)}  wall {tot / iters * 1e6:7.2f} us  "
