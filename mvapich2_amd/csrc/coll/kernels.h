@@ -48,6 +48,11 @@ struct OneShotArgs {
     // block at run time (arena_peer / arena_own then point at half 0; `half` = bytes per half)
     DevSeq *dseq;
     size_t half;
+    // reduce-scatter (rs = 1): rank j reduces only elements [wlo[j], wlo[j] + wcnt[j]) of the
+    // operand (wlo[j] a multiple of 16 / sizeof(T)) into its recv from the start; each rank
+    // pushes every peer only that peer's block (coll/kernels_impl.h k_oneshot_rs)
+    int rs;
+    size_t wlo[kMaxRanks], wcnt[kMaxRanks];
 };
 
 // ---------------------------------------------------------------------------

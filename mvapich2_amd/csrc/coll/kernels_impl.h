@@ -359,12 +359,81 @@ __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
     block_done(a.done);
 }
 
+// One-shot reduce-scatter (small messages): workgroup b pushes, to every peer j, partition b of
+// j's block of my operand, flags, then reduces partition b of my own block from the n slots in
+// program order — the flag it waits for covers exactly the vectors it reads.  Block tails
+// (elements past the last whole vector) go through workgroup 0 on both sides.
+template <class Rd>
+__global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
+    using T = typename Rd::T;
+    constexpr int N = 16 / sizeof(T);
+    const int blk = blockIdx.x, G = gridDim.x;
+    uint64_t epoch = a.epoch;
+    size_t poff = 0;
+    if (a.dseq) {
+        const SeqBase q = dseq_read(a.dseq);
+        epoch = q.epoch + 1;
+        poff = (q.os & 1) * a.half;
+    }
+    const v4u *send = (const v4u *)a.send;
+    for (int j = 0; j < a.n; ++j) {
+        if (j == a.me) continue;
+        const size_t v0 = a.wlo[j] / N, v1 = (a.wlo[j] + a.wcnt[j]) / N;
+        const size_t per = (v1 - v0 + G - 1) / G;
+        const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
+        v4u *dst = (v4u *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes);
+        for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) dst[i] = send[i];
+        if (blk == 0)
+            for (size_t e = v1 * N + threadIdx.x; e < a.wlo[j] + a.wcnt[j]; e += kThreads)
+                ((T *)dst)[e] = ((const T *)a.send)[e];
+    }
+    signal_peers(a.sig_peer, a.n, a.me, blk, epoch, a.light != 0);
+    if (wait_peers(a.sig_own, a.n, blk, epoch, a.err, a.timeout, a.light != 0)) {
+        const char *arena_own = a.arena_own + poff;
+        const size_t lo = a.wlo[a.me], hi = lo + a.wcnt[a.me];
+        const size_t v0 = lo / N, v1 = hi / N;
+        const size_t per = (v1 - v0 + G - 1) / G;
+        const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
+        int fb = -1;
+        if (b1 > b0) {
+            const int p0 = prog_block(a.tp.ps, b0 * N), p1 = prog_block(a.tp.ps, b1 * N - 1);
+            if (p0 == p1) fb = p0;
+        }
+        for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) {
+            v4u v[kMaxRanks];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                v[j] = (j >= a.n) ? v4u{0, 0, 0, 0}
+                                  : (j == a.me) ? send[i] : ld_nt((const v4u *)(arena_own + (size_t)j * a.slot_bytes) + i);
+            ((v4u *)a.recv)[i - v0] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
+        }
+        if (blk == 0)
+            for (size_t e = v1 * N + threadIdx.x; e < hi; e += kThreads) {
+                T col[kMaxRanks];
+#pragma unroll
+                for (int j = 0; j < kMaxRanks; ++j)
+                    col[j] = (j >= a.n || j == a.me) ? ((const T *)a.send)[e]
+                                                     : ld_nt_elem((const T *)(arena_own + (size_t)j * a.slot_bytes) + e);
+                ((T *)a.recv)[e - lo] = prog_eval<Rd>(col, a.tp.ps.p[prog_block(a.tp.ps, e)]);
+            }
+    }
+    if (a.dseq) dseq_advance(a.dseq, 1, 0, 1);
+    block_done(a.done);
+}
+
 template <int OP, int K>
 struct LOneShot {
     static int run(const OneShotArgs &a, const LaunchCfg &cfg) {
         const bool prog = a.tp.linear == 4;
         static const int cap0 = resident_grid((const void *)k_oneshot<R<OP, K>, false>, cfg);
         static const int cap1 = resident_grid((const void *)k_oneshot<R<OP, K>, true>, cfg);
+        if (a.rs) {
+            if (!prog) return E_ARG;  // a reduce-scatter block is always evaluated in program order
+            static const int cap2 = resident_grid((const void *)k_oneshot_rs<R<OP, K>>, cfg);
+            const int g = cfg.grid < cap2 ? cfg.grid : cap2;
+            hipLaunchKernelGGL((k_oneshot_rs<R<OP, K>>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+            return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+        }
         const int cap = prog ? cap1 : cap0;
         const int g = cfg.grid < cap ? cfg.grid : cap;
         if (prog) hipLaunchKernelGGL((k_oneshot<R<OP, K>, true>), dim3(g), dim3(kThreads), 0, cfg.stream, a);

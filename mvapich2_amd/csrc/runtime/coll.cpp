@@ -501,6 +501,47 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
     return rc;
 }
 
+// The one-shot kernels' per-call part: this call's arena half and flag epoch (or, on the graph
+// lane, where the kernel reads them), the peers, the error word, the completion word.
+static void oneshot_common(OneShotArgs &a, hipStream_t st) {
+    World &w = world();
+    const int n = w.size;
+    const size_t half = (size_t)kMaxRanks * w.slot_bytes;
+    if (w.graph) {  // graph lane: the kernel picks the half and the epoch from the device
+        for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.g_peer_arena[j];
+        a.arena_own = w.g_arena;
+        a.sig_peer = w.g_peer_sig;
+        a.sig_own = w.g_sig;
+        a.dseq = w.dseq;
+        a.half = half;
+    } else {
+        const size_t par = (w.os_calls++ & 1) * half;
+        for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j] + par;
+        a.arena_own = w.arena + par;
+        a.sig_peer = w.peer_sig;
+        a.sig_own = w.sig;
+        a.epoch = ++w.epoch;
+    }
+    a.slot_bytes = w.slot_bytes;
+    a.n = n;
+    a.me = w.rank;
+    a.err = w.h_err;
+    a.timeout = w.timeout_ticks;
+    a.light = w.light_release;
+    a.done = arm_done(st);
+}
+
+static long env_long_coll(const char *name, long dflt);
+// one 16-B vector per thread of a 256-thread workgroup, up to 64 workgroups (256 KiB): the
+// one-shot kernels are latency-bound, and each further vector a thread owns costs it another
+// dependent memory round trip (MV2AMD_ONESHOT_VECS_PER_WG / _MAX_WG override)
+static int oneshot_grid(size_t nvec, int gcap) {
+    static const long vpw = std::max(64L, env_long_coll("MV2AMD_ONESHOT_VECS_PER_WG", 256));
+    static const int wmax = (int)std::min(1024L, std::max(1L, env_long_coll("MV2AMD_ONESHOT_MAX_WG", 64)));
+    const int g = (int)((nvec + vpw - 1) / vpw);
+    return std::max(1, std::min(g, std::min(gcap, wmax)));
+}
+
 }  // namespace mv2
 
 // the node-level allreduce (defined with the C-ABI below): MPI_Init's self-test and tiling
@@ -1221,41 +1262,13 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
             }
         }
         OneShotArgs a{};
+        oneshot_common(a, st);
         a.send = s.send;
         a.recv = s.recv;
-        const size_t half = (size_t)kMaxRanks * w.slot_bytes;
-        if (w.graph) {  // graph lane: the kernel picks the half and the epoch from the device
-            for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.g_peer_arena[j];
-            a.arena_own = w.g_arena;
-            a.sig_peer = w.g_peer_sig;
-            a.sig_own = w.g_sig;
-            a.dseq = w.dseq;
-            a.half = half;
-        } else {
-            const size_t par = (w.os_calls++ & 1) * half;
-            for (int j = 0; j < n; ++j) a.arena_peer.p[j] = w.peer_arena[j] + par;
-            a.arena_own = w.arena + par;
-            a.sig_peer = w.peer_sig;
-            a.sig_own = w.sig;
-            a.epoch = ++w.epoch;
-        }
         a.count = count;
         a.nvec = nvec;
-        a.slot_bytes = w.slot_bytes;
-        a.n = n;
-        a.me = w.rank;
         a.tp = tp;
-        a.err = w.h_err;
-        a.timeout = w.timeout_ticks;
-        a.light = w.light_release;
-        a.done = arm_done(st);
-        // one 16-B vector per thread of a 256-thread workgroup, up to 64 workgroups (256 KiB):
-        // the kernel is latency-bound, and each further vector a thread owns costs it another
-        // dependent memory round trip (MV2AMD_ONESHOT_VECS_PER_WG / _MAX_WG override)
-        static const long vpw = std::max(64L, env_long_coll("MV2AMD_ONESHOT_VECS_PER_WG", 256));
-        static const int wmax = (int)std::min(1024L, std::max(1L, env_long_coll("MV2AMD_ONESHOT_MAX_WG", 64)));
-        int g = (int)((nvec + vpw - 1) / vpw);
-        g = std::max(1, std::min(g, std::min(gcap, wmax)));
+        const int g = oneshot_grid(nvec, gcap);
         LaunchCfg cfg = coll_cfg(g, st);
         tmark0(st);
         rc = launch_oneshot(oi, dt->kind, a, dt->extent, cfg);
@@ -1495,6 +1508,55 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
             hipMemcpyAsync(recvbuf, (const char *)send + off * ext, mycnt * ext, hipMemcpyDefault, st);
         return finish(st, false);
     }
+    // small messages: the one-shot reduce-scatter (each peer pushed only its own block, one flag
+    // exchange, this rank's block reduced in program order) when the operand fits an arena slot,
+    // every block starts on a 16-byte boundary and the algorithm is not the ring (whose rotated
+    // chain only the pipelined kernel evaluates).  Only the counts, the type and the plan enter
+    // the choice, so every rank makes it alike.
+    Plan p;
+    if ((rc = plan_reduce_scatter(n, w.rank, recvcounts, dt->size, dt->extent, &p))) return rc;
+    bool os = !in_place && p.algo != ALG_RS_RING && (size_t)dt->size == ext && 16 % ext == 0 &&
+              total * ext <= std::min(w.oneshot_max, w.slot_bytes);
+    for (size_t j = 0, off0 = 0; os && j < (size_t)n; off0 += recvcounts[j], ++j) os = (off0 * ext) % 16 == 0;
+    if (os) {
+        log_plan("reduce_scatter", p, total);
+        pvar_note(PV_COLL_REDUCE_SCATTER, p, false, total, n);
+        const char *src = (const char *)send;
+        if (!is_device(send) || (uintptr_t)send % 16) {
+            char *t = (char *)get_scratch(0, total * ext);
+            if (!t) return E_NO_MEM;
+            beacon(BC_STAGE);
+            hipMemcpyAsync(t, send, total * ext, hipMemcpyDefault, st);
+            src = t;
+        }
+        const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0;
+        char *dst = (char *)recvbuf;
+        if (!direct && mycnt && !(dst = (char *)get_scratch(1, mycnt * ext))) return E_NO_MEM;
+        OneShotArgs o{};
+        oneshot_common(o, st);
+        o.send = src;
+        o.recv = dst;
+        o.count = total;
+        o.nvec = total * ext / 16;
+        o.rs = 1;
+        size_t vmax = 0;
+        for (size_t j = 0, e = 0; j < (size_t)n; e += recvcounts[j], ++j) {
+            o.wlo[j] = e;
+            o.wcnt[j] = recvcounts[j];
+            vmax = std::max(vmax, (recvcounts[j] * ext + 15) / 16);
+        }
+        TreeParams tp = tree_base(n);
+        tp.linear = 4;
+        tp.ps = p.ps;
+        o.tp = tp;
+        LaunchCfg cfg = coll_cfg(oneshot_grid(vmax, grid_cap()), st);
+        tmark0(st);
+        rc = launch_oneshot(oi, dt->kind, o, dt->extent, cfg);
+        tmark1(st);
+        if (rc) return rc;
+        if (!direct && mycnt) enq_copy_last(recvbuf, dst, mycnt * ext, st);
+        return finish(st, w.timing);
+    }
     PipeArgs a{};
     a.mode = PIPE_RS;
     a.esize = (int)ext;
@@ -1541,8 +1603,6 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     a.recv_off[w.rank] = direct ? 0 : mis;
     // MPIR_Reduce_scatter_MV2's one-node choice (orders.cpp plan_reduce_scatter): ring,
     // recursive halving, pairwise or reduce + scatter, each in its own order
-    Plan p;
-    if ((rc = plan_reduce_scatter(n, w.rank, recvcounts, dt->size, dt->extent, &p))) return rc;
     log_plan("reduce_scatter", p, total);
     pvar_note(PV_COLL_REDUCE_SCATTER, p, false, total, n);
     TreeParams tp = tree_base(n);
