@@ -68,11 +68,39 @@ def cpu_baseline_reduce_local(seconds=10.0):
                       f"1 core of '{cpu_info()}'; reference device path adds D2H 2S + H2D S over PCIe"}
 
 
+def host_allreduce_record(out):
+    """Parse oracle/host_allreduce's output into bench's record: the JSONHDR placement row (the
+    inherited cpuset, each rank's CPU, distinct CPUs / physical cores, oversubscription, cgroup
+    quota) and the per-size JSON rows (latency, busbw, sched_yield fallbacks, CFS throttling)."""
+    hdr = next((json.loads(l[8:]) for l in out.splitlines() if l.startswith("JSONHDR ")), None)
+    rows = [json.loads(l[5:]) for l in out.splitlines() if l.startswith("JSON ")]
+    by = {r["bytes"]: r for r in rows}
+    if hdr is None or 8 not in by or (64 << 20) not in by or (1 << 20) not in by:
+        return {"error": "incomplete host_allreduce output"}
+    ranks = hdr["ranks"]
+    if hdr["oversubscribed"]:
+        placement = f"{ranks} ranks on {hdr['cpus_used']} CPUs: OVERSUBSCRIBED (cpuset holds {hdr['cpus_available']})"
+    elif hdr["smt_shared"]:
+        placement = f"{ranks} ranks pinned 1/CPU on {hdr['cores_used']} physical cores (SMT siblings shared)"
+    else:
+        placement = f"{ranks} ranks pinned 1/core"
+    return {"latency_8B_us": by[8]["lat_us"], "busbw_64MiB_GBps": by[64 << 20]["busbw_GBps"],
+            "busbw_1MiB_GBps": by[1 << 20]["busbw_GBps"], "all_ok": all(r["ok"] for r in rows),
+            "cores": hdr["cpus_used"], "cpus_available": hdr["cpus_available"], "cpus_used": hdr["cpus_used"],
+            "cores_used": hdr["cores_used"], "oversubscribed": hdr["oversubscribed"], "smt_shared": hdr["smt_shared"],
+            "rank_cpus": hdr["rank_cpus"], "cgroup_cpu_quota": hdr["cgroup_cpu_quota"],
+            "yields_8B": by[8].get("yields"), "throttled_periods_8B": by[8].get("throttled"),
+            "yields_all_sizes": sum(r.get("yields", 0) for r in rows),
+            "throttled_periods_all_sizes": sum(r.get("throttled", 0) for r in rows),
+            "kind": "port", "cpu": cpu_info(), "placement": placement}
+
+
 def cpu_baseline_host_allreduce(seconds=10.0, ranks=8):
-    """The reference's host-buffer ch3 shared-memory MPI_Allreduce, fp32 SUM,
-    `ranks` processes pinned one per core (oracle/host_allreduce.c: the
-    reference-algorithm host restatement, BASELINE.json configs[0]).  Bounded
-    sample: 8 B .. 64 MiB, each size capped at ~seconds/12 s."""
+    """The reference's host-buffer ch3 shared-memory MPI_Allreduce, fp32 SUM, `ranks` processes
+    pinned one per CPU of the inherited cpuset, physical cores first (oracle/host_allreduce.c: the
+    reference-algorithm host restatement, BASELINE.json configs[0]).  Bounded sample: 8 B .. 64 MiB,
+    each size capped at ~seconds/12 s.  The record names the CPUs it ran on and whether ranks had
+    to share one."""
     exe = os.path.join(ROOT, "oracle", "host_allreduce")
     if not os.path.exists(exe):
         return {"error": "oracle/host_allreduce not built"}
@@ -82,29 +110,29 @@ def cpu_baseline_host_allreduce(seconds=10.0, ranks=8):
                              capture_output=True, text=True, timeout=max(60.0, 40 * cap)).stdout
     except subprocess.TimeoutExpired:
         return {"error": "host_allreduce timed out"}
-    rows = [json.loads(l[5:]) for l in out.splitlines() if l.startswith("JSON ")]
-    by = {r["bytes"]: r for r in rows}
-    if 8 not in by or (64 << 20) not in by:
-        return {"error": "incomplete host_allreduce output"}
-    return {"latency_8B_us": by[8]["lat_us"], "busbw_64MiB_GBps": by[64 << 20]["busbw_GBps"],
-            "busbw_1MiB_GBps": by[1 << 20]["busbw_GBps"], "all_ok": all(r["ok"] for r in rows), "cores": ranks,
-            "kind": "port", "cpu": cpu_info(),
-            "what": "reference host path (topology-aware degree-4 shm tree <= 2 KiB, pt2pt_rs to 2 MiB, flat ring from 2 MiB, single-copy exchange), "
-                    f"{ranks} ranks pinned 1/core, OSU loop, sizes 8 B..64 MiB, <= {cap:.2f} s per size"}
+    rec = host_allreduce_record(out)
+    if "error" not in rec:
+        rec["what"] = ("reference host path (topology-aware degree-4 shm tree <= 2 KiB, pt2pt_rs to 2 MiB, flat ring "
+                       f"from 2 MiB, single-copy exchange), {rec['placement']}, CPUs {rec['rank_cpus']}, OSU loop, "
+                       f"sizes 8 B..64 MiB, <= {cap:.2f} s per size")
+    return rec
 
 
 def cpu_baseline_nranks(seconds):
     """The N > 1 line's cpu_baseline: configs[0]'s host allreduce at the largest size it covers
-    (64 MiB busbw, 8 ranks on 8 cores), with its 8-byte latency in the sample text."""
-    h = cpu_baseline_host_allreduce(seconds)
+    (64 MiB busbw, 8 ranks), with its 8-byte latency and placement in the sample text."""
+    return cpu_baseline_nranks_from(cpu_baseline_host_allreduce(seconds))
+
+
+def cpu_baseline_nranks_from(h):
     if "error" in h:
-        return {"value": None, "unit": "GB/s", "cores": 8, "kind": "port", "sample": h["error"]}
-    return {"value": h["busbw_64MiB_GBps"], "unit": "GB/s", "cores": h["cores"], "kind": "port",
-            "correct": h["all_ok"],
+        return {"value": None, "unit": "GB/s", "cores": None, "kind": "port", "sample": h["error"]}
+    return {"value": h["busbw_64MiB_GBps"], "unit": "GB/s", "cores": h["cpus_used"], "kind": "port",
+            "correct": h["all_ok"], "cpus_available": h["cpus_available"], "cpus_used": h["cpus_used"],
+            "oversubscribed": h["oversubscribed"], "rank_cpus": h["rank_cpus"],
             "sample": f"configs[0]: reference host-buffer ch3 shared-memory MPI_Allreduce fp32 SUM restated "
                       f"(oracle/host_allreduce.c), 64 MiB busbw; 8 B latency {h['latency_8B_us']} us, 1 MiB busbw "
-                      f"{h['busbw_1MiB_GBps']} GB/s; {h['cores']} ranks pinned 1/core of '{h['cpu']}'; "
-                      f"{h['what']}"}
+                      f"{h['busbw_1MiB_GBps']} GB/s; {h['placement']} of '{h['cpu']}'; {h['what']}"}
 
 
 def reduce_local_run(L, type_name, op_name, nbytes, steps, warmup):
@@ -553,36 +581,18 @@ def bench_nranks(args, L, rank, size):
     dr = m.DeviceBuffer(vals.nbytes)
     m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, len(vals), F64, MAX, world), "max")
     got = dr.download(np.float64)
-    (step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat_s, lat_k_ms, bad, p2p_s, sq_s) = got[:15]
-    for u, t in zip(uops["lines"], got[15:]):
-        u["s"] = float(t)
-    f = (size - 1) / size
-    busbw = 2.0 * f * S_BYTES / step_s / 1e9
-    kbus = 2.0 * f * S_BYTES / (kms / 1e3) / 1e9
-    peak_all = (size - 1) * XGMI_LINK
-
-    def line4(t, k, bytes_bus):
-        return {"busbw_GBps": round(bytes_bus / t / 1e9, 2), "kernel_busbw_GBps": round(bytes_bus / (k / 1e3) / 1e9, 2),
-                "ms": round(t * 1e3, 4)}
-
-    extra = {
-        "reduce_scatter_f32_sum": line4(rs_s, rs_k, f * S_BYTES),
-        "allgather_char": line4(ag_s, ag_k, f * S_BYTES),
-        "bcast_char": line4(bc_s, bc_k, S_BYTES),
-        "allreduce_maxloc_double_int": line4(ml_s, ml_k, 2.0 * f * nrec * 12),
-        **{u["name"]: {"payload_busbw_GBps": round(2.0 * f * u["payload"] / u["s"] / 1e9, 2), "ms": round(u["s"] * 1e3, 3),
-                       "phases_ms_rank0": u["phases_ms_rank0"], "what": u["what"]} for u in uops["lines"]},
-        "pt2pt_bw_16MiB_x8": {"GBps": round(pbytes * win / p2p_s / 1e9, 2), "ms_per_window": round(p2p_s * 1e3, 3),
-                              "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
-    }
+    keys = ("step_s", "kms", "rs_s", "rs_k", "ag_s", "ag_k", "bc_s", "bc_k", "ml_s", "ml_k", "lat_s", "lat_k_ms", "bad",
+            "p2p_s", "sq_s")
+    t = {k: float(v) for k, v in zip(keys, got[:15])}
+    for u, tu in zip(uops["lines"], got[15:]):
+        u["s"] = float(tu)
     # HBM traffic of k_pipe (PIPE_AR) per launch on one rank: the PMC ratio (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py) of a committed pass taken at THIS rank
     # count, ranks per GPU and tiling knobs, times this call's per-rank algorithmic HBM bytes
     # 2S(1 + 2(n-1)/n): reads of the operand, the RS and the AG slots; writes of the peers' RS
     # pushes, the own segment, the peers' AG pushes and the gathered segments.  No matching pass:
     # traffic is null and the nearest pass's configuration is named instead.
-    pipe_alg = 2.0 * S_BYTES * (1.0 + 2.0 * (size - 1) / size)
-    pipe_traffic, pipe_tsrc, pipe_tnote = pipe_traffic_for(size, nshare, pipe_alg)
+    traffic = pipe_traffic_for(size, nshare, pipe_alg_bytes(size))
     tiling = {"grid": m.info("pipe_grid"), "bytes_per_workgroup_round": m.info("pipe_sub"),
               "remote_stores": "non-temporal" if m.info("pipe_rnt") else "plain",
               "autotuned_at_init": bool(m.info("pipe_tuned")),
@@ -593,43 +603,93 @@ def bench_nranks(args, L, rank, size):
               "oneshot_max_bytes": m.info("oneshot_max"),
               "mpi_init_ms_rank0": round(m.info("init_us") / 1e3, 1),
               "mpi_init_selftest_ms": round(m.info("selftest_us") / 1e3, 1),
+              "mpi_init_selftest_calls": m.info("selftest_calls"),
               "mpi_init_autotune_ms": round(m.info("autotune_us") / 1e3, 1),
               "oneshot_vs_pipe_us": [{"bytes": (32 << 10) << i, "oneshot": m.info(f"os_tune_one_{i}"),
                                       "pipe": m.info(f"os_tune_pipe_{i}")} for i in range(m.info("os_tune_n"))]}
     del sb, rb, rsb
     if args.rccl and m.info("nshare") > 1:
-        extra["rccl_comparator"] = {"skipped": "ranks share one GPU: RCCL refuses several ranks on one device"}
+        rccl = {"skipped": "ranks share one GPU: RCCL refuses several ranks on one device"}
     elif args.rccl:
         try:
-            extra["rccl_comparator"] = rccl_comparator(L, world, rank, size, max(5, args.steps // 2))
+            rccl = rccl_comparator(L, world, rank, size, max(5, args.steps // 2))
         except Exception as e:  # comparator only: never fail the bench line on it
-            extra["rccl_comparator"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+            rccl = {"error": f"{type(e).__name__}: {e}"[:200]}
+    else:
+        rccl = None
+    return assemble_nranks_line(size, nshare, args.steps, args.warmup, t, lat_avg, uops["lines"], nrec, pbytes * win,
+                                tiling, traffic, rccl)
+
+
+def pipe_alg_bytes(size):
+    """Per-rank algorithmic HBM bytes of one PIPE_AR call on S bytes: 2S(1 + 2(n-1)/n)."""
+    return 2.0 * S_BYTES * (1.0 + 2.0 * (size - 1) / size)
+
+
+def assemble_nranks_line(size, nshare, steps, warmup, t, lat_avg, uop_lines, nrec, p2p_bytes, tiling, traffic, rccl,
+                         cpu_baseline=None):
+    """The N > 1 bench line from max-over-ranks measurements (pure: no GPU, no library calls, so the
+    branches the 1-GPU box never takes -- nshare == 1, a successful or failed RCCL comparator -- are
+    CPU-tested: tests/test_bench_line.py).  `t` holds seconds per call (`*_s`) and HIP-event kernel
+    milliseconds (`kms`, `*_k`, `lat_k_ms`); `traffic` = pipe_traffic_for(...)."""
+    f = (size - 1) / size
+    busbw = 2.0 * f * S_BYTES / t["step_s"] / 1e9
+    kbus = 2.0 * f * S_BYTES / (t["kms"] / 1e3) / 1e9
+    peak_all = (size - 1) * XGMI_LINK
+    pipe_alg = pipe_alg_bytes(size)
+    pipe_traffic, pipe_tsrc, pipe_tnote = traffic
+
+    def line4(ts, k, bytes_bus):
+        return {"busbw_GBps": round(bytes_bus / ts / 1e9, 2), "kernel_busbw_GBps": round(bytes_bus / (k / 1e3) / 1e9, 2),
+                "ms": round(ts * 1e3, 4)}
+
+    extra = {
+        "reduce_scatter_f32_sum": line4(t["rs_s"], t["rs_k"], f * S_BYTES),
+        "allgather_char": line4(t["ag_s"], t["ag_k"], f * S_BYTES),
+        "bcast_char": line4(t["bc_s"], t["bc_k"], S_BYTES),
+        "allreduce_maxloc_double_int": line4(t["ml_s"], t["ml_k"], 2.0 * f * nrec * 12),
+        **{u["name"]: {"payload_busbw_GBps": round(2.0 * f * u["payload"] / u["s"] / 1e9, 2), "ms": round(u["s"] * 1e3, 3),
+                       "phases_ms_rank0": u["phases_ms_rank0"], "what": u["what"]} for u in uop_lines},
+        "pt2pt_bw_16MiB_x8": {"GBps": round(p2p_bytes / t["p2p_s"] / 1e9, 2), "ms_per_window": round(t["p2p_s"] * 1e3, 3),
+                              "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
+    }
+    if rccl is not None:
+        extra["rccl_comparator"] = rccl
+        if "busbw_GBps" in rccl:
+            extra["rccl_comparator"]["ours_over_rccl"] = round(busbw / rccl["busbw_GBps"], 3)
+    kernel = "k_pipe<R<SUM,F32>> (PIPE_AR)"
+    if nshare == 1:
+        roof = {"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
+                "frac": round(kbus / peak_all, 4), "traffic": pipe_traffic, "traffic_source": pipe_tsrc,
+                "traffic_note": pipe_tnote, "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg),
+                "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": kernel, "kernel_ms": round(t["kms"], 4),
+                "peak_note": f"direct RS+AG over the {size - 1} xGMI links each rank has to its peers: "
+                             f"busbw peak = (n-1) x {XGMI_LINK} GB/s per link per direction"}
+    else:
+        roof = {"bound": "shared-gpu", "achieved": round(kbus, 1), "peak": None, "unit": "GB/s", "frac": None,
+                "traffic": pipe_traffic, "traffic_source": pipe_tsrc, "traffic_note": pipe_tnote,
+                "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg), "kernel": kernel,
+                "kernel_ms": round(t["kms"], 4),
+                "note": f"{nshare} ranks share one GPU: every 'remote' store lands in the same HBM, no xGMI "
+                        "link is used, so no xGMI roofline fraction applies"}
     line = {
-        "metric": METRIC, "value": round(busbw, 2), "unit": "GB/s", "n_gpus": size, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "metric": METRIC, "value": round(busbw, 2), "unit": "GB/s", "n_gpus": size, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(t["step_s"] * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "configs[2]: osu_allreduce -d rocm fp32 SUM 256 MiB, 1 rank per GPU over xGMI",
-                   "count": count, "bytes": S_BYTES, "algorithm": "pipelined direct RS+AG (pushes into peer arenas over xGMI)",
-                   "latency_8B_us": round(lat_avg * 1e6, 2), "latency_8B_max_over_ranks_us": round(lat_s * 1e6, 2),
-                   "latency_8B_kernel_us": round(lat_k_ms * 1e3, 2),
-                   "allreduce_8B_stream_ordered_us_per_call": round(sq_s * 1e6, 2),
+                   "count": S_BYTES // 4, "bytes": S_BYTES,
+                   "algorithm": "pipelined direct RS+AG (pushes into peer arenas over xGMI)",
+                   "latency_8B_us": round(lat_avg * 1e6, 2), "latency_8B_max_over_ranks_us": round(t["lat_s"] * 1e6, 2),
+                   "latency_8B_kernel_us": round(t["lat_k_ms"] * 1e3, 2),
+                   "allreduce_8B_stream_ordered_us_per_call": round(t["sq_s"] * 1e6, 2),
                    **({"stream_ordered_note": "ranks share one GPU: each rank's queued kernels spin until the other "
                        "processes' queues are scheduled (DESIGN.md §4 Stream order); not a one-GPU-per-rank figure"}
                       if nshare > 1 else {}),
-                   "correct": not bool(bad), "validation": "whole 256 MiB result vs exact expected sum, before and after timing",
+                   "correct": not bool(t["bad"]),
+                   "validation": "whole 256 MiB result vs exact expected sum, before and after timing",
                    "pipe_tiling": tiling},
-        "roofline": ({"bound": "xgmi", "achieved": round(kbus, 1), "peak": peak_all, "unit": "GB/s",
-                      "frac": round(kbus / peak_all, 4), "traffic": pipe_traffic, "traffic_source": pipe_tsrc,
-                      "traffic_note": pipe_tnote,
-                      "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg),
-                      "frac_vs_single_ring": round(kbus / XGMI_LINK, 3), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)",
-                      "kernel_ms": round(kms, 4)} if nshare == 1 else
-                     {"bound": "shared-gpu", "achieved": round(kbus, 1), "peak": None, "unit": "GB/s", "frac": None,
-                      "traffic": pipe_traffic, "traffic_source": pipe_tsrc, "traffic_note": pipe_tnote,
-                      "traffic_algorithmic_hbm_bytes_per_rank": round(pipe_alg), "kernel": "k_pipe<R<SUM,F32>> (PIPE_AR)", "kernel_ms": round(kms, 4),
-                      "note": f"{nshare} ranks share one GPU: every 'remote' store lands in the same HBM, no xGMI "
-                              "link is used, so no xGMI roofline fraction applies"}),
-        "cpu_baseline": None,
+        "roofline": roof,
+        "cpu_baseline": cpu_baseline,
         "extra": extra,
     }
     return line

@@ -14,7 +14,8 @@ namespace mv2 {
     int grp_reduce_n_##g(int, int, const void *const *, int, void *, size_t, const TreeParams &,     \
                          const LaunchCfg &);                                                         \
     int grp_oneshot_##g(int, int, const OneShotArgs &, const LaunchCfg &);                           \
-    int grp_pipe_##g(int, int, const PipeArgs &, const LaunchCfg &);
+    int grp_pipe_##g(int, int, const PipeArgs &, const LaunchCfg &);                                 \
+    int grp_touch_##g(hipStream_t);
 MV2_GROUPS(MV2_DECL)
 #undef MV2_DECL
 
@@ -58,6 +59,80 @@ int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg
 
 int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg) {
     hipLaunchKernelGGL((k_pipe<NoReduce>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+}
+
+// ---------------------------------------------------------------------------
+// Code-object loading.  HIP loads a translation unit's gfx950 code object at the first launch of
+// one of its kernels; MPI_Init launches one empty kernel per unit so that the load happens (and
+// is timed) there rather than inside an application's first call of each type group.
+// ---------------------------------------------------------------------------
+__global__ void k_touch_dispatch() {}
+int launch_pack_touch(hipStream_t st);  // pack/pack.hip
+
+int launch_touch_all(hipStream_t st) {
+    hipLaunchKernelGGL(k_touch_dispatch, dim3(1), dim3(64), 0, st);
+    if (hipGetLastError() != hipSuccess) return E_INTERN;
+#define X(g) \
+    if (grp_touch_##g(st)) return E_INTERN;
+    MV2_GROUPS(X)
+#undef X
+    return launch_pack_touch(st);
+}
+
+// ---------------------------------------------------------------------------
+// MPI_Init self-test operands (runtime/coll.cpp coll_selftest): rank r's element i of call
+// `seed` is st_hash(seed, r, i); the check recomputes what every element of a result must be
+// and counts the elements that differ (integer arithmetic mod 2^32: any reduction order agrees).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t st_hash(uint32_t seed, uint32_t r, uint64_t i) {
+    uint32_t x = (uint32_t)i * 0x9E3779B1u ^ (uint32_t)(i >> 32) ^ seed ^ (r + 1u) * 0x85EBCA77u;
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__global__ __launch_bounds__(kThreads) void k_st_fill(uint32_t *p, size_t n, uint32_t seed, int rank) {
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads)
+        p[i] = st_hash(seed, (uint32_t)rank, i);
+}
+
+// mode 0: element i = sum over ranks of st_hash(seed, r, base + i)   (allreduce, reduce-scatter block)
+// mode 1: element i = st_hash(seed, arg, base + i)                  (broadcast from rank arg)
+// mode 2: element i = st_hash(seed, i / arg, i % arg)               (allgather of arg elements per rank)
+__global__ __launch_bounds__(kThreads) void k_st_check(const uint32_t *p, size_t n, uint32_t seed, int nranks,
+                                                       int mode, int arg, uint64_t base, uint32_t *bad) {
+    uint32_t nb = 0;
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads) {
+        uint32_t want = 0;
+        if (mode == 0) {
+            for (int r = 0; r < nranks; ++r) want += st_hash(seed, (uint32_t)r, base + i);
+        } else if (mode == 1) {
+            want = st_hash(seed, (uint32_t)arg, base + i);
+        } else {
+            want = st_hash(seed, (uint32_t)(i / (size_t)arg), i % (size_t)arg);
+        }
+        nb += p[i] != want ? 1u : 0u;
+    }
+    if (nb) atomicAdd(bad, nb);
+}
+
+static unsigned st_grid(size_t n) {
+    const size_t g = (n + kThreads - 1) / kThreads;
+    return (unsigned)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
+}
+
+int launch_selftest_fill(uint32_t *p, size_t n, uint32_t seed, int rank, hipStream_t st) {
+    hipLaunchKernelGGL(k_st_fill, dim3(st_grid(n)), dim3(kThreads), 0, st, p, n, seed, rank);
+    return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+}
+
+int launch_selftest_check(const uint32_t *p, size_t n, uint32_t seed, int nranks, int mode, int arg, uint64_t base,
+                          uint32_t *bad, hipStream_t st) {
+    hipLaunchKernelGGL(k_st_check, dim3(st_grid(n)), dim3(kThreads), 0, st, p, n, seed, nranks, mode, arg, base, bad);
     return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
 }
 

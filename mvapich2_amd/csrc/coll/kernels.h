@@ -154,6 +154,12 @@ int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg
 int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg);
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride,
                         int unpack, hipStream_t stream, Done done = Done{});
+// MPI_Init: one empty kernel per translation unit (loads every code object; timed there)
+int launch_touch_all(hipStream_t stream);
+// MPI_Init self-test operands and checks (coll/dispatch.hip k_st_fill / k_st_check)
+int launch_selftest_fill(uint32_t *p, size_t n, uint32_t seed, int rank, hipStream_t stream);
+int launch_selftest_check(const uint32_t *p, size_t n, uint32_t seed, int nranks, int mode, int arg, uint64_t base,
+                          uint32_t *bad, hipStream_t stream);
 int launch_pack_runs(const void *src, void *dst, size_t count, size_t extent, const int64_t *offs,
                      const int64_t *lens, int nseg, int unpack, hipStream_t stream, Done done = Done{});
 

@@ -227,11 +227,13 @@ struct LReduceN {
             hipLaunchKernelGGL((k_reduce_n_elem<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream, pt, n,
                                (char *)dst, count, tp);
         } else {
+            // one vector per thread in flight: the n-source reduction serves the order tests and
+            // the leaders' steps across nodes (host-staged, link-bound), so its code stays small
             const size_t nvec = count / VPT;
-            size_t g = (nvec + 2 * kThreads - 1) / (2 * kThreads);
+            size_t g = (nvec + kThreads - 1) / kThreads;
             if (g > (size_t)cfg.grid) g = cfg.grid;
             if (g == 0) g = 1;
-            hipLaunchKernelGGL((k_reduce_n<Rd, 2>), dim3(g), dim3(kThreads), 0, cfg.stream, pt, n,
+            hipLaunchKernelGGL((k_reduce_n<Rd, 1>), dim3(g), dim3(kThreads), 0, cfg.stream, pt, n,
                                (char *)dst, count, nvec, tp);
         }
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
@@ -424,27 +426,33 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
 template <int OP, int K>
 struct LOneShot {
     static int run(const OneShotArgs &a, const LaunchCfg &cfg) {
+        using Rd = R<OP, K>;
         const bool prog = a.tp.linear == 4;
-        static const int cap0 = resident_grid((const void *)k_oneshot<R<OP, K>, false>, cfg);
-        static const int cap1 = resident_grid((const void *)k_oneshot<R<OP, K>, true>, cfg);
         if (a.rs) {
             if (!prog) return E_ARG;  // a reduce-scatter block is always evaluated in program order
-            static const int cap2 = resident_grid((const void *)k_oneshot_rs<R<OP, K>>, cfg);
+            static const int cap2 = resident_grid((const void *)k_oneshot_rs<Rd>, cfg);
             const int g = cfg.grid < cap2 ? cfg.grid : cap2;
-            hipLaunchKernelGGL((k_oneshot_rs<R<OP, K>>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+            hipLaunchKernelGGL((k_oneshot_rs<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
             return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
         }
-        const int cap = prog ? cap1 : cap0;
-        const int g = cfg.grid < cap ? cfg.grid : cap;
-        if (prog) hipLaunchKernelGGL((k_oneshot<R<OP, K>, true>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
-        else hipLaunchKernelGGL((k_oneshot<R<OP, K>, false>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+        static const int cap0 = resident_grid((const void *)k_oneshot<Rd, false>, cfg);
+        if constexpr (Rd::kOrderFree) {  // every order gives the same bits: the LINEAR body
+            const int g = cfg.grid < cap0 ? cfg.grid : cap0;
+            hipLaunchKernelGGL((k_oneshot<Rd, false>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+        } else {
+            static const int cap1 = resident_grid((const void *)k_oneshot<Rd, true>, cfg);
+            const int cap = prog ? cap1 : cap0;
+            const int g = cfg.grid < cap ? cfg.grid : cap;
+            if (prog) hipLaunchKernelGGL((k_oneshot<Rd, true>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+            else hipLaunchKernelGGL((k_oneshot<Rd, false>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+        }
         return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
     }
 };
 // ---------------- runtime (op, kind) -> template dispatch ----------------
 template <template <int, int> class L, int OP, int K, class... A>
 inline int call_if(A &&...args) {
-    if constexpr (legal<OP, K>()) return L<OP, K>::run(static_cast<A &&>(args)...);
+    if constexpr (legal<OP, K>()) return L<OP, canon_kind<OP, K>()>::run(static_cast<A &&>(args)...);
     else return E_OP;
 }
 

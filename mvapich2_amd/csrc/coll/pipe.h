@@ -382,6 +382,18 @@ __device__ __forceinline__ void scatter_round(const PipeArgs &a, uint64_t round0
 // PROG: the program-order variant (tp.linear == 4) is a kernel of its own so
 // that its register demand never lowers the occupancy of the hot ring /
 // butterfly kernel.
+// (op, kind) pairs whose pipelined reduction keeps the n <= 4 body with four operand columns and
+// two vectors in flight per thread (more loads outstanding per wave; the 2-rank 256 MiB allreduce
+// busbw rose with it, r02): the fp SUM / MAX / MIN and the DOUBLE_INT MAXLOC / MINLOC of the
+// benchmarks (configs[1]-[4]; DOUBLE_INT MAXLOC at 2 shared ranks: 445 GB/s wide, 401 GB/s eight
+// columns, r05a).  Every other pair runs the eight-column body at every n, which halves its share of
+// libmpi.so's code objects.
+template <class Rd> struct WidePipe : std::false_type {};
+template <int OP, int K>
+struct WidePipe<R<OP, K, void>>
+    : std::integral_constant<bool, ((K == K_F32 || K == K_F64) && (OP == OP_SUM || OP == OP_MAX || OP == OP_MIN)) ||
+                                       (K == K_P_DOUBLEINT && (OP == OP_MAXLOC || OP == OP_MINLOC))> {};
+
 template <class Rd, bool PROG>
 __device__ __forceinline__ void reduce_round(const PipeArgs &a, uint64_t round0, int k) {
     const uint64_t par = (round0 + (uint64_t)k) & 1;
@@ -445,8 +457,15 @@ __device__ __forceinline__ void reduce_round(const PipeArgs &a, uint64_t round0,
     const size_t len_body = body;
     // fewer sources -> more columns per thread, so >= 4 loads stay in flight
     // one specialised loop per (unroll, order); the order is uniform over the call
-    if constexpr (PROG) {
+    if constexpr (Rd::kOrderFree) {  // any order gives the same bits: the LINEAR body only
+        if (a.n <= 4) blk_reduce<Rd, 2, 1, 4>(a, src, d, len_body, e0);
+        else blk_reduce<Rd, 1, 1>(a, src, d, len_body, e0);
+    } else if constexpr (PROG) {
         blk_reduce<Rd, 1, 4>(a, src, d, len_body, (size_t)((int64_t)e0 + a.eshift));
+    } else if constexpr (!WidePipe<Rd>::value) {
+        if (a.tp.linear == 2) blk_reduce<Rd, 1, 2>(a, src, d, len_body, e0);
+        else if (a.tp.linear) blk_reduce<Rd, 1, 1>(a, src, d, len_body, e0);
+        else blk_reduce<Rd, 1, 0>(a, src, d, len_body, e0);
     } else if (a.n <= 4) {
         if (a.tp.linear == 2) blk_reduce<Rd, 2, 2, 4>(a, src, d, len_body, e0);
         else if (a.tp.linear) blk_reduce<Rd, 2, 1, 4>(a, src, d, len_body, e0);
@@ -570,7 +589,9 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeArgs a) {
 template <int OP, int K>
 struct LPipe {
     static int run(const PipeArgs &a, const LaunchCfg &cfg) {
-        if (a.tp.linear == 4)
+        if constexpr (R<OP, K>::kOrderFree)
+            hipLaunchKernelGGL((k_pipe<R<OP, K>, false>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
+        else if (a.tp.linear == 4)
             hipLaunchKernelGGL((k_pipe<R<OP, K>, true>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);
         else
             hipLaunchKernelGGL((k_pipe<R<OP, K>, false>), dim3(cfg.grid), dim3(kPipeThreads), 0, cfg.stream, a);

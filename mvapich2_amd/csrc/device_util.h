@@ -256,6 +256,13 @@ template <class Rd, int ORD = -1>
 __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[kMaxRanks], int n,
                                                       int linear, int pof2, int rem, int owner) {
     using T = typename Rd::T;
+    if constexpr (Rd::kOrderFree) {  // ops/functors.h: every order gives these bits
+        T acc = v[0];
+#pragma unroll
+        for (int i = 1; i < kMaxRanks; ++i)
+            if (i < n) acc = Rd::apply(acc, v[i]);
+        return acc;
+    }
     if (ORD >= 0) linear = ORD;
     if (linear == 2) {
         // RING (MPIR_Reduce_scatter_ring red_scat_osu.c:1121-1141): sources pre-rotated so
@@ -331,6 +338,23 @@ __device__ __forceinline__ typename Rd::T tree_reduce(const typename Rd::T (&v)[
 template <class Rd>
 __device__ __forceinline__ typename Rd::T prog_eval(const typename Rd::T (&v)[kMaxRanks], const Prog &p) {
     using T = typename Rd::T;
+    if constexpr (Rd::kOrderFree) {
+        // every order gives these bits (ops/functors.h): fold the program's leaves (each register
+        // it names is one rank's operand, used once) in index order
+        unsigned leaves = p.nsteps ? 0u : 1u << p.res;
+#pragma unroll
+        for (int s = 0; s < kMaxRanks - 1; ++s)
+            if (s < p.nsteps) leaves |= (1u << p.dst[s]) | (1u << p.src[s]);
+        T acc = v[0];
+        bool have = false;
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j)
+            if ((leaves >> j) & 1u) {
+                acc = have ? Rd::apply(acc, v[j]) : v[j];
+                have = true;
+            }
+        return acc;
+    }
     T w[kMaxRanks];
 #pragma unroll
     for (int j = 0; j < kMaxRanks; ++j) w[j] = v[j];

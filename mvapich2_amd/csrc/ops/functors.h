@@ -142,9 +142,17 @@ template <int K> constexpr bool is_int_kind() { return K >= K_I8 && K <= K_U64; 
 template <int K> constexpr bool is_fp_kind() { return K == K_F32 || K == K_F64; }
 template <int K> constexpr bool is_scalar_kind() { return is_int_kind<K>() || is_fp_kind<K>(); }
 
+// kOrderFree: the reduction order cannot change a single result bit, so the kernels evaluate any
+// algorithm's order as the LINEAR chain and the order-specialised bodies are not instantiated
+// (code size: libmpi.so's gfx950 code objects).  True for the integer kinds -- wrapping SUM / PROD,
+// MAX / MIN, the logical and the bitwise ops are all exactly associative and commutative -- and
+// for MPI_2INT MAXLOC / MINLOC (the largest / smallest value with the smallest loc among its ties,
+// and no padding bytes whose source would depend on the order).  Floating point, complex and the
+// padded pair kinds keep every order.
 template <int OP, int K>
 struct R<OP, K, typename std::enable_if<is_scalar_kind<K>()>::type> {
     using T = typename KT<K>::T;
+    static constexpr bool kOrderFree = is_int_kind<K>();
     static __device__ __forceinline__ T apply(T a, T b) {
         if constexpr (OP == OP_SUM) {
             if constexpr (is_int_kind<K>()) return wadd(a, b); else return fadd(a, b);
@@ -176,6 +184,7 @@ struct R<OP, K, typename std::enable_if<is_scalar_kind<K>()>::type> {
 template <int OP, int K>
 struct R<OP, K, typename std::enable_if<(K >= K_CF32_C99 && K <= K_CF64_S)>::type> {
     using T = typename KT<K>::T;
+    static constexpr bool kOrderFree = false;
     static __device__ __forceinline__ T apply(T a, T b) {
         T r;
         if constexpr (OP == OP_SUM) {
@@ -200,6 +209,7 @@ struct R<OP, K, typename std::enable_if<(K >= K_CF32_C99 && K <= K_CF64_S)>::typ
 template <int OP, int K>
 struct R<OP, K, typename std::enable_if<(K >= K_P_2INT && K <= K_P_2F64)>::type> {
     using T = typename KT<K>::T;
+    static constexpr bool kOrderFree = K == K_P_2INT;
     static __device__ __forceinline__ T apply(T a, T b) {
         static_assert(OP == OP_MAXLOC || OP == OP_MINLOC, "pair kinds take MAXLOC/MINLOC");
         const bool an = a.value != a.value, bn = b.value != b.value;
@@ -231,5 +241,22 @@ template <int OP, int K> constexpr bool legal() {
     if (is_int_kind<K>()) return OP < OP_MINLOC;
     return false;
 }
+
+// The kind an (OP, K) pair is instantiated with.  Signed and unsigned integers of one width give
+// the same bits under every op but MAX / MIN (two's-complement wrapping SUM / PROD, the logical
+// ops' 0 / 1, the bitwise ops), and the struct and C99 complex kinds the same SUM, so those pairs
+// share one instantiation: the signed kind runs as its unsigned twin, struct complex SUM as C99.
+template <int OP, int K> constexpr int canon_kind() {
+    if constexpr (is_int_kind<K>()) {
+        if (OP != OP_MAX && OP != OP_MIN && (K == K_I8 || K == K_I16 || K == K_I32 || K == K_I64)) return K + 1;
+        return K;
+    } else if constexpr (K == K_CF32_S || K == K_CF64_S) {
+        return OP == OP_SUM ? K - 2 : K;
+    } else {
+        return K;
+    }
+}
+static_assert(K_U8 == K_I8 + 1 && K_U64 == K_I64 + 1 && K_CF32_C99 == K_CF32_S - 2 && K_CF64_C99 == K_CF64_S - 2,
+              "canon_kind relies on the Kind order");
 
 }  // namespace mv2

@@ -274,4 +274,11 @@ int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, 
     return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
 }
 
+// an empty kernel of this unit (MPI_Init loads every code object up front, coll/dispatch.hip)
+__global__ void k_touch_pack() {}
+int launch_pack_touch(hipStream_t st) {
+    hipLaunchKernelGGL(k_touch_pack, dim3(1), dim3(64), 0, st);
+    return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+}
+
 }  // namespace mv2

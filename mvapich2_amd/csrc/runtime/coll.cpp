@@ -552,77 +552,6 @@ static int allreduce_entry(const void *sendbuf, void *recvbuf, size_t count, int
 
 namespace mv2 {
 
-// Init-time check of the cross-GPU publish protocol on this node's topology.
-// The pipelined and one-shot kernels publish arena stores with the light
-// release (stores acknowledged, no L2 writeback), which is right only if
-// peer-mapped uncached arenas are not write-back cached by the writer.  A
-// 4 MiB pipelined int32 SUM allreduce (two calls: both slot parities) and a
-// 4 KiB one-shot one are checked element by element on every rank; the
-// verdict is agreed through the host control segment (no GPU path involved).
-// On a mismatch every rank falls back to the full system-scope release and
-// re-checks; a second failure fails MPI_Init loudly instead of returning
-// wrong sums later.
-int coll_selftest() {
-    World &w = world();
-    const int n = w.size;
-    const size_t count = (size_t)1 << 20;
-    const size_t bytes = count * 4;
-    std::vector<uint32_t> h(count), want(count), got(count);
-    for (size_t i = 0; i < count; ++i) {
-        h[i] = (uint32_t)(i * 2654435761u) ^ (uint32_t)(w.rank * 0x9E3779B9u + 17u);
-        uint32_t acc = 0;
-        for (int r = 0; r < n; ++r) acc += (uint32_t)(i * 2654435761u) ^ (uint32_t)(r * 0x9E3779B9u + 17u);
-        want[i] = acc;
-    }
-    void *sb = nullptr, *rb = nullptr;
-    if (hipMalloc(&sb, bytes) != hipSuccess || hipMalloc(&rb, bytes) != hipSuccess) {
-        MV2_ERR("self-test: device allocation failed");
-        return E_NO_MEM;
-    }
-    hipMemcpy(sb, h.data(), bytes, hipMemcpyHostToDevice);
-    const int MPI_INT_H = 0x4c000405, MPI_SUM_H = 0x58000003;
-    int verdict = 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        int ok = 1;
-        // pipelined (4 MiB, both parities) then one-shot (first 1024 elements)
-        const size_t sizes[3] = {count, count, 1024};
-        for (int call = 0; call < 3 && ok; ++call) {
-            const size_t c = sizes[call];
-            hipMemset(rb, 0, bytes);
-            hipDeviceSynchronize();
-            if (::allreduce_entry(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr)  /* this node */ != 0) {
-                ok = 0;
-                break;
-            }
-            hipMemcpy(got.data(), rb, c * 4, hipMemcpyDeviceToHost);
-            ok = memcmp(got.data(), want.data(), c * 4) == 0;
-        }
-        w.shm->r[w.rank].selftest_ok = ok;
-        host_barrier();
-        int all_ok = 1;
-        for (int j = 0; j < n; ++j) all_ok &= w.shm->r[j].selftest_ok;
-        host_barrier();  // every rank has read every verdict
-        if (all_ok) {
-            verdict = 0;
-            MV2_DEBUG("self-test passed (light_release=%d)", w.light_release);
-            break;
-        }
-        verdict = E_INTERN;
-        if (w.light_release) {
-            if (w.rank == 0)
-                fprintf(stderr, "[mv2amd] warning: device collective self-test failed with the light release; "
-                                "using the full system-scope release\n");
-            w.light_release = 0;
-        } else {
-            break;
-        }
-    }
-    hipFree(sb);
-    hipFree(rb);
-    if (verdict) MV2_ERR("device collective self-test failed at MPI_Init (ranks %d): cross-GPU protocol broken", n);
-    return verdict;
-}
-
 // Init-time choice of the pipelined kernels' tiling (workgroups x bytes per workgroup per
 // round) on this node's links.  The link rate of a peer store stream and the cost of a
 // round's flag exchange are properties of the machine, not of the message, so MPI_Init times
@@ -874,6 +803,10 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "init_us")) *value = (long)(w.init_ms * 1e3 + 0.5);
     else if (!strcmp(key, "selftest_us")) *value = (long)(w.selftest_ms * 1e3 + 0.5);
     else if (!strcmp(key, "autotune_us")) *value = (long)(w.tune_ms * 1e3 + 0.5);
+    else if (!strcmp(key, "hip_init_us")) *value = (long)(w.hip_init_ms * 1e3 + 0.5);
+    else if (!strcmp(key, "code_load_us")) *value = (long)(w.code_load_ms * 1e3 + 0.5);
+    else if (!strcmp(key, "selftest_calls")) *value = w.selftest_calls;
+    else if (!strcmp(key, "call_allocs")) *value = (long)w.call_allocs;
     else if (!strcmp(key, "uop_in_bytes")) *value = (long)w.uop_in_bytes;
     else if (!strcmp(key, "uop_area_bytes")) *value = (long)w.uop_area_bytes;
     else if (!strcmp(key, "uop_stage_us")) *value = (long)(w.uop_ns[0] / 1000);
@@ -3137,3 +3070,208 @@ int mv2h_copy_enqueue(void *dst, const void *src, size_t bytes, void *stream) {
 int mv2h_enqueue_check(void) { return check_err_word(); }
 
 }  // extern "C"
+
+// ===========================================================================
+// MPI_Init self-test of the cross-GPU publish protocol on this node's topology
+// ===========================================================================
+namespace mv2 {
+
+// The one-shot and pipelined kernels publish arena stores with the light release (stores
+// acknowledged, no L2 writeback) and read them with the light acquire, which is right only if a
+// peer-mapped uncached arena is not write-back cached by its writer -- a property of the links
+// that the one-GPU box cannot show.  A rare ordering failure would not show in one call either, so
+// MPI_Init runs every kernel that crosses GPUs, over both slot parities / arena halves, with a
+// new operand pattern per call (an element of a stale slot never matches), and checks every
+// element of every result on the device:
+//   one-shot allreduce (6 sizes x 2 halves), one-shot reduce-scatter (3 x 2), pipelined allreduce
+//   (ring order, 4 MiB, x 4; butterfly order x 2; ring + remainder), a multi-round pipelined
+//   allreduce (small rounds: both parities inside one call) x 2, pipelined reduce-scatter,
+//   allgather and broadcast x 2 each, and, with the graph lane, a captured one-shot and a
+//   captured pipelined allreduce replayed 3 times each (its own arenas and device sequence).
+// The per-call mismatch counts are read once at the end; the verdict is agreed through the
+// host control segment.  On a mismatch every rank falls back to the full system-scope release
+// and runs the whole set again; a second failure fails MPI_Init instead of returning wrong
+// sums later.  (Protocol contract: device_util.h:1-13.)
+int coll_selftest() {
+    World &w = world();
+    const int n = w.size, me = w.rank;
+    const int MPI_INT_H = 0x4c000405, MPI_SUM_H = 0x58000003;
+    const size_t cap = ((size_t)1 << 20) + 64;  // elements per buffer
+    constexpr int kMaxCalls = 96;
+    uint32_t *sb = nullptr, *rb = nullptr, *bad = nullptr;
+    if (hipMalloc((void **)&sb, cap * 4) != hipSuccess || hipMalloc((void **)&rb, cap * 4) != hipSuccess ||
+        hipMalloc((void **)&bad, kMaxCalls * 4) != hipSuccess) {
+        MV2_ERR("self-test: device allocation failed");
+        if (sb) hipFree(sb);
+        if (rb) hipFree(rb);
+        return E_NO_MEM;
+    }
+    hipStream_t st = w.stream;
+    const char *what[kMaxCalls] = {};
+    int verdict = 0, calls = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        hipMemsetAsync(bad, 0, kMaxCalls * 4, st);
+        int rc = 0;
+        calls = 0;
+        auto seed_of = [&](int k) { return (uint32_t)(0x51ed270bu * (uint32_t)(k + 1) + 0x1000193u * (uint32_t)attempt); };
+        // one checked call: fill this rank's operand, run the call, check its result on the device
+        auto fill = [&](uint32_t *p, size_t c, int k, int as_rank) {
+            if (!rc) rc = launch_selftest_fill(p, c, seed_of(k), as_rank, st);
+        };
+        auto check = [&](const uint32_t *p, size_t c, int k, int mode, int arg, uint64_t base, const char *name) {
+            if (!rc) rc = launch_selftest_check(p, c, seed_of(k), n, mode, arg, base, bad + k, st);
+            what[k] = name;
+        };
+        // one-shot allreduce: sizes up to the one-shot limit, each on both arena halves
+        const size_t os_max = std::min(w.oneshot_max, w.slot_bytes) / 4;
+        const size_t os_sizes[6] = {2, 1027, 4096, 16389, os_max > 3 ? os_max - 3 : 1, os_max};
+        for (int i = 0; i < 6 && !rc; ++i)
+            for (int h = 0; h < 2 && !rc; ++h) {
+                const int k = calls++;
+                const size_t c = std::max<size_t>(1, std::min(os_sizes[i], cap));
+                fill(sb, c, k, me);
+                if (!rc) rc = ::allreduce_entry(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr);
+                check(rb, c, k, 0, 0, 0, "one-shot allreduce");
+            }
+        // one-shot reduce-scatter (equal blocks of 16-byte multiples, below the ring threshold)
+        const size_t rs_small[3] = {4, 1024, 2048};
+        for (int i = 0; i < 3 && !rc; ++i)
+            for (int h = 0; h < 2 && !rc; ++h) {
+                const int k = calls++;
+                const size_t c = rs_small[i];
+                size_t counts[kMaxRanks];
+                for (int j = 0; j < n; ++j) counts[j] = c;
+                fill(sb, c * n, k, me);
+                if (!rc) rc = ::reduce_scatter_entry(sb, rb, counts, MPI_INT_H, MPI_SUM_H, nullptr);
+                check(rb, c, k, 0, 0, (uint64_t)me * c, "one-shot reduce-scatter");
+            }
+        // pipelined allreduce: ring order (4 MiB) on both slot parities twice, the butterfly
+        // (pt2pt_rs, 1 MiB + 5), the ring with a remainder (4 MiB + 3)
+        const size_t pa_sizes[7] = {(size_t)1 << 20, (size_t)1 << 20, (size_t)1 << 20, (size_t)1 << 20,
+                                    ((size_t)1 << 18) + 5, ((size_t)1 << 18) + 5, ((size_t)1 << 20) + 3};
+        for (int i = 0; i < 7 && !rc; ++i) {
+            const int k = calls++;
+            fill(sb, pa_sizes[i], k, me);
+            if (!rc) rc = ::allreduce_entry(sb, rb, pa_sizes[i], MPI_INT_H, MPI_SUM_H, nullptr);
+            check(rb, pa_sizes[i], k, 0, 0, 0, "pipelined allreduce");
+        }
+        // multi-round pipelined allreduce: small rounds, so one call alternates slot parities
+        {
+            const int g0 = w.pipe_grid;
+            const size_t s0 = w.pipe_sub;
+            w.pipe_grid = std::min(g0, 32);
+            w.pipe_sub = 4096;
+            for (int i = 0; i < 2 && !rc; ++i) {
+                const int k = calls++;
+                const size_t c = ((size_t)1 << 20) - 7 * (size_t)i;
+                fill(sb, c, k, me);
+                if (!rc) rc = ::allreduce_entry(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr);
+                check(rb, c, k, 0, 0, 0, "multi-round pipelined allreduce");
+            }
+            w.pipe_grid = g0;
+            w.pipe_sub = s0;
+        }
+        // pipelined reduce-scatter (ring, 4 MiB in all), allgather, broadcast
+        for (int i = 0; i < 2 && !rc; ++i) {
+            const int k = calls++;
+            const size_t c = ((size_t)1 << 20) / (size_t)n;
+            size_t counts[kMaxRanks];
+            for (int j = 0; j < n; ++j) counts[j] = c;
+            fill(sb, c * n, k, me);
+            if (!rc) rc = ::reduce_scatter_entry(sb, rb, counts, MPI_INT_H, MPI_SUM_H, nullptr);
+            check(rb, c, k, 0, 0, (uint64_t)me * c, "pipelined reduce-scatter");
+        }
+        for (int i = 0; i < 2 && !rc; ++i) {
+            const int k = calls++;
+            const size_t c = ((size_t)1 << 20) / (size_t)n - 4 * (size_t)i;
+            fill(sb, c, k, me);
+            if (!rc) rc = allgather_node(sb, rb, c * 4, nullptr);
+            check(rb, c * n, k, 2, (int)c, 0, "pipelined allgather");
+        }
+        for (int i = 0; i < 2 && !rc; ++i) {
+            const int k = calls++;
+            const int root = i == 0 ? 0 : n - 1;
+            const size_t c = ((size_t)1 << 18) + 3 * (size_t)i;
+            if (me == root) fill(rb, c, k, root);
+            else if (!rc) rc = hipMemsetAsync(rb, 0xA5, c * 4, st) == hipSuccess ? 0 : E_INTERN;
+            if (!rc) rc = bcast_node(rb, c * 4, root, nullptr);
+            check(rb, c, k, 1, root, 0, "pipelined broadcast");
+        }
+        // graph lane: a captured one-shot and a captured pipelined allreduce, replayed
+        if (w.graph_lane && !rc) {
+            hipStream_t cs = nullptr;
+            const size_t gc[2] = {4096, (((size_t)1 << 20) / (16 * (size_t)n)) * 16 * (size_t)n};
+            hipGraph_t graph[2] = {};
+            hipGraphExec_t ex[2] = {};
+            if (hipStreamCreate(&cs) != hipSuccess) rc = E_INTERN;
+            for (int g = 0; g < 2 && !rc; ++g) {
+                if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) {
+                    rc = E_INTERN;
+                    break;
+                }
+                int crc;
+                {
+                    EnqueueScope q(true);
+                    crc = ::allreduce_entry(sb + (size_t)g * 8192, rb + (size_t)g * 8192, gc[g], MPI_INT_H, MPI_SUM_H, cs);
+                }
+                if (hipStreamEndCapture(cs, &graph[g]) != hipSuccess || crc ||
+                    hipGraphInstantiate(&ex[g], graph[g], nullptr, nullptr, 0) != hipSuccess)
+                    rc = crc ? crc : E_INTERN;
+            }
+            hipStreamSynchronize(st);  // the blocking calls above are done before the replays
+            for (int rep = 0; rep < 3 && !rc; ++rep)
+                for (int g = 0; g < 2 && !rc; ++g) {
+                    const int k = calls++;
+                    if ((rc = launch_selftest_fill(sb + (size_t)g * 8192, gc[g], seed_of(k), me, cs))) break;
+                    if (hipGraphLaunch(ex[g], cs) != hipSuccess) rc = E_INTERN;
+                    if (!rc) rc = launch_selftest_check(rb + (size_t)g * 8192, gc[g], seed_of(k), n, 0, 0, 0, bad + k, cs);
+                    what[k] = "graph-lane allreduce";
+                }
+            if (cs && hipStreamSynchronize(cs) != hipSuccess) rc = rc ? rc : E_INTERN;
+            if (!rc && check_err_word()) rc = E_OTHER;
+            for (int g = 0; g < 2; ++g) {
+                if (ex[g]) hipGraphExecDestroy(ex[g]);
+                if (graph[g]) hipGraphDestroy(graph[g]);
+            }
+            if (cs) hipStreamDestroy(cs);
+        }
+        uint32_t hb[kMaxCalls] = {};
+        if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(hb, bad, sizeof(hb), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = rc ? rc : E_INTERN;
+        int ok = rc == 0;
+        for (int k = 0; k < calls && ok; ++k)
+            if (hb[k]) {
+                MV2_ERR("self-test (%s release): call %d (%s) returned %u wrong elements",
+                        w.light_release ? "light" : "full", k, what[k] ? what[k] : "?", hb[k]);
+                ok = 0;
+            }
+        if (rc) MV2_ERR("self-test: a call failed (MPI error class %d)", rc);
+        w.shm->r[me].selftest_ok = ok;
+        host_barrier();
+        int all_ok = 1;
+        for (int j = 0; j < n; ++j) all_ok &= w.shm->r[j].selftest_ok;
+        host_barrier();  // every rank has read every verdict
+        if (all_ok) {
+            verdict = 0;
+            MV2_DEBUG("self-test passed: %d calls (light_release=%d)", calls, w.light_release);
+            break;
+        }
+        verdict = E_INTERN;
+        if (w.light_release && rc == 0) {
+            if (me == 0)
+                fprintf(stderr, "[mv2amd] warning: device collective self-test failed with the light release; "
+                                "using the full system-scope release\n");
+            w.light_release = 0;
+        } else {
+            break;
+        }
+    }
+    w.selftest_calls = calls;
+    hipFree(sb);
+    hipFree(rb);
+    hipFree(bad);
+    if (verdict) MV2_ERR("device collective self-test failed at MPI_Init (ranks %d): cross-GPU protocol broken", n);
+    return verdict;
+}
+
+}  // namespace mv2

@@ -316,8 +316,41 @@ static int limit_hw_queues_if_shared(int local_size) {
     return (int)want;
 }
 
+// Is HIP already running in this process (a host framework or an earlier call touched the GPU
+// first)?  The ROCm runtime opens /dev/kfd when it starts, so an open descriptor on it says so;
+// GPU_MAX_HW_QUEUES is read once at that start, so setting it later has no effect.
+static bool hip_already_running() {
+    char path[64], target[64];
+    for (int fd = 0; fd < 4096; ++fd) {
+        snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+        const ssize_t k = readlink(path, target, sizeof(target) - 1);
+        if (k <= 0) continue;
+        target[k] = 0;
+        if (!strcmp(target, "/dev/kfd")) return true;
+    }
+    return false;
+}
+
+static int env_local_size() {
+    const char *lsn[] = {"MV2_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "OMPI_COMM_WORLD_LOCAL_SIZE", "LOCAL_WORLD_SIZE",
+                         nullptr};
+    const char *sn[] = {"MV2_COMM_WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "WORLD_SIZE", nullptr};
+    return env_int(lsn, env_int(sn, 1));
+}
+
+// limit_hw_queues_if_shared before this library's own HIP start-up: records what was set (> 0),
+// or -k when k queues were wanted but HIP was already running (the setting came too late)
+static void apply_hw_queue_limit(int local_size) {
+    World &w = g_world;
+    if (w.stream || w.hw_queues_set) return;
+    const bool late = hip_already_running();
+    const int q = limit_hw_queues_if_shared(local_size);
+    w.hw_queues_set = late && q > 0 ? -q : q;
+}
+
 static int setup_device_common() {
     World &w = g_world;
+    const auto t_hip = std::chrono::steady_clock::now();
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         MV2_ERR("no HIP device visible: this library runs its reduction path on MI355X only");
@@ -354,12 +387,24 @@ static int setup_device_common() {
     knobs_reload();  // MV2_* algorithm-selection knobs (orders.cpp)
     hipEventCreate(&w.ev0);
     hipEventCreate(&w.ev1);
+    w.hip_init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_hip).count();
+    // every code object of the library loaded here, timed (MV2AMD_PRELOAD_KERNELS=0: left to HIP's
+    // deferred loading at each unit's first launch)
+    if (env_long("MV2AMD_PRELOAD_KERNELS", 1) != 0) {
+        const auto t_load = std::chrono::steady_clock::now();
+        if (launch_touch_all(w.stream) != 0 || hipStreamSynchronize(w.stream) != hipSuccess) {
+            MV2_ERR("loading the library's gfx950 code objects failed: %s", hipGetErrorString(hipGetLastError()));
+            return E_OTHER;
+        }
+        w.code_load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_load).count();
+    }
     return 0;
 }
 
 int ensure_init_for_device() {
     World &w = g_world;
     if (w.stream) return 0;
+    if (!getenv("MV2AMD_CONTROL_PLANE_ONLY")) apply_hw_queue_limit(env_local_size());
     return setup_device_common();
 }
 
@@ -534,7 +579,7 @@ int world_init() {
     const char *cpo = getenv("MV2AMD_CONTROL_PLANE_ONLY");
     const bool control_only = cpo && *cpo == '1';
     if (!w.stream && !control_only) {
-        w.hw_queues_set = limit_hw_queues_if_shared(w.size);
+        apply_hw_queue_limit(w.size);
         int rc = setup_device_common();
         if (rc) return rc;
     }
@@ -766,15 +811,20 @@ int world_init() {
         int g256 = 0;
         size_t t256 = 0;
         pipe_tiling_for(((size_t)256 << 20) / (size_t)w.size, &g256, &t256);  // a 256 MiB allreduce's segment
+        char qnote[160] = "";
+        if (w.hw_queues_set > 0)
+            snprintf(qnote, sizeof(qnote), "; GPU shared: GPU_MAX_HW_QUEUES lowered to %d", w.hw_queues_set);
+        else if (w.hw_queues_set < 0)
+            snprintf(qnote, sizeof(qnote), "; GPU shared, but HIP was already running: GPU_MAX_HW_QUEUES=%d came too "
+                     "late (set it before the process starts HIP)", -w.hw_queues_set);
         fprintf(stderr,
-                "[mv2amd] MPI_Init: %d ranks (%d per node, %d node%s, %d per GPU); self-test %s; tiling %s, %s stores "
-                "(256 MiB allreduce: %d workgroups x %zu KiB per round); one-shot up to %zu KiB; init %.1f ms "
-                "(self-test %.1f, autotune %.1f)%s%s\n",
-                w.gsize, w.size, w.nnodes, w.nnodes > 1 ? "s" : "", w.nshare,
-                !ran ? "not run" : w.light_release ? "passed, light release" : "passed, full system-scope release",
+                "[mv2amd] MPI_Init: %d ranks (%d per node, %d node%s, %d per GPU); self-test %s%d calls checked%s; "
+                "tiling %s, %s stores (256 MiB allreduce: %d workgroups x %zu KiB per round); one-shot up to %zu KiB; "
+                "init %.1f ms (HIP start %.1f, code objects %.1f, self-test %.1f, autotune %.1f)%s\n",
+                w.gsize, w.size, w.nnodes, w.nnodes > 1 ? "s" : "", w.nshare, !ran ? "not run (" : "passed (",
+                w.selftest_calls, !ran ? ")" : w.light_release ? "), light release" : "), full system-scope release",
                 w.pipe_tuned ? "autotuned" : "default", w.pipe_rnt ? "non-temporal" : "plain", g256, t256 >> 10,
-                w.oneshot_max >> 10, w.init_ms, w.selftest_ms, w.tune_ms,
-                w.hw_queues_set ? "; GPU shared: GPU_MAX_HW_QUEUES lowered to " : "", w.hw_queues_set ? getenv("GPU_MAX_HW_QUEUES") : "");
+                w.oneshot_max >> 10, w.init_ms, w.hip_init_ms, w.code_load_ms, w.selftest_ms, w.tune_ms, qnote);
         fflush(stderr);
     }
     MV2_DEBUG("init rank %d/%d local %d device %d nshare %d (node %d of %d): %.1f ms (self-test %.1f, autotune %.1f)",

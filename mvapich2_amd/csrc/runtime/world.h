@@ -165,14 +165,21 @@ struct World {
     int tune_grid[kTuneMax] = {};
     size_t tune_sub[kTuneMax] = {};
     double tune_us[kTuneMax] = {};                // max over ranks per candidate
-    double init_ms = 0, selftest_ms = 0, tune_ms = 0;
-    size_t uop_in_bytes = 0, uop_area_bytes = 0;
+    double init_ms = 0, selftest_ms = 0, tune_ms = 0;  // MPI_Init wall time and its self-test / autotune parts
+    // HIP start-up (first HIP call through stream creation) and the first kernel launch of this
+    // library (loads its gfx950 code object: HIP defers that to the first launch)
+    double hip_init_ms = 0, code_load_ms = 0;
+    int selftest_calls = 0;  // collective calls MPI_Init's self-test checked (all ranks, every element)
+    // device allocations made inside MPI calls (scratch growth: hipMalloc, each paired with a
+    // hipFree that synchronises the device); stays flat once the scratch caches are warm
+    uint64_t call_allocs = 0;
+    size_t uop_in_bytes = 0, uop_area_bytes = 0;  // last host-evaluated reduction: operand bytes received, area
     // host-evaluated reductions, cumulative ns per phase (mpi/user_coll.cpp UopPhase): staging the
     // operands (device pack + exchange), fetching them to the host (D2H + unpack), evaluating (uop
     // calls + result pack), delivering (H2D + results' exchange + device unpack)
     uint64_t uop_ns[4] = {0, 0, 0, 0};
     uint64_t api_calls = 0;  // library calls entered (the beacon's call number)
-    int hw_queues_set = 0;   // GPU_MAX_HW_QUEUES this library set before HIP started (ranks sharing a GPU)  // last host-evaluated reduction: operand bytes received, area  // MPI_Init wall time and its self-test / autotune parts
+    int hw_queues_set = 0;   // GPU_MAX_HW_QUEUES this library set before HIP started (ranks sharing a GPU)
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)

@@ -34,9 +34,22 @@
  * per size, `skip` untimed then `iters` timed iterations of
  * barrier; t0; allreduce; t1 — average over ranks of the per-rank mean.
  *
+ * Placement (a label of "8 ranks pinned 1/core" must be
+ * checkable).  Before forking, the parent reads the inherited affinity mask
+ * (the job's cpuset), orders its CPUs one hardware thread per physical core
+ * first (sysfs core / package ids; SMT siblings only after every core has one
+ * rank), and assigns rank r the (p + r)-th CPU of that order.  More ranks than
+ * CPUs in the mask is *oversubscription*: ranks then share a CPU and the spin
+ * waits degrade into sched_yield hand-offs (the latency-bound sizes collapse),
+ * so the program says so instead of wrapping silently.  One header row
+ * (prefix "JSONHDR ") carries the mask size, each rank's CPU, the distinct CPU
+ * and physical-core counts, the oversubscription flag and the cgroup's CPU
+ * quota; each size row carries the spin loops that fell back to sched_yield
+ * (summed over ranks) and the cgroup's CFS throttling during that size.
+ *
  * Usage: host_allreduce [-n ranks] [-m min:max] [-i iters_small] [-I iters_large]
- *                       [-c (validate)] [-T seconds per size cap]
- * Prints an OSU-style table and one JSON line (prefix "JSON ").
+ *                       [-c (validate)] [-T seconds per size cap] [-p first cpu index]
+ * Prints an OSU-style table, one "JSONHDR " line and one "JSON " line per size.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -74,6 +87,7 @@ typedef struct {
     padded_t bc_done[MAXR];     /* two-level: rank r copied the bcast slot (gen) */
     double lat[MAXR];
     int bad[MAXR];
+    unsigned long yields[MAXR]; /* spin waits that fell back to sched_yield, this size */
 } ctrl_t;
 
 static ctrl_t *C;
@@ -86,10 +100,12 @@ static unsigned long gen_bar, gen_slot;
 
 static inline void cpu_relax(void) { __builtin_ia32_pause(); }
 
+static unsigned long my_yields;
+
 static void spin_until(atomic_ulong *p, unsigned long g) {
     unsigned spins = 0;
     while (atomic_load_explicit(p, memory_order_acquire) < g)
-        if (++spins > 4096) { sched_yield(); spins = 0; } else cpu_relax();
+        if (++spins > 4096) { sched_yield(); spins = 0; ++my_yields; } else cpu_relax();
 }
 
 static void barrier(void) {
@@ -316,22 +332,123 @@ static double now(void) {
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-/* pin to the k-th CPU of the inherited affinity mask (the job's cpuset) */
-static int pin(int k) {
-    cpu_set_t s, one;
-    if (sched_getaffinity(0, sizeof(s), &s)) return -1;
-    int cnt = CPU_COUNT(&s);
-    if (cnt <= 0) return -1;
-    k %= cnt;
-    for (int c = 0; c < CPU_SETSIZE; c++) {
-        if (!CPU_ISSET(c, &s)) continue;
-        if (k-- == 0) {
-            CPU_ZERO(&one);
-            CPU_SET(c, &one);
-            return sched_setaffinity(0, sizeof(one), &one) ? -1 : c;
+/* ---- placement ---------------------------------------------------------- */
+
+static long read_long_file(const char *path, long dflt) {
+    FILE *f = fopen(path, "r");
+    if (!f) return dflt;
+    long v = dflt;
+    if (fscanf(f, "%ld", &v) != 1) v = dflt;
+    fclose(f);
+    return v;
+}
+
+/* physical core key of a CPU: package id * 65536 + core id (sysfs; -1 when absent) */
+static long core_key(int cpu) {
+    char p[128];
+    snprintf(p, sizeof p, "/sys/devices/system/cpu/cpu%d/topology/core_id", cpu);
+    long core = read_long_file(p, -1);
+    snprintf(p, sizeof p, "/sys/devices/system/cpu/cpu%d/topology/physical_package_id", cpu);
+    long pkg = read_long_file(p, 0);
+    return core < 0 ? -1 - cpu : pkg * 65536 + core;
+}
+
+/* the cgroup's CPU quota in CPUs (cgroup v2 cpu.max, else v1 cfs_quota/period); -1 = none */
+static double cgroup_quota_cpus(void) {
+    FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char q[32] = {0};
+        long per = 0;
+        int k = fscanf(f, "%31s %ld", q, &per);
+        fclose(f);
+        if (k == 2 && strcmp(q, "max") != 0 && per > 0) return atof(q) / (double)per;
+        if (k >= 1) return -1;
+    }
+    long q = read_long_file("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", -1);
+    long per = read_long_file("/sys/fs/cgroup/cpu/cpu.cfs_period_us", 0);
+    return (q > 0 && per > 0) ? (double)q / (double)per : -1;
+}
+
+/* cumulative CFS throttling of this cgroup: events and microseconds (0 / 0 if unreadable) */
+static void cgroup_throttled(long *events, double *usec) {
+    *events = 0;
+    *usec = 0;
+    FILE *f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+    int v2 = f != NULL;
+    if (!f) f = fopen("/sys/fs/cgroup/cpu/cpu.stat", "r");
+    if (!f) return;
+    char key[64];
+    long long val;
+    while (fscanf(f, "%63s %lld", key, &val) == 2) {
+        if (!strcmp(key, "nr_throttled")) *events = (long)val;
+        else if (v2 && !strcmp(key, "throttled_usec")) *usec = (double)val;
+        else if (!v2 && !strcmp(key, "throttled_time")) *usec = (double)val / 1e3;
+    }
+    fclose(f);
+}
+
+static int RANK_CPU[MAXR];
+
+/* Plan every rank's CPU from the inherited mask (see the header) and print the
+ * JSONHDR row.  Returns the number of distinct CPUs used. */
+static int plan_placement(int first) {
+    cpu_set_t s;
+    int cpus[CPU_SETSIZE], ncpu = 0;
+    if (sched_getaffinity(0, sizeof(s), &s) == 0)
+        for (int c = 0; c < CPU_SETSIZE; c++)
+            if (CPU_ISSET(c, &s)) cpus[ncpu++] = c;
+    /* one thread per physical core first: round t takes the t-th thread of every core */
+    int order[CPU_SETSIZE], no = 0, used[CPU_SETSIZE] = {0};
+    long keys[CPU_SETSIZE];
+    for (int i = 0; i < ncpu; i++) keys[i] = core_key(cpus[i]);
+    while (no < ncpu) {
+        long seen[CPU_SETSIZE];
+        int ns = 0;
+        for (int i = 0; i < ncpu; i++) {
+            if (used[i]) continue;
+            int dup = 0;
+            for (int j = 0; j < ns && !dup; j++) dup = seen[j] == keys[i];
+            if (dup) continue;
+            seen[ns++] = keys[i];
+            used[i] = 1;
+            order[no++] = cpus[i];
         }
     }
-    return -1;
+    int distinct = 0, dcores = 0;
+    long ckeys[MAXR];
+    for (int r = 0; r < N; r++) {
+        RANK_CPU[r] = ncpu ? order[(first + r) % ncpu] : -1;
+        int dup = 0;
+        for (int j = 0; j < r && !dup; j++) dup = RANK_CPU[j] == RANK_CPU[r];
+        distinct += !dup;
+        long k = RANK_CPU[r] >= 0 ? core_key(RANK_CPU[r]) : -1;
+        dup = 0;
+        for (int j = 0; j < r && !dup; j++) dup = ckeys[j] == k;
+        ckeys[r] = k;
+        dcores += !dup;
+    }
+    const double quota = cgroup_quota_cpus();
+    printf("JSONHDR {\"ranks\": %d, \"cpus_available\": %d, \"cpus_used\": %d, \"cores_used\": %d, "
+           "\"oversubscribed\": %s, \"smt_shared\": %s, \"first_cpu_index\": %d, \"rank_cpus\": [",
+           N, ncpu, distinct, dcores, distinct < N ? "true" : "false", dcores < distinct ? "true" : "false", first);
+    for (int r = 0; r < N; r++) printf("%s%d", r ? ", " : "", RANK_CPU[r]);
+    printf("], \"cgroup_cpu_quota\": ");
+    if (quota > 0) printf("%.3f", quota);
+    else printf("null");
+    printf("}\n");
+    if (distinct < N)
+        fprintf(stderr, "host_allreduce: WARNING %d ranks on %d distinct CPUs (the inherited mask holds %d): "
+                        "oversubscribed, latency figures are not one rank per core\n", N, distinct, ncpu);
+    fflush(stdout);
+    return distinct;
+}
+
+static int pin_cpu(int c) {
+    cpu_set_t one;
+    if (c < 0) return -1;
+    CPU_ZERO(&one);
+    CPU_SET(c, &one);
+    return sched_setaffinity(0, sizeof(one), &one) ? -1 : c;
 }
 
 int main(int argc, char **argv) {
@@ -362,6 +479,7 @@ int main(int argc, char **argv) {
     SHM_DATA = mmap(NULL, RSTRIDE * N, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (C == MAP_FAILED || SHM_DATA == MAP_FAILED) { perror("mmap"); return 1; }
     memset(C, 0, sizeof(ctrl_t));
+    plan_placement(first_core);
     pid_t pids[MAXR];
     for (int r = 0; r < N; r++) {
         pid_t p = fork();
@@ -369,7 +487,7 @@ int main(int argc, char **argv) {
         if (p == 0) {
             prctl(PR_SET_PDEATHSIG, SIGKILL);
             ME = r;
-            const int core = pin(first_core + r);
+            const int core = pin_cpu(RANK_CPU[r]);
             float *send = (float *)send_of(r);
             float *recvp = malloc(mx);
             memset(send, 0, mx);
@@ -390,6 +508,10 @@ int main(int argc, char **argv) {
                 for (long i = 0; i < count; i++) send[i] = (float)((i % 100) + 1) * (float)(ME + 1);
                 double tsum = 0;
                 int done_it = 0;
+                long thr0 = 0;
+                double thr0_us = 0;
+                if (ME == 0) cgroup_throttled(&thr0, &thr0_us);
+                my_yields = 0;
                 double t_start = now();
                 for (int i = 0; i < iters + skip; i++) {
                     barrier();
@@ -414,19 +536,26 @@ int main(int argc, char **argv) {
                 }
                 C->lat[ME] = tsum / (done_it ? done_it : 1);
                 C->bad[ME] = bad;
+                C->yields[ME] = my_yields; /* this size's loop, before the bookkeeping barrier */
                 barrier();
                 if (ME == 0) {
                     double avg = 0;
                     int anybad = 0;
-                    for (int j = 0; j < N; j++) { avg += C->lat[j]; anybad |= C->bad[j]; }
+                    unsigned long ylds = 0;
+                    for (int j = 0; j < N; j++) { avg += C->lat[j]; anybad |= C->bad[j]; ylds += C->yields[j]; }
                     avg /= N;
+                    long thr1 = 0;
+                    double thr1_us = 0;
+                    cgroup_throttled(&thr1, &thr1_us);
                     double busbw = 2.0 * (N - 1) / N * (double)sz / avg / 1e9;
-                    printf("%-14zu %14.2f %14.3f %10s  (%d iters)\n", sz, avg * 1e6, busbw,
-                           validate ? (anybad ? "FAIL" : "ok") : "-", done_it);
+                    printf("%-14zu %14.2f %14.3f %10s  (%d iters, %lu yields)\n", sz, avg * 1e6, busbw,
+                           validate ? (anybad ? "FAIL" : "ok") : "-", done_it, ylds);
                     fflush(stdout);
                     /* JSON row for bench.py */
-                    printf("JSON {\"bytes\": %zu, \"lat_us\": %.3f, \"busbw_GBps\": %.4f, \"ok\": %s, \"iters\": %d}\n",
-                           sz, avg * 1e6, busbw, (validate && anybad) ? "false" : "true", done_it);
+                    printf("JSON {\"bytes\": %zu, \"lat_us\": %.3f, \"busbw_GBps\": %.4f, \"ok\": %s, \"iters\": %d, "
+                           "\"yields\": %lu, \"throttled\": %ld, \"throttled_us\": %.0f}\n",
+                           sz, avg * 1e6, busbw, (validate && anybad) ? "false" : "true", done_it, ylds,
+                           thr1 - thr0, thr1_us - thr0_us);
                     fflush(stdout);
                 }
                 barrier();
