@@ -88,7 +88,8 @@ def host_allreduce_record(out):
             "busbw_1MiB_GBps": by[1 << 20]["busbw_GBps"], "all_ok": all(r["ok"] for r in rows),
             "cores": hdr["cpus_used"], "cpus_available": hdr["cpus_available"], "cpus_used": hdr["cpus_used"],
             "cores_used": hdr["cores_used"], "oversubscribed": hdr["oversubscribed"], "smt_shared": hdr["smt_shared"],
-            "rank_cpus": hdr["rank_cpus"], "cgroup_cpu_quota": hdr["cgroup_cpu_quota"],
+            "rank_cpus": hdr["rank_cpus"], "rank_cpu_busy_pct_before": hdr.get("rank_cpu_busy_pct"),
+            "placement_policy": hdr.get("placement_policy"), "cgroup_cpu_quota": hdr["cgroup_cpu_quota"],
             "yields_8B": by[8].get("yields"), "throttled_periods_8B": by[8].get("throttled"),
             "yields_all_sizes": sum(r.get("yields", 0) for r in rows),
             "throttled_periods_all_sizes": sum(r.get("throttled", 0) for r in rows),

@@ -36,8 +36,12 @@
  *
  * Placement (a label of "8 ranks pinned 1/core" must be
  * checkable).  Before forking, the parent reads the inherited affinity mask
- * (the job's cpuset), orders its CPUs one hardware thread per physical core
- * first (sysfs core / package ids; SMT siblings only after every core has one
+ * (the job's cpuset), orders its CPUs by how busy each was over a 200 ms sample
+ * of /proc/stat when the mask holds more CPUs than ranks (the GPU boxes hand a
+ * job the whole machine's 256 CPUs under a 16-CPU CFS quota, shared with other
+ * tenants: a rank pinned next to someone else's thread spins in sched_yield;
+ * -S keeps the mask order), then one hardware thread per physical core first
+ * (sysfs core / package ids; SMT siblings only after every core has one
  * rank), and assigns rank r the (p + r)-th CPU of that order.  More ranks than
  * CPUs in the mask is *oversubscription*: ranks then share a CPU and the spin
  * waits degrade into sched_yield hand-offs (the latency-bound sizes collapse),
@@ -49,6 +53,7 @@
  *
  * Usage: host_allreduce [-n ranks] [-m min:max] [-i iters_small] [-I iters_large]
  *                       [-c (validate)] [-T seconds per size cap] [-p first cpu index]
+ *                       [-S (sequential placement: no idleness sample)]
  * Prints an OSU-style table, one "JSONHDR " line and one "JSON " line per size.
  */
 #define _GNU_SOURCE
@@ -389,14 +394,62 @@ static void cgroup_throttled(long *events, double *usec) {
 
 static int RANK_CPU[MAXR];
 
+/* per-CPU busy and total jiffies from /proc/stat (0 when unreadable) */
+static void cpu_jiffies(unsigned long long *busy, unsigned long long *total) {
+    FILE *f = fopen("/proc/stat", "r");
+    if (!f) return;
+    char line[512];
+    while (fgets(line, sizeof line, f)) {
+        int c;
+        unsigned long long v[10] = {0};
+        if (strncmp(line, "cpu", 3) || line[3] < '0' || line[3] > '9') continue;
+        if (sscanf(line + 3, "%d %llu %llu %llu %llu %llu %llu %llu %llu", &c, &v[0], &v[1], &v[2], &v[3], &v[4],
+                   &v[5], &v[6], &v[7]) < 5 || c < 0 || c >= CPU_SETSIZE)
+            continue;
+        unsigned long long t = 0;
+        for (int k = 0; k < 8; k++) t += v[k];
+        total[c] = t;
+        busy[c] = t - v[3] - v[4]; /* minus idle and iowait */
+    }
+    fclose(f);
+}
+
+static double BUSY[CPU_SETSIZE]; /* busy fraction of each CPU over the sampling window, -1 unknown */
+
 /* Plan every rank's CPU from the inherited mask (see the header) and print the
- * JSONHDR row.  Returns the number of distinct CPUs used. */
-static int plan_placement(int first) {
+ * JSONHDR row.  idlest = 1: when the mask holds more CPUs than ranks (a shared
+ * host whose job cpuset is the whole machine, as on the GPU boxes), the CPUs are
+ * ordered by how busy they were over a 200 ms sample of /proc/stat first -- other
+ * tenants' threads on a rank's CPU turn its spin waits into sched_yield
+ * hand-offs -- then one thread per physical core as above.  Returns the number
+ * of distinct CPUs used. */
+static int plan_placement(int first, int idlest) {
     cpu_set_t s;
     int cpus[CPU_SETSIZE], ncpu = 0;
     if (sched_getaffinity(0, sizeof(s), &s) == 0)
         for (int c = 0; c < CPU_SETSIZE; c++)
             if (CPU_ISSET(c, &s)) cpus[ncpu++] = c;
+    for (int c = 0; c < CPU_SETSIZE; c++) BUSY[c] = -1;
+    if (idlest && ncpu > N) {
+        static unsigned long long b0[CPU_SETSIZE], t0[CPU_SETSIZE], b1[CPU_SETSIZE], t1[CPU_SETSIZE];
+        cpu_jiffies(b0, t0);
+        usleep(200000);
+        cpu_jiffies(b1, t1);
+        for (int c = 0; c < CPU_SETSIZE; c++)
+            if (t1[c] > t0[c]) BUSY[c] = (double)(b1[c] - b0[c]) / (double)(t1[c] - t0[c]);
+        /* stable insertion sort by busy fraction (unknown counts as busy) */
+        for (int i = 1; i < ncpu; i++) {
+            int x = cpus[i], j = i - 1;
+            double bx = BUSY[x] < 0 ? 2 : BUSY[x];
+            while (j >= 0 && (BUSY[cpus[j]] < 0 ? 2 : BUSY[cpus[j]]) > bx + 0.05) {
+                cpus[j + 1] = cpus[j];
+                j--;
+            }
+            cpus[j + 1] = x;
+        }
+    } else {
+        idlest = 0;
+    }
     /* one thread per physical core first: round t takes the t-th thread of every core */
     int order[CPU_SETSIZE], no = 0, used[CPU_SETSIZE] = {0};
     long keys[CPU_SETSIZE];
@@ -432,7 +485,13 @@ static int plan_placement(int first) {
            "\"oversubscribed\": %s, \"smt_shared\": %s, \"first_cpu_index\": %d, \"rank_cpus\": [",
            N, ncpu, distinct, dcores, distinct < N ? "true" : "false", dcores < distinct ? "true" : "false", first);
     for (int r = 0; r < N; r++) printf("%s%d", r ? ", " : "", RANK_CPU[r]);
-    printf("], \"cgroup_cpu_quota\": ");
+    printf("], \"rank_cpu_busy_pct\": [");
+    for (int r = 0; r < N; r++) {
+        const double b = RANK_CPU[r] >= 0 ? BUSY[RANK_CPU[r]] : -1;
+        if (b < 0) printf("%snull", r ? ", " : "");
+        else printf("%s%.1f", r ? ", " : "", 100.0 * b);
+    }
+    printf("], \"placement_policy\": \"%s\", \"cgroup_cpu_quota\": ", idlest ? "idlest" : "sequential");
     if (quota > 0) printf("%.3f", quota);
     else printf("null");
     printf("}\n");
@@ -456,11 +515,11 @@ int main(int argc, char **argv) {
     size_t mn = 4, mx = 64u << 20;
     int it_small = 1000, it_large = 100, validate = 0;
     double tcap = 3.0;
-    int first_core = 0;
+    int first_core = 0, idlest = 1;
     int c;
     const char *topo = getenv("MV2_USE_TOPO_AWARE_ALLREDUCE");
     if (topo) TOPO = atoi(topo) != 0;
-    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:")) != -1) {
+    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:S")) != -1) {
         switch (c) {
         case 'n': N = atoi(optarg); break;
         case 'm': sscanf(optarg, "%zu:%zu", &mn, &mx); break;
@@ -469,7 +528,8 @@ int main(int argc, char **argv) {
         case 'c': validate = 1; break;
         case 'T': tcap = atof(optarg); break;
         case 'p': first_core = atoi(optarg); break;
-        default: fprintf(stderr, "usage: %s [-n ranks] [-m min:max] [-i it] [-I it] [-c] [-T s] [-p core0]\n", argv[0]); return 2;
+        case 'S': idlest = 0; break; /* sequential placement: mask order, no idleness sample */
+        default: fprintf(stderr, "usage: %s [-n ranks] [-m min:max] [-i it] [-I it] [-c] [-T s] [-p core0] [-S]\n", argv[0]); return 2;
         }
     }
     if (N < 1 || N > MAXR || mn < 4) return 2;
@@ -479,7 +539,7 @@ int main(int argc, char **argv) {
     SHM_DATA = mmap(NULL, RSTRIDE * N, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (C == MAP_FAILED || SHM_DATA == MAP_FAILED) { perror("mmap"); return 1; }
     memset(C, 0, sizeof(ctrl_t));
-    plan_placement(first_core);
+    plan_placement(first_core, idlest);
     pid_t pids[MAXR];
     for (int r = 0; r < N; r++) {
         pid_t p = fork();
