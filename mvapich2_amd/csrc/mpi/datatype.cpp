@@ -21,6 +21,7 @@
 
 #include "../../../include/mv2h.h"
 #include "../common.h"
+#include "../runtime/world.h"
 
 namespace {
 
@@ -233,35 +234,32 @@ int pack_impl(const char *in, int count, MPI_Datatype dt, char *out, bool unpack
         // mixed: stage the host side on the device so that the layout work runs on the GPU
         const long span = count ? (long)(count - 1) * ext + (d ? d->true_lb + d->true_extent : ext) : 0;
         const long packed = (long)count * size;
+        // device staging from the pool (runtime/world.cpp pool_get): no hipMalloc / hipFree per call
         void *tmp = nullptr;
+        int rc;
         if (!unpack) {
             // pack: src strided, dst packed
             if (!din) {
-                if (mv2h_malloc(&tmp, span)) return MPI_ERR_NO_MEM;
+                if (!(tmp = mv2::pool_get(span))) return MPI_ERR_NO_MEM;
                 mv2h_memcpy_htod(tmp, in, span);
-                int rc = pack_impl((const char *)tmp, count, dt, out, false);
-                mv2h_free(tmp);
-                return rc;
+                rc = pack_impl((const char *)tmp, count, dt, out, false);
+            } else {
+                if (!(tmp = mv2::pool_get(packed))) return MPI_ERR_NO_MEM;
+                rc = pack_impl(in, count, dt, (char *)tmp, false);
+                if (!rc) mv2h_memcpy_dtoh(out, tmp, packed);
             }
-            if (mv2h_malloc(&tmp, packed)) return MPI_ERR_NO_MEM;
-            int rc = pack_impl(in, count, dt, (char *)tmp, false);
-            if (!rc) mv2h_memcpy_dtoh(out, tmp, packed);
-            mv2h_free(tmp);
-            return rc;
-        }
-        if (!din) {
-            if (mv2h_malloc(&tmp, packed)) return MPI_ERR_NO_MEM;
+        } else if (!din) {
+            if (!(tmp = mv2::pool_get(packed))) return MPI_ERR_NO_MEM;
             mv2h_memcpy_htod(tmp, in, packed);
-            int rc = pack_impl((const char *)tmp, count, dt, out, true);
-            mv2h_free(tmp);
-            return rc;
+            rc = pack_impl((const char *)tmp, count, dt, out, true);
+        } else {
+            // unpack into a host destination: copy its current bytes so gaps survive
+            if (!(tmp = mv2::pool_get(span))) return MPI_ERR_NO_MEM;
+            mv2h_memcpy_htod(tmp, out, span);
+            rc = pack_impl(in, count, dt, (char *)tmp, true);
+            if (!rc) mv2h_memcpy_dtoh(out, tmp, span);
         }
-        // unpack into a host destination: copy its current bytes so gaps survive
-        if (mv2h_malloc(&tmp, span)) return MPI_ERR_NO_MEM;
-        mv2h_memcpy_htod(tmp, out, span);
-        int rc = pack_impl(in, count, dt, (char *)tmp, true);
-        if (!rc) mv2h_memcpy_dtoh(out, tmp, span);
-        mv2h_free(tmp);
+        mv2::pool_put(tmp);
         return rc;
     }
     // device <-> device

@@ -622,10 +622,9 @@ static int allgather_derived(const void *sendbuf, int sendcount, MPI_Datatype se
     if (sendbuf != MPI_IN_PLACE && dtype_size(sendtype) * sendcount != psize) return MPI_ERR_TRUNCATE;
     if (psize == 0) return MPI_SUCCESS;
     const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size(), me = comm == MPI_COMM_SELF ? 0 : mv2h_rank();
-    void *mine = nullptr, *all = nullptr;
-    if (mv2h_malloc(&mine, (size_t)psize)) return MPI_ERR_NO_MEM;
-    if (mv2h_malloc(&all, (size_t)psize * n)) {
-        mv2h_free(mine);
+    void *mine = pool_get((size_t)psize), *all = mine ? pool_get((size_t)psize * n) : nullptr;
+    if (!all) {
+        if (mine) pool_put(mine);
         return MPI_ERR_NO_MEM;
     }
     int pos = 0, rc;
@@ -637,8 +636,8 @@ static int allgather_derived(const void *sendbuf, int sendcount, MPI_Datatype se
     if (!rc) rc = n > 1 ? mv2h_allgather(mine, all, (size_t)psize, nullptr) : mv2h_memcpy_dtod(all, mine, (size_t)psize);
     pos = 0;
     if (!rc) rc = PMPI_Unpack(all, (int)(psize * n), &pos, recvbuf, recvcount * n, recvtype, comm);
-    mv2h_free(mine);
-    mv2h_free(all);
+    pool_put(mine);
+    pool_put(all);
     return rc;
 }
 
@@ -681,14 +680,14 @@ int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm
     // packed bytes, unpack on device everywhere else
     int psize = 0;
     PMPI_Pack_size(count, dt, comm, &psize);
-    void *packed = nullptr;
-    if (mv2h_malloc(&packed, (size_t)psize)) return err_return(comm, MPI_ERR_NO_MEM, fn);
+    void *packed = pool_get((size_t)psize);
+    if (!packed) return err_return(comm, MPI_ERR_NO_MEM, fn);
     int pos = 0, rc = MPI_SUCCESS;
     if (mv2h_rank() == root) rc = PMPI_Pack(buffer, count, dt, packed, psize, &pos, comm);
     if (!rc) rc = mv2h_bcast(packed, (size_t)psize, root, nullptr);
     pos = 0;
     if (!rc && mv2h_rank() != root) rc = PMPI_Unpack(packed, psize, &pos, buffer, count, dt, comm);
-    mv2h_free(packed);
+    pool_put(packed);
     return err_return(comm, rc, fn);
 }
 int MPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm) WEAK(MPI_Bcast);
@@ -867,7 +866,7 @@ void status_set(MPI_Status *st, int src, int tag, size_t bytes, int err) {
 
 void tmp_free(MReq &r) {
     if (!r.tmp) return;
-    if (r.tmp_dev) mv2h_free(r.tmp);
+    if (r.tmp_dev) pool_put(r.tmp);
     else free(r.tmp);
     r.tmp = nullptr;
 }
@@ -954,7 +953,7 @@ int isend_impl(const void *buf, int count, MPI_Datatype dt, int dest, int tag, M
         PMPI_Pack_size(count, dt, MPI_COMM_WORLD, &psize);
         r.tmp_dev = is_dev(buf);
         if (r.tmp_dev) {
-            if (mv2h_malloc(&r.tmp, (size_t)psize)) return MPI_ERR_NO_MEM;
+            if (!(r.tmp = pool_get((size_t)psize))) return MPI_ERR_NO_MEM;
         } else if (!(r.tmp = malloc((size_t)psize + 1))) {
             return MPI_ERR_NO_MEM;
         }
@@ -993,7 +992,7 @@ int irecv_impl(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_R
         PMPI_Pack_size(count, dt, MPI_COMM_WORLD, &psize);
         r.tmp_dev = is_dev(buf);
         if (r.tmp_dev) {
-            if (mv2h_malloc(&r.tmp, (size_t)psize)) return MPI_ERR_NO_MEM;
+            if (!(r.tmp = pool_get((size_t)psize))) return MPI_ERR_NO_MEM;
         } else if (!(r.tmp = malloc((size_t)psize + 1))) {
             return MPI_ERR_NO_MEM;
         }

@@ -82,9 +82,12 @@ char *dev_scratch(int slot, size_t bytes) {
     static size_t cap[DS_COUNT];
     if (bytes == 0) bytes = 1;
     if (bytes > cap[slot]) {
-        if (p[slot]) mv2h_free(p[slot]);
+        // an abandoned collective receive may still be arriving into the old block (DS_ALL /
+        // DS_RES_ALL are receive areas): then it is left allocated rather than freed under it
+        if (p[slot] && !coll_context_poisoned()) mv2h_free(p[slot]);
         p[slot] = nullptr;
         cap[slot] = 0;
+        ++world().call_allocs;
         if (mv2h_malloc(&p[slot], bytes)) return (char *)(p[slot] = nullptr);
         cap[slot] = bytes;
     }

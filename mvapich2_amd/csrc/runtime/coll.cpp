@@ -273,7 +273,10 @@ static hipError_t enq_copy_last(void *dst, const void *src, size_t bytes, hipStr
         const Done d = arm_done(st);
         if (d.flag) {
             beacon(BC_COPY_OUT);
-            return launch_pack_strided(src, dst, 1, bytes, bytes, 0, st, d) == 0 ? hipSuccess : hipErrorLaunchFailure;
+            if (launch_pack_strided(src, dst, 1, bytes, bytes, 0, st, d) == 0) return hipSuccess;
+            world().pending = 0;  // no kernel will raise the word: finish() must not wait for it
+            MV2_ERR("launching the result copy-out failed: %s", hipGetErrorString(hipGetLastError()));
+            return hipErrorLaunchFailure;
         }
     }
     return enq_copy(dst, src, bytes, st);
@@ -1153,8 +1156,11 @@ static int stage_in(const void *send, void *recv, size_t sbytes, size_t rbytes, 
     return 0;
 }
 
-static void stage_out(const Staged &s, hipStream_t st) {
-    if (s.copy_back) enq_copy_last(s.user_recv, s.recv, s.bytes, st);
+// the staged result copied back to the caller's buffer; E_INTERN when the copy cannot be
+// enqueued (the call must then fail rather than return with the result never delivered)
+static int stage_out(const Staged &s, hipStream_t st) {
+    if (s.copy_back && enq_copy_last(s.user_recv, s.recv, s.bytes, st) != hipSuccess) return E_INTERN;
+    return 0;
 }
 
 // One allreduce over `count` elements in the order `tp` (ring = true: the flat
@@ -1170,14 +1176,14 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     const int n = w.size;
     if (n == 1 || oi == OP_NO_OP) {
         if (!in_place && oi != OP_NO_OP) hipMemcpyAsync(s.recv, s.send, bytes, hipMemcpyDeviceToDevice, st);
-        stage_out(s, st);
+        if ((rc = stage_out(s, st))) return rc;
         return finish(st, false);
     }
     if (oi == OP_REPLACE) {
         // result of REPLACE over ranks 0..n-1 in rank order: rank n-1's data; take the two-level
         // linear chain semantics: recv = x_{n-1} everywhere.  Realised as a broadcast from n-1.
         if (!in_place) hipMemcpyAsync(s.recv, s.send, bytes, hipMemcpyDeviceToDevice, st);
-        stage_out(s, st);
+        if ((rc = stage_out(s, st))) return rc;
         rc = finish(st, false);
         if (rc) return rc;
         return mv2h_bcast(recvbuf, bytes, n - 1, nullptr);
@@ -1207,7 +1213,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         rc = launch_oneshot(oi, dt->kind, a, dt->extent, cfg);
         tmark1(st);
         if (rc) return rc;
-        stage_out(s, st);
+        if ((rc = stage_out(s, st))) return rc;
         return finish(st, w.timing);
     }
     // pipelined direct reduce-scatter + all-gather, pushed through the arenas
@@ -1244,7 +1250,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
             if (hipMemcpy2DAsync(s.recv, cb, pr, pcb, cb, n, hipMemcpyDeviceToDevice, st) != hipSuccess)
                 return E_INTERN;
             world().pending = 0;
-            stage_out(s, st);
+            if ((rc = stage_out(s, st))) return rc;
             return finish(st, w.timing);
         }
     } else {
@@ -1252,7 +1258,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
     }
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
-    stage_out(s, st);
+    if ((rc = stage_out(s, st))) return rc;
     return finish(st, w.timing);
 }
 
@@ -1392,7 +1398,7 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
     a.tp = tp;
     even_segments(a, bytes, w.size);
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
-    if (is_root) stage_out(s, st);
+    if (is_root && (rc = stage_out(s, st))) return rc;
     return finish(st, w.timing);
 }
 int mv2h_reduce(const void *sendbuf, void *recvbuf, size_t count, int dtype, int op, int root, void *stream) {
@@ -1487,7 +1493,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
         rc = launch_oneshot(oi, dt->kind, o, dt->extent, cfg);
         tmark1(st);
         if (rc) return rc;
-        if (!direct && mycnt) enq_copy_last(recvbuf, dst, mycnt * ext, st);
+        if (!direct && mycnt && enq_copy_last(recvbuf, dst, mycnt * ext, st) != hipSuccess) return E_INTERN;
         return finish(st, w.timing);
     }
     PipeArgs a{};
@@ -1548,7 +1554,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     }
     a.tp = tp;
     if ((rc = run_pipe(a, oi, dt, st))) return rc;
-    if (!direct && mycnt) enq_copy_last(recvbuf, dst, mycnt * ext, st);
+    if (!direct && mycnt && enq_copy_last(recvbuf, dst, mycnt * ext, st) != hipSuccess) return E_INTERN;
     return finish(st, w.timing);
 }
 int mv2h_reduce_scatter(const void *sendbuf, void *recvbuf, const size_t *recvcounts, int dtype, int op,
@@ -1638,7 +1644,7 @@ static int bcast_node(void *buffer, size_t bytes, int root, void *stream) {
     a.esize = 1;
     even_segments(a, bytes, w.size);
     if ((rc = run_pipe(a, 0, nullptr, st))) return rc;
-    if (!direct && w.rank != root) enq_copy_last(buffer, buf, bytes, st);
+    if (!direct && w.rank != root && enq_copy_last(buffer, buf, bytes, st) != hipSuccess) return E_INTERN;
     return finish(st, w.timing);
 }
 

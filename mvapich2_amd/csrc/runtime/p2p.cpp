@@ -511,6 +511,8 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
     return progress(&moved);
 }
 
+bool mv2::coll_context_poisoned() { return g_coll_poisoned; }
+
 void mv2::p2p_abandon(unsigned long long id) {
     auto it = g_reqs.find(id);
     if (it == g_reqs.end()) return;

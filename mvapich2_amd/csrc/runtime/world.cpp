@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <thread>
+#include <vector>
 
 #include "log.h"
 #include "orders.h"
@@ -261,15 +262,101 @@ void *get_scratch(int idx, size_t bytes) {
     if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];
     beacon(BC_SCRATCH);
     if (w.scratch[idx]) {
-        hipStreamSynchronize(w.stream);
-        hipFree(w.scratch[idx]);
+        // a collective abandoned with a receive still arriving may target this block: it is left
+        // allocated (never reused) rather than freed under the transport (runtime/p2p.cpp)
+        if (!coll_context_poisoned()) {
+            hipStreamSynchronize(w.stream);
+            hipFree(w.scratch[idx]);
+        }
         w.scratch[idx] = nullptr;
         w.scratch_bytes[idx] = 0;
     }
     size_t sz = bytes < 4096 ? 4096 : bytes;
+    ++w.call_allocs;
     if (hipMalloc(&w.scratch[idx], sz) != hipSuccess) return nullptr;
     w.scratch_bytes[idx] = sz;
     return w.scratch[idx];
+}
+
+// ---------------------------------------------------------------------------
+// Device temporaries of MPI calls: derived-type staging (MPI_Bcast / MPI_Allgather of a
+// non-contiguous type, MPI_Pack / MPI_Unpack between host and device memory) and the packed
+// payload of a non-contiguous MPI_Isend / MPI_Irecv, which lives until the request completes, so
+// several can be held at once.  Blocks are kept for reuse instead of a hipMalloc / hipFree per
+// call (hipFree synchronises the whole device, serialising the call against every stream); the
+// reference keeps its device staging the same way (device_stage_alloc, ch3_shmem_coll.c:3433).
+// Sizes round up to a power of two (>= 64 KiB) so that nearby sizes share blocks; a failed
+// allocation first returns the idle blocks to HIP and tries once more.
+// ---------------------------------------------------------------------------
+namespace {
+struct PoolBlock {
+    void *p;
+    size_t cap;
+    bool used;
+};
+std::vector<PoolBlock> g_pool;
+}  // namespace
+
+// MV2AMD_POOL=0: a hipMalloc per pool_get and a hipFree per pool_put (round 4's behaviour, kept
+// as a knob for the before / after measurement)
+static bool pool_on() {
+    static const bool on = env_long("MV2AMD_POOL", 1) != 0;
+    return on;
+}
+
+void *pool_get(size_t bytes) {
+    World &w = g_world;
+    if (!pool_on()) {
+        void *p = nullptr;
+        ++w.call_allocs;
+        return hipMalloc(&p, bytes ? bytes : 1) == hipSuccess ? p : nullptr;
+    }
+    PoolBlock *best = nullptr;
+    for (PoolBlock &b : g_pool)
+        if (!b.used && b.cap >= bytes && (!best || b.cap < best->cap)) best = &b;
+    if (best) {
+        best->used = true;
+        return best->p;
+    }
+    size_t cap = (size_t)64 << 10;
+    while (cap < bytes) cap <<= 1;
+    beacon(BC_SCRATCH);
+    ++w.call_allocs;
+    void *p = nullptr;
+    if (hipMalloc(&p, cap) != hipSuccess) {
+        (void)hipGetLastError();
+        if (w.stream) hipStreamSynchronize(w.stream);
+        for (size_t i = 0; i < g_pool.size();)
+            if (!g_pool[i].used) {
+                hipFree(g_pool[i].p);
+                g_pool.erase(g_pool.begin() + (long)i);
+            } else {
+                ++i;
+            }
+        if (hipMalloc(&p, cap) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    }
+    g_pool.push_back(PoolBlock{p, cap, true});
+    return p;
+}
+
+void pool_put(void *p) {
+    if (!pool_on()) {
+        if (p) hipFree(p);
+        return;
+    }
+    for (PoolBlock &b : g_pool)
+        if (b.p == p) {
+            b.used = false;
+            return;
+        }
+}
+
+static void pool_release_all() {
+    for (PoolBlock &b : g_pool) hipFree(b.p);
+    g_pool.clear();
 }
 
 // GPUs this process can see, counted without initialising HIP: the KFD topology's GPU nodes,
@@ -875,6 +962,7 @@ int world_finalize() {
     }
     for (int i = 0; i < (int)(sizeof(w.scratch) / sizeof(w.scratch[0])); ++i)
         if (w.scratch[i]) hipFree(w.scratch[i]);
+    pool_release_all();
     if (w.sig) hipFree(w.sig);
     if (w.arena) hipFree(w.arena);
     if (w.pipe_rs) hipFree(w.pipe_rs);

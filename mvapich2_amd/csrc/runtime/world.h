@@ -225,6 +225,10 @@ const char *beacon_name(int phase);
 int global_barrier();  // node barrier, leaders' barrier across nodes, node barrier
 int ensure_init_for_device();  // singleton-safe lazy device setup (for Reduce_local before Init)
 void *get_scratch(int idx, size_t bytes);
+// device temporaries of MPI calls, kept for reuse (world.cpp): a block of >= bytes, or nullptr
+void *pool_get(size_t bytes);
+void pool_put(void *p);  // back to the pool (the device work using it has completed)
+bool coll_context_poisoned();  // runtime/p2p.cpp: an abandoned collective request is still in flight
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
 void pipe_tiling_for(size_t seg_bytes, int *grid, size_t *tsub);  // coll.cpp: a segment's grid and bytes per round
 int pipe_autotune();  // coll.cpp: init-time choice of the pipelined kernels' tiling

@@ -5,6 +5,7 @@ import ctypes
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -268,6 +269,70 @@ P = ctypes.c_void_p  # the plugin entries have no ctypes prototypes: pass pointe
 _COMM = ctypes.c_void_p(0xC0FFEE0)  # stands for MVAPICH2's MPID_Comm * (opaque to the plugin)
 
 
+def derived_no_alloc(L, case, rank, n):
+    """Derived-type MPI_Bcast, MPI_Allgather and non-contiguous MPI_Isend / MPI_Irecv on device
+    buffers: every result checked against its closed form; returns [wrong results, device
+    allocations inside the calls after the warm-up round (mv2h_get_info "call_allocs"), the
+    OSU-style mean latency of the derived MPI_Bcast in us]."""
+    F = TYPES["MPI_FLOAT"][0]
+    nb = case["nblocks"]  # MPI_Type_vector(nb, 4, 8, MPI_FLOAT): 16 * nb packed bytes
+    vt = ctypes.c_int()
+    assert L.MPI_Type_vector(nb, 4, 8, F, ctypes.byref(vt)) == 0
+    assert L.MPI_Type_commit(ctypes.byref(vt)) == 0
+    span = nb * 8
+    onmap = (np.arange(span) % 8) < 4
+    pat = lambda r: (np.arange(span, dtype=np.int64) * 3 + 101 * r).astype(np.float32)  # noqa: E731
+    bb, ag = m.DeviceBuffer(span * 4), m.DeviceBuffer(span * 4 * n)
+    sb, rb = m.DeviceBuffer.from_array(pat(rank)), m.DeviceBuffer(span * 4)
+    bad = 0
+
+    def one_round(check):
+        nonlocal bad
+        bb.upload(pat(0) if rank == 0 else np.full(span, -1, dtype=np.float32))
+        assert L.MPI_Bcast(bb.ptr, 1, vt.value, 0, WORLD) == 0
+        ag.upload(np.full(span * n, -2, dtype=np.float32))
+        assert L.MPI_Allgather(sb.ptr, 1, vt.value, ag.ptr, 1, vt.value, WORLD) == 0
+        rb.upload(np.full(span, -3, dtype=np.float32))
+        rq = (ctypes.c_int * 2)()
+        q = ctypes.c_int()
+        assert L.MPI_Irecv(rb.ptr, 1, vt.value, (rank - 1) % n, 9, WORLD, ctypes.byref(q)) == 0
+        rq[0] = q.value
+        assert L.MPI_Isend(sb.ptr, 1, vt.value, (rank + 1) % n, 9, WORLD, ctypes.byref(q)) == 0
+        rq[1] = q.value
+        assert L.MPI_Waitall(2, rq, None) == 0
+        if check:
+            b = bb.download(np.float32, count=span)
+            want = np.where(onmap, pat(0), np.float32(-1) if rank else pat(0))
+            bad += int(not np.array_equal(b, want))
+            # block r of the receive buffer starts r extents in (extent = span - 4 floats)
+            ext = span - 4
+            want = np.full(span * n, -2, dtype=np.float32)
+            for r in range(n):
+                want[r * ext:(r + 1) * ext] = np.where(onmap[:ext], pat(r)[:ext], np.float32(-2))
+            bad += int(not np.array_equal(ag.download(np.float32, count=span * n), want))
+            g = rb.download(np.float32, count=span)
+            bad += int(not np.array_equal(g, np.where(onmap, pat((rank - 1) % n), np.float32(-3))))
+
+    one_round(True)  # warm-up: grows the pooled device temporaries once
+    a0 = m.info("call_allocs")
+    for _ in range(case.get("rounds", 10)):
+        one_round(True)
+    allocs = m.info("call_allocs") - a0
+    # osu_bcast.c pattern: barrier, then per iteration t0 / MPI_Bcast / t1 / barrier; mean over ranks
+    iters = case.get("lat_iters", 200)
+    for _ in range(20):
+        L.MPI_Bcast(bb.ptr, 1, vt.value, 0, WORLD)
+    L.MPI_Barrier(WORLD)
+    tot = 0.0
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        L.MPI_Bcast(bb.ptr, 1, vt.value, 0, WORLD)
+        tot += time.perf_counter() - t0
+        L.MPI_Barrier(WORLD)
+    assert L.MPI_Type_free(ctypes.byref(vt)) == 0
+    return np.array([bad, allocs, tot / iters * 1e6], dtype=np.float64)
+
+
 def collops_comm(L, rank, n):
     assert L.MV2AMD_Comm_attach(_COMM, rank, n) == 0
     return _COMM
@@ -519,6 +584,8 @@ def main():
             L.MPI_Type_free(ctypes.byref(vt))
         elif k.startswith("big_") or k in ("huge", "gib_allreduce"):
             res = big_case(L, case, rank, n)
+        elif k == "derived_no_alloc":
+            res = derived_no_alloc(L, case, rank, n)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)
             vt = ctypes.c_int()

@@ -821,3 +821,31 @@ def test_gpu_topology_levels(n, topo, tmp_path):
                 assert_bytes_equal(res(case["id"], n - 1), want, case["type"], case["count"], f"{case['id']} {topo}")
     finally:
         oracle.set_topology([], n)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_derived_type_calls_make_no_device_allocations(n, tmp_path):
+    """Derived-type MPI_Bcast / MPI_Allgather and non-contiguous MPI_Isend / MPI_Irecv stage
+    through pooled device temporaries (runtime/world.cpp pool_get): after one warm-up round, ten
+    more rounds make no hipMalloc inside the calls (mv2h_get_info "call_allocs" stays flat), with
+    every result right.  MV2AMD_POOL=0 (a hipMalloc / hipFree per call, round 4's behaviour)
+    allocates on every round; the OSU-style latency of the 64 KiB derived MPI_Bcast is recorded
+    for both (MV2AMD_TEST_RECORD: a JSON file the numbers are appended to)."""
+    lat = {}
+    for pool in ("1", "0"):
+        case = {"id": f"dna{pool}", "kind": "derived_no_alloc", "nblocks": 4096, "rounds": 10, "lat_iters": 200}
+        (tmp_path / f"p{pool}").mkdir()
+        res = run_workers(n, [case], tmp_path / f"p{pool}", extra_env={"MV2AMD_POOL": pool})
+        got = [res(case["id"], r) for r in range(n)]
+        for r in range(n):
+            assert got[r][0] == 0, f"rank {r}: wrong results with MV2AMD_POOL={pool}"
+            if pool == "1":
+                assert got[r][1] == 0, f"rank {r}: {got[r][1]} device allocations inside warm calls"
+            else:
+                assert got[r][1] > 0
+        lat[f"pool={pool}"] = round(float(np.mean([g[2] for g in got])), 2)
+    rec = os.environ.get("MV2AMD_TEST_RECORD")
+    if rec:
+        with open(rec, "a") as f:
+            f.write(json.dumps({"test": "derived MPI_Bcast 64 KiB (MPI_Type_vector(4096,4,8,MPI_FLOAT)) OSU latency us",
+                                "ranks": n, **lat}) + "\n")
