@@ -338,10 +338,37 @@ def rccl_child():
     tt = torch.tensor([t], dtype=torch.float64, device=dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     t = float(tt.item())
+    del x
+    # the same sizes as the library's OSU sweep (8 B .. 1 GiB, x4), timed as osu_nccl_allreduce.c:
+    # per iteration t_start, ncclAllReduce, stream synchronise, t_stop, barrier; mean over ranks
+    sweep = []
+    if os.environ.get("MV2AMD_RCCL_SWEEP", "1") != "0":
+        big = torch.empty(SWEEP_MAX // 4, dtype=torch.float32, device=dev)
+        nb = 8
+        while nb <= SWEEP_MAX:
+            v = big[:max(1, nb // 4)]
+            large = nb > 8192 * 4
+            iters, skip = (20, 5) if large else (200, 20)
+            tot = 0.0
+            for i in range(iters + skip):
+                t0 = time.perf_counter()
+                dist.all_reduce(v)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                if i >= skip:
+                    tot += t1 - t0
+                dist.barrier()
+            lt = torch.tensor([tot / iters], dtype=torch.float64, device=dev)
+            dist.all_reduce(lt)
+            lat = float(lt.item()) / size
+            sweep.append([nb, round(lat * 1e6, 2), round(2.0 * (size - 1) / size * nb / lat / 1e9, 3)])
+            nb *= 4
+        del big
     dist.destroy_process_group()
     if rank == 0:
         print(json.dumps({"busbw_GBps": round(2.0 * (size - 1) / size * S_BYTES / t / 1e9, 2), "ms": round(t * 1e3, 4),
-                          "what": "torch.distributed all_reduce (RCCL) fp32 SUM 256 MiB, comparator only"}), flush=True)
+                          "what": "torch.distributed all_reduce (RCCL) fp32 SUM 256 MiB, comparator only",
+                          "sweep_columns": ["bytes", "lat_us", "busbw_GBps"], "sweep": sweep}), flush=True)
 
 
 def rccl_comparator(L, world, rank, size, steps, timeout=150):
@@ -373,6 +400,50 @@ def rccl_comparator(L, world, rank, size, steps, timeout=150):
         except Exception:
             return {"error": "no comparator line"}
     return None
+
+
+SWEEP_MAX = 1 << 30        # configs[2]: osu_allreduce 8 B .. 1 GiB
+SWEEP_CAP = 256 << 20      # configs[3]: reduce_scatter / allgather / bcast up to 256 MiB
+
+
+def osu_sweep(L, world, rank, size, timeout=300):
+    """configs[2] and [3] as OSU sweeps in the same run: every rank starts one child job of
+    tools/osu/osu_coll (the OSU loop restated in C against include/mpi.h and linked with
+    libmpi.so, osu_allreduce.c:98-163) with -c all: allreduce 8 B .. 1 GiB and reduce_scatter /
+    allgather / bcast 8 B .. 256 MiB, sizes x4, every result validated against its closed form.
+    The child is its own MPI job (own control segment and arenas, MV2AMD_JOBID agreed through an
+    MPI_Bcast); rank 0 returns its rows."""
+    exe = os.path.join(ROOT, "tools", "osu", "osu_coll")
+    if not os.path.exists(exe):
+        return {"error": "tools/osu/osu_coll not built"}
+    key = np.zeros(1, dtype=np.int64)
+    if rank == 0:
+        key[0] = int.from_bytes(os.urandom(6), "little")
+    m.check(L.MPI_Bcast(key.ctypes.data, 8, TYPES["MPI_BYTE"][0], 0, world), "MPI_Bcast(job key)")
+    env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(size), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(size),
+               MV2AMD_JOBID=f"sweep{int(key[0])}", MV2AMD_INIT_REPORT="0")
+    cmd = [exe, "-c", "all", "-m", f"8:{SWEEP_MAX}", "-f", "4", "-C", str(SWEEP_CAP), "-i", "200", "-I", "20",
+           "-v", "-j"]
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return {"error": f"osu sweep timed out after {timeout} s"}
+    if p.returncode != 0:
+        return {"error": ((err or "").strip().splitlines() or ["no output"])[-1][-300:], "returncode": p.returncode}
+    if rank != 0:
+        return None
+    rows = [json.loads(l[5:]) for l in out.splitlines() if l.startswith("JSON ")]
+    res = {"what": "tools/osu/osu_coll -c all (OSU loop in C through libmpi.so, device buffers, every size "
+                   "validated): allreduce 8 B..1 GiB, reduce_scatter / allgather / bcast 8 B..256 MiB, x4 sizes",
+           "columns": ["bytes", "lat_us", "busbw_GBps", "valid"], "seconds": round(time.perf_counter() - t0, 1),
+           "all_valid": all(r["valid"] is True for r in rows)}
+    for c in ("allreduce", "reduce_scatter", "allgather", "bcast"):
+        res[c] = [[r["bytes"], r["lat_us"], r["busbw_GBps"], r["valid"]] for r in rows if r["coll"] == c]
+    return res
 
 
 def user_op_lines(L, world, sb, rb, size):
@@ -609,6 +680,12 @@ def bench_nranks(args, L, rank, size):
               "oneshot_vs_pipe_us": [{"bytes": (32 << 10) << i, "oneshot": m.info(f"os_tune_one_{i}"),
                                       "pipe": m.info(f"os_tune_pipe_{i}")} for i in range(m.info("os_tune_n"))]}
     del sb, rb, rsb
+    sweep = None
+    if args.sweep:
+        try:
+            sweep = osu_sweep(L, world, rank, size)
+        except Exception as e:  # a sweep problem never loses the headline line
+            sweep = {"error": f"{type(e).__name__}: {e}"[:200]}
     if args.rccl and m.info("nshare") > 1:
         rccl = {"skipped": "ranks share one GPU: RCCL refuses several ranks on one device"}
     elif args.rccl:
@@ -618,8 +695,17 @@ def bench_nranks(args, L, rank, size):
             rccl = {"error": f"{type(e).__name__}: {e}"[:200]}
     else:
         rccl = None
-    return assemble_nranks_line(size, nshare, args.steps, args.warmup, t, lat_avg, uops["lines"], nrec, pbytes * win,
+    line = assemble_nranks_line(size, nshare, args.steps, args.warmup, t, lat_avg, uops["lines"], nrec, pbytes * win,
                                 tiling, traffic, rccl)
+    if sweep is not None:
+        line["extra"]["osu_sweep"] = sweep
+        rs = {r[0]: r[2] for r in (rccl or {}).get("sweep", [])}
+        if rs and isinstance(sweep.get("allreduce"), list):
+            line["extra"]["allreduce_busbw_vs_rccl_by_size"] = {
+                "columns": ["bytes", "ours_GBps", "rccl_GBps", "ours_over_rccl"],
+                "rows": [[b, bw, rs[b], round(bw / rs[b], 3) if rs[b] else None]
+                         for b, _, bw, _ in sweep["allreduce"] if b in rs]}
+    return line
 
 
 def pipe_alg_bytes(size):
@@ -704,6 +790,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--lat-iters", type=int, default=1000)
     ap.add_argument("--rccl", type=int, default=1, help="N > 1: also time RCCL all_reduce as a comparator")
+    ap.add_argument("--sweep", type=int, default=1, help="N > 1: OSU sweeps of configs[2] / [3] (tools/osu/osu_coll)")
     ap.add_argument("--rccl-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.rccl_child:

@@ -6,8 +6,12 @@
  * report the average over ranks of per-rank mean latency), with `-d rocm`
  * device buffers and busbw columns added (OMB prints latency only).
  *
- *   osu_coll -c allreduce|reduce|reduce_scatter|allgather|bcast|reduce_local|latency|bw
- *            [-m min:max bytes] [-i iters] [-x warmup] [-d rocm|host] [-v]
+ *   osu_coll -c allreduce|reduce|reduce_scatter|allgather|bcast|reduce_local|latency|bw|all
+ *            [-m min:max bytes] [-f size factor (2)] [-i iters] [-I large-message iters]
+ *            [-x warmup] [-C cap bytes for -c all's reduce_scatter/allgather/bcast]
+ *            [-d rocm|host] [-v (validate every collective)] [-j (JSON rows)]
+ * -c all runs allreduce over [min, max] and reduce_scatter, allgather, bcast over
+ * [min, min(max, cap)] in one job (bench.py's N > 1 sweep: configs[2] and [3]).
  */
 #include <hip/hip_runtime.h>
 #include <mpi.h>
@@ -16,9 +20,9 @@
 #include <string.h>
 
 static const char *coll = "allreduce";
-static size_t min_sz = 8, max_sz = 1 << 20;
+static size_t min_sz = 8, max_sz = 1 << 20, cap_sz = (size_t)256 << 20, factor = 2;
 static int iters_small = 1000, iters_large = 100, skip_small = 100, skip_large = 10;
-static int device = 1, validate = 0;
+static int device = 1, validate = 0, json = 0;
 
 static void *alloc_buf(size_t bytes) {
     void *p = NULL;
@@ -81,6 +85,103 @@ static int run_pt2pt(int rank, void *sbuf, void *rbuf) {
     return 0;
 }
 
+/* result check of one collective (-v): every element against its closed form for the OMB fill
+ * (i % 100 + 1) * (rank + 1); returns 1 when right */
+static int check(const char *c, const void *rbuf, size_t count, size_t sz, int rank, int size, const int *counts) {
+    if (!strcmp(c, "reduce") || !strcmp(c, "reduce_local")) return 1;
+    size_t n = !strcmp(c, "allgather") ? sz * (size_t)size : !strcmp(c, "bcast") ? sz : count * sizeof(float);
+    if (!strcmp(c, "reduce_scatter")) n = (size_t)counts[rank] * sizeof(float);
+    char *h = (char *)malloc(n ? n : 1);
+    if (device) hipMemcpy(h, !strcmp(c, "bcast") ? rbuf : rbuf, n, hipMemcpyDeviceToHost);
+    else memcpy(h, rbuf, n);
+    int ok = 1;
+    const float tot = (float)(size * (size + 1) / 2);
+    if (!strcmp(c, "allreduce")) {
+        const float *f = (const float *)h;
+        for (size_t i = 0; i < count && ok; ++i) ok = f[i] == (float)(i % 100 + 1) * tot;
+    } else if (!strcmp(c, "reduce_scatter")) {
+        size_t off = 0;
+        for (int r = 0; r < rank; ++r) off += (size_t)counts[r];
+        const float *f = (const float *)h;
+        for (size_t i = 0; i < (size_t)counts[rank] && ok; ++i) ok = f[i] == (float)((off + i) % 100 + 1) * tot;
+    } else {
+        /* allgather: block j = rank j's first sz bytes of its fill; bcast: rank 0's (bytes of floats) */
+        float *want = (float *)malloc((sz / 4 + 1) * sizeof(float));
+        for (int j = 0; j < (!strcmp(c, "allgather") ? size : 1) && ok; ++j) {
+            for (size_t i = 0; i < sz / 4 + 1; ++i) want[i] = (float)((i % 100 + 1) * (j + 1));
+            ok = memcmp(h + (size_t)j * sz, want, sz) == 0;
+        }
+        free(want);
+    }
+    free(h);
+    return ok;
+}
+
+static int run_coll(const char *c, int rank, int size, void *sbuf, void *rbuf, size_t lo, size_t hi) {
+    if (rank == 0 && !json) {
+        printf("# mvapich2_amd osu_coll -c %s, %d ranks, %s buffers\n", c, size, device ? "ROCm device" : "host");
+        printf("%-12s %14s %14s %14s %12s\n", "# Size(B)", "Avg Lat(us)", "algbw(GB/s)", "busbw(GB/s)", "valid");
+    }
+    int *counts = (int *)malloc(sizeof(int) * size);
+    int bad_any = 0;
+    for (size_t sz = lo; sz <= hi; sz *= factor) {
+        const size_t count = sz / sizeof(float) ? sz / sizeof(float) : 1;
+        const int large = count > 8192; /* osu_allreduce.c:101 */
+        const int iters = large ? iters_large : iters_small, skip = large ? skip_large : skip_small;
+        /* the fill covers what allgather / bcast send (sz bytes) and the reducing operands */
+        fill(sbuf, (sz + 3) / 4 > count ? (sz + 3) / 4 : count, rank);
+        if (!strcmp(c, "bcast") && rank != 0) {
+            if (device) hipMemset(sbuf, 0xA5, sz);
+            else memset(sbuf, 0xA5, sz);
+        }
+        double total = 0.0;
+        int rc = 0;
+        {
+            int base = (int)(count / size), rem = (int)(count % size);
+            for (int r = 0; r < size; ++r) counts[r] = base + (r < rem);
+        }
+        for (int it = 0; it < iters + skip; ++it) {
+            MPI_Barrier(MPI_COMM_WORLD);
+            double t0 = MPI_Wtime();
+            if (!strcmp(c, "allreduce")) rc |= MPI_Allreduce(sbuf, rbuf, (int)count, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
+            else if (!strcmp(c, "reduce")) rc |= MPI_Reduce(sbuf, rbuf, (int)count, MPI_FLOAT, MPI_SUM, 0, MPI_COMM_WORLD);
+            else if (!strcmp(c, "reduce_local")) rc |= MPI_Reduce_local(sbuf, rbuf, (int)count, MPI_FLOAT, MPI_SUM);
+            /* osu_reduce_scatter.c:116-131: size/n each, first size%n ranks one more */
+            else if (!strcmp(c, "reduce_scatter")) rc |= MPI_Reduce_scatter(sbuf, rbuf, counts, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
+            else if (!strcmp(c, "allgather")) rc |= MPI_Allgather(sbuf, (int)sz, MPI_CHAR, rbuf, (int)sz, MPI_CHAR, MPI_COMM_WORLD);
+            else if (!strcmp(c, "bcast")) rc |= MPI_Bcast(sbuf, (int)sz, MPI_CHAR, 0, MPI_COMM_WORLD);
+            double t1 = MPI_Wtime();
+            if (it >= skip) total += t1 - t0;
+        }
+        double lat = total / iters * 1e6, sum = 0.0;
+        MPI_Allreduce(MPI_IN_PLACE, &lat, 1, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
+        sum = lat / size;
+        int valid = 1;
+        if (validate) {
+            int mine = check(c, !strcmp(c, "bcast") ? sbuf : rbuf, count, sz, rank, size, counts), all = 0;
+            MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+            valid = all == size;
+        }
+        double algbw = sz / (sum * 1e-6) / 1e9;
+        double bf = 1.0;
+        if (!strcmp(c, "allreduce")) bf = 2.0 * (size - 1) / size;
+        else if (!strcmp(c, "reduce_scatter") || !strcmp(c, "allgather")) bf = (double)(size - 1) / size;
+        if (!strcmp(c, "allgather")) algbw *= size;
+        if (!strcmp(c, "reduce_local")) { bf = 3.0; }
+        bad_any |= rc || (validate && !valid);
+        if (rank == 0 && json)
+            printf("JSON {\"coll\": \"%s\", \"bytes\": %zu, \"lat_us\": %.2f, \"algbw_GBps\": %.3f, \"busbw_GBps\": %.3f, "
+                   "\"iters\": %d, \"valid\": %s}\n", c, sz, sum, algbw, algbw * bf, iters,
+                   rc ? "false" : (validate ? (valid ? "true" : "false") : "null"));
+        else if (rank == 0)
+            printf("%-12zu %14.2f %14.2f %14.2f %12s\n", sz, sum, algbw, algbw * bf,
+                   rc ? "ERROR" : (validate ? (valid ? "ok" : "WRONG") : "-"));
+        if (rank == 0) fflush(stdout);
+    }
+    free(counts);
+    return bad_any;
+}
+
 int main(int argc, char **argv) {
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "-c") && i + 1 < argc) coll = argv[++i];
@@ -92,12 +193,18 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "-x") && i + 1 < argc) skip_small = skip_large = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-d") && i + 1 < argc) device = strcmp(argv[++i], "host") != 0;
         else if (!strcmp(argv[i], "-v")) validate = 1;
+        else if (!strcmp(argv[i], "-I") && i + 1 < argc) iters_large = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-f") && i + 1 < argc) factor = strtoull(argv[++i], NULL, 10);
+        else if (!strcmp(argv[i], "-C") && i + 1 < argc) cap_sz = strtoull(argv[++i], NULL, 10);
+        else if (!strcmp(argv[i], "-j")) json = 1;
+        else { fprintf(stderr, "osu_coll: unknown argument %s\n", argv[i]); return 2; }
     }
     MPI_Init(&argc, &argv);
     int rank, size;
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
     MPI_Comm_size(MPI_COMM_WORLD, &size);
-    const size_t maxb = max_sz * (size_t)size;
+    const size_t gather_max = (!strcmp(coll, "all") ? (max_sz < cap_sz ? max_sz : cap_sz) : max_sz) * (size_t)size;
+    const size_t maxb = gather_max > max_sz ? gather_max : max_sz;
     void *sbuf = alloc_buf(maxb), *rbuf = alloc_buf(maxb);
     if (!sbuf || !rbuf) { fprintf(stderr, "allocation failed\n"); MPI_Abort(MPI_COMM_WORLD, 1); }
     if (!strcmp(coll, "latency") || !strcmp(coll, "bw")) {
@@ -109,59 +216,15 @@ int main(int argc, char **argv) {
         MPI_Finalize();
         return 0;
     }
-    if (rank == 0) {
-        printf("# mvapich2_amd osu_coll -c %s, %d ranks, %s buffers\n", coll, size, device ? "ROCm device" : "host");
-        printf("%-12s %14s %14s %14s %12s\n", "# Size(B)", "Avg Lat(us)", "algbw(GB/s)", "busbw(GB/s)", "valid");
+    if (factor < 2) factor = 2;
+    int rc = 0;
+    if (!strcmp(coll, "all")) {
+        static const char *const all[4] = {"allreduce", "reduce_scatter", "allgather", "bcast"};
+        for (int k = 0; k < 4 && !rc; ++k)
+            rc = run_coll(all[k], rank, size, sbuf, rbuf, min_sz, k ? (max_sz < cap_sz ? max_sz : cap_sz) : max_sz);
+    } else {
+        rc = run_coll(coll, rank, size, sbuf, rbuf, min_sz, max_sz);
     }
-    int *counts = (int *)malloc(sizeof(int) * size);
-    for (size_t sz = min_sz; sz <= max_sz; sz *= 2) {
-        const size_t count = sz / sizeof(float) ? sz / sizeof(float) : 1;
-        const int large = count > 8192; /* osu_allreduce.c:101 */
-        const int iters = large ? iters_large : iters_small, skip = large ? skip_large : skip_small;
-        fill(sbuf, count, rank);
-        double total = 0.0;
-        int rc = 0;
-        for (int it = 0; it < iters + skip; ++it) {
-            MPI_Barrier(MPI_COMM_WORLD);
-            double t0 = MPI_Wtime();
-            if (!strcmp(coll, "allreduce")) rc |= MPI_Allreduce(sbuf, rbuf, (int)count, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
-            else if (!strcmp(coll, "reduce")) rc |= MPI_Reduce(sbuf, rbuf, (int)count, MPI_FLOAT, MPI_SUM, 0, MPI_COMM_WORLD);
-            else if (!strcmp(coll, "reduce_local")) rc |= MPI_Reduce_local(sbuf, rbuf, (int)count, MPI_FLOAT, MPI_SUM);
-            else if (!strcmp(coll, "reduce_scatter")) {
-                /* osu_reduce_scatter.c:116-131: size/n each, first size%n ranks one more */
-                int base = (int)(count / size), rem = (int)(count % size);
-                for (int r = 0; r < size; ++r) counts[r] = base + (r < rem);
-                rc |= MPI_Reduce_scatter(sbuf, rbuf, counts, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
-            } else if (!strcmp(coll, "allgather")) rc |= MPI_Allgather(sbuf, (int)sz, MPI_CHAR, rbuf, (int)sz, MPI_CHAR, MPI_COMM_WORLD);
-            else if (!strcmp(coll, "bcast")) rc |= MPI_Bcast(sbuf, (int)sz, MPI_CHAR, 0, MPI_COMM_WORLD);
-            double t1 = MPI_Wtime();
-            if (it >= skip) total += t1 - t0;
-        }
-        double lat = total / iters * 1e6, sum = 0.0;
-        MPI_Allreduce(device ? MPI_IN_PLACE : MPI_IN_PLACE, &lat, 1, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
-        sum = lat / size;
-        int valid = 1;
-        if (validate && !strcmp(coll, "allreduce")) {
-            float *h = (float *)malloc(count * sizeof(float));
-            if (device) hipMemcpy(h, rbuf, count * sizeof(float), hipMemcpyDeviceToHost);
-            else memcpy(h, rbuf, count * sizeof(float));
-            for (size_t i = 0; i < count && valid; ++i) {
-                float want = (float)((i % 100 + 1) * (size * (size + 1) / 2));
-                if (h[i] != want) valid = 0;
-            }
-            free(h);
-        }
-        double algbw = sz / (sum * 1e-6) / 1e9;
-        double factor = 1.0;
-        if (!strcmp(coll, "allreduce")) factor = 2.0 * (size - 1) / size;
-        else if (!strcmp(coll, "reduce_scatter") || !strcmp(coll, "allgather")) factor = (double)(size - 1) / size;
-        if (!strcmp(coll, "allgather")) algbw *= size;
-        if (!strcmp(coll, "reduce_local")) { factor = 3.0; }
-        if (rank == 0)
-            printf("%-12zu %14.2f %14.2f %14.2f %12s\n", sz, sum, algbw, algbw * factor,
-                   rc ? "ERROR" : (validate ? (valid ? "ok" : "WRONG") : "-"));
-    }
-    free(counts);
     MPI_Finalize();
-    return 0;
+    return rc;
 }
