@@ -73,6 +73,7 @@ def host_allreduce_record(out):
     inherited cpuset, each rank's CPU, distinct CPUs / physical cores, oversubscription, cgroup
     quota) and the per-size JSON rows (latency, busbw, sched_yield fallbacks, CFS throttling)."""
     hdr = next((json.loads(l[8:]) for l in out.splitlines() if l.startswith("JSONHDR ")), None)
+    stream = next((json.loads(l[11:]) for l in out.splitlines() if l.startswith("JSONSTREAM ")), None)
     rows = [json.loads(l[5:]) for l in out.splitlines() if l.startswith("JSON ")]
     by = {r["bytes"]: r for r in rows}
     if hdr is None or 8 not in by or (64 << 20) not in by or (1 << 20) not in by:
@@ -93,6 +94,9 @@ def host_allreduce_record(out):
             "yields_8B": by[8].get("yields"), "throttled_periods_8B": by[8].get("throttled"),
             "yields_all_sizes": sum(r.get("yields", 0) for r in rows),
             "throttled_periods_all_sizes": sum(r.get("throttled", 0) for r in rows),
+            "dram_triad_GBps": stream["triad_GBps"] if stream else None,
+            "dram_triad_what": "STREAM triad on the same pinned CPUs at once (24 B/element), the host memory "
+                               "bound of this baseline (SURVEY.md §8(d) row 1)" if stream else None,
             "kind": "port", "cpu": cpu_info(), "placement": placement}
 
 
@@ -107,7 +111,7 @@ def cpu_baseline_host_allreduce(seconds=10.0, ranks=8):
         return {"error": "oracle/host_allreduce not built"}
     cap = max(0.2, seconds / 12.0)
     try:
-        out = subprocess.run([exe, "-n", str(ranks), "-m", "8:67108864", "-c", "-T", f"{cap:.2f}"],
+        out = subprocess.run([exe, "-n", str(ranks), "-m", "8:67108864", "-c", "-T", f"{cap:.2f}", "-B", "1.0"],
                              capture_output=True, text=True, timeout=max(60.0, 40 * cap)).stdout
     except subprocess.TimeoutExpired:
         return {"error": "host_allreduce timed out"}
@@ -420,8 +424,12 @@ def osu_sweep(L, world, rank, size, timeout=300):
     if rank == 0:
         key[0] = int.from_bytes(os.urandom(6), "little")
     m.check(L.MPI_Bcast(key.ctypes.data, 8, TYPES["MPI_BYTE"][0], 0, world), "MPI_Bcast(job key)")
+    # the child runs with this job's MPI_Init choices (tiling, store flavour, one-shot limit) instead of
+    # autotuning again: the sweep measures the configuration the headline line measured
     env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(size), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(size),
-               MV2AMD_JOBID=f"sweep{int(key[0])}", MV2AMD_INIT_REPORT="0")
+               MV2AMD_JOBID=f"sweep{int(key[0])}", MV2AMD_INIT_REPORT="0", MV2AMD_PIPE_GRID=str(m.info("pipe_grid")),
+               MV2AMD_PIPE_SUB=str(m.info("pipe_sub")), MV2AMD_PIPE_RNT=str(m.info("pipe_rnt")),
+               MV2AMD_ONESHOT_MAX=str(m.info("oneshot_max")))
     cmd = [exe, "-c", "all", "-m", f"8:{SWEEP_MAX}", "-f", "4", "-C", str(SWEEP_CAP), "-i", "200", "-I", "20",
            "-v", "-j"]
     t0 = time.perf_counter()

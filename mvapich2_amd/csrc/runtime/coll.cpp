@@ -810,6 +810,7 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "code_load_us")) *value = (long)(w.code_load_ms * 1e3 + 0.5);
     else if (!strcmp(key, "selftest_calls")) *value = w.selftest_calls;
     else if (!strcmp(key, "call_allocs")) *value = (long)w.call_allocs;
+    else if (!strcmp(key, "hw_queues_set")) *value = w.hw_queues_set;
     else if (!strcmp(key, "uop_in_bytes")) *value = (long)w.uop_in_bytes;
     else if (!strcmp(key, "uop_area_bytes")) *value = (long)w.uop_area_bytes;
     else if (!strcmp(key, "uop_stage_us")) *value = (long)(w.uop_ns[0] / 1000);

@@ -469,6 +469,7 @@ static int setup_device_common() {
     w.max_grid = (int)env_long("MV2AMD_MAX_GRID", w.max_grid);
     w.pipe_grid = (int)env_long("MV2AMD_PIPE_GRID", w.pipe_grid);
     w.pipe_sub = (size_t)env_long("MV2AMD_PIPE_SUB", (long)w.pipe_sub);
+    w.pipe_rnt = env_long("MV2AMD_PIPE_RNT", w.pipe_rnt) != 0;  // stores into peers' arenas: non-temporal / plain
     w.light_release = (int)env_long("MV2AMD_LIGHT_RELEASE", w.light_release);
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
     knobs_reload();  // MV2_* algorithm-selection knobs (orders.cpp)

@@ -53,8 +53,9 @@
  *
  * Usage: host_allreduce [-n ranks] [-m min:max] [-i iters_small] [-I iters_large]
  *                       [-c (validate)] [-T seconds per size cap] [-p first cpu index]
- *                       [-S (sequential placement: no idleness sample)]
- * Prints an OSU-style table, one "JSONHDR " line and one "JSON " line per size.
+ *                       [-S (sequential placement: no idleness sample)] [-B seconds of STREAM triad]
+ * Prints an OSU-style table, one "JSONHDR " line, with -B one "JSONSTREAM " line (the DRAM
+ * bound: STREAM triad on every rank's CPU at once) and one "JSON " line per size.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -394,6 +395,44 @@ static void cgroup_throttled(long *events, double *usec) {
 
 static int RANK_CPU[MAXR];
 
+/* The DRAM bound of configs[0]: STREAM triad a[i] = b[i] + s*c[i] on
+ * every rank at once, each on its own pinned CPU and its own 3 x 32 MiB arrays (first-touched on
+ * that CPU), for `secs` seconds; rank 0 prints the aggregate rate (24 bytes per element, the
+ * STREAM convention: two reads and one write, write-allocate traffic not counted). */
+static double TRIAD_GBPS[MAXR];
+static void barrier(void);
+static double now(void);
+static void triad(double secs) {
+    const size_t n = (size_t)4 << 20;
+    double *a = malloc(n * sizeof(double)), *b = malloc(n * sizeof(double)), *c = malloc(n * sizeof(double));
+    if (!a || !b || !c) return;
+    for (size_t i = 0; i < n; i++) { a[i] = 0; b[i] = 1.0 + (double)(i & 7); c[i] = 2.0; }
+    barrier();
+    const double s = 3.0, t0 = now();
+    long reps = 0;
+    do {
+        for (size_t i = 0; i < n; i++) a[i] = b[i] + s * c[i];
+        ++reps;
+        __asm__ volatile("" ::"r"(a) : "memory");
+    } while (now() - t0 < secs);
+    const double t = now() - t0;
+    barrier();
+    TRIAD_GBPS[ME] = 24.0 * (double)n * (double)reps / t / 1e9;
+    ((volatile double *)C->lat)[ME] = TRIAD_GBPS[ME];
+    barrier();
+    if (ME == 0) {
+        double tot = 0;
+        for (int r = 0; r < N; r++) tot += ((volatile double *)C->lat)[r];
+        printf("JSONSTREAM {\"triad_GBps\": %.2f, \"ranks\": %d, \"bytes_per_array\": %zu, \"seconds\": %.2f}\n",
+               tot, N, n * sizeof(double), secs);
+        fflush(stdout);
+    }
+    barrier();
+    free(a);
+    free(b);
+    free(c);
+}
+
 /* per-CPU busy and total jiffies from /proc/stat (0 when unreadable) */
 static void cpu_jiffies(unsigned long long *busy, unsigned long long *total) {
     FILE *f = fopen("/proc/stat", "r");
@@ -516,10 +555,11 @@ int main(int argc, char **argv) {
     int it_small = 1000, it_large = 100, validate = 0;
     double tcap = 3.0;
     int first_core = 0, idlest = 1;
+    double stream_s = 0;
     int c;
     const char *topo = getenv("MV2_USE_TOPO_AWARE_ALLREDUCE");
     if (topo) TOPO = atoi(topo) != 0;
-    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:S")) != -1) {
+    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:SB:")) != -1) {
         switch (c) {
         case 'n': N = atoi(optarg); break;
         case 'm': sscanf(optarg, "%zu:%zu", &mn, &mx); break;
@@ -529,6 +569,7 @@ int main(int argc, char **argv) {
         case 'T': tcap = atof(optarg); break;
         case 'p': first_core = atoi(optarg); break;
         case 'S': idlest = 0; break; /* sequential placement: mask order, no idleness sample */
+        case 'B': stream_s = atof(optarg); break; /* STREAM triad first, for this many seconds */
         default: fprintf(stderr, "usage: %s [-n ranks] [-m min:max] [-i it] [-I it] [-c] [-T s] [-p core0] [-S]\n", argv[0]); return 2;
         }
     }
@@ -555,6 +596,7 @@ int main(int argc, char **argv) {
             printf("# rank %d pinned to cpu %d\n", ME, core);
             fflush(stdout);
             barrier();
+            if (stream_s > 0) triad(stream_s);
             if (ME == 0) {
                 printf("# host_allreduce: %d ranks, MPI_FLOAT MPI_SUM, reference-algorithm host restatement\n", N);
                 printf("# %-12s %14s %14s %10s\n", "Size", "Avg Latency(us)", "busbw(GB/s)", "check");

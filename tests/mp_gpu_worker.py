@@ -343,6 +343,9 @@ def main():
     out = sys.argv[2]
     rank = int(os.environ["RANK"])
     n = int(os.environ["WORLD_SIZE"])
+    if os.environ.get("MV2AMD_TEST_HIP_FIRST") == "1":  # a host framework started HIP before the library
+        nd = ctypes.c_int()
+        assert ctypes.CDLL("libamdhip64.so").hipGetDeviceCount(ctypes.byref(nd)) == 0 and nd.value > 0
     L = m.lib()
     m.check(L.MPI_Init(None, None), "MPI_Init")
     L.MPI_Comm_set_errhandler(WORLD, 0x54000001)
@@ -395,7 +398,8 @@ def main():
         elif k == "enqueue_seq":  # stream-ordered collectives (MPIX_*_enqueue) mixed with a blocking call
             res = enqueue_seq(L, case, rank, n)
         elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)
-            keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n", "pipe_rnt", "oneshot_max", "os_tune_n"]
+            keys = ["pipe_tuned", "pipe_grid", "pipe_sub", "tune_n", "pipe_rnt", "oneshot_max", "os_tune_n",
+                    "selftest_calls", "hw_queues_set", "code_load_us"]
             res = np.array([m.info(key) for key in keys], dtype=np.int64)
         elif k == "mpit_counts":  # MPI_T: start every counter, run the calls, read the counters
             prov = ctypes.c_int()

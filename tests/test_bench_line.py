@@ -96,7 +96,8 @@ def _fake_host_record():
            "smt_shared": False, "first_cpu_index": 0, "rank_cpus": list(range(8)), "cgroup_cpu_quota": None}
     rows = [{"bytes": b, "lat_us": 0.3 * (1 + b / 1e4), "busbw_GBps": 5.0, "ok": True, "iters": 10, "yields": 0,
              "throttled": 0, "throttled_us": 0} for b in (8, 1 << 20, 64 << 20)]
-    out = "JSONHDR " + json.dumps(hdr) + "\n" + "".join("JSON " + json.dumps(r) + "\n" for r in rows)
+    out = ("JSONHDR " + json.dumps(hdr) + "\n" + 'JSONSTREAM {"triad_GBps": 123.4, "ranks": 8}\n' +
+           "".join("JSON " + json.dumps(r) + "\n" for r in rows))
     rec = bench.host_allreduce_record(out)
     rec["what"] = "w"
     return rec
@@ -105,6 +106,7 @@ def _fake_host_record():
 def test_host_record_parsing():
     rec = _fake_host_record()
     assert rec["cores"] == 8 and rec["cpus_available"] == 16 and rec["placement"] == "8 ranks pinned 1/core"
+    assert rec["dram_triad_GBps"] == 123.4
     assert bench.host_allreduce_record("JSON {}\n".replace("{}", '{"bytes": 8}'))["error"]
 
 
@@ -137,7 +139,7 @@ def test_host_allreduce_flags_oversubscription():
 def test_host_allreduce_distinct_cpus_when_they_fit():
     avail = sorted(os.sched_getaffinity(0))
     n = min(4, len(avail))
-    hdr, rows, _ = _run_host(["-n", str(n), "-m", "8:4096", "-c", "-i", "20", "-T", "0.2"])
+    hdr, rows, _ = _run_host(["-n", str(n), "-m", "8:4096", "-c", "-i", "20", "-T", "0.2", "-B", "0.2"])
     assert hdr["cpus_used"] == n and hdr["oversubscribed"] is False
     assert set(hdr["rank_cpus"]) <= set(avail) and len(set(hdr["rank_cpus"])) == n
     assert all(r["ok"] for r in rows)
