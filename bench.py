@@ -448,9 +448,13 @@ def osu_sweep(L, world, rank, size, timeout=300):
     res = {"what": "tools/osu/osu_coll -c all (OSU loop in C through libmpi.so, device buffers, every size "
                    "validated): allreduce 8 B..1 GiB, reduce_scatter / allgather / bcast 8 B..256 MiB, x4 sizes",
            "columns": ["bytes", "lat_us", "busbw_GBps", "valid"], "seconds": round(time.perf_counter() - t0, 1),
-           "all_valid": all(r["valid"] is True for r in rows)}
+           "all_valid": bool(rows) and all(r["valid"] is True for r in rows if "valid" in r)}
     for c in ("allreduce", "reduce_scatter", "allgather", "bcast"):
         res[c] = [[r["bytes"], r["lat_us"], r["busbw_GBps"], r["valid"]] for r in rows if r["coll"] == c]
+    # device point-to-point between ranks 0 and 1 (§8(f) rank 1): osu_latency (half round trip) and
+    # osu_bw (a window of 64 MPI_Isend, the receiver's ack), 8 B .. 16 MiB
+    res["osu_latency_us"] = [[r["bytes"], r["lat_us"]] for r in rows if r["coll"] == "osu_latency"]
+    res["osu_bw_GBps"] = [[r["bytes"], r["bw_GBps"]] for r in rows if r["coll"] == "osu_bw"]
     return res
 
 

@@ -48,6 +48,7 @@
 #include "internode.h"
 #include "log.h"
 #include "world.h"
+#include "../coll/kernels.h"
 
 namespace mv2 {
 
@@ -58,6 +59,8 @@ struct Req {
     bool done = false;
     int err = 0;
     // send
+    bool sdev = false;  // sbuf is device memory (chunk copies as kernels)
+    bool rdev = false;  // rbuf is device memory
     const char *sbuf = nullptr;
     size_t bytes = 0, off = 0;
     int peer = -1, tag = 0;
@@ -133,6 +136,21 @@ char *slot_ptr(char *arena, int src, uint64_t pos) {
     return arena + ((size_t)src * kP2PSlots + (size_t)(pos % kP2PSlots)) * kP2PChunk;
 }
 
+// Chunk copies between device buffers and the arenas run as copy kernels (coll/kernels.h
+// launch_pack_strided, one contiguous row), the last of a progress pass raising a completion word
+// of the point-to-point stream's own (counters + pinned host word, separate from the collectives'
+// one: a nonblocking collective may be in flight on the library stream meanwhile).  hipMemcpyAsync
+// plus hipStreamSynchronize cost 26 us per message below 32 KiB and 53-58 us from 32 KiB to
+// 8 MiB on the shared MI355X (profiles/r05f: SDMA or blit engines alike); host buffers and the
+// unexpected-message buffers keep hipMemcpyAsync.  MV2AMD_P2P_KERNEL_COPY=0 keeps the old path.
+struct P2PDone {
+    uint32_t *ctr = nullptr;
+    uint64_t *flag = nullptr;
+    uint64_t seq = 0;
+};
+P2PDone g_pdone;
+bool g_kcopy = true;
+
 int ready() {
     World &w = world();
     if (!w.inited || !w.p2p || (w.size > 1 && !w.shm)) {
@@ -141,7 +159,87 @@ int ready() {
     }
     // created on first use: an idle extra stream still costs a hardware queue, and
     // collective-only jobs (several ranks sharing a GPU in tests) measured slower with it
-    if (!w.p2p_stream && hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
+    if (!w.p2p_stream) {
+        if (hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
+        const char *v = getenv("MV2AMD_P2P_KERNEL_COPY");
+        g_kcopy = !(v && *v == '0');
+        if (g_kcopy && (hipMalloc((void **)&g_pdone.ctr, kDoneBytes) != hipSuccess ||
+                        hipMemset(g_pdone.ctr, 0, kDoneBytes) != hipSuccess ||
+                        hipHostMalloc((void **)&g_pdone.flag, 64, hipHostMallocDefault) != hipSuccess)) {
+            (void)hipGetLastError();
+            g_kcopy = false;  // the copy engines then (hipMemcpyAsync + stream synchronisation)
+        }
+        if (g_pdone.flag) memset(g_pdone.flag, 0, 64);
+        if (g_kcopy) hipDeviceSynchronize();
+    }
+    return 0;
+}
+
+bool dev_ptr(const void *p) {
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+// one chunk copy of a progress pass
+struct Copy {
+    char *dst;
+    const char *src;
+    size_t len;
+    bool kernel;  // both sides device memory: a copy kernel
+};
+
+// Issue a pass's copies on the point-to-point stream and wait for all of them: a completion word
+// when the pass ends in a copy kernel, else a stream synchronisation.
+int run_copies(const std::vector<Copy> &cp) {
+    World &w = world();
+    const hipStream_t st = w.p2p_stream;
+    for (size_t i = 0; i < cp.size(); ++i) {
+        const Copy &c = cp[i];
+        if (!c.len) continue;
+        if (c.kernel) {
+            Done d{};
+            if (i + 1 == cp.size()) d = Done{g_pdone.ctr, g_pdone.flag, ++g_pdone.seq};
+            if (launch_pack_strided(c.src, c.dst, 1, c.len, c.len, 0, st, d) != 0) {
+                MV2_ERR("point-to-point copy kernel failed to launch: %s", hipGetErrorString(hipGetLastError()));
+                return E_INTERN;
+            }
+        } else if (hipMemcpyAsync(c.dst, c.src, c.len, hipMemcpyDefault, st) != hipSuccess) {
+            MV2_ERR("point-to-point chunk copy failed: %s", hipGetErrorString(hipGetLastError()));
+            return E_INTERN;
+        }
+    }
+    const bool word = !cp.empty() && cp.back().kernel && cp.back().len;
+    if (word) {
+        // the word is the normal path; the stream is consulted once it is 200 us late, then every 100 us
+        const uint64_t want = g_pdone.seq;
+        auto t0 = std::chrono::steady_clock::now();
+        double next_us = 200.0;
+        for (unsigned spins = 0;; ++spins) {
+            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return 0;
+            if ((spins & 255u) != 0) continue;
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            if (us < next_us) continue;
+            next_us = us + 100.0;
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return 0;
+            if (q == hipSuccess) {  // finished without raising the word: counters reset, done
+                MV2_DEBUG("point-to-point copy finished without its completion word");
+                hipMemsetAsync(g_pdone.ctr, 0, kDoneBytes, st);
+                return hipStreamSynchronize(st) == hipSuccess ? 0 : E_INTERN;
+            }
+            MV2_ERR("point-to-point copies failed: %s", hipGetErrorString(q));
+            return E_INTERN;
+        }
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        MV2_ERR("point-to-point copies failed: %s", hipGetErrorString(hipGetLastError()));
+        return E_INTERN;
+    }
     return 0;
 }
 
@@ -285,6 +383,7 @@ int progress(bool *moved) {
     };
     std::vector<SendPub> sp;
     std::vector<RecvPub> rp;
+    std::vector<Copy> cp;
     const int base = node_base();
     if (!w.shm) return net_progress(moved);
 
@@ -296,11 +395,7 @@ int progress(bool *moved) {
         while (!g_sendq[d].empty() && tail - head < (uint64_t)kP2PSlots) {
             Req *r = g_sendq[d].front();
             const size_t len = std::min(kP2PChunk, r->bytes - r->off);
-            if (len && hipMemcpyAsync(slot_ptr(w.peer_p2p[d], me, tail), r->sbuf + r->off, len, hipMemcpyDefault,
-                                      w.p2p_stream) != hipSuccess) {
-                MV2_ERR("point-to-point chunk copy to rank %d failed", d);
-                return E_INTERN;
-            }
+            if (len) cp.push_back({slot_ptr(w.peer_p2p[d], me, tail), r->sbuf + r->off, len, g_kcopy && r->sdev});
             P2PRec rec{r->msg, r->tag, 0, r->bytes, r->off, len};
             r->off += len;
             const bool last = r->off >= r->bytes;
@@ -343,16 +438,11 @@ int progress(bool *moved) {
                 }
             }
             const char *src = slot_ptr(w.p2p, s, head);
-            hipError_t e = hipSuccess;
             if (a.req) {
                 const size_t room = a.req->cap > rec.off ? std::min<size_t>(rec.len, a.req->cap - rec.off) : 0;
-                if (room) e = hipMemcpyAsync(a.req->rbuf + rec.off, src, room, hipMemcpyDefault, w.p2p_stream);
+                if (room) cp.push_back({a.req->rbuf + rec.off, src, room, g_kcopy && a.req->rdev});
             } else if (rec.len) {
-                e = hipMemcpyAsync(a.ux->data.data() + rec.off, src, rec.len, hipMemcpyDefault, w.p2p_stream);
-            }
-            if (e != hipSuccess) {
-                MV2_ERR("point-to-point chunk copy from rank %d failed", s);
-                return E_INTERN;
+                cp.push_back({a.ux->data.data() + rec.off, src, (size_t)rec.len, false});
             }
             a.got += rec.len;
             ++head;
@@ -366,10 +456,7 @@ int progress(bool *moved) {
     if (rc) return rc;
     if (sp.empty() && rp.empty()) return 0;
     *moved = true;
-    if (hipStreamSynchronize(w.p2p_stream) != hipSuccess) {
-        MV2_ERR("point-to-point copies failed: %s", hipGetErrorString(hipGetLastError()));
-        return E_INTERN;
-    }
+    if ((rc = run_copies(cp))) return rc;
     // data is in place: publish records / free slots, complete requests
     for (const SendPub &p : sp) {
         p.c->rec[p.pos % kP2PSlots] = p.rec;
@@ -421,6 +508,7 @@ int mv2::p2p_isend(const void *buf, size_t bytes, int dest, int tag, unsigned lo
     Req *r = new Req{};
     r->send = true;
     r->sbuf = (const char *)buf;
+    r->sdev = g_kcopy && dev_ptr(buf);
     r->bytes = bytes;
     r->peer = dest;
     r->tag = tag;
@@ -474,6 +562,7 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
     Req *r = new Req{};
     r->send = false;
     r->rbuf = (char *)buf;
+    r->rdev = g_kcopy && dev_ptr(buf);
     r->cap = cap;
     r->src_want = source;
     r->tag_want = tag;

@@ -11,7 +11,8 @@
  *            [-x warmup] [-C cap bytes for -c all's reduce_scatter/allgather/bcast]
  *            [-d rocm|host] [-v (validate every collective)] [-j (JSON rows)]
  * -c all runs allreduce over [min, max] and reduce_scatter, allgather, bcast over
- * [min, min(max, cap)] in one job (bench.py's N > 1 sweep: configs[2] and [3]).
+ * [min, min(max, cap)] in one job (bench.py's N > 1 sweep: configs[2] and [3]), then the
+ * device point-to-point latency and bandwidth between ranks 0 and 1 up to 16 MiB.
  */
 #include <hip/hip_runtime.h>
 #include <mpi.h>
@@ -46,10 +47,10 @@ static void fill(void *p, size_t count, int rank) {
 /* osu_latency / osu_bw patterns between ranks 0 and 1 (osu_latency.c, osu_bw.c):
  * latency = half the ping-pong round trip; bw = a window of 64 Isend/Irecv then
  * the receiver's 4-byte ack, bytes / time. */
-static int run_pt2pt(int rank, void *sbuf, void *rbuf) {
+static int run_pt2pt(int rank, void *sbuf, void *rbuf, size_t lo, size_t hi) {
     const int window = 64;
     MPI_Request reqs[64];
-    for (size_t sz = min_sz; sz <= max_sz; sz *= 2) {
+    for (size_t sz = lo; sz <= hi; sz *= factor) {
         const int large = sz > 8192;
         const int iters = large ? iters_large : iters_small, skip = large ? skip_large : skip_small;
         double t0 = 0.0;
@@ -77,7 +78,15 @@ static int run_pt2pt(int rank, void *sbuf, void *rbuf) {
             }
         }
         const double t = MPI_Wtime() - t0;
-        if (rank == 0) {
+        if (rank == 0 && json) {
+            if (!strcmp(coll, "latency"))
+                printf("JSON {\"coll\": \"osu_latency\", \"bytes\": %zu, \"lat_us\": %.2f, \"iters\": %d}\n", sz,
+                       t / iters / 2 * 1e6, iters);
+            else
+                printf("JSON {\"coll\": \"osu_bw\", \"bytes\": %zu, \"bw_GBps\": %.3f, \"iters\": %d}\n", sz,
+                       (double)sz * window * iters / t / 1e9, iters);
+            fflush(stdout);
+        } else if (rank == 0) {
             if (!strcmp(coll, "latency")) printf("%-12zu %14.2f\n", sz, t / iters / 2 * 1e6);
             else printf("%-12zu %14.2f\n", sz, (double)sz * window * iters / t / 1e9);
         }
@@ -212,7 +221,7 @@ int main(int argc, char **argv) {
         if (rank == 0)
             printf("# mvapich2_amd osu_%s (pt2pt, ranks 0 <-> 1), %s buffers\n%-12s %14s\n", coll,
                    device ? "ROCm device" : "host", "# Size(B)", !strcmp(coll, "latency") ? "Latency(us)" : "BW(GB/s)");
-        run_pt2pt(rank, sbuf, rbuf);
+        run_pt2pt(rank, sbuf, rbuf, min_sz, max_sz);
         MPI_Finalize();
         return 0;
     }
@@ -222,6 +231,14 @@ int main(int argc, char **argv) {
         static const char *const all[4] = {"allreduce", "reduce_scatter", "allgather", "bcast"};
         for (int k = 0; k < 4 && !rc; ++k)
             rc = run_coll(all[k], rank, size, sbuf, rbuf, min_sz, k ? (max_sz < cap_sz ? max_sz : cap_sz) : max_sz);
+        /* device point-to-point, ranks 0 <-> 1 (osu_latency.c / osu_bw.c patterns) up to 16 MiB */
+        const size_t p2p_hi = max_sz < ((size_t)16 << 20) ? max_sz : ((size_t)16 << 20);
+        if (!rc && size >= 2) {
+            coll = "latency";
+            rc = run_pt2pt(rank, sbuf, rbuf, min_sz, p2p_hi);
+            coll = "bw";
+            if (!rc) rc = run_pt2pt(rank, sbuf, rbuf, min_sz, p2p_hi);
+        }
     } else {
         rc = run_coll(coll, rank, size, sbuf, rbuf, min_sz, max_sz);
     }
