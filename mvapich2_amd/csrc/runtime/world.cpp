@@ -6,6 +6,7 @@
 #include "world.h"
 #include "internode.h"
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <sched.h>
 #include <stdio.h>
@@ -407,15 +408,23 @@ static int limit_hw_queues_if_shared(int local_size) {
 // first)?  The ROCm runtime opens /dev/kfd when it starts, so an open descriptor on it says so;
 // GPU_MAX_HW_QUEUES is read once at that start, so setting it later has no effect.
 static bool hip_already_running() {
-    char path[64], target[64];
-    for (int fd = 0; fd < 4096; ++fd) {
-        snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+    DIR *d = opendir("/proc/self/fd");
+    if (!d) return false;
+    bool found = false;
+    char path[300], target[64];
+    while (struct dirent *e = readdir(d)) {
+        if (e->d_name[0] == '.') continue;
+        snprintf(path, sizeof(path), "/proc/self/fd/%s", e->d_name);
         const ssize_t k = readlink(path, target, sizeof(target) - 1);
         if (k <= 0) continue;
         target[k] = 0;
-        if (!strcmp(target, "/dev/kfd")) return true;
+        if (!strcmp(target, "/dev/kfd")) {
+            found = true;
+            break;
+        }
     }
-    return false;
+    closedir(d);
+    return found;
 }
 
 static int env_local_size() {
