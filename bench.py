@@ -410,45 +410,38 @@ SWEEP_MAX = 1 << 30        # configs[2]: osu_allreduce 8 B .. 1 GiB
 SWEEP_CAP = 256 << 20      # configs[3]: reduce_scatter / allgather / bcast up to 256 MiB
 
 
-def osu_sweep(L, world, rank, size, timeout=300):
-    """configs[2] and [3] as OSU sweeps in the same run: every rank starts one child job of
-    tools/osu/osu_coll (the OSU loop restated in C against include/mpi.h and linked with
-    libmpi.so, osu_allreduce.c:98-163) with -c all: allreduce 8 B .. 1 GiB and reduce_scatter /
-    allgather / bcast 8 B .. 256 MiB, sizes x4, every result validated against its closed form.
-    The child is its own MPI job (own control segment and arenas, MV2AMD_JOBID agreed through an
-    MPI_Bcast); rank 0 returns its rows."""
-    exe = os.path.join(ROOT, "tools", "osu", "osu_coll")
-    if not os.path.exists(exe):
-        return {"error": "tools/osu/osu_coll not built"}
-    key = np.zeros(1, dtype=np.int64)
-    if rank == 0:
-        key[0] = int.from_bytes(os.urandom(6), "little")
-    m.check(L.MPI_Bcast(key.ctypes.data, 8, TYPES["MPI_BYTE"][0], 0, world), "MPI_Bcast(job key)")
-    # the child runs with this job's MPI_Init choices (tiling, store flavour, one-shot limit) instead of
-    # autotuning again: the sweep measures the configuration the headline line measured
-    env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(size), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(size),
-               MV2AMD_JOBID=f"sweep{int(key[0])}", MV2AMD_INIT_REPORT="0", MV2AMD_PIPE_GRID=str(m.info("pipe_grid")),
-               MV2AMD_PIPE_SUB=str(m.info("pipe_sub")), MV2AMD_PIPE_RNT=str(m.info("pipe_rnt")),
-               MV2AMD_ONESHOT_MAX=str(m.info("oneshot_max")))
-    cmd = [exe, "-c", "all", "-m", f"8:{SWEEP_MAX}", "-f", "4", "-C", str(SWEEP_CAP), "-i", "200", "-I", "20",
-           "-v", "-j"]
+def osu_sweep(L, world, rank, size):
+    """configs[2] and [3] as OSU sweeps in the same run: every rank calls tools/osu/libosu_coll.so's
+    osu_coll_main -- the OSU loop restated in C against include/mpi.h (osu_allreduce.c:98-163),
+    here inside this job's MPI world, so on its MPI_Init tuning and with no second process per GPU
+    -- with -c all: allreduce 8 B .. 1 GiB and reduce_scatter / allgather / bcast 8 B .. 256 MiB,
+    sizes x4, every result validated against its closed form, then osu_latency / osu_bw between
+    ranks 0 and 1 up to 16 MiB.  Rank 0's rows come back through a JSON file."""
+    so = os.path.join(ROOT, "tools", "osu", "libosu_coll.so")
+    if not os.path.exists(so):
+        return {"error": "tools/osu/libosu_coll.so not built"}
+    lib = ctypes.CDLL(so)
+    lib.osu_coll_main.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
+    lib.osu_coll_main.restype = ctypes.c_int
+    path = os.path.join("/tmp", f"mv2amd_sweep_{os.getpid()}.jsonl")
+    args = ["osu_coll", "-c", "all", "-m", f"8:{SWEEP_MAX}", "-f", "4", "-C", str(SWEEP_CAP), "-i", "200", "-I", "20",
+            "-v", "-j", "-o", path]
+    argv = (ctypes.c_char_p * len(args))(*[a.encode() for a in args])
     t0 = time.perf_counter()
-    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    try:
-        out, err = p.communicate(timeout=timeout)
-    except subprocess.TimeoutExpired:
-        p.kill()
-        p.communicate()
-        return {"error": f"osu sweep timed out after {timeout} s"}
-    if p.returncode != 0:
-        return {"error": ((err or "").strip().splitlines() or ["no output"])[-1][-300:], "returncode": p.returncode}
+    rc = lib.osu_coll_main(len(args), argv)
+    secs = time.perf_counter() - t0
     if rank != 0:
         return None
-    rows = [json.loads(l[5:]) for l in out.splitlines() if l.startswith("JSON ")]
-    res = {"what": "tools/osu/osu_coll -c all (OSU loop in C through libmpi.so, device buffers, every size "
-                   "validated): allreduce 8 B..1 GiB, reduce_scatter / allgather / bcast 8 B..256 MiB, x4 sizes",
-           "columns": ["bytes", "lat_us", "busbw_GBps", "valid"], "seconds": round(time.perf_counter() - t0, 1),
-           "all_valid": bool(rows) and all(r["valid"] is True for r in rows if "valid" in r)}
+    try:
+        rows = [json.loads(l[5:]) for l in open(path) if l.startswith("JSON ")]
+        os.unlink(path)
+    except OSError as e:
+        return {"error": f"no sweep rows: {e}", "returncode": rc}
+    res = {"what": "tools/osu/osu_coll -c all (OSU loop in C through libmpi.so inside this job, device buffers, "
+                   "every size validated): allreduce 8 B..1 GiB, reduce_scatter / allgather / bcast 8 B..256 MiB, "
+                   "x4 sizes",
+           "columns": ["bytes", "lat_us", "busbw_GBps", "valid"], "seconds": round(secs, 1), "returncode": rc,
+           "all_valid": rc == 0 and bool(rows) and all(r["valid"] is True for r in rows if "valid" in r)}
     for c in ("allreduce", "reduce_scatter", "allgather", "bcast"):
         res[c] = [[r["bytes"], r["lat_us"], r["busbw_GBps"], r["valid"]] for r in rows if r["coll"] == c]
     # device point-to-point between ranks 0 and 1 (§8(f) rank 1): osu_latency (half round trip) and

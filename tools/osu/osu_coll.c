@@ -24,6 +24,7 @@ static const char *coll = "allreduce";
 static size_t min_sz = 8, max_sz = 1 << 20, cap_sz = (size_t)256 << 20, factor = 2;
 static int iters_small = 1000, iters_large = 100, skip_small = 100, skip_large = 10;
 static int device = 1, validate = 0, json = 0;
+static FILE *jout = NULL; /* JSON rows: stdout, or the -o file (rank 0) */
 
 static void *alloc_buf(size_t bytes) {
     void *p = NULL;
@@ -80,12 +81,12 @@ static int run_pt2pt(int rank, void *sbuf, void *rbuf, size_t lo, size_t hi) {
         const double t = MPI_Wtime() - t0;
         if (rank == 0 && json) {
             if (!strcmp(coll, "latency"))
-                printf("JSON {\"coll\": \"osu_latency\", \"bytes\": %zu, \"lat_us\": %.2f, \"iters\": %d}\n", sz,
+                fprintf(jout, "JSON {\"coll\": \"osu_latency\", \"bytes\": %zu, \"lat_us\": %.2f, \"iters\": %d}\n", sz,
                        t / iters / 2 * 1e6, iters);
             else
-                printf("JSON {\"coll\": \"osu_bw\", \"bytes\": %zu, \"bw_GBps\": %.3f, \"iters\": %d}\n", sz,
+                fprintf(jout, "JSON {\"coll\": \"osu_bw\", \"bytes\": %zu, \"bw_GBps\": %.3f, \"iters\": %d}\n", sz,
                        (double)sz * window * iters / t / 1e9, iters);
-            fflush(stdout);
+            fflush(jout);
         } else if (rank == 0) {
             if (!strcmp(coll, "latency")) printf("%-12zu %14.2f\n", sz, t / iters / 2 * 1e6);
             else printf("%-12zu %14.2f\n", sz, (double)sz * window * iters / t / 1e9);
@@ -179,19 +180,28 @@ static int run_coll(const char *c, int rank, int size, void *sbuf, void *rbuf, s
         if (!strcmp(c, "reduce_local")) { bf = 3.0; }
         bad_any |= rc || (validate && !valid);
         if (rank == 0 && json)
-            printf("JSON {\"coll\": \"%s\", \"bytes\": %zu, \"lat_us\": %.2f, \"algbw_GBps\": %.3f, \"busbw_GBps\": %.3f, "
+            fprintf(jout, "JSON {\"coll\": \"%s\", \"bytes\": %zu, \"lat_us\": %.2f, \"algbw_GBps\": %.3f, \"busbw_GBps\": %.3f, "
                    "\"iters\": %d, \"valid\": %s}\n", c, sz, sum, algbw, algbw * bf, iters,
                    rc ? "false" : (validate ? (valid ? "true" : "false") : "null"));
         else if (rank == 0)
             printf("%-12zu %14.2f %14.2f %14.2f %12s\n", sz, sum, algbw, algbw * bf,
                    rc ? "ERROR" : (validate ? (valid ? "ok" : "WRONG") : "-"));
-        if (rank == 0) fflush(stdout);
+        if (rank == 0) fflush(json ? jout : stdout);
     }
     free(counts);
     return bad_any;
 }
 
-int main(int argc, char **argv) {
+/* The whole program.  init = 0: MPI is already initialised by the caller (bench.py loads this file
+ * as libosu_coll.so into its ranks and calls osu_coll_main: the sweep then runs in the bench's
+ * own MPI job, on its tuning, with no second process per GPU); MPI_Finalize is left to it too. */
+static int osu_run(int argc, char **argv, int init) {
+    /* defaults again: the library entry may be called more than once */
+    coll = "allreduce";
+    min_sz = 8, max_sz = 1 << 20, cap_sz = (size_t)256 << 20, factor = 2;
+    iters_small = 1000, iters_large = 100, skip_small = 100, skip_large = 10;
+    device = 1, validate = 0, json = 0;
+    const char *jpath = NULL;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "-c") && i + 1 < argc) coll = argv[++i];
         else if (!strcmp(argv[i], "-m") && i + 1 < argc) {
@@ -206,12 +216,18 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "-f") && i + 1 < argc) factor = strtoull(argv[++i], NULL, 10);
         else if (!strcmp(argv[i], "-C") && i + 1 < argc) cap_sz = strtoull(argv[++i], NULL, 10);
         else if (!strcmp(argv[i], "-j")) json = 1;
+        else if (!strcmp(argv[i], "-o") && i + 1 < argc) jpath = argv[++i];
         else { fprintf(stderr, "osu_coll: unknown argument %s\n", argv[i]); return 2; }
     }
-    MPI_Init(&argc, &argv);
+    if (init) MPI_Init(&argc, &argv);
     int rank, size;
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
     MPI_Comm_size(MPI_COMM_WORLD, &size);
+    jout = stdout;
+    if (json && jpath && rank == 0 && !(jout = fopen(jpath, "w"))) {
+        fprintf(stderr, "osu_coll: cannot write %s\n", jpath);
+        jout = stdout;
+    }
     const size_t gather_max = (!strcmp(coll, "all") ? (max_sz < cap_sz ? max_sz : cap_sz) : max_sz) * (size_t)size;
     const size_t maxb = gather_max > max_sz ? gather_max : max_sz;
     void *sbuf = alloc_buf(maxb), *rbuf = alloc_buf(maxb);
@@ -222,7 +238,14 @@ int main(int argc, char **argv) {
             printf("# mvapich2_amd osu_%s (pt2pt, ranks 0 <-> 1), %s buffers\n%-12s %14s\n", coll,
                    device ? "ROCm device" : "host", "# Size(B)", !strcmp(coll, "latency") ? "Latency(us)" : "BW(GB/s)");
         run_pt2pt(rank, sbuf, rbuf, min_sz, max_sz);
-        MPI_Finalize();
+        if (device) {
+            hipFree(sbuf);
+            hipFree(rbuf);
+        } else {
+            free(sbuf);
+            free(rbuf);
+        }
+        if (init) MPI_Finalize();
         return 0;
     }
     if (factor < 2) factor = 2;
@@ -242,6 +265,21 @@ int main(int argc, char **argv) {
     } else {
         rc = run_coll(coll, rank, size, sbuf, rbuf, min_sz, max_sz);
     }
-    MPI_Finalize();
+    if (device) {
+        hipFree(sbuf);
+        hipFree(rbuf);
+    } else {
+        free(sbuf);
+        free(rbuf);
+    }
+    if (jout && jout != stdout) fclose(jout);
+    jout = NULL;
+    if (init) MPI_Finalize();
     return rc;
 }
+
+#ifdef OSU_COLL_LIB
+int osu_coll_main(int argc, char **argv) { return osu_run(argc, argv, 0); }
+#else
+int main(int argc, char **argv) { return osu_run(argc, argv, 1); }
+#endif
