@@ -141,8 +141,11 @@ char *slot_ptr(char *arena, int src, uint64_t pos) {
 // of the point-to-point stream's own (counters + pinned host word, separate from the collectives'
 // one: a nonblocking collective may be in flight on the library stream meanwhile).  hipMemcpyAsync
 // plus hipStreamSynchronize cost 26 us per message below 32 KiB and 53-58 us from 32 KiB to
-// 8 MiB on the shared MI355X (profiles/r05f: SDMA or blit engines alike); host buffers and the
-// unexpected-message buffers keep hipMemcpyAsync.  MV2AMD_P2P_KERNEL_COPY=0 keeps the old path.
+// 8 MiB on the shared MI355X (profiles/r05f: SDMA or blit engines alike), the kernels 17 / 22-26 us
+// (r05g).  With more than two ranks on one GPU the copy engines stay: eight processes' copy kernels
+// contending for the shared GPU's compute queues slowed an all-to-all of 2 MiB ranges 4.5x
+// (user-op staging at 8 shared ranks 4.1 -> 18.5 ms per call, r05k against r05j).  Host buffers and
+// the unexpected-message buffers keep hipMemcpyAsync.  MV2AMD_P2P_KERNEL_COPY=0 / 1 forces either.
 struct P2PDone {
     uint32_t *ctr = nullptr;
     uint64_t *flag = nullptr;
@@ -162,7 +165,7 @@ int ready() {
     if (!w.p2p_stream) {
         if (hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
         const char *v = getenv("MV2AMD_P2P_KERNEL_COPY");
-        g_kcopy = !(v && *v == '0');
+        g_kcopy = (v && *v) ? *v != '0' : w.nshare <= 2;
         if (g_kcopy && (hipMalloc((void **)&g_pdone.ctr, kDoneBytes) != hipSuccess ||
                         hipMemset(g_pdone.ctr, 0, kDoneBytes) != hipSuccess ||
                         hipHostMalloc((void **)&g_pdone.flag, 64, hipHostMallocDefault) != hipSuccess)) {
