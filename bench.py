@@ -679,6 +679,8 @@ def bench_nranks(args, L, rank, size):
                   for k in range(m.info("tune_n"))],
               "oneshot_max_bytes": m.info("oneshot_max"),
               "mpi_init_ms_rank0": round(m.info("init_us") / 1e3, 1),
+              "mpi_init_hip_start_ms": round(m.info("hip_init_us") / 1e3, 1),
+              "mpi_init_code_objects_ms": round(m.info("code_load_us") / 1e3, 1),
               "mpi_init_selftest_ms": round(m.info("selftest_us") / 1e3, 1),
               "mpi_init_selftest_calls": m.info("selftest_calls"),
               "mpi_init_autotune_ms": round(m.info("autotune_us") / 1e3, 1),
