@@ -143,3 +143,18 @@ def test_host_allreduce_distinct_cpus_when_they_fit():
     assert hdr["cpus_used"] == n and hdr["oversubscribed"] is False
     assert set(hdr["rank_cpus"]) <= set(avail) and len(set(hdr["rank_cpus"])) == n
     assert all(r["ok"] for r in rows)
+
+
+def test_osu_sweep_library_exports_its_entry():
+    """bench.py's N > 1 sweep loads tools/osu/libosu_coll.so into its ranks (no second process per
+    GPU) and calls osu_coll_main; the library must exist after build() and export it."""
+    import ctypes
+    so = os.path.join(ROOT, "tools", "osu", "libosu_coll.so")
+    if not os.path.exists(so):
+        pytest.skip("tools/osu not built")
+    assert hasattr(ctypes.CDLL(so), "osu_coll_main")
+
+
+def test_sweep_without_library_reports_instead_of_raising(monkeypatch):
+    monkeypatch.setattr(bench, "ROOT", "/nonexistent")
+    assert "error" in bench.osu_sweep(None, 0x44000000, 0, 2)
