@@ -142,10 +142,12 @@ char *slot_ptr(char *arena, int src, uint64_t pos) {
 // one: a nonblocking collective may be in flight on the library stream meanwhile).  hipMemcpyAsync
 // plus hipStreamSynchronize cost 26 us per message below 32 KiB and 53-58 us from 32 KiB to
 // 8 MiB on the shared MI355X (profiles/r05f: SDMA or blit engines alike), the kernels 17 / 22-26 us
-// (r05g).  With more than two ranks on one GPU the copy engines stay: eight processes' copy kernels
-// contending for the shared GPU's compute queues slowed an all-to-all of 2 MiB ranges 4.5x
-// (user-op staging at 8 shared ranks 4.1 -> 18.5 ms per call, r05k against r05j).  Host buffers and
-// the unexpected-message buffers keep hipMemcpyAsync.  MV2AMD_P2P_KERNEL_COPY=0 / 1 forces either.
+// (r05g).  With more than four ranks on one GPU the copy engines stay: eight processes' copy
+// kernels contending for the shared GPU's compute queues made the user-op line's all-to-all of
+// 2 MiB ranges 2.4x slower (C-op line at 8 shared ranks 18.1 ms with kernels, 7.5 ms on the
+// engines: r05j / r05l), while at 4 shared ranks the kernels still win (5.0 vs 5.4 ms; osu_bw pattern
+// 442 vs 145 GB/s: r05i / r05l).  Host buffers and the unexpected-message buffers keep
+// hipMemcpyAsync.  MV2AMD_P2P_KERNEL_COPY=0 / 1 forces either.
 struct P2PDone {
     uint32_t *ctr = nullptr;
     uint64_t *flag = nullptr;
@@ -165,7 +167,7 @@ int ready() {
     if (!w.p2p_stream) {
         if (hipStreamCreate(&w.p2p_stream) != hipSuccess) return E_OTHER;
         const char *v = getenv("MV2AMD_P2P_KERNEL_COPY");
-        g_kcopy = (v && *v) ? *v != '0' : w.nshare <= 2;
+        g_kcopy = (v && *v) ? *v != '0' : w.nshare <= 4;
         if (g_kcopy && (hipMalloc((void **)&g_pdone.ctr, kDoneBytes) != hipSuccess ||
                         hipMemset(g_pdone.ctr, 0, kDoneBytes) != hipSuccess ||
                         hipHostMalloc((void **)&g_pdone.flag, 64, hipHostMallocDefault) != hipSuccess)) {
