@@ -63,6 +63,65 @@ int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg) {
 }
 
 // ---------------------------------------------------------------------------
+// One-shot allgather / broadcast (messages up to the one-shot limit): the pipelined kernel's two
+// flag exchanges per round cost ~4 us more than the one-shot allreduce's one (osu 8 B at 2 shared
+// ranks: allgather 15.8, bcast 15.0 against allreduce 11.2 us, profiles/r05c).  Workgroup b pushes
+// partition b of the block this rank contributes (allgather: its own block; broadcast: the root's
+// buffer, at the root only) into slot [me] of every peer's one-shot arena (this call's half), every
+// rank raises its flag -- the non-roots of a broadcast too, so that no rank can reach call i + 2
+// while a peer still reads call i's half (the one-shot allreduce's argument) -- waits for its
+// peers' flags of workgroup b, and copies partition b of the slots it needs out of its own arena.
+// Blocks are 16-byte multiples (the host takes this path only then); a broadcast's tail bytes go
+// through workgroup 0.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_oneshot_mv(OneShotArgs a) {
+    const int blk = blockIdx.x, G = gridDim.x;
+    const size_t per = (a.nvec + G - 1) / G;
+    const size_t vb = (size_t)blk * per < a.nvec ? (size_t)blk * per : a.nvec;
+    const size_t ve = vb + per < a.nvec ? vb + per : a.nvec;
+    const bool bc = a.mv == 2;
+    const size_t tail0 = a.nvec * 16;
+    const size_t myslot = (size_t)a.me * a.slot_bytes;
+    if (!bc || a.me == a.root) {
+        const v4u *src = (const v4u *)a.send;
+        for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
+            const v4u x = src[i];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j)
+                if (j < a.n && j != a.me) ((v4u *)(a.arena_peer.p[j] + myslot))[i] = x;
+            if (!bc && a.send != a.recv + (size_t)a.me * a.pitch) ((v4u *)(a.recv + (size_t)a.me * a.pitch))[i] = x;
+        }
+        if (blk == 0)
+            for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {
+                const char c = a.send[e];
+#pragma unroll
+                for (int j = 0; j < kMaxRanks; ++j)
+                    if (j < a.n && j != a.me) a.arena_peer.p[j][myslot + e] = c;
+            }
+    }
+    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
+    if (wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout, a.light != 0)) {
+        for (int j = 0; j < a.n; ++j) {
+            if (j == a.me || (bc && j != a.root)) continue;
+            const char *slot = a.arena_own + (size_t)j * a.slot_bytes;
+            char *dst = bc ? a.recv : a.recv + (size_t)j * a.pitch;
+            for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) ((v4u *)dst)[i] = ld_nt((const v4u *)slot + i);
+            if (blk == 0)
+                for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads)
+                    dst[e] = __builtin_nontemporal_load(slot + e);
+        }
+    }
+    block_done(a.done);
+}
+
+int launch_oneshot_mv(const OneShotArgs &a, const LaunchCfg &cfg) {
+    static const int cap = resident_grid((const void *)k_oneshot_mv, cfg);
+    const int g = cfg.grid < cap ? cfg.grid : cap;
+    hipLaunchKernelGGL(k_oneshot_mv, dim3(g), dim3(kThreads), 0, cfg.stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+}
+
+// ---------------------------------------------------------------------------
 // Code-object loading.  HIP loads a translation unit's gfx950 code object at the first launch of
 // one of its kernels; MPI_Init launches one empty kernel per unit so that the load happens (and
 // is timed) there rather than inside an application's first call of each type group.

@@ -53,6 +53,10 @@ struct OneShotArgs {
     // pushes every peer only that peer's block (coll/kernels_impl.h k_oneshot_rs)
     int rs;
     size_t wlo[kMaxRanks], wcnt[kMaxRanks];
+    // data movement (k_oneshot_mv, coll/dispatch.hip): 0 = reducing; 1 = allgather (count bytes per
+    // rank from send, rank j's block to recv + j * pitch); 2 = broadcast (count bytes of recv from root)
+    int mv, root;
+    size_t pitch;
 };
 
 // ---------------------------------------------------------------------------
@@ -152,6 +156,8 @@ int launch_oneshot(int op, int kind, const OneShotArgs &a, size_t esize, const L
 int launch_pipe_reduce(int op, int kind, const PipeArgs &a, const LaunchCfg &cfg);
 // data-movement pipeline modes (AG / BC)
 int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg);
+// one-shot allgather / broadcast (small messages; a.mv = 1 / 2)
+int launch_oneshot_mv(const OneShotArgs &a, const LaunchCfg &cfg);
 int launch_pack_strided(const void *src, void *dst, size_t nblocks, size_t blk, size_t stride,
                         int unpack, hipStream_t stream, Done done = Done{});
 // MPI_Init: one empty kernel per translation unit (loads every code object; timed there)

@@ -1597,6 +1597,36 @@ static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void
         if (!in_place) hipMemcpyAsync(recvbuf, src, bytes, hipMemcpyDefault, st);
         return finish(st, false);
     }
+    // small blocks of whole 16-byte vectors: the one-shot kernel (one flag exchange; the choice reads
+    // only the size and the node's shared limits, so every rank makes it alike)
+    if (bytes % 16 == 0 && bytes <= std::min(w.oneshot_max, w.slot_bytes)) {
+        char *od = direct ? (char *)recvbuf : (char *)get_scratch(1, bytes * n);
+        if (!od) return E_NO_MEM;
+        const char *os = in_place ? od + (size_t)me * bytes : (const char *)sendbuf;
+        if (in_place && !direct) {
+            hipMemcpyAsync(od + (size_t)me * bytes, (const char *)recvbuf + (size_t)me * bytes, bytes, hipMemcpyDefault, st);
+        } else if (!in_place && !(is_device(sendbuf) && (uintptr_t)sendbuf % 16 == 0)) {
+            char *t = (char *)get_scratch(0, bytes);
+            if (!t) return E_NO_MEM;
+            hipMemcpyAsync(t, sendbuf, bytes, hipMemcpyDefault, st);
+            os = t;
+        }
+        OneShotArgs a{};
+        oneshot_common(a, st);
+        a.mv = 1;
+        a.send = os;
+        a.recv = od;
+        a.count = bytes;
+        a.nvec = bytes / 16;
+        a.pitch = bytes;
+        LaunchCfg cfg = coll_cfg(oneshot_grid(a.nvec, grid_cap()), st);
+        tmark0(st);
+        rc = launch_oneshot_mv(a, cfg);
+        tmark1(st);
+        if (rc) return rc;
+        if (!direct && enq_copy_last(recvbuf, od, bytes * n, st) != hipSuccess) return E_INTERN;
+        return finish(st, w.timing);
+    }
     const size_t mis = ((size_t)me * pitch) & 15;
     if (!(direct && in_place) && !(is_device(src) && (uintptr_t)src % 16 == mis)) {
         char *t = (char *)get_scratch(0, bytes + 16);
@@ -1636,6 +1666,25 @@ static int bcast_node(void *buffer, size_t bytes, int root, void *stream) {
         buf = (char *)get_scratch(1, bytes);
         if (!buf) return E_NO_MEM;
         if (w.rank == root) hipMemcpyAsync(buf, buffer, bytes, hipMemcpyDefault, st);
+    }
+    // small messages: the one-shot kernel (the root pushes its buffer into every peer's arena slot,
+    // one flag exchange); the choice reads only the size and the node's shared limits
+    if (bytes <= std::min(w.oneshot_max, w.slot_bytes)) {
+        OneShotArgs a{};
+        oneshot_common(a, st);
+        a.mv = 2;
+        a.root = root;
+        a.send = buf;
+        a.recv = buf;
+        a.count = bytes;
+        a.nvec = bytes / 16;
+        LaunchCfg cfg = coll_cfg(oneshot_grid(a.nvec, grid_cap()), st);
+        tmark0(st);
+        rc = launch_oneshot_mv(a, cfg);
+        tmark1(st);
+        if (rc) return rc;
+        if (!direct && w.rank != root && enq_copy_last(buffer, buf, bytes, st) != hipSuccess) return E_INTERN;
+        return finish(st, w.timing);
     }
     PipeArgs a{};
     a.mode = PIPE_BC;
@@ -3093,8 +3142,9 @@ namespace mv2 {
 //   one-shot allreduce (6 sizes x 2 halves), one-shot reduce-scatter (3 x 2), pipelined allreduce
 //   (ring order, 4 MiB, x 4; butterfly order x 2; ring + remainder), a multi-round pipelined
 //   allreduce (small rounds: both parities inside one call) x 2, pipelined reduce-scatter,
-//   allgather and broadcast x 2 each, and, with the graph lane, a captured one-shot and a
-//   captured pipelined allreduce replayed 3 times each (its own arenas and device sequence).
+//   allgather and broadcast x 2 each, one-shot allgather and broadcast x 2 each, and, with the
+//   graph lane, a captured one-shot and a captured pipelined allreduce replayed 3 times each (its
+//   own arenas and device sequence).
 // The per-call mismatch counts are read once at the end; the verdict is agreed through the
 // host control segment.  On a mismatch every rank falls back to the full system-scope release
 // and runs the whole set again; a second failure fails MPI_Init instead of returning wrong
@@ -3194,6 +3244,22 @@ int coll_selftest() {
             fill(sb, c, k, me);
             if (!rc) rc = allgather_node(sb, rb, c * 4, nullptr);
             check(rb, c * n, k, 2, (int)c, 0, "pipelined allgather");
+        }
+        // one-shot allgather and broadcast (k_oneshot_mv): 16-byte blocks, and a broadcast with a tail
+        const size_t os_ag[2] = {64, 4096}, os_bc[2] = {3, 16387};
+        for (int i = 0; i < 2 && !rc; ++i) {
+            const int k = calls++;
+            fill(sb, os_ag[i], k, me);
+            if (!rc) rc = allgather_node(sb, rb, os_ag[i] * 4, nullptr);
+            check(rb, os_ag[i] * n, k, 2, (int)os_ag[i], 0, "one-shot allgather");
+        }
+        for (int i = 0; i < 2 && !rc; ++i) {
+            const int k = calls++;
+            const int root = i == 0 ? n - 1 : 0;
+            if (me == root) fill(rb, os_bc[i], k, root);
+            else if (!rc) rc = hipMemsetAsync(rb, 0x5A, os_bc[i] * 4, st) == hipSuccess ? 0 : E_INTERN;
+            if (!rc) rc = bcast_node(rb, os_bc[i] * 4, root, nullptr);
+            check(rb, os_bc[i], k, 1, root, 0, "one-shot broadcast");
         }
         for (int i = 0; i < 2 && !rc; ++i) {
             const int k = calls++;

@@ -539,7 +539,7 @@ def test_pipe_autotune_agrees_and_keeps_results(n, tmp_path):
     infos = [res("ti", r).view(np.int64) for r in range(n)]
     assert infos[0][0] == 1 and infos[0][3] >= 1 and infos[0][6] >= 1, infos[0]
     assert (16 << 10) <= infos[0][5] <= (256 << 10), infos[0]
-    assert infos[0][7] == 39, infos[0]  # MPI_Init's self-test: every cross-GPU kernel, graph lane included
+    assert infos[0][7] == 43, infos[0]  # MPI_Init's self-test: every cross-GPU kernel, graph lane included
     for r in range(1, n):
         assert np.array_equal(infos[r][:9], infos[0][:9]), (r, infos[r], infos[0])  # [9]: this rank's load time
     for case in cases[1:]:
