@@ -673,7 +673,8 @@ int pipe_autotune() {
 int oneshot_autotune() {
     World &w = world();
     const int MPI_FLOAT_H = 0x4c00040a, MPI_SUM_H = 0x58000003;
-    const size_t top = w.oneshot_max < w.slot_bytes ? w.oneshot_max : w.slot_bytes;
+    // probe up to the slot (1 MiB when the node tunes, world.cpp), or to an explicit MV2AMD_ONESHOT_MAX
+    const size_t top = getenv("MV2AMD_ONESHOT_MAX") ? std::min(w.oneshot_max, w.slot_bytes) : w.slot_bytes;
     void *sb = nullptr, *rb = nullptr;
     if (top < ((size_t)32 << 10) || hipMalloc(&sb, top) != hipSuccess || hipMalloc(&rb, top) != hipSuccess) {
         if (sb) hipFree(sb);
@@ -688,7 +689,7 @@ int oneshot_autotune() {
     int rc = 0;
     for (int i = 0; i < ns && !rc; ++i) {
         for (int path = 0; path < 2 && !rc; ++path) {  // 0: one-shot, 1: pipelined
-            w.oneshot_max = path ? 0 : keep;
+            w.oneshot_max = path ? 0 : top;  // one-shot up to the probed size, or never
             double best = 1e30;
             for (int it = 0; it < 6 && !rc; ++it) {
                 host_barrier();

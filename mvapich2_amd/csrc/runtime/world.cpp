@@ -754,6 +754,17 @@ int world_init() {
             }
             hipMemset(w.sig, 0, sig_bytes);
             w.slot_bytes = (w.oneshot_max + 4095) & ~(size_t)4095;
+            // when MPI_Init will time the one-shot / pipelined crossover on this node's links (one
+            // rank per GPU, or MV2AMD_PIPE_AUTOTUNE=1) and no limit is set, the slots hold up to
+            // 1 MiB so that the probe can find a crossover above the 256 KiB default: on xGMI a
+            // one-shot call of 512 KiB - 1 MiB moves (n-1) x size per rank in one flag exchange
+            // against the pipelined kernel's two (coll.cpp oneshot_autotune)
+            {
+                const long at = env_long("MV2AMD_PIPE_AUTOTUNE", -1);
+                const bool tunes = at == 1 || (at < 0 && w.nshare == 1);
+                if (tunes && !getenv("MV2AMD_ONESHOT_MAX") && !getenv("MV2AMD_PIPE_GRID") && !getenv("MV2AMD_PIPE_SUB"))
+                    w.slot_bytes = std::max(w.slot_bytes, (size_t)1 << 20);
+            }
             const size_t arena_bytes = 2 * (size_t)kMaxRanks * w.slot_bytes;
             if (hipExtMallocWithFlags((void **)&w.arena, arena_bytes, hipDeviceMallocUncached) != hipSuccess) {
                 MV2_ERR("hipExtMallocWithFlags(uncached) for the one-shot arena failed");
