@@ -266,7 +266,11 @@ int mv2h_set_tuning(const char *key, long value);
 /* runtime facts: "nshare" (most ranks sharing one GPU), "device", "cus", "light_release", "oneshot_max",
  * "pipe_grid" / "pipe_sub" (pipelined kernels' tiling), "pipe_tuned" (1: chosen by the MPI_Init
  * autotune), "tune_n" and per candidate k "tune_grid_<k>", "tune_sub_<k>", "tune_us_<k>" (max over ranks),
- * "init_us" / "selftest_us" / "autotune_us" (this rank's MPI_Init wall time and its parts) */
+ * "init_us" / "hip_init_us" / "code_load_us" / "selftest_us" / "autotune_us" (this rank's MPI_Init
+ * wall time and its parts), "selftest_calls" (collective calls MPI_Init's self-test checked),
+ * "call_allocs" (device allocations made inside MPI calls: scratch growth, pooled temporaries),
+ * "hw_queues_set" (GPU_MAX_HW_QUEUES set before HIP started; negative: wanted, but HIP was already
+ * running) */
 int mv2h_get_info(const char *key, long *value);
 
 #ifdef __cplusplus
