@@ -287,6 +287,15 @@ int pack_impl(const char *in, int count, MPI_Datatype dt, char *out, bool unpack
 
 bool dtype_valid(MPI_Datatype dt) { return mv2::dtype_lookup(dt) != nullptr || derived(dt) != nullptr; }
 bool dtype_is_builtin(MPI_Datatype dt) { return mv2::dtype_lookup(dt) != nullptr; }
+bool dtype_committed(MPI_Datatype dt) {
+    if (mv2::dtype_lookup(dt)) return true;
+    Derived *d = derived(dt);
+    return d && d->committed;
+}
+long dtype_true_lb(MPI_Datatype dt) {
+    Derived *d = derived(dt);
+    return d ? d->true_lb : 0;
+}
 bool dtype_is_contiguous(MPI_Datatype dt) {
     // builtin pair types carry padding; copying it with the data is harmless for movement-only collectives
     if (mv2::dtype_lookup(dt)) return true;
@@ -495,7 +504,10 @@ int MPI_Type_create_resized(MPI_Datatype old, MPI_Aint lb, MPI_Aint extent, MPI_
 int PMPI_Type_dup(MPI_Datatype old, MPI_Datatype *nt) {
     long lb = 0, ext = 0;
     if (!type_bounds(old, lb, ext)) return MPI_ERR_TYPE;
-    return PMPI_Type_create_resized(old, lb, ext, nt);
+    const int rc = PMPI_Type_create_resized(old, lb, ext, nt);
+    // the copy has the committed state of the original, a builtin's copy is committed (MPI-3.1 §4.1.10)
+    if (!rc) derived(*nt)->committed = dtype_committed(old);
+    return rc;
 }
 int MPI_Type_dup(MPI_Datatype old, MPI_Datatype *nt) WEAK(MPI_Type_dup);
 
@@ -576,12 +588,18 @@ int PMPI_Pack_size(int incount, MPI_Datatype dt, MPI_Comm, int *size) {
 }
 int MPI_Pack_size(int incount, MPI_Datatype dt, MPI_Comm comm, int *size) WEAK(MPI_Pack_size);
 
-int PMPI_Pack(const void *inbuf, int incount, MPI_Datatype dt, void *outbuf, int outsize, int *position, MPI_Comm) {
+// Argument checks in pack.c:207-276's order: communicator, counts, null output buffer or
+// position (MPI_ERR_ARG), datatype valid and committed, then a packed size that does not fit
+// in outsize - *position: MPI_ERR_ARG (**argpackbuf), not MPI_ERR_TRUNCATE
+int PMPI_Pack(const void *inbuf, int incount, MPI_Datatype dt, void *outbuf, int outsize, int *position,
+              MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
-    if (incount < 0) return MPI_ERR_COUNT;
+    if (comm != MPI_COMM_WORLD && comm != MPI_COMM_SELF) return MPI_ERR_COMM;
+    if (incount < 0 || outsize < 0) return MPI_ERR_COUNT;
+    if ((incount > 0 && !outbuf) || !position) return MPI_ERR_ARG;
+    if (!dtype_valid(dt) || !dtype_committed(dt)) return MPI_ERR_TYPE;
     const long s = dtype_size(dt);
-    if (s < 0) return MPI_ERR_TYPE;
-    if (*position + s * incount > outsize) return MPI_ERR_TRUNCATE;
+    if (*position < 0 || s * incount > (long)outsize - *position) return MPI_ERR_ARG;
     if (incount == 0) return MPI_SUCCESS;
     int rc = pack_impl((const char *)inbuf, incount, dt, (char *)outbuf + *position, false);
     if (!rc) *position += (int)(s * incount);
@@ -589,12 +607,18 @@ int PMPI_Pack(const void *inbuf, int incount, MPI_Datatype dt, void *outbuf, int
 }
 int MPI_Pack(const void *inbuf, int incount, MPI_Datatype dt, void *outbuf, int outsize, int *position, MPI_Comm comm) WEAK(MPI_Pack);
 
-int PMPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount, MPI_Datatype dt, MPI_Comm) {
+// Argument checks of unpack.c:207-229: null input buffer (MPI_ERR_ARG), counts, communicator,
+// datatype valid and committed.  The reference does not check the packed size against insize
+// (its unpack reads past the buffer); here that is MPI_ERR_TRUNCATE.
+int PMPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount, MPI_Datatype dt,
+                MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
-    if (outcount < 0) return MPI_ERR_COUNT;
+    if ((insize > 0 && !inbuf) || !position) return MPI_ERR_ARG;
+    if (insize < 0 || outcount < 0) return MPI_ERR_COUNT;
+    if (comm != MPI_COMM_WORLD && comm != MPI_COMM_SELF) return MPI_ERR_COMM;
+    if (!dtype_valid(dt) || !dtype_committed(dt)) return MPI_ERR_TYPE;
     const long s = dtype_size(dt);
-    if (s < 0) return MPI_ERR_TYPE;
-    if (*position + s * outcount > insize) return MPI_ERR_TRUNCATE;
+    if (*position < 0 || *position + s * outcount > insize) return MPI_ERR_TRUNCATE;
     if (outcount == 0) return MPI_SUCCESS;
     int rc = pack_impl((const char *)inbuf + *position, outcount, dt, (char *)outbuf, true);
     if (!rc) *position += (int)(s * outcount);

@@ -5,6 +5,9 @@
 bool dtype_valid(MPI_Datatype dt);
 bool dtype_is_builtin(MPI_Datatype dt);
 bool dtype_is_contiguous(MPI_Datatype dt);
+// builtin types, and derived types after MPI_Type_commit (MPID_Datatype_committed_ptr)
+bool dtype_committed(MPI_Datatype dt);
+long dtype_true_lb(MPI_Datatype dt);
 long dtype_size(MPI_Datatype dt);
 long dtype_extent(MPI_Datatype dt);
 // bytes from the first to one past the last byte touched by `count` elements (lb = 0)

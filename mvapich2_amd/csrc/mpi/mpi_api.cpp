@@ -35,7 +35,7 @@ extern "C" int PMPI_Type_get_extent(MPI_Datatype dt, MPI_Aint *lb, MPI_Aint *ext
 namespace {
 
 std::recursive_mutex g_cs;  // global critical section (allreduce.c:838)
-MPI_Errhandler g_eh[2] = {MPI_ERRORS_ARE_FATAL, MPI_ERRORS_ARE_FATAL};
+MPI_Errhandler g_eh[2] = {MPI_ERRORS_ARE_FATAL, MPI_ERRHANDLER_NULL};  // SELF: unset, WORLD's applies
 bool g_initialized = false, g_finalized = false;
 
 struct UserOp {
@@ -71,11 +71,13 @@ int comm_index(MPI_Comm c) {
     return -1;
 }
 
-// MPIR_Err_return_comm (allreduce.c:956): fatal handler aborts, return handler passes the code
+// MPIR_Err_return_comm (allreduce.c:956, errutil.c:249-289): fatal handler aborts, return
+// handler passes the code; an invalid communicator, or one whose handler was never set
+// (MPI_COMM_SELF's until MPI_Comm_set_errhandler), takes MPI_COMM_WORLD's handler
 int err_return(MPI_Comm comm, int code, const char *fn) {
     if (code == MPI_SUCCESS) return code;
     const int ci = comm_index(comm);
-    const MPI_Errhandler eh = ci >= 0 ? g_eh[ci] : MPI_ERRORS_ARE_FATAL;
+    const MPI_Errhandler eh = ci >= 0 && g_eh[ci] != MPI_ERRHANDLER_NULL ? g_eh[ci] : g_eh[0];
     if (eh == MPI_ERRORS_ARE_FATAL) {
         fprintf(stderr, "[mv2amd rank %d] Fatal error in %s: %s\n", mv2h_rank(), fn, err_name(code));
         fflush(stderr);
@@ -334,7 +336,7 @@ int MPI_Errhandler_set(MPI_Comm comm, MPI_Errhandler eh) WEAK(MPI_Errhandler_set
 int PMPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler *eh) {
     const int ci = comm_index(comm);
     if (ci < 0) return MPI_ERR_COMM;
-    *eh = g_eh[ci];
+    *eh = g_eh[ci] == MPI_ERRHANDLER_NULL ? MPI_ERRORS_ARE_FATAL : g_eh[ci];  // comm_get_errhandler.c: unset reads FATAL
     return MPI_SUCCESS;
 }
 int MPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler *eh) WEAK(MPI_Comm_get_errhandler);
@@ -417,8 +419,11 @@ int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype
     if (count < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COUNT, fn);
     if (!op_valid(op)) return err_return(MPI_COMM_WORLD, MPI_ERR_OP, fn);
     if (!dtype_valid(dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_TYPE, fn);
+    if (!dtype_committed(dt)) return err_return(MPI_COMM_WORLD, MPI_ERR_TYPE, fn);
     if (count == 0) return MPI_SUCCESS;
-    if (inbuf == MPI_IN_PLACE || inoutbuf == MPI_IN_PLACE) return err_return(MPI_COMM_WORLD, MPI_ERR_BUFFER, fn);
+    // reduce_local.c:233-237: aliased operands (MPIR_ERRTEST_ALIAS_COLL), then MPI_IN_PLACE
+    if (inbuf == inoutbuf || inbuf == MPI_IN_PLACE || inoutbuf == MPI_IN_PLACE)
+        return err_return(MPI_COMM_WORLD, MPI_ERR_BUFFER, fn);
     if (UserOp *u = user_op(op)) return err_return(MPI_COMM_WORLD, user_reduce_local(inbuf, inoutbuf, count, dt, u), fn);
     return err_return(MPI_COMM_WORLD, builtin_reduce_local(inbuf, inoutbuf, count, dt, op), fn);
 }
@@ -493,21 +498,82 @@ int MPIR_Op_errno(void) {
     return e;
 }
 
-static int coll_checks(MPI_Comm comm, int count, MPI_Datatype dt, MPI_Op op) {
+// The buffer checks of the reference's MPI layer, MPI_ERR_BUFFER each (mpierrs.h):
+// MPIR_ERRTEST_USERBUFFER (:313-331) — no buffer for count > 0 elements of a builtin type, or of
+// a derived type whose true lb is 0 and size > 0 (a null buffer is MPI_BOTTOM otherwise);
+// MPIR_ERRTEST_{SEND,RECV,}BUF_INPLACE (:274-301) — MPI_IN_PLACE where the call has no in-place
+// form; MPIR_ERRTEST_ALIAS_COLL (:132-140, MPIR_CVAR_COLL_ALIAS_CHECK's default 1) — the send
+// buffer is the receive buffer.
+static bool null_userbuf(const void *buf, long count, MPI_Datatype dt) {
+    if (count <= 0 || buf) return false;
+    return dtype_is_builtin(dt) || (dtype_valid(dt) && dtype_true_lb(dt) == 0 && dtype_size(dt) > 0);
+}
+static bool inplace_buf(const void *buf, long count) { return count > 0 && buf == MPI_IN_PLACE; }
+
+// allreduce.c:880-888
+static int allreduce_buf_checks(const void *sendbuf, const void *recvbuf, int count, MPI_Datatype dt) {
+    if (count != 0 && sendbuf != MPI_IN_PLACE && sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    if (sendbuf != MPI_IN_PLACE && null_userbuf(sendbuf, count, dt)) return MPI_ERR_BUFFER;
+    if (inplace_buf(recvbuf, count) || null_userbuf(recvbuf, count, dt)) return MPI_ERR_BUFFER;
+    return MPI_SUCCESS;
+}
+
+// reduce.c:1190-1202: the receive buffer matters at the root only; elsewhere MPI_IN_PLACE is
+// not a send buffer
+static int reduce_buf_checks(const void *sendbuf, const void *recvbuf, int count, MPI_Datatype dt, bool at_root) {
+    if (sendbuf != MPI_IN_PLACE && null_userbuf(sendbuf, count, dt)) return MPI_ERR_BUFFER;
+    if (!at_root) return inplace_buf(sendbuf, count) ? MPI_ERR_BUFFER : MPI_SUCCESS;
+    if (inplace_buf(recvbuf, count) || null_userbuf(recvbuf, count, dt)) return MPI_ERR_BUFFER;
+    if (count != 0 && sendbuf != MPI_IN_PLACE && sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    return MPI_SUCCESS;
+}
+
+// red_scat.c:1182-1189 (and red_scat_block.c:1147-1154, the same with every count equal)
+static int reduce_scatter_buf_checks(const void *sendbuf, const void *recvbuf, long mine, long sum, MPI_Datatype dt) {
+    if (inplace_buf(recvbuf, mine)) return MPI_ERR_BUFFER;
+    if (sendbuf != MPI_IN_PLACE && sum != 0 && sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    if (null_userbuf(recvbuf, mine, dt) || null_userbuf(sendbuf, sum, dt)) return MPI_ERR_BUFFER;
+    return MPI_SUCCESS;
+}
+
+// allgather.c:952-958, before any other argument check: the send buffer is this rank's block
+// of the receive buffer, the block measured in recvtype's size (as the reference measures it)
+static bool allgather_alias(const void *sendbuf, int sendcount, MPI_Datatype sendtype, const void *recvbuf,
+                            int recvcount, MPI_Datatype recvtype, int rank) {
+    return sendbuf != MPI_IN_PLACE && sendtype == recvtype && recvcount != 0 && sendcount != 0 &&
+           dtype_valid(recvtype) && sendbuf == (const char *)recvbuf + (long)rank * recvcount * dtype_size(recvtype);
+}
+
+// allgather.c:961-987, after the counts and types
+static int allgather_buf_checks(const void *sendbuf, int sendcount, MPI_Datatype sendtype, const void *recvbuf,
+                                int recvcount, MPI_Datatype recvtype) {
+    if (sendbuf != MPI_IN_PLACE && null_userbuf(sendbuf, sendcount, sendtype)) return MPI_ERR_BUFFER;
+    if (inplace_buf(recvbuf, recvcount) || null_userbuf(recvbuf, recvcount, recvtype)) return MPI_ERR_BUFFER;
+    return MPI_SUCCESS;
+}
+
+// The checks every reduction shares, in allreduce.c:863-899's order: communicator, count,
+// datatype, op handle, a derived type committed, then the call's buffer checks (buf_rc,
+// computed by the caller), then the op against the type (MPIR_OP_HDL_TO_DTYPE_FN)
+static int coll_checks(MPI_Comm comm, int count, MPI_Datatype dt, MPI_Op op, int buf_rc = MPI_SUCCESS) {
     if (!g_initialized || g_finalized) return MPI_ERR_OTHER;
     if (comm_index(comm) < 0) return MPI_ERR_COMM;
     if (count < 0) return MPI_ERR_COUNT;
     if (!dtype_valid(dt)) return MPI_ERR_TYPE;
     if (!op_valid(op)) return MPI_ERR_OP;
+    if (!dtype_committed(dt)) return MPI_ERR_TYPE;
+    if (buf_rc) return buf_rc;
     if (is_builtin_op(op) && !dtype_is_builtin(dt)) return MPI_ERR_OP;  // e.g. opsum.c:119-121
     if (is_builtin_op(op) && mv2h_op_check(op, dt)) return MPI_ERR_OP;
     return MPI_SUCCESS;
 }
 
+static int comm_rank_of(MPI_Comm comm) { return comm == MPI_COMM_SELF ? 0 : mv2h_rank(); }
+
 int PMPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPI_Allreduce";
-    int rc = coll_checks(comm, count, dt, op);
+    int rc = coll_checks(comm, count, dt, op, allreduce_buf_checks(sendbuf, recvbuf, count, dt));
     if (rc) return err_return(comm, rc, fn);
     if (count == 0) return MPI_SUCCESS;
     if (comm == MPI_COMM_SELF) {
@@ -532,10 +598,12 @@ int MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt
 int PMPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPI_Reduce";
-    int rc = coll_checks(comm, count, dt, op);
-    if (rc) return err_return(comm, rc, fn);
+    if (!g_initialized || g_finalized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(comm, MPI_ERR_COMM, fn);
     int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
-    if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);  // reduce.c:1178, before the count
+    int rc = coll_checks(comm, count, dt, op, reduce_buf_checks(sendbuf, recvbuf, count, dt, comm_rank_of(comm) == root));
+    if (rc) return err_return(comm, rc, fn);
     if (count == 0) return MPI_SUCCESS;
     if (comm == MPI_COMM_SELF) {
         if (sendbuf != MPI_IN_PLACE && sendbuf != recvbuf) {
@@ -560,16 +628,19 @@ int PMPI_Reduce_scatter(const void *sendbuf, void *recvbuf, const int recvcounts
                         MPI_Comm comm) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPI_Reduce_scatter";
-    int rc = coll_checks(comm, 0, dt, op);
-    if (rc) return err_return(comm, rc, fn);
+    if (!g_initialized || g_finalized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(comm, MPI_ERR_COMM, fn);
     const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     std::vector<size_t> rc_sz(n);
     size_t total = 0;
-    for (int j = 0; j < n; ++j) {
+    for (int j = 0; j < n; ++j) {  // red_scat.c:1168-1171: the counts first
         if (recvcounts[j] < 0) return err_return(comm, MPI_ERR_COUNT, fn);
         rc_sz[j] = (size_t)recvcounts[j];
         total += rc_sz[j];
     }
+    int rc = coll_checks(comm, 0, dt, op,
+                         reduce_scatter_buf_checks(sendbuf, recvbuf, recvcounts[comm_rank_of(comm)], (long)total, dt));
+    if (rc) return err_return(comm, rc, fn);
     if (total == 0) return MPI_SUCCESS;
     if (UserOp *u = user_op(op))
         if (comm != MPI_COMM_SELF)
@@ -647,9 +718,15 @@ int PMPI_Allgather(const void *sendbuf, int sendcount, MPI_Datatype sendtype, vo
     const char *fn = "MPI_Allgather";
     if (!g_initialized) return err_return(comm, MPI_ERR_OTHER, fn);
     if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
+    if (allgather_alias(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, comm_rank_of(comm)))
+        return err_return(comm, MPI_ERR_BUFFER, fn);
     if (recvcount < 0 || (sendbuf != MPI_IN_PLACE && sendcount < 0)) return err_return(comm, MPI_ERR_COUNT, fn);
     if (!dtype_valid(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_valid(sendtype)))
         return err_return(comm, MPI_ERR_TYPE, fn);
+    if (!dtype_committed(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_committed(sendtype)))
+        return err_return(comm, MPI_ERR_TYPE, fn);
+    if (const int rc = allgather_buf_checks(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype))
+        return err_return(comm, rc, fn);
     if (!dtype_is_contiguous(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_is_contiguous(sendtype)))
         return err_return(comm, allgather_derived(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, comm), fn);
     const size_t rbytes = (size_t)dtype_span(recvtype, recvcount);
@@ -674,6 +751,8 @@ int PMPI_Bcast(void *buffer, int count, MPI_Datatype dt, int root, MPI_Comm comm
     if (!dtype_valid(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
     const int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (!dtype_committed(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
+    if (inplace_buf(buffer, count) || null_userbuf(buffer, count, dt)) return err_return(comm, MPI_ERR_BUFFER, fn);  // bcast.c:1581-1582
     if (count == 0 || size == 1) return MPI_SUCCESS;
     if (dtype_is_contiguous(dt)) return err_return(comm, mv2h_bcast(buffer, (size_t)dtype_span(dt, count), root, nullptr), fn);
     // derived (non-contiguous) type: pack on device at the root, broadcast the
@@ -709,7 +788,7 @@ int PMPIX_Allreduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_D
                             void *stream) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPIX_Allreduce_enqueue";
-    int rc = coll_checks(comm, count, dt, op);
+    int rc = coll_checks(comm, count, dt, op, allreduce_buf_checks(sendbuf, recvbuf, count, dt));
     if (!rc) rc = enqueue_arg_checks(dt, op, stream);
     if (rc) return err_return(comm, rc, fn);
     if (count == 0) return MPI_SUCCESS;
@@ -727,11 +806,13 @@ int PMPIX_Reduce_enqueue(const void *sendbuf, void *recvbuf, int count, MPI_Data
                          MPI_Comm comm, void *stream) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPIX_Reduce_enqueue";
-    int rc = coll_checks(comm, count, dt, op);
-    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
-    if (rc) return err_return(comm, rc, fn);
+    if (!g_initialized || g_finalized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(comm, MPI_ERR_COMM, fn);
     const int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    int rc = coll_checks(comm, count, dt, op, reduce_buf_checks(sendbuf, recvbuf, count, dt, comm_rank_of(comm) == root));
+    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
+    if (rc) return err_return(comm, rc, fn);
     if (count == 0) return MPI_SUCCESS;
     if (comm == MPI_COMM_SELF) return PMPIX_Allreduce_enqueue(sendbuf, recvbuf, count, dt, op, comm, stream);
     return err_return(comm, mv2h_reduce_enqueue(sendbuf, recvbuf, (size_t)count, dt, op, root, stream), fn);
@@ -743,9 +824,8 @@ int PMPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int r
                                  MPI_Comm comm, void *stream) {
     std::lock_guard<std::recursive_mutex> lk(g_cs);
     const char *fn = "MPIX_Reduce_scatter_enqueue";
-    int rc = coll_checks(comm, 0, dt, op);
-    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
-    if (rc) return err_return(comm, rc, fn);
+    if (!g_initialized || g_finalized) return err_return(comm, MPI_ERR_OTHER, fn);
+    if (comm_index(comm) < 0) return err_return(comm, MPI_ERR_COMM, fn);
     if (!recvcounts) return err_return(comm, MPI_ERR_ARG, fn);
     const int n = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     std::vector<size_t> rc_sz(n);
@@ -755,6 +835,10 @@ int PMPIX_Reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const int r
         rc_sz[j] = (size_t)recvcounts[j];
         total += rc_sz[j];
     }
+    int rc = coll_checks(comm, 0, dt, op,
+                         reduce_scatter_buf_checks(sendbuf, recvbuf, recvcounts[comm_rank_of(comm)], (long)total, dt));
+    if (!rc) rc = enqueue_arg_checks(dt, op, stream);
+    if (rc) return err_return(comm, rc, fn);
     if (total == 0) return MPI_SUCCESS;
     if (comm == MPI_COMM_SELF) return PMPIX_Allreduce_enqueue(sendbuf, recvbuf, recvcounts[0], dt, op, comm, stream);
     return err_return(comm, mv2h_reduce_scatter_enqueue(sendbuf, recvbuf, rc_sz.data(), dt, op, stream), fn);
@@ -769,9 +853,15 @@ int PMPIX_Allgather_enqueue(const void *sendbuf, int sendcount, MPI_Datatype sen
     if (!g_initialized) return err_return(comm, MPI_ERR_OTHER, fn);
     if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
     if (!stream) return err_return(comm, MPI_ERR_ARG, fn);
+    if (allgather_alias(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, comm_rank_of(comm)))
+        return err_return(comm, MPI_ERR_BUFFER, fn);
     if (recvcount < 0 || (sendbuf != MPI_IN_PLACE && sendcount < 0)) return err_return(comm, MPI_ERR_COUNT, fn);
     if (!dtype_valid(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_valid(sendtype)))
         return err_return(comm, MPI_ERR_TYPE, fn);
+    if (!dtype_committed(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_committed(sendtype)))
+        return err_return(comm, MPI_ERR_TYPE, fn);
+    if (const int rc = allgather_buf_checks(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype))
+        return err_return(comm, rc, fn);
     if (!dtype_is_contiguous(recvtype) || (sendbuf != MPI_IN_PLACE && !dtype_is_contiguous(sendtype)))
         return err_return(comm, MPI_ERR_TYPE, fn);
     const size_t rbytes = (size_t)dtype_span(recvtype, recvcount);
@@ -795,10 +885,11 @@ int PMPIX_Bcast_enqueue(void *buffer, int count, MPI_Datatype dt, int root, MPI_
     if (comm_index(comm) < 0) return err_return(MPI_COMM_WORLD, MPI_ERR_COMM, fn);
     if (!stream) return err_return(comm, MPI_ERR_ARG, fn);
     if (count < 0) return err_return(comm, MPI_ERR_COUNT, fn);
-    if (!dtype_valid(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
+    if (!dtype_valid(dt) || !dtype_committed(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
     if (!dtype_is_contiguous(dt)) return err_return(comm, MPI_ERR_TYPE, fn);
     const int size = comm == MPI_COMM_SELF ? 1 : mv2h_size();
     if (root < 0 || root >= size) return err_return(comm, MPI_ERR_ROOT, fn);
+    if (inplace_buf(buffer, count) || null_userbuf(buffer, count, dt)) return err_return(comm, MPI_ERR_BUFFER, fn);
     if (count == 0 || size == 1) return MPI_SUCCESS;
     return err_return(comm, mv2h_bcast_enqueue(buffer, (size_t)dtype_span(dt, count), root, stream), fn);
 }
@@ -931,7 +1022,7 @@ int p2p_checks(MPI_Comm comm, int count, MPI_Datatype dt, int tag, bool recv) {
     if (!g_initialized) return MPI_ERR_OTHER;
     if (comm != MPI_COMM_WORLD) return comm_index(comm) < 0 ? MPI_ERR_COMM : MPI_ERR_UNSUPPORTED_OPERATION;
     if (count < 0) return MPI_ERR_COUNT;
-    if (!dtype_valid(dt)) return MPI_ERR_TYPE;
+    if (!dtype_valid(dt) || !dtype_committed(dt)) return MPI_ERR_TYPE;
     if (recv ? (tag < 0 && tag != MPI_ANY_TAG) : tag < 0) return MPI_ERR_TAG;
     return MPI_SUCCESS;
 }

@@ -333,6 +333,70 @@ def derived_no_alloc(L, case, rank, n):
     return np.array([bad, allocs, tot / iters * 1e6], dtype=np.float64)
 
 
+def arg_checks(L, rank, n):
+    """The reference's argument checks on the device path (mpierrs.h buffer tests, committed
+    types, MPI_Pack's space check): every call below fails on every rank that makes it, before
+    entering a collective, with the class the reference returns; then one valid MPI_Allreduce
+    proves no rank was left inside a collective.  Returns [got, want] pairs per call, and the
+    valid call's wrong elements last."""
+    I, SUM = TYPES["MPI_INT"][0], OPS["MPI_SUM"]
+    P = ctypes.c_void_p
+    IN_PLACE, NULL = P(-1 & 0xFFFFFFFFFFFFFFFF), P(0)
+    BUF, TYPE, COMM, ARG = 1, 3, 5, 12
+    x = np.arange(4 * n, dtype=np.int32) + 10 * rank
+    a, b = m.DeviceBuffer.from_array(x), m.DeviceBuffer(16 * n)
+    vt, vd, vu = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert L.MPI_Type_vector(2, 1, 2, I, ctypes.byref(vt)) == 0 and L.MPI_Type_commit(ctypes.byref(vt)) == 0
+    assert L.MPI_Type_dup(vt.value, ctypes.byref(vd)) == 0  # a committed type's copy is committed
+    assert L.MPI_Type_vector(2, 1, 2, I, ctypes.byref(vu)) == 0  # never committed
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+    counts = (ctypes.c_int * n)(*([4] * n))
+    req, pos = ctypes.c_int(-7), ctypes.c_int(0)
+    out = m.DeviceBuffer(64)
+    calls = [
+        (L.MPI_Reduce_local(P(a.ptr), P(a.ptr), 4, I, SUM), BUF),  # reduce_local.c:234
+        (L.MPI_Allreduce(P(a.ptr), P(a.ptr), 4, I, SUM, WORLD), BUF),  # allreduce.c:881
+        (L.MPI_Allreduce(P(a.ptr), IN_PLACE, 4, I, SUM, WORLD), BUF),  # :887
+        (L.MPI_Allreduce(NULL, P(b.ptr), 4, I, SUM, WORLD), BUF),  # :885
+        (L.MPI_Allreduce(P(a.ptr), NULL, 4, I, SUM, WORLD), BUF),  # :888
+        (L.MPI_Allreduce(P(a.ptr), P(a.ptr), 0, I, SUM, WORLD), 0),  # count 0: no alias test, no call
+        # reduce.c:1194-1202: aliasing at the root; MPI_IN_PLACE is no send buffer elsewhere
+        (L.MPI_Reduce(P(a.ptr), P(a.ptr), 4, I, SUM, 0, WORLD) if rank == 0 else
+         L.MPI_Reduce(IN_PLACE, P(b.ptr), 4, I, SUM, 0, WORLD), BUF),
+        (L.MPI_Reduce_scatter(P(a.ptr), P(a.ptr), counts, I, SUM, WORLD), BUF),  # red_scat.c:1186
+        (L.MPI_Reduce_scatter_block(P(a.ptr), P(a.ptr), 4, I, SUM, WORLD), BUF),  # red_scat_block.c:1151
+        (L.MPI_Reduce_scatter_block(P(a.ptr), IN_PLACE, 4, I, SUM, WORLD), BUF),  # :1147
+        # allgather.c:957: the send buffer is this rank's block of the receive buffer
+        (L.MPI_Allgather(P(a.ptr + 16 * rank), 4, I, P(a.ptr), 4, I, WORLD), BUF),
+        (L.MPI_Allgather(P(a.ptr), 4, I, IN_PLACE, 4, I, WORLD), BUF),  # :976
+        (L.MPI_Bcast(NULL, 4, I, 0, WORLD), BUF),  # bcast.c:1582
+        (L.MPI_Bcast(IN_PLACE, 4, I, 0, WORLD), BUF),  # :1581
+        # uncommitted derived types (MPID_Datatype_committed_ptr)
+        (L.MPI_Bcast(P(b.ptr), 1, vu.value, 0, WORLD), TYPE),
+        (L.MPI_Allgather(P(a.ptr), 1, vu.value, P(b.ptr), 1, vu.value, WORLD), TYPE),
+        (L.MPI_Pack(P(a.ptr), 1, vu.value, P(out.ptr), 64, ctypes.byref(pos), WORLD), TYPE),  # pack.c:241
+        (L.MPI_Pack(P(a.ptr), 1, vd.value, P(out.ptr), 64, ctypes.byref(pos), WORLD), 0),
+        (L.MPI_Pack(P(a.ptr), 4, vt.value, P(out.ptr), 16, ctypes.byref(pos), WORLD), ARG),  # pack.c:272
+        (L.MPI_Pack(P(a.ptr), 1, vt.value, P(out.ptr), 64, ctypes.byref(pos), 0x1234), COMM),
+        (L.MPI_Iallreduce(P(a.ptr), P(a.ptr), 4, I, SUM, WORLD, ctypes.byref(req)), BUF),
+        (req.value, -7),  # no request was made
+        (L.MPIX_Allreduce_enqueue(P(a.ptr), P(a.ptr), 4, I, SUM, WORLD, st), BUF),
+        (L.MPIX_Bcast_enqueue(NULL, 4, I, 0, WORLD, st), BUF),
+        # MPI_COMM_SELF has no handler of its own: MPI_COMM_WORLD's (ERRORS_RETURN here) applies
+        (L.MPI_Allreduce(P(a.ptr), P(a.ptr), 4, I, SUM, 0x44000001), BUF),
+    ]
+    assert hip.hipStreamSynchronize(st) == 0
+    hip.hipStreamDestroy(st)
+    for t in (vt, vd, vu):
+        L.MPI_Type_free(ctypes.byref(t))
+    assert L.MPI_Allreduce(P(a.ptr), P(b.ptr), 4 * n, I, SUM, WORLD) == 0
+    want = sum(np.arange(4 * n, dtype=np.int32) + 10 * r for r in range(n))
+    bad = int(np.count_nonzero(b.download(np.int32, count=4 * n) != want))
+    return np.array([v for c in calls for v in c] + [bad], dtype=np.int64)
+
+
 def collops_comm(L, rank, n):
     assert L.MV2AMD_Comm_attach(_COMM, rank, n) == 0
     return _COMM
@@ -590,6 +654,8 @@ def main():
             res = big_case(L, case, rank, n)
         elif k == "derived_no_alloc":
             res = derived_no_alloc(L, case, rank, n)
+        elif k == "arg_checks":
+            res = arg_checks(L, rank, n)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)
             vt = ctypes.c_int()

@@ -852,6 +852,22 @@ def test_derived_type_calls_make_no_device_allocations(n, tmp_path):
                                 "ranks": n, **lat}) + "\n")
 
 
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_argument_checks_follow_the_reference(n, tmp_path):
+    """The buffer checks of the reference's MPI layer (mpierrs.h MPIR_ERRTEST_ALIAS_COLL,
+    *_INPLACE, USERBUFFER), uncommitted derived types and MPI_Pack's space check return the
+    reference's error class on every rank, before any rank enters a collective: one valid
+    MPI_Allreduce afterwards completes with the right sums (mp_gpu_worker.arg_checks)."""
+    case = {"id": "args", "kind": "arg_checks"}
+    res = run_workers(n, [case], tmp_path)
+    for r in range(n):
+        got = res(case["id"], r)
+        pairs, bad = got[:-1].reshape(-1, 2), got[-1]
+        wrong = [(i, int(g), int(w)) for i, (g, w) in enumerate(pairs) if g != w]
+        assert not wrong, f"rank {r}: (call, got, want) {wrong}"
+        assert bad == 0, f"rank {r}: the valid MPI_Allreduce after the refused calls is wrong"
+
+
 def test_hw_queue_limit_reported_when_too_late(tmp_path):
     """Ranks sharing a GPU ask HIP for 2 hardware queues per process before HIP starts (world.cpp
     limit_hw_queues_if_shared: five ranks with 4 queues each starved a kernel for 30 s, r04f).
