@@ -397,6 +397,102 @@ def arg_checks(L, rank, n):
     return np.array([v for c in calls for v in c] + [bad], dtype=np.int64)
 
 
+def soak(L, case, rank, n):
+    """A long seeded sequence of small and mid-size calls back to back on the same buffers —
+    blocking, nonblocking and stream-ordered collectives of every kind, one-shot and pipelined
+    sizes, rotating roots, and point-to-point rings through the copy kernels — each result checked
+    in place against its closed form (int32 SUM / MAX / BXOR, exact whatever the order).  The
+    arenas' two slot parities, the epochs and both completion words turn over thousands of times,
+    which a visibility or slot-reuse hazard that strikes once in thousands of calls would not
+    survive.  Returns [wrong calls, calls made, first wrong call index or -1]."""
+    I = TYPES["MPI_INT"][0]
+    ops = [("MPI_SUM", OPS["MPI_SUM"]), ("MPI_MAX", OPS["MPI_MAX"]), ("MPI_BXOR", OPS["MPI_BXOR"])]
+    kinds = ["allreduce", "allreduce_inplace", "iallreduce", "enqueue", "reduce", "reduce_scatter_block",
+             "allgather", "bcast", "sendrecv"]
+    sizes = case.get("sizes", [1, 3, 64, 1000, 4096, 16385, 65536, 262143, 1 << 20])
+    rng = np.random.default_rng(case["seed"])  # the same sequence on every rank
+    mx = max(sizes)
+    base = (np.arange(mx * n, dtype=np.int64) * 2654435761) % (1 << 31)
+    sb, rb = m.DeviceBuffer(mx * n * 4), m.DeviceBuffer(mx * n * 4)
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+    P = ctypes.c_void_p
+    IN_PLACE = P(-1 & 0xFFFFFFFFFFFFFFFF)
+    req = ctypes.c_int()
+
+    def pat(r, i, cnt):
+        return (base[:cnt] + r * 131 + i * 7).astype(np.int32)
+
+    def fold(op, arrs):
+        out = arrs[0].astype(np.int64)
+        for a in arrs[1:]:
+            a = a.astype(np.int64)
+            out = out + a if op == "MPI_SUM" else (np.maximum(out, a) if op == "MPI_MAX" else out ^ a)
+        return out.astype(np.int32)
+
+    wrong, first = 0, -1
+    calls = case["calls"]
+    for i in range(calls):
+        k = kinds[int(rng.integers(len(kinds)))]
+        cnt = int(sizes[int(rng.integers(len(sizes)))])
+        oname, op = ops[int(rng.integers(len(ops)))]
+        root = int(rng.integers(n))
+        if k == "reduce_scatter_block" or k == "allgather":
+            cnt = max(1, cnt // n)
+        mine = pat(rank, i, cnt * (n if k == "reduce_scatter_block" else 1))
+        if k == "allreduce_inplace":
+            rb.upload(mine)
+        else:
+            sb.upload(mine)
+        rc = 0
+        if k == "allreduce":
+            rc = L.MPI_Allreduce(P(sb.ptr), P(rb.ptr), cnt, I, op, WORLD)
+        elif k == "allreduce_inplace":
+            rc = L.MPI_Allreduce(IN_PLACE, P(rb.ptr), cnt, I, op, WORLD)
+        elif k == "iallreduce":
+            rc = L.MPI_Iallreduce(P(sb.ptr), P(rb.ptr), cnt, I, op, WORLD, ctypes.byref(req))
+            rc = rc or L.MPI_Wait(ctypes.byref(req), None)
+        elif k == "enqueue":
+            rc = L.MPIX_Allreduce_enqueue(P(sb.ptr), P(rb.ptr), cnt, I, op, WORLD, st)
+            rc = rc or hip.hipStreamSynchronize(st)
+        elif k == "reduce":
+            rc = L.MPI_Reduce(P(sb.ptr), P(rb.ptr), cnt, I, op, root, WORLD)
+        elif k == "reduce_scatter_block":
+            rc = L.MPI_Reduce_scatter_block(P(sb.ptr), P(rb.ptr), cnt, I, op, WORLD)
+        elif k == "allgather":
+            rc = L.MPI_Allgather(P(sb.ptr), cnt, I, P(rb.ptr), cnt, I, WORLD)
+        elif k == "bcast":
+            if rank != root:
+                sb.upload(np.full(cnt, -5, dtype=np.int32))
+            rc = L.MPI_Bcast(P(sb.ptr), cnt, I, root, WORLD)
+        else:  # a ring of point-to-point messages
+            rc = L.MPI_Sendrecv(P(sb.ptr), cnt, I, (rank + 1) % n, i % 30000, P(rb.ptr), cnt, I, (rank - 1) % n,
+                                i % 30000, WORLD, None)
+        if rc:
+            raise RuntimeError(f"call {i} ({k}, {cnt}) returned {rc}")
+        if k in ("allreduce", "allreduce_inplace", "iallreduce", "enqueue"):
+            got, want = rb.download(np.int32, count=cnt), fold(oname, [pat(r, i, cnt) for r in range(n)])
+        elif k == "reduce":
+            if rank != root:
+                continue
+            got, want = rb.download(np.int32, count=cnt), fold(oname, [pat(r, i, cnt) for r in range(n)])
+        elif k == "reduce_scatter_block":
+            got = rb.download(np.int32, count=cnt)
+            want = fold(oname, [pat(r, i, cnt * n)[rank * cnt:(rank + 1) * cnt] for r in range(n)])
+        elif k == "allgather":
+            got, want = rb.download(np.int32, count=cnt * n), np.concatenate([pat(r, i, cnt) for r in range(n)])
+        elif k == "bcast":
+            got, want = sb.download(np.int32, count=cnt), pat(root, i, cnt)
+        else:
+            got, want = rb.download(np.int32, count=cnt), pat((rank - 1) % n, i, cnt)
+        if not np.array_equal(got, want):
+            wrong += 1
+            first = i if first < 0 else first
+    hip.hipStreamDestroy(st)
+    return np.array([wrong, calls, first], dtype=np.int64)
+
+
 def collops_comm(L, rank, n):
     assert L.MV2AMD_Comm_attach(_COMM, rank, n) == 0
     return _COMM
@@ -656,6 +752,8 @@ def main():
             res = derived_no_alloc(L, case, rank, n)
         elif k == "arg_checks":
             res = arg_checks(L, rank, n)
+        elif k == "soak":
+            res = soak(L, case, rank, n)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)
             vt = ctypes.c_int()

@@ -852,6 +852,21 @@ def test_derived_type_calls_make_no_device_allocations(n, tmp_path):
                                 "ranks": n, **lat}) + "\n")
 
 
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("n,calls,seed", [(2, 16000, 11), (4, 10000, 12), (8, 5000, 13)])
+def test_soak_thousands_of_calls(n, calls, seed, tmp_path):
+    """mp_gpu_worker.soak: thousands of blocking / nonblocking / stream-ordered collectives and
+    point-to-point rings back to back on the same buffers, every result checked against its
+    closed form (a visibility hazard that strikes once in thousands of calls
+    survives a suite of short tests).  MV2AMD_SOAK_CALLS scales the count for a long run."""
+    calls = int(os.environ.get("MV2AMD_SOAK_CALLS", calls))
+    case = {"id": "soak", "kind": "soak", "calls": calls, "seed": seed}
+    res = run_workers(n, [case], tmp_path, timeout=380)
+    for r in range(n):
+        wrong, made, first = (int(v) for v in res(case["id"], r))
+        assert made == calls and wrong == 0, f"rank {r}: {wrong} wrong calls of {made}, the first at {first}"
+
+
 @pytest.mark.parametrize("n", [1, 2, 3])
 def test_argument_checks_follow_the_reference(n, tmp_path):
     """The buffer checks of the reference's MPI layer (mpierrs.h MPIR_ERRTEST_ALIAS_COLL,
