@@ -852,16 +852,30 @@ def test_derived_type_calls_make_no_device_allocations(n, tmp_path):
                                 "ranks": n, **lat}) + "\n")
 
 
+SOAK = [  # (ranks, calls, seed, environment, ranks per emulated node)
+    (2, 16000, 11, {}, None), (4, 10000, 12, {}, None), (8, 5000, 13, {}, None),
+    # the full-release fallback a node adopts when the light release fails its self-test
+    (3, 5000, 14, {"MV2AMD_LIGHT_RELEASE": "0"}, None),
+    # small pipeline rounds and a narrow one-shot limit: many rounds and slot turns per call
+    (4, 4000, 15, {"MV2AMD_PIPE_GRID": "64", "MV2AMD_PIPE_SUB": str(16 << 10), "MV2AMD_ONESHOT_MAX": str(16 << 10)}, None),
+    # point-to-point on the copy engines instead of the copy kernels
+    (2, 4000, 16, {"MV2AMD_P2P_KERNEL_COPY": "0"}, None),
+    # two emulated nodes: two-level collectives, leaders over TCP
+    (4, 1500, 17, {}, 2),
+]
+
+
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("n,calls,seed", [(2, 16000, 11), (4, 10000, 12), (8, 5000, 13)])
-def test_soak_thousands_of_calls(n, calls, seed, tmp_path):
+@pytest.mark.parametrize("n,calls,seed,env,ppn", SOAK)
+def test_soak_thousands_of_calls(n, calls, seed, env, ppn, tmp_path):
     """mp_gpu_worker.soak: thousands of blocking / nonblocking / stream-ordered collectives and
     point-to-point rings back to back on the same buffers, every result checked against its
     closed form (a visibility hazard that strikes once in thousands of calls
-    survives a suite of short tests).  MV2AMD_SOAK_CALLS scales the count for a long run."""
+    survives a suite of short tests), with the protocol settings a node may adopt.
+    MV2AMD_SOAK_CALLS scales the count for a long run."""
     calls = int(os.environ.get("MV2AMD_SOAK_CALLS", calls))
     case = {"id": "soak", "kind": "soak", "calls": calls, "seed": seed}
-    res = run_workers(n, [case], tmp_path, timeout=380)
+    res = run_workers(n, [case], tmp_path, timeout=380, extra_env=env, ppn=ppn)
     for r in range(n):
         wrong, made, first = (int(v) for v in res(case["id"], r))
         assert made == calls and wrong == 0, f"rank {r}: {wrong} wrong calls of {made}, the first at {first}"

@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/r05s
 mkdir -p $O
 export TMPDIR=/tmp
-for spec in "2-100000:2-16000-11" "4-60000:4-10000-12" "8-30000:8-5000-13"; do
+for spec in "2-100000:2-16000-11-env0-None" "4-60000:4-10000-12-env1-None" "8-30000:8-5000-13-env2-None"; do
   calls=${spec%%:*}; calls=${calls#*-}; id=${spec#*:}
   MV2AMD_SOAK_CALLS=$calls timeout -k 10 420 python -u -m pytest -x -v -m gpu --timeout 400 --timeout-method thread \
     "tests/test_gpu_collectives_mp.py::test_soak_thousands_of_calls[$id]" --durations=1 > $O/soak_$id.log 2>&1 \
