@@ -71,8 +71,8 @@ int launch_pipe_copy(const PipeArgs &a, const LaunchCfg &cfg) {
 // rank raises its flag -- the non-roots of a broadcast too, so that no rank can reach call i + 2
 // while a peer still reads call i's half (the one-shot allreduce's argument) -- waits for its
 // peers' flags of workgroup b, and copies partition b of the slots it needs out of its own arena.
-// Blocks are 16-byte multiples (the host takes this path only then); a broadcast's tail bytes go
-// through workgroup 0.
+// Allgather blocks of 16-byte multiples move as vectors; a small block of any other size moves
+// byte by byte through workgroup 0 (nvec = 0), as does a broadcast's tail.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_oneshot_mv(OneShotArgs a) {
     const int blk = blockIdx.x, G = gridDim.x;
@@ -97,6 +97,7 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_mv(OneShotArgs a) {
 #pragma unroll
                 for (int j = 0; j < kMaxRanks; ++j)
                     if (j < a.n && j != a.me) a.arena_peer.p[j][myslot + e] = c;
+                if (!bc && a.send != a.recv + (size_t)a.me * a.pitch) a.recv[(size_t)a.me * a.pitch + e] = c;
             }
     }
     signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);

@@ -1598,15 +1598,19 @@ static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void
         if (!in_place) hipMemcpyAsync(recvbuf, src, bytes, hipMemcpyDefault, st);
         return finish(st, false);
     }
-    // small blocks of whole 16-byte vectors: the one-shot kernel (one flag exchange; the choice reads
-    // only the size and the node's shared limits, so every rank makes it alike)
-    if (bytes % 16 == 0 && bytes <= std::min(w.oneshot_max, w.slot_bytes)) {
+    // small blocks: the one-shot kernel (one flag exchange; the choice reads only the size and the
+    // node's shared limits, so every rank makes it alike).  Whole 16-byte vectors move as vectors;
+    // a block of up to kOneShotBytewise bytes of any other size moves byte by byte (osu_allgather
+    // 8 B at 2 shared ranks: 15.6 us through the pipelined kernel)
+    constexpr size_t kOneShotBytewise = 2048;
+    const bool vec = bytes % 16 == 0;
+    if ((vec || bytes <= kOneShotBytewise) && bytes <= std::min(w.oneshot_max, w.slot_bytes)) {
         char *od = direct ? (char *)recvbuf : (char *)get_scratch(1, bytes * n);
         if (!od) return E_NO_MEM;
         const char *os = in_place ? od + (size_t)me * bytes : (const char *)sendbuf;
         if (in_place && !direct) {
             hipMemcpyAsync(od + (size_t)me * bytes, (const char *)recvbuf + (size_t)me * bytes, bytes, hipMemcpyDefault, st);
-        } else if (!in_place && !(is_device(sendbuf) && (uintptr_t)sendbuf % 16 == 0)) {
+        } else if (!in_place && !(is_device(sendbuf) && (!vec || (uintptr_t)sendbuf % 16 == 0))) {
             char *t = (char *)get_scratch(0, bytes);
             if (!t) return E_NO_MEM;
             hipMemcpyAsync(t, sendbuf, bytes, hipMemcpyDefault, st);
@@ -1618,7 +1622,7 @@ static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void
         a.send = os;
         a.recv = od;
         a.count = bytes;
-        a.nvec = bytes / 16;
+        a.nvec = vec ? bytes / 16 : 0;
         a.pitch = bytes;
         LaunchCfg cfg = coll_cfg(oneshot_grid(a.nvec, grid_cap()), st);
         tmark0(st);
@@ -3246,8 +3250,9 @@ int coll_selftest() {
             if (!rc) rc = allgather_node(sb, rb, c * 4, nullptr);
             check(rb, c * n, k, 2, (int)c, 0, "pipelined allgather");
         }
-        // one-shot allgather and broadcast (k_oneshot_mv): 16-byte blocks, and a broadcast with a tail
-        const size_t os_ag[2] = {64, 4096}, os_bc[2] = {3, 16387};
+        // one-shot allgather and broadcast (k_oneshot_mv): a 12-byte block (byte by byte) and 16-byte
+        // blocks, and a broadcast with a tail
+        const size_t os_ag[2] = {3, 4096}, os_bc[2] = {3, 16387};
         for (int i = 0; i < 2 && !rc; ++i) {
             const int k = calls++;
             fill(sb, os_ag[i], k, me);
