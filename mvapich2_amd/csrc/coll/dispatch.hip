@@ -81,7 +81,14 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_mv(OneShotArgs a) {
     const size_t ve = vb + per < a.nvec ? vb + per : a.nvec;
     const bool bc = a.mv == 2;
     const size_t tail0 = a.nvec * 16;
-    const size_t myslot = (size_t)a.me * a.slot_bytes;
+    uint64_t epoch = a.epoch;
+    size_t poff = 0;
+    if (a.dseq) {  // graph lane: this replay's epoch and arena half
+        const SeqBase q = dseq_read(a.dseq);
+        epoch = q.epoch + 1;
+        poff = (q.os & 1) * a.half;
+    }
+    const size_t myslot = poff + (size_t)a.me * a.slot_bytes;
     if (!bc || a.me == a.root) {
         const v4u *src = (const v4u *)a.send;
         for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
@@ -100,11 +107,11 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_mv(OneShotArgs a) {
                 if (!bc && a.send != a.recv + (size_t)a.me * a.pitch) a.recv[(size_t)a.me * a.pitch + e] = c;
             }
     }
-    signal_peers(a.sig_peer, a.n, a.me, blk, a.epoch, a.light != 0);
-    if (wait_peers(a.sig_own, a.n, blk, a.epoch, a.err, a.timeout, a.light != 0)) {
+    signal_peers(a.sig_peer, a.n, a.me, blk, epoch, a.light != 0);
+    if (wait_peers(a.sig_own, a.n, blk, epoch, a.err, a.timeout, a.light != 0)) {
         for (int j = 0; j < a.n; ++j) {
             if (j == a.me || (bc && j != a.root)) continue;
-            const char *slot = a.arena_own + (size_t)j * a.slot_bytes;
+            const char *slot = a.arena_own + poff + (size_t)j * a.slot_bytes;
             char *dst = bc ? a.recv : a.recv + (size_t)j * a.pitch;
             for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) ((v4u *)dst)[i] = ld_nt((const v4u *)slot + i);
             if (blk == 0)
@@ -112,6 +119,7 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_mv(OneShotArgs a) {
                     dst[e] = __builtin_nontemporal_load(slot + e);
         }
     }
+    if (a.dseq) dseq_advance(a.dseq, 1, 0, 1);
     block_done(a.done);
 }
 

@@ -1370,7 +1370,7 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
     // (one-shot); non-roots discard theirs
     if (w.size == 1 || oi >= OP_REPLACE || (bytes <= w.oneshot_max && bytes <= w.slot_bytes)) {
         if (is_root) return allreduce_impl(sendbuf, recvbuf, count, dt, oi, st, tp);
-        void *tmp = get_scratch(2, bytes);
+        void *tmp = call_scratch(2, bytes);
         if (!tmp) return E_NO_MEM;
         return allreduce_impl(in_place ? recvbuf : sendbuf, tmp, count, dt, oi, st, tp);
     }
@@ -1385,7 +1385,7 @@ static int reduce_entry(const void *sendbuf, void *recvbuf, size_t count, int dt
         if (is_device(src) && (uintptr_t)src % 16 == 0) {
             s.send = (const char *)src;
         } else {
-            char *t = (char *)get_scratch(0, bytes);
+            char *t = (char *)call_scratch(0, bytes);
             if (!t) return E_NO_MEM;
             hipMemcpyAsync(t, src, bytes, hipMemcpyDefault, st);
             s.send = t;
@@ -1464,7 +1464,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
         pvar_note(PV_COLL_REDUCE_SCATTER, p, false, total, n);
         const char *src = (const char *)send;
         if (!is_device(send) || (uintptr_t)send % 16) {
-            char *t = (char *)get_scratch(0, total * ext);
+            char *t = (char *)call_scratch(0, total * ext);
             if (!t) return E_NO_MEM;
             beacon(BC_STAGE);
             hipMemcpyAsync(t, send, total * ext, hipMemcpyDefault, st);
@@ -1472,7 +1472,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
         }
         const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0;
         char *dst = (char *)recvbuf;
-        if (!direct && mycnt && !(dst = (char *)get_scratch(1, mycnt * ext))) return E_NO_MEM;
+        if (!direct && mycnt && !(dst = (char *)call_scratch(1, mycnt * ext))) return E_NO_MEM;
         OneShotArgs o{};
         oneshot_common(o, st);
         o.send = src;
@@ -1515,7 +1515,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
             o += recvcounts[j];
         }
     } else {
-        char *t = (char *)get_scratch(0, padded);
+        char *t = (char *)call_scratch(0, padded);
         if (!t) return E_NO_MEM;
         beacon(BC_STAGE);
         size_t o = 0, po = 0;
@@ -1536,7 +1536,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     char *dst = (char *)recvbuf;
     a.recv_off[w.rank] = 0;
     if (!direct && mycnt) {
-        char *t = (char *)get_scratch(1, mycnt * ext + 16);
+        char *t = (char *)call_scratch(1, mycnt * ext + 16);
         if (!t) return E_NO_MEM;
         dst = t + mis;
     }
@@ -1591,7 +1591,7 @@ static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void
     // contribution must then share its block's misalignment
     const bool direct = is_device(recvbuf) && (uintptr_t)recvbuf % 16 == 0;
     const size_t pitch = direct ? bytes : (bytes + 15) & ~(size_t)15;
-    char *dst = direct ? (char *)recvbuf : (char *)get_scratch(1, pitch * n);
+    char *dst = direct ? (char *)recvbuf : (char *)call_scratch(1, pitch * n);
     if (!dst) return E_NO_MEM;
     const char *src = in_place ? (const char *)recvbuf + (size_t)me * bytes : (const char *)sendbuf;
     if (n == 1) {
@@ -1605,13 +1605,13 @@ static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void
     constexpr size_t kOneShotBytewise = 2048;
     const bool vec = bytes % 16 == 0;
     if ((vec || bytes <= kOneShotBytewise) && bytes <= std::min(w.oneshot_max, w.slot_bytes)) {
-        char *od = direct ? (char *)recvbuf : (char *)get_scratch(1, bytes * n);
+        char *od = direct ? (char *)recvbuf : (char *)call_scratch(1, bytes * n);
         if (!od) return E_NO_MEM;
         const char *os = in_place ? od + (size_t)me * bytes : (const char *)sendbuf;
         if (in_place && !direct) {
             hipMemcpyAsync(od + (size_t)me * bytes, (const char *)recvbuf + (size_t)me * bytes, bytes, hipMemcpyDefault, st);
         } else if (!in_place && !(is_device(sendbuf) && (!vec || (uintptr_t)sendbuf % 16 == 0))) {
-            char *t = (char *)get_scratch(0, bytes);
+            char *t = (char *)call_scratch(0, bytes);
             if (!t) return E_NO_MEM;
             hipMemcpyAsync(t, sendbuf, bytes, hipMemcpyDefault, st);
             os = t;
@@ -1634,7 +1634,7 @@ static int allgather_node(const void *sendbuf, void *recvbuf, size_t bytes, void
     }
     const size_t mis = ((size_t)me * pitch) & 15;
     if (!(direct && in_place) && !(is_device(src) && (uintptr_t)src % 16 == mis)) {
-        char *t = (char *)get_scratch(0, bytes + 16);
+        char *t = (char *)call_scratch(0, bytes + 16);
         if (!t) return E_NO_MEM;
         hipMemcpyAsync(t + mis, src, bytes, hipMemcpyDefault, st);
         src = t + mis;
@@ -1668,7 +1668,7 @@ static int bcast_node(void *buffer, size_t bytes, int root, void *stream) {
     char *buf = (char *)buffer;
     const bool direct = is_device(buffer) && (uintptr_t)buffer % 16 == 0;
     if (!direct) {
-        buf = (char *)get_scratch(1, bytes);
+        buf = (char *)call_scratch(1, bytes);
         if (!buf) return E_NO_MEM;
         if (w.rank == root) hipMemcpyAsync(buf, buffer, bytes, hipMemcpyDefault, st);
     }
@@ -3054,12 +3054,12 @@ static int enqueue_checks(const void *send, const void *recv, void *stream, bool
     if (capturing(stream)) {
         const World &w = world();
         if (!graph_ok || !w.graph_lane || w.size < 2 || w.nnodes > 1) {
-            MV2_ERR("only MPI_Allreduce on one node can be captured into a HIP graph (graph lane %s)",
+            MV2_ERR("only collectives on one node can be captured into a HIP graph (graph lane %s)",
                     w.graph_lane ? "on" : "off");
             return E_UNSUPPORTED;
         }
         if ((uintptr_t)recv % 16 || (send && send != (const void *)-1 && (uintptr_t)send % 16)) {
-            MV2_ERR("a captured allreduce needs 16-byte-aligned buffers (no staging inside a graph)");
+            MV2_ERR("a captured collective needs 16-byte-aligned buffers");
             return E_ARG;
         }
     }
@@ -3084,9 +3084,11 @@ int mv2h_reduce_enqueue(const void *sendbuf, void *recvbuf, size_t count, int dt
     const World &w = world();
     // recvbuf is significant at the root only
     int rc = enqueue_checks(sendbuf, w.grank == root ? recvbuf : (sendbuf == (const void *)-1 ? nullptr : sendbuf),
-                            stream);
+                            stream, true);
     if (rc) return rc;
-    EnqueueScope q;
+    const bool graph = capturing(stream);
+    if (graph && op_index(op) >= OP_REPLACE) return E_OP;  // those run as a broadcast after a host wait
+    EnqueueScope q(graph);
     return mv2h_reduce(sendbuf, recvbuf, count, dtype, op, root, stream);
 }
 
@@ -3095,23 +3097,23 @@ int mv2h_reduce_scatter_enqueue(const void *sendbuf, void *recvbuf, const size_t
     const World &w = world();
     if (!recvcounts) return E_ARG;
     int rc = enqueue_checks(sendbuf, recvcounts[w.rank] ? recvbuf : (sendbuf == (const void *)-1 ? nullptr : sendbuf),
-                            stream);
+                            stream, true);
     if (rc) return rc;
-    EnqueueScope q;
+    EnqueueScope q(capturing(stream));
     return mv2h_reduce_scatter(sendbuf, recvbuf, recvcounts, dtype, op, stream);
 }
 
 int mv2h_allgather_enqueue(const void *sendbuf, void *recvbuf, size_t bytes, void *stream) {
-    int rc = bytes ? enqueue_checks(sendbuf, recvbuf, stream) : 0;
+    int rc = bytes ? enqueue_checks(sendbuf, recvbuf, stream, true) : 0;
     if (rc || !bytes) return rc;
-    EnqueueScope q;
+    EnqueueScope q(capturing(stream));
     return mv2h_allgather(sendbuf, recvbuf, bytes, stream);
 }
 
 int mv2h_bcast_enqueue(void *buffer, size_t bytes, int root, void *stream) {
-    int rc = bytes ? enqueue_checks(nullptr, buffer, stream) : 0;
+    int rc = bytes ? enqueue_checks(nullptr, buffer, stream, true) : 0;
     if (rc || !bytes) return rc;
-    EnqueueScope q;
+    EnqueueScope q(capturing(stream));
     return mv2h_bcast(buffer, bytes, root, stream);
 }
 

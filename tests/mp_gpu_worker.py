@@ -60,11 +60,11 @@ def enqueue_seq(L, case, rank, n):
     hx = np.zeros(4, dtype=np.float32)
     assert L.MPIX_Allreduce_enqueue(P(hx.ctypes.data), P(y.ptr), 4, F, SUM, WORLD, P(s)) != 0
     assert L.MPIX_Allreduce_enqueue(P(sb.ptr), P(y.ptr), 4, F, SUM, WORLD, None) != 0
-    # refused: a collective other than Allreduce on a stream being captured into a HIP graph
+    # refused: a captured collective on a buffer off a 16-byte boundary (no staging in a graph)
     cap, graph = ctypes.c_void_p(), ctypes.c_void_p()
     assert hip.hipStreamCreate(ctypes.byref(cap)) == 0
     assert hip.hipStreamBeginCapture(cap, 2) == 0  # hipStreamCaptureModeRelaxed
-    rc_cap = L.MPIX_Bcast_enqueue(P(xb.ptr), c, F, 0, WORLD, cap)  # only Allreduce takes the graph lane
+    rc_cap = L.MPIX_Bcast_enqueue(P(xb.ptr + 4), c - 1, F, 0, WORLD, cap)
     assert hip.hipStreamEndCapture(cap, ctypes.byref(graph)) == 0
     if graph.value:
         hip.hipGraphDestroy(graph)
@@ -123,6 +123,72 @@ def graph_allreduce(L, case, rank, n):
         hip.hipGraphDestroy(bufs[g][2])
     hip.hipStreamDestroy(st)
     return np.concatenate(out)
+
+
+def graph_collectives(L, case, rank, n):
+    """HIP graph capture of every stream-ordered collective (graph lane): one capture holds
+    MPIX_Reduce_scatter_enqueue, MPIX_Allgather_enqueue, MPIX_Bcast_enqueue, MPIX_Reduce_enqueue
+    and MPIX_Allreduce_enqueue back to back, for small (one-shot) and large (pipelined) sizes;
+    each graph is replayed `reps` times with new operands, a blocking MPI_Allgather between
+    replays (the host lane).  int32 SUM / MAX: exact whatever the order.  Returns the number of
+    wrong results."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    I, SUM, MAX = TYPES["MPI_INT"][0], OPS["MPI_SUM"], OPS["MPI_MAX"]
+    P = ctypes.c_void_p
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+    rb_root, bc_root = 0, 1 % n
+    graphs = []
+    for c in case["counts"]:  # elements per rank block
+        bufs = {k: m.DeviceBuffer(c * n * 4) for k in ("rs_s", "rs_r", "ag_s", "ag_r", "bc", "rd_s", "rd_r", "ar_s", "ar_r")}
+        counts = (ctypes.c_int * n)(*([c] * n))
+        graph, ex = ctypes.c_void_p(), ctypes.c_void_p()
+        assert hip.hipStreamBeginCapture(st, 2) == 0  # hipStreamCaptureModeRelaxed
+        rcs = [L.MPIX_Reduce_scatter_enqueue(P(bufs["rs_s"].ptr), P(bufs["rs_r"].ptr), counts, I, SUM, WORLD, st),
+               L.MPIX_Allgather_enqueue(P(bufs["ag_s"].ptr), c, I, P(bufs["ag_r"].ptr), c, I, WORLD, st),
+               L.MPIX_Bcast_enqueue(P(bufs["bc"].ptr), c, I, bc_root, WORLD, st),
+               L.MPIX_Reduce_enqueue(P(bufs["rd_s"].ptr), P(bufs["rd_r"].ptr), c, I, MAX, rb_root, WORLD, st),
+               L.MPIX_Allreduce_enqueue(P(bufs["ar_s"].ptr), P(bufs["ar_r"].ptr), c, I, SUM, WORLD, st)]
+        assert hip.hipStreamEndCapture(st, ctypes.byref(graph)) == 0
+        assert rcs == [0] * 5, rcs
+        assert hip.hipGraphInstantiate(ctypes.byref(ex), graph, None, None, 0) == 0
+        graphs.append((c, bufs, graph, ex))
+    hs, hr = m.DeviceBuffer(64 * 4), m.DeviceBuffer(64 * 4 * n)
+    bad = 0
+
+    def pat(r, k, g, cnt):
+        return ((np.arange(cnt, dtype=np.int64) * 40503 + r * 977 + k * 131 + g * 7) % 1000003).astype(np.int32)
+
+    for k in range(case["reps"]):
+        for g, (c, b, _, ex) in enumerate(graphs):
+            b["rs_s"].upload(pat(rank, k, g, c * n))
+            b["ag_s"].upload(pat(rank, k, g + 1, c))
+            b["bc"].upload(pat(rank, k, g + 2, c) if rank == bc_root else np.full(c, -1, dtype=np.int32))
+            b["rd_s"].upload(pat(rank, k, g + 3, c))
+            b["ar_s"].upload(pat(rank, k, g + 4, c))
+            assert hip.hipGraphLaunch(ex, st) == 0
+            assert hip.hipStreamSynchronize(st) == 0
+            want_rs = sum(pat(r, k, g, c * n)[rank * c:(rank + 1) * c].astype(np.int64) for r in range(n))
+            bad += int(not np.array_equal(b["rs_r"].download(np.int32, count=c), want_rs.astype(np.int32)))
+            bad += int(not np.array_equal(b["ag_r"].download(np.int32, count=c * n),
+                                          np.concatenate([pat(r, k, g + 1, c) for r in range(n)])))
+            bad += int(not np.array_equal(b["bc"].download(np.int32, count=c), pat(bc_root, k, g + 2, c)))
+            if rank == rb_root:
+                want = np.max(np.stack([pat(r, k, g + 3, c) for r in range(n)]), axis=0)
+                bad += int(not np.array_equal(b["rd_r"].download(np.int32, count=c), want))
+            want_ar = sum(pat(r, k, g + 4, c).astype(np.int64) for r in range(n)).astype(np.int32)
+            bad += int(not np.array_equal(b["ar_r"].download(np.int32, count=c), want_ar))
+        # the host lane between replays
+        hs.upload(pat(rank, k, 99, 64))
+        assert L.MPI_Allgather(hs.ptr, 64, I, hr.ptr, 64, I, WORLD) == 0
+        bad += int(not np.array_equal(hr.download(np.int32, count=64 * n),
+                                      np.concatenate([pat(r, k, 99, 64) for r in range(n)])))
+    assert L.MPIX_Enqueue_check(WORLD) == 0
+    for _, _, graph, ex in graphs:
+        hip.hipGraphExecDestroy(ex)
+        hip.hipGraphDestroy(graph)
+    hip.hipStreamDestroy(st)
+    return np.array([bad], dtype=np.int64)
 
 
 def big_case(L, case, rank, n):
@@ -555,6 +621,8 @@ def main():
             res = rb.download(np.uint8, count=count * ext)
         elif k == "graph_allreduce":  # HIP graph capture of MPIX_Allreduce_enqueue (graph lane)
             res = graph_allreduce(L, case, rank, n)
+        elif k == "graph_collectives":  # every stream-ordered collective in one captured graph
+            res = graph_collectives(L, case, rank, n)
         elif k == "enqueue_seq":  # stream-ordered collectives (MPIX_*_enqueue) mixed with a blocking call
             res = enqueue_seq(L, case, rank, n)
         elif k == "tiling_info":  # pipelined kernels' tiling after MPI_Init (pipe_autotune)

@@ -795,6 +795,19 @@ def test_graph_captured_allreduce(n, tmp_path):
         off += 4096 * 4
 
 
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_graph_captured_collectives(n, tmp_path):
+    """Every stream-ordered collective captured into one HIP graph (reduce-scatter, allgather,
+    broadcast, reduce, allreduce back to back; the one-shot kernels at 3 and 100 elements per
+    rank — 3 is a byte-wise allgather block — the pipelined kernels at 300,007), each graph
+    replayed four times with new operands and a blocking MPI_Allgather between replays; every
+    result checked against its closed form (mp_gpu_worker.graph_collectives)."""
+    case = {"id": "gc", "kind": "graph_collectives", "counts": [3, 100, 300007], "reps": 4}
+    res = run_workers(n, [case], tmp_path)
+    for r in range(n):
+        assert res("gc", r)[0] == 0, f"rank {r}: {int(res('gc', r)[0])} wrong results"
+
+
 @pytest.mark.parametrize("n,topo", [(4, "0,1,0,1"), (8, "0,1,0,1,0,1,0,1"), (8, "0,0,1,1,2,2,3,3;0,0,0,0,1,1,1,1")])
 def test_gpu_topology_levels(n, topo, tmp_path):
     """The topology-aware shm tree over several levels (MV2AMD_TOPO sets every rank's NUMA / socket
