@@ -378,22 +378,25 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
         poff = (q.os & 1) * a.half;
     }
     const v4u *send = (const v4u *)a.send;
+    // nvec == 0: small blocks that do not start on 16-byte boundaries, element by element in
+    // workgroup 0 (the vector range of every block is then empty)
+    const bool sc = a.nvec == 0;
     for (int j = 0; j < a.n; ++j) {
         if (j == a.me) continue;
-        const size_t v0 = a.wlo[j] / N, v1 = (a.wlo[j] + a.wcnt[j]) / N;
+        const size_t v0 = a.wlo[j] / N, v1 = sc ? v0 : (a.wlo[j] + a.wcnt[j]) / N;
         const size_t per = (v1 - v0 + G - 1) / G;
         const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
         v4u *dst = (v4u *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes);
         for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) dst[i] = send[i];
         if (blk == 0)
-            for (size_t e = v1 * N + threadIdx.x; e < a.wlo[j] + a.wcnt[j]; e += kThreads)
+            for (size_t e = (sc ? a.wlo[j] : v1 * N) + threadIdx.x; e < a.wlo[j] + a.wcnt[j]; e += kThreads)
                 ((T *)dst)[e] = ((const T *)a.send)[e];
     }
     signal_peers(a.sig_peer, a.n, a.me, blk, epoch, a.light != 0);
     if (wait_peers(a.sig_own, a.n, blk, epoch, a.err, a.timeout, a.light != 0)) {
         const char *arena_own = a.arena_own + poff;
         const size_t lo = a.wlo[a.me], hi = lo + a.wcnt[a.me];
-        const size_t v0 = lo / N, v1 = hi / N;
+        const size_t v0 = lo / N, v1 = sc ? v0 : hi / N;
         const size_t per = (v1 - v0 + G - 1) / G;
         const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
         int fb = -1;
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
             ((v4u *)a.recv)[i - v0] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
         }
         if (blk == 0)
-            for (size_t e = v1 * N + threadIdx.x; e < hi; e += kThreads) {
+            for (size_t e = (sc ? lo : v1 * N) + threadIdx.x; e < hi; e += kThreads) {
                 T col[kMaxRanks];
 #pragma unroll
                 for (int j = 0; j < kMaxRanks; ++j)

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <chrono>
 #include <vector>
+#include <unistd.h>
 
 #include "../../../include/mv2h.h"
 #include "log.h"
@@ -811,6 +812,7 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "code_load_us")) *value = (long)(w.code_load_ms * 1e3 + 0.5);
     else if (!strcmp(key, "selftest_calls")) *value = w.selftest_calls;
     else if (!strcmp(key, "call_allocs")) *value = (long)w.call_allocs;
+    else if (!strcmp(key, "p2p_unexpected")) *value = (long)p2p_unexpected_matched();
     else if (!strcmp(key, "hw_queues_set")) *value = w.hw_queues_set;
     else if (!strcmp(key, "uop_in_bytes")) *value = (long)w.uop_in_bytes;
     else if (!strcmp(key, "uop_area_bytes")) *value = (long)w.uop_area_bytes;
@@ -1207,7 +1209,7 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.send = s.send;
         a.recv = s.recv;
         a.count = count;
-        a.nvec = nvec;
+        a.nvec = nvec;  // (an element-wise body for small operands measured no faster here, r05z)
         a.tp = tp;
         const int g = oneshot_grid(nvec, gcap);
         LaunchCfg cfg = coll_cfg(g, st);
@@ -1456,9 +1458,18 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
     // the choice, so every rank makes it alike.
     Plan p;
     if ((rc = plan_reduce_scatter(n, w.rank, recvcounts, dt->size, dt->extent, &p))) return rc;
+    // Blocks off 16-byte boundaries take the same kernel element by element when the whole operand
+    // is small (kOneShotScalar; osu_reduce_scatter 8 B at 2 shared ranks: 16.4 us pipelined).
+    constexpr size_t kOneShotScalar = 2048;
     bool os = !in_place && p.algo != ALG_RS_RING && (size_t)dt->size == ext && 16 % ext == 0 &&
               total * ext <= std::min(w.oneshot_max, w.slot_bytes);
-    for (size_t j = 0, off0 = 0; os && j < (size_t)n; off0 += recvcounts[j], ++j) os = (off0 * ext) % 16 == 0;
+    bool aligned = true;
+    for (size_t j = 0, off0 = 0; j < (size_t)n; off0 += recvcounts[j], ++j) aligned = aligned && (off0 * ext) % 16 == 0;
+    if (!aligned && total * ext > kOneShotScalar) os = false;
+    // small operands element by element even when aligned: 1.9 / 2.3 us faster at 2 / 4 shared
+    // ranks from 32 B to 4 KiB than the vector body (profiles/r05y)
+    static const long scalar_max = env_long_coll("MV2AMD_RS_SCALAR_MAX", 4096);
+    if (total * ext <= (size_t)scalar_max) aligned = false;
     if (os) {
         log_plan("reduce_scatter", p, total);
         pvar_note(PV_COLL_REDUCE_SCATTER, p, false, total, n);
@@ -1478,7 +1489,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
         o.send = src;
         o.recv = dst;
         o.count = total;
-        o.nvec = total * ext / 16;
+        o.nvec = aligned ? total * ext / 16 : 0;
         o.rs = 1;
         size_t vmax = 0;
         for (size_t j = 0, e = 0; j < (size_t)n; e += recvcounts[j], ++j) {
@@ -1490,7 +1501,7 @@ static int reduce_scatter_entry(const void *sendbuf, void *recvbuf, const size_t
         tp.linear = 4;
         tp.ps = p.ps;
         o.tp = tp;
-        LaunchCfg cfg = coll_cfg(oneshot_grid(vmax, grid_cap()), st);
+        LaunchCfg cfg = coll_cfg(oneshot_grid(aligned ? vmax : 0, grid_cap()), st);
         tmark0(st);
         rc = launch_oneshot(oi, dt->kind, o, dt->extent, cfg);
         tmark1(st);
@@ -2222,6 +2233,92 @@ static int gather_node_leader(const void *mine, char *G, size_t S) {
     return 0;
 }
 
+// MV2AMD_DEBUG_GATHER=1 (diagnosis): every rank hashes the operand it gave the gather in 64 KiB
+// blocks and sends the hashes to its node leader, which hashes what landed in G and prints the
+// blocks that differ, now and after a device synchronisation and 2 ms (a wrong copy stays
+// different, a late one heals), with the unexpected-message matches of the gather
+static void host_block_hashes(const void *dev, size_t S, std::vector<uint64_t> &out) {
+    std::vector<unsigned char> h(S);
+    out.assign((S + 65535) / 65536, 0);
+    if (hipMemcpy(h.data(), dev, S, hipMemcpyDefault) != hipSuccess) return;
+    for (size_t b = 0; b < out.size(); ++b) {
+        uint64_t x = 1469598103934665603ull;
+        for (size_t i = b * 65536; i < std::min(S, (b + 1) * 65536); ++i) x = (x ^ h[i]) * 1099511628211ull;
+        out[b] = x;
+    }
+}
+static bool debug_gather_on() {
+    static const bool on = getenv("MV2AMD_DEBUG_GATHER") && *getenv("MV2AMD_DEBUG_GATHER") == '1';
+    return on;
+}
+static std::vector<uint64_t> g_dbg_before;  // this rank's operand's block hashes at the gather's start
+static void debug_gather_pre(const void *mine, size_t S) {
+    if (debug_gather_on()) host_block_hashes(mine, S, g_dbg_before);
+}
+static long blocks_differ(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b, long *b0, long *b1) {
+    long nb = 0;
+    *b0 = *b1 = -1;
+    for (size_t i = 0; i < a.size() && i < b.size(); ++i)
+        if (a[i] != b[i]) {
+            ++nb;
+            if (*b0 < 0) *b0 = (long)i;
+            *b1 = (long)i;
+        }
+    return nb;
+}
+static int debug_gather_check(const void *mine, const char *G, size_t S, unsigned long long ux_before) {
+    static uint64_t call = 0;
+    ++call;
+    if (!debug_gather_on()) return 0;
+    World &w = world();
+    const int L = w.size, base = w.node * w.size;
+    const unsigned long long ux = p2p_unexpected_matched() - ux_before;
+    const size_t nbk = (S + 65535) / 65536;
+    std::vector<uint64_t> two, got, after;
+    long b0, b1;
+    int rc = 0;
+    if (w.rank != 0) {  // before and after the send, both to the leader
+        host_block_hashes(mine, S, after);
+        two = g_dbg_before;
+        two.insert(two.end(), after.begin(), after.end());
+        const long changed = blocks_differ(g_dbg_before, after, &b0, &b1);
+        if (changed)
+            MV2_ERR("debug gather: call %llu node %d local rank %d: MY operand changed during the gather (%ld blocks, %ld..%ld)",
+                    (unsigned long long)call, w.node, w.rank, changed, b0, b1);
+        unsigned long long q = 0;
+        if ((rc = p2p_isend(two.data(), two.size() * 8, base, kCollTagBase - 60, &q))) return rc;
+        return mv2h_p2p_wait(q, nullptr, nullptr, nullptr);
+    }
+    host_block_hashes(G, S, got);  // the leader's own operand, copied by hipMemcpy
+    if (const long nb = blocks_differ(g_dbg_before, got, &b0, &b1))
+        MV2_ERR("debug gather: call %llu node %d leader's own operand in G: %ld blocks differ (%ld..%ld)",
+                (unsigned long long)call, w.node, nb, b0, b1);
+    for (int l = 1; l < L; ++l) {
+        two.assign(2 * nbk, 0);
+        unsigned long long q = 0;
+        if ((rc = p2p_irecv(two.data(), two.size() * 8, base + l, kCollTagBase - 60, &q)) ||
+            (rc = mv2h_p2p_wait(q, nullptr, nullptr, nullptr)))
+            return rc;
+        const std::vector<uint64_t> pre(two.begin(), two.begin() + nbk), post(two.begin() + nbk, two.end());
+        host_block_hashes(G + (size_t)l * S, S, got);
+        const long nb = blocks_differ(post, got, &b0, &b1);
+        if (nb) {
+            long c0, c1;
+            const long vs_pre = blocks_differ(pre, got, &c0, &c1);
+            hipDeviceSynchronize();
+            usleep(2000);
+            host_block_hashes(G + (size_t)l * S, S, after);
+            long d0, d1;
+            const long nb2 = blocks_differ(post, after, &d0, &d1);
+            MV2_ERR("debug gather: call %llu node %d local rank %d operand of %zu bytes: %ld of %zu 64 KiB blocks differ "
+                    "(blocks %ld..%ld; %ld against the sender's operand before its send), %ld after a synchronisation; "
+                    "unexpected matches in this gather %llu",
+                    (unsigned long long)call, w.node, l, S, nb, nbk, b0, b1, vs_pre, nb2, ux);
+        }
+    }
+    return 0;
+}
+
 // Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
 // chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
 // the accumulator always inout (uop(comp_chunk, recv_chunk), :3958).  Here each node gathers its
@@ -2242,7 +2339,9 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     if (w.rank == 0) {
         char *G = (char *)get_scratch(6, (size_t)L * S);  // the node's operands, local rank order
         if (!G) return E_NO_MEM;
-        if ((rc = gather_node_leader(sendbuf, G, S))) return rc;
+        const unsigned long long ux0 = p2p_unexpected_matched();
+        debug_gather_pre(sendbuf, S);
+        if ((rc = gather_node_leader(sendbuf, G, S)) || (rc = debug_gather_check(sendbuf, G, S, ux0))) return rc;
         if ((rc = mn_reserve(std::max(main_bytes, sect)))) return rc;
         char *A = g_mn.d0;  // partial chunks of the group in hand
         auto X = [&](int l, size_t byte_off) { return (const char *)G + (size_t)l * S + byte_off; };
@@ -2279,7 +2378,8 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
                 return rc;
         }
         if ((rc = mn_h2d(recvbuf, g_mn.h1, main_bytes))) return rc;
-    } else if ((rc = gather_node_leader(sendbuf, nullptr, S))) {
+    } else if ((debug_gather_pre(sendbuf, S), rc = gather_node_leader(sendbuf, nullptr, S)) ||
+               (rc = debug_gather_check(sendbuf, nullptr, S, 0))) {
         return rc;
     }
     if ((rc = bcast_node(recvbuf, main_bytes, 0, stream))) return rc;
@@ -3197,8 +3297,9 @@ int coll_selftest() {
                 if (!rc) rc = ::allreduce_entry(sb, rb, c, MPI_INT_H, MPI_SUM_H, nullptr);
                 check(rb, c, k, 0, 0, 0, "one-shot allreduce");
             }
-        // one-shot reduce-scatter (equal blocks of 16-byte multiples, below the ring threshold)
-        const size_t rs_small[3] = {4, 1024, 2048};
+        // one-shot reduce-scatter below the ring threshold: 12-byte blocks (element by element),
+        // blocks of 16-byte multiples
+        const size_t rs_small[3] = {3, 1024, 2048};
         for (int i = 0; i < 3 && !rc; ++i)
             for (int h = 0; h < 2 && !rc; ++h) {
                 const int k = calls++;

@@ -73,12 +73,19 @@ struct Req {
     size_t total = 0;
 };
 
+// An unexpected message from a rank of this node keeps its payload in device memory (`dev`, a
+// pooled block: arena -> block -> the receive's buffer, never through the host); one from the rank
+// mesh, or when no device block can be had, in host memory (`data`).
 struct Unexp {
     int src, tag;
     size_t total;
-    size_t got = 0;  // bytes landed in `data` (copies synchronised)
+    size_t got = 0;  // bytes landed in `dev` / `data` (copies synchronised)
     bool complete = false;
     std::vector<char> data;
+    char *dev = nullptr;
+    ~Unexp() {
+        if (dev) pool_put(dev);
+    }
 };
 
 // message currently arriving on the channel from one source
@@ -95,6 +102,7 @@ uint64_t g_msg_seq = 0;
 std::deque<Req *> g_sendq[kMaxRanks];  // per destination, FIFO (one message at a time per channel)
 std::list<Req *> g_posted;             // unmatched receives in posting order
 std::list<Unexp *> g_unexp;            // unexpected messages in arrival order
+uint64_t g_unexp_matched = 0;          // unexpected messages later taken by a receive (mv2h_get_info)
 Arrival g_in[kMaxRanks];
 
 // rank mesh (ranks on other nodes)
@@ -206,8 +214,12 @@ int run_copies(const std::vector<Copy> &cp) {
         const Copy &c = cp[i];
         if (!c.len) continue;
         if (c.kernel) {
-            Done d{};
-            if (i + 1 == cp.size()) d = Done{g_pdone.ctr, g_pdone.flag, ++g_pdone.seq};
+            // every copy kernel carries the word (the host waits for the last value only): its
+            // completion writes back the L2 of each XCD its workgroups ran on.  A kernel without it
+            // left dirty lines in the L2s the next, smaller kernel's write-back did not reach
+            // (block_done flushes the XCDs of its own workgroups), and a receiver on this node read
+            // the arena slot stale there (r05al: 3-5 blocks of 64 KiB of a 4 MiB operand)
+            const Done d{g_pdone.ctr, g_pdone.flag, ++g_pdone.seq};
             if (launch_pack_strided(c.src, c.dst, 1, c.len, c.len, 0, st, d) != 0) {
                 MV2_ERR("point-to-point copy kernel failed to launch: %s", hipGetErrorString(hipGetLastError()));
                 return E_INTERN;
@@ -217,7 +229,11 @@ int run_copies(const std::vector<Copy> &cp) {
             return E_INTERN;
         }
     }
-    const bool word = !cp.empty() && cp.back().kernel && cp.back().len;
+    // the word alone proves the pass complete only when every copy of it is a kernel: a host
+    // buffer's hipMemcpyAsync may finish (staged through pinned memory) after the kernels behind it
+    bool all_kernels = true;
+    for (const Copy &c : cp) all_kernels = all_kernels && (c.kernel || !c.len);
+    const bool word = all_kernels && !cp.empty() && cp.back().kernel && cp.back().len;
     if (word) {
         // the word is the normal path; the stream is consulted once it is 200 us late, then every 100 us
         const uint64_t want = g_pdone.seq;
@@ -279,7 +295,10 @@ int net_deliver(NetIn &in) {
     if (in.req) {
         Req *r = in.req;
         const size_t n = std::min(r->total, r->cap);
-        if (n && hipMemcpy(r->rbuf, in.stage.data(), n, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+        if (n) {  // complete (stream-synchronised) before the receive is
+            const std::vector<Copy> one{{r->rbuf, in.stage.data(), n, false}};
+            if (const int rc = run_copies(one)) return rc;
+        }
         if (r->total > r->cap) r->err = E_TRUNCATE;
         r->done = true;
     } else if (in.ux) {
@@ -438,7 +457,8 @@ int progress(bool *moved) {
                     a.req->total = rec.total;
                 } else {
                     a.ux = new Unexp{base + s, rec.tag, (size_t)rec.total};
-                    a.ux->data.resize(rec.total ? rec.total : 1);
+                    if (!(a.ux->dev = rec.total ? (char *)pool_get((size_t)rec.total) : nullptr))
+                        a.ux->data.resize(rec.total ? rec.total : 1);
                     g_unexp.push_back(a.ux);
                 }
             }
@@ -447,7 +467,8 @@ int progress(bool *moved) {
                 const size_t room = a.req->cap > rec.off ? std::min<size_t>(rec.len, a.req->cap - rec.off) : 0;
                 if (room) cp.push_back({a.req->rbuf + rec.off, src, room, g_kcopy && a.req->rdev});
             } else if (rec.len) {
-                cp.push_back({a.ux->data.data() + rec.off, src, (size_t)rec.len, false});
+                if (a.ux->dev) cp.push_back({a.ux->dev + rec.off, src, (size_t)rec.len, g_kcopy});
+                else cp.push_back({a.ux->data.data() + rec.off, src, (size_t)rec.len, false});
             }
             a.got += rec.len;
             ++head;
@@ -576,11 +597,15 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
     for (auto it = g_unexp.begin(); it != g_unexp.end(); ++it) {
         Unexp *u = *it;
         if (!matches(r, u->src, u->tag)) continue;
+        ++g_unexp_matched;
         r->src = u->src;
         r->rtag = u->tag;
         r->total = u->total;
         const size_t have = std::min(u->got, cap);
-        if (have && hipMemcpy(buf, u->data.data(), have, hipMemcpyDefault) != hipSuccess) return E_INTERN;
+        if (have) {  // complete before the receive can be: the caller may read buf on any stream next
+            const std::vector<Copy> one{{(char *)buf, u->dev ? u->dev : u->data.data(), have, u->dev && r->rdev}};
+            if ((rc = run_copies(one))) return rc;
+        }
         g_unexp.erase(it);
         if (u->complete) {
             if (u->total > cap) r->err = E_TRUNCATE;
@@ -606,6 +631,7 @@ int mv2::p2p_irecv(void *buf, size_t cap, int source, int tag, unsigned long lon
 }
 
 bool mv2::coll_context_poisoned() { return g_coll_poisoned; }
+unsigned long long mv2::p2p_unexpected_matched() { return g_unexp_matched; }
 
 void mv2::p2p_abandon(unsigned long long id) {
     auto it = g_reqs.find(id);

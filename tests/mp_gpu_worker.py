@@ -473,8 +473,8 @@ def soak(L, case, rank, n):
     survive.  Returns [wrong calls, calls made, first wrong call index or -1]."""
     I = TYPES["MPI_INT"][0]
     ops = [("MPI_SUM", OPS["MPI_SUM"]), ("MPI_MAX", OPS["MPI_MAX"]), ("MPI_BXOR", OPS["MPI_BXOR"])]
-    kinds = ["allreduce", "allreduce_inplace", "iallreduce", "enqueue", "reduce", "reduce_scatter_block",
-             "allgather", "bcast", "sendrecv"]
+    kinds = case.get("kinds", ["allreduce", "allreduce_inplace", "iallreduce", "enqueue", "reduce",
+                               "reduce_scatter_block", "allgather", "bcast", "sendrecv"])
     sizes = case.get("sizes", [1, 3, 64, 1000, 4096, 16385, 65536, 262143, 1 << 20])
     rng = np.random.default_rng(case["seed"])  # the same sequence on every rank
     mx = max(sizes)
@@ -498,6 +498,8 @@ def soak(L, case, rank, n):
         return out.astype(np.int32)
 
     wrong, first = 0, -1
+    detail, ux_calls = [], 0
+    sb_pre_bad, sb_post_bad, sb_detail = 0, 0, []
     calls = case["calls"]
     for i in range(calls):
         k = kinds[int(rng.integers(len(kinds)))]
@@ -511,6 +513,11 @@ def soak(L, case, rank, n):
             rb.upload(mine)
         else:
             sb.upload(mine)
+        if case.get("sync_upload"):  # diagnosis: the upload finished on the device before the call
+            m.check(L.mv2h_device_synchronize(), "mv2h_device_synchronize")
+        ux0 = m.info("p2p_unexpected") if case.get("detail") == 1 else 0
+        if case.get("check_sb") and k == "allreduce":  # diagnosis: the operand as uploaded, before the call
+            sb_pre_bad += int(not np.array_equal(sb.download(np.int32, count=cnt), mine))
         rc = 0
         if k == "allreduce":
             rc = L.MPI_Allreduce(P(sb.ptr), P(rb.ptr), cnt, I, op, WORLD)
@@ -537,6 +544,14 @@ def soak(L, case, rank, n):
                                 i % 30000, WORLD, None)
         if rc:
             raise RuntimeError(f"call {i} ({k}, {cnt}) returned {rc}")
+        if case.get("check_sb") and k == "allreduce":  # ... and after it: a send buffer is read only
+            post = sb.download(np.int32, count=cnt)
+            if not np.array_equal(post, mine):
+                sb_post_bad += 1
+                if len(sb_detail) < 30:
+                    bad = np.nonzero(post != mine)[0]
+                    d = post[bad[0]].astype(np.int64) - mine[bad[0]].astype(np.int64)
+                    sb_detail.extend([i, len(bad), int(bad[0]), int(bad[-1]), int(d)])
         if k in ("allreduce", "allreduce_inplace", "iallreduce", "enqueue"):
             got, want = rb.download(np.int32, count=cnt), fold(oname, [pat(r, i, cnt) for r in range(n)])
         elif k == "reduce":
@@ -555,8 +570,16 @@ def soak(L, case, rank, n):
         if not np.array_equal(got, want):
             wrong += 1
             first = i if first < 0 else first
+            if case.get("detail") and len(detail) < 40:  # diagnosis: call, op, count, wrong-element span
+                bad = np.nonzero(got != want)[0]
+                detail.extend([i, ops.index((oname, op)), cnt, len(bad), int(bad[0]), int(bad[-1]),
+                               m.info("p2p_unexpected") - ux0 if case.get("detail") == 1 else -1])
+        if case.get("detail") == 1:
+            ux_calls += int(m.info("p2p_unexpected") > ux0)
     hip.hipStreamDestroy(st)
-    return np.array([wrong, calls, first], dtype=np.int64)
+    if case.get("check_sb"):
+        return np.array([wrong, calls, first, sb_pre_bad, sb_post_bad] + sb_detail, dtype=np.int64)
+    return np.array([wrong, calls, first] + ([ux_calls] if case.get("detail") else []) + detail, dtype=np.int64)
 
 
 def collops_comm(L, rank, n):

@@ -1,0 +1,12 @@
+set -o pipefail
+# Round 5, pass z: one-shot allreduce, vector body vs element-wise body for small operands
+# (MV2AMD_AR_SCALAR_MAX), OSU allreduce 4 B .. 16 KiB at 2 / 4 / 8 shared ranks
+O=gpurun_out/r05z
+mkdir -p $O
+export TMPDIR=/tmp
+for n in 2 4 8; do
+  for sm in 0 4096; do
+    MV2AMD_AR_SCALAR_MAX=$sm timeout -k 10 200 python -m mvapich2_amd.mv2run -n $n --share-gpu --timeout 190 tools/osu/osu_coll -c allreduce -m 4:16384 -i 1000 -x 100 -v > $O/ar_${n}_${sm}.txt 2>&1 || { tail -20 $O/ar_${n}_${sm}.txt; exit 1; }
+  done
+  paste $O/ar_${n}_0.txt $O/ar_${n}_4096.txt | grep -v MPI_Init | awk '{print $1, $2, $7}'
+done
