@@ -2133,8 +2133,18 @@ static int mn_select(int ppn, int gsize, long nbytes, int *intra, int *inter) {
 // two-level reduce helper, Reduce_scatter the basic algorithm) — correct for every builtin op,
 // its fp order not the reference's (unpinned; integer, bitwise, logical and LOC results exact).
 enum MnRoute { MN_TWO_LEVEL_R = 0, MN_RING_R = 1, MN_FLAT_PROG = 2, MN_SCHED = 3, MN_FALLBACK = 4, MN_BASIC_R = 5 };
+// The most ranks a flat algorithm runs as per-element programs: kMaxRanks, or fewer with
+// MV2AMD_MN_PROG_MAX (tests: the message schedules on jobs small enough to share one GPU without
+// oversubscribing its hardware scheduler, DESIGN.md "Ranks per GPU")
+static int mn_prog_max() {
+    static const int m = [] {
+        const long v = env_long_coll("MV2AMD_MN_PROG_MAX", kMaxRanks);
+        return (int)(v < 1 ? 1 : v > kMaxRanks ? kMaxRanks : v);
+    }();
+    return m;
+}
 static int mn_flat_route(int gsize) {
-    return gsize <= kMaxRanks ? MN_FLAT_PROG : gsize <= kMeshMaxRanks ? MN_SCHED : MN_FALLBACK;
+    return gsize <= mn_prog_max() ? MN_FLAT_PROG : gsize <= kMeshMaxRanks ? MN_SCHED : MN_FALLBACK;
 }
 // MPI_Allreduce / MPI_Iallreduce (nbc = the call's mv2h_nbc kind).  *rem_route: the route of the
 // ring wrapper's count % gsize remainder (pt2pt_rs over every rank), -1 when there is none.
@@ -2487,7 +2497,7 @@ static int mn_flat_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     const bool in_place = sendbuf == (const void *)-1;
     const size_t S = count * (size_t)dt->extent;
     const int n = w.gsize;
-    if (n > kMaxRanks && root < 0 && (algo == ALG_PT2PT_RS || algo == ALG_PT2PT_RD))
+    if (n > mn_prog_max() && root < 0 && (algo == ALG_PT2PT_RS || algo == ALG_PT2PT_RD))
         return mn_flat_route(n) == MN_SCHED ? mn_sched_allreduce(sendbuf, recvbuf, count, dtype, op, algo)
                                             : mn_allreduce_2lvl(sendbuf, recvbuf, count, dtype, op, stream);
     Plan p;
@@ -2883,7 +2893,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
     s->kind = MN_FLAT;
     s->coll = coll;
     s->U = 0;
-    const bool big = n > kMaxRanks;
+    const bool big = n > mn_prog_max();
     int rc = 0;
     if (coll == MN_COLL_REDUCE) {
         if (opk == OPK_USER_NONCOMM || nbc_kind() == NBC_IREDUCE) {
@@ -2973,7 +2983,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         }
         return 0;
     }
-    if (sel == 1 && n <= kMaxRanks) {  // the flat ring wrapper over every rank
+    if (sel == 1 && n <= mn_prog_max()) {  // the flat ring wrapper over every rank
         const int chain[3] = {PV_AR_RING_WRAPPER, PV_AR_RING, PV_AR_SHM_RS};
         if (!in_place && count >= (size_t)n) {
             pvar_note_ids(chain, count % (size_t)n ? 3 : 2);
@@ -2993,7 +3003,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         if (!s->U) s->p = s->rem;
         return rc;
     }
-    if ((sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD) && n <= kMaxRanks) {
+    if ((sel == ALG_PT2PT_RS || sel == ALG_PT2PT_RD) && n <= mn_prog_max()) {
         s->forced = sel;
         if ((rc = plan_allreduce(n, me, count, tsize, textent, in_place, sel, &s->p, opk))) return rc;
         pvar_note(PV_COLL_ALLREDUCE, s->p, in_place, count, n);

@@ -744,6 +744,15 @@ int world_init() {
         // the other nodes' ranks too, which this node's segment cannot see
         const long ns = env_long("MV2AMD_NSHARE", 0);
         if (ns > w.nshare) w.nshare = (int)ns;
+        // above 8 processes on one GPU its hardware scheduler time-slices them instead of running
+        // them all at once: device-side waits between the ranks then take milliseconds per step and
+        // the 12- and 9-process emulations stalled and lost cross-process stores (DESIGN.md "Ranks
+        // per GPU", profiles/r05as, r05at)
+        if (w.nshare > kHwsProcs && w.rank == 0 && env_long("MV2AMD_QUIET_NSHARE", 0) == 0)
+            fprintf(stderr,
+                    "[mv2amd rank %d] warning: %d processes share one GPU, more than the %d its hardware "
+                    "scheduler runs at once; device collectives between them are not supported there\n",
+                    log_rank(), w.nshare, kHwsProcs);
 
         if (w.size <= kMaxRanks && !control_only) {
             // signal page + one-shot arena, IPC-exported

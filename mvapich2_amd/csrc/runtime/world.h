@@ -86,6 +86,7 @@ struct alignas(64) ShmRank {
     std::atomic<uint32_t> bh_pos;
 };
 
+constexpr int kHwsProcs = 8;  // processes one GPU's hardware scheduler runs at once (KFD's VMIDs)
 constexpr int kMeshMaxRanks = 64;  // jobs up to this many ranks get the rank mesh (p2p across nodes)
 
 struct ShmSeg {
