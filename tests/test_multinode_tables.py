@@ -5,6 +5,7 @@ nemesis_INTEL_XEON_E5_2680_16_MLX_CX_FDR_{1,2,16}ppn.h by tests/golden/gen_mn_al
 tests/test_gpu_multinode_mp.py table_cell), every numproc entry, including each two-level entry's
 intra-node function (allreduce_osu.c:1727-1745)."""
 import ctypes
+import os
 import json
 from pathlib import Path
 
@@ -141,3 +142,27 @@ def test_reduce_table_reads_duplicate_first_entries_by_index():
     assert L.mv2h_mn_reduce_table(2, 4, 4096, None, None, None, None) == 1
     assert L.mv2h_mn_reduce_table(16, 32, 4096, None, None, None, None) == 1
     assert L.mv2h_mn_reduce_table(16, 64, 4096, None, None, None, None) == 2
+
+
+def test_prog_max_knob_moves_flat_calls_onto_the_message_schedules():
+    """MV2AMD_MN_PROG_MAX (coll.cpp mn_prog_max): with it at 4, an 8-rank job takes the message
+    schedules that jobs above 8 ranks take, so the GPU tests cover them on 8 processes (DESIGN.md §5
+    "Ranks per GPU"); unset, 8 ranks run as programs.  Read once per process: a child process."""
+    import subprocess
+    import sys
+    code = ("import ctypes, mvapich2_amd as m; L = m.lib(); r = ctypes.c_int(); "
+            "print(L.mv2h_mn_route(0, 4, 8, 64, 16, 0, 1, ctypes.byref(r)), "
+            "L.mv2h_mn_route(0, 4, 8, 1 << 22, 1 << 20, 0, 0, ctypes.byref(r)), r.value)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    got = {}
+    for v in (None, "4"):
+        env = dict(os.environ)
+        env.pop("MV2AMD_MN_PROG_MAX", None)
+        if v:
+            env["MV2AMD_MN_PROG_MAX"] = v
+        out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        got[v] = [int(x) for x in out.stdout.split()]
+    # MPI_Iallreduce: flat over the job; 4 MiB allreduce: the ring with its remainder route
+    assert got[None][0] == 2 and got["4"][0] == 3, got
+    assert got[None][1] == got["4"][1], got
