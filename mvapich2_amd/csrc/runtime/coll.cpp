@@ -2243,92 +2243,6 @@ static int gather_node_leader(const void *mine, char *G, size_t S) {
     return 0;
 }
 
-// MV2AMD_DEBUG_GATHER=1 (diagnosis): every rank hashes the operand it gave the gather in 64 KiB
-// blocks and sends the hashes to its node leader, which hashes what landed in G and prints the
-// blocks that differ, now and after a device synchronisation and 2 ms (a wrong copy stays
-// different, a late one heals), with the unexpected-message matches of the gather
-static void host_block_hashes(const void *dev, size_t S, std::vector<uint64_t> &out) {
-    std::vector<unsigned char> h(S);
-    out.assign((S + 65535) / 65536, 0);
-    if (hipMemcpy(h.data(), dev, S, hipMemcpyDefault) != hipSuccess) return;
-    for (size_t b = 0; b < out.size(); ++b) {
-        uint64_t x = 1469598103934665603ull;
-        for (size_t i = b * 65536; i < std::min(S, (b + 1) * 65536); ++i) x = (x ^ h[i]) * 1099511628211ull;
-        out[b] = x;
-    }
-}
-static bool debug_gather_on() {
-    static const bool on = getenv("MV2AMD_DEBUG_GATHER") && *getenv("MV2AMD_DEBUG_GATHER") == '1';
-    return on;
-}
-static std::vector<uint64_t> g_dbg_before;  // this rank's operand's block hashes at the gather's start
-static void debug_gather_pre(const void *mine, size_t S) {
-    if (debug_gather_on()) host_block_hashes(mine, S, g_dbg_before);
-}
-static long blocks_differ(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b, long *b0, long *b1) {
-    long nb = 0;
-    *b0 = *b1 = -1;
-    for (size_t i = 0; i < a.size() && i < b.size(); ++i)
-        if (a[i] != b[i]) {
-            ++nb;
-            if (*b0 < 0) *b0 = (long)i;
-            *b1 = (long)i;
-        }
-    return nb;
-}
-static int debug_gather_check(const void *mine, const char *G, size_t S, unsigned long long ux_before) {
-    static uint64_t call = 0;
-    ++call;
-    if (!debug_gather_on()) return 0;
-    World &w = world();
-    const int L = w.size, base = w.node * w.size;
-    const unsigned long long ux = p2p_unexpected_matched() - ux_before;
-    const size_t nbk = (S + 65535) / 65536;
-    std::vector<uint64_t> two, got, after;
-    long b0, b1;
-    int rc = 0;
-    if (w.rank != 0) {  // before and after the send, both to the leader
-        host_block_hashes(mine, S, after);
-        two = g_dbg_before;
-        two.insert(two.end(), after.begin(), after.end());
-        const long changed = blocks_differ(g_dbg_before, after, &b0, &b1);
-        if (changed)
-            MV2_ERR("debug gather: call %llu node %d local rank %d: MY operand changed during the gather (%ld blocks, %ld..%ld)",
-                    (unsigned long long)call, w.node, w.rank, changed, b0, b1);
-        unsigned long long q = 0;
-        if ((rc = p2p_isend(two.data(), two.size() * 8, base, kCollTagBase - 60, &q))) return rc;
-        return mv2h_p2p_wait(q, nullptr, nullptr, nullptr);
-    }
-    host_block_hashes(G, S, got);  // the leader's own operand, copied by hipMemcpy
-    if (const long nb = blocks_differ(g_dbg_before, got, &b0, &b1))
-        MV2_ERR("debug gather: call %llu node %d leader's own operand in G: %ld blocks differ (%ld..%ld)",
-                (unsigned long long)call, w.node, nb, b0, b1);
-    for (int l = 1; l < L; ++l) {
-        two.assign(2 * nbk, 0);
-        unsigned long long q = 0;
-        if ((rc = p2p_irecv(two.data(), two.size() * 8, base + l, kCollTagBase - 60, &q)) ||
-            (rc = mv2h_p2p_wait(q, nullptr, nullptr, nullptr)))
-            return rc;
-        const std::vector<uint64_t> pre(two.begin(), two.begin() + nbk), post(two.begin() + nbk, two.end());
-        host_block_hashes(G + (size_t)l * S, S, got);
-        const long nb = blocks_differ(post, got, &b0, &b1);
-        if (nb) {
-            long c0, c1;
-            const long vs_pre = blocks_differ(pre, got, &c0, &c1);
-            hipDeviceSynchronize();
-            usleep(2000);
-            host_block_hashes(G + (size_t)l * S, S, after);
-            long d0, d1;
-            const long nb2 = blocks_differ(post, after, &d0, &d1);
-            MV2_ERR("debug gather: call %llu node %d local rank %d operand of %zu bytes: %ld of %zu 64 KiB blocks differ "
-                    "(blocks %ld..%ld; %ld against the sender's operand before its send), %ld after a synchronisation; "
-                    "unexpected matches in this gather %llu",
-                    (unsigned long long)call, w.node, l, S, nb, nbk, b0, b1, vs_pre, nb2, ux);
-        }
-    }
-    return 0;
-}
-
 // Flat ring over every rank of the job (MPIR_Allreduce_pt2pt_ring_MV2, allreduce_osu.c:3916-3968):
 // chunk c of (count / n) elements ends as x_c (+) x_{c+1} (+) ... (+) x_{c-1} over the global ranks,
 // the accumulator always inout (uop(comp_chunk, recv_chunk), :3958).  Here each node gathers its
@@ -2349,9 +2263,7 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
     if (w.rank == 0) {
         char *G = (char *)get_scratch(6, (size_t)L * S);  // the node's operands, local rank order
         if (!G) return E_NO_MEM;
-        const unsigned long long ux0 = p2p_unexpected_matched();
-        debug_gather_pre(sendbuf, S);
-        if ((rc = gather_node_leader(sendbuf, G, S)) || (rc = debug_gather_check(sendbuf, G, S, ux0))) return rc;
+        if ((rc = gather_node_leader(sendbuf, G, S))) return rc;
         if ((rc = mn_reserve(std::max(main_bytes, sect)))) return rc;
         char *A = g_mn.d0;  // partial chunks of the group in hand
         auto X = [&](int l, size_t byte_off) { return (const char *)G + (size_t)l * S + byte_off; };
@@ -2388,8 +2300,7 @@ static int mn_ring_allreduce(const void *sendbuf, void *recvbuf, size_t count, i
                 return rc;
         }
         if ((rc = mn_h2d(recvbuf, g_mn.h1, main_bytes))) return rc;
-    } else if ((debug_gather_pre(sendbuf, S), rc = gather_node_leader(sendbuf, nullptr, S)) ||
-               (rc = debug_gather_check(sendbuf, nullptr, S, 0))) {
+    } else if ((rc = gather_node_leader(sendbuf, nullptr, S))) {
         return rc;
     }
     if ((rc = bcast_node(recvbuf, main_bytes, 0, stream))) return rc;
