@@ -877,6 +877,9 @@ SOAK = [  # (ranks, calls, seed, environment, ranks per emulated node)
     (2, 4000, 16, {"MV2AMD_P2P_KERNEL_COPY": "0"}, None),
     # two emulated nodes: two-level collectives, leaders over TCP
     (4, 1500, 17, {}, 2),
+    # two nodes of four: the most processes the GPU runs at once (DESIGN.md §5 "Ranks per GPU"),
+    # the 4 MiB calls on the leaders' ring that failed at 12 processes
+    (8, 1000, 18, {}, 4),
 ]
 
 
