@@ -1074,6 +1074,8 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     const Typed t = typed(dt);
     if (t.tsize < 0 || t.extent <= 0) return MPI_ERR_TYPE;
     const int n = J.n, me = J.me;
+    // across nodes MV2AMD_MN_PROG_MAX may lower the programs' limit (runtime/coll.cpp mn_prog_max)
+    const int pm = world().nnodes > 1 ? mn_prog_max() : kMaxRanks;
     long total = 0, disp = 0;
     std::vector<size_t> cz(n);
     for (int j = 0; j < n; ++j) {
@@ -1085,7 +1087,7 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     Plan p;
     int rc;
     const bool noncomm = op.opk == OPK_USER_NONCOMM;
-    if (n > kMaxRanks && noncomm) {
+    if (n > pm && noncomm) {
         // MPIR_Reduce_scatter_non_comm_MV2 (red_scat_osu.c:1367-1760) and the nonblocking / block
         // forms' same choice (orders.cpp plan_rs_noncomm) beyond a program's registers: this rank's
         // block evaluated from the algorithm's expression; a power-of-two size with equal counts
@@ -1094,7 +1096,7 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
         for (int j = 1; j < n; ++j) equal = equal && counts[j] == counts[0];
         p.algo = (n & (n - 1)) == 0 && equal ? ALG_RS_NONCOMM_POF2 : ALG_RS_NONCOMM_RD;
         if (nbc_kind() == NBC_NONE) pvar_note(PV_COLL_REDUCE_SCATTER, p, false, (size_t)total, n);
-    } else if (n > kMaxRanks) {
+    } else if (n > pm) {
         // more ranks than a program holds: the algorithm's schedule evaluated for this rank's block
         const int algo = reduce_scatter_algo(n, total * t.tsize);
         p.algo = algo;
@@ -1151,7 +1153,7 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
     if ((rc = fetch(o, disp, disp + c, W, rspan))) return rc;
     R.resize((size_t)c * (size_t)t.tsize + 1);
     if (!R.data()) return MPI_ERR_NO_MEM;
-    if (n > kMaxRanks && noncomm) {
+    if (n > pm && noncomm) {
         // the expression's tree over the n operands' block, uop(in = b, inout = a) per node
         std::vector<ExprNode> nodes;
         const int root = rs_noncomm_expr(n, me, p.algo == ALG_RS_NONCOMM_POF2, nodes);
@@ -1161,7 +1163,7 @@ int host_reduce_scatter(const void *sendbuf, void *recvbuf, const int *counts, M
         if ((rc = dtype_pack(out.data(), c, t.dt, R.data()))) return rc;
         return dtype_unpack(R.data(), c, t.dt, recvbuf);
     }
-    if (n > kMaxRanks) {
+    if (n > pm) {
         BigEval ev{W.data(), rspan, n, c, &t, op.fn, true, {}};
         std::vector<char> out((size_t)rspan + 1);
         if (p.algo == ALG_RS_RING) ev.rs_ring(me, out.data());

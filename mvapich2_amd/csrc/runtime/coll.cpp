@@ -2133,16 +2133,6 @@ static int mn_select(int ppn, int gsize, long nbytes, int *intra, int *inter) {
 // two-level reduce helper, Reduce_scatter the basic algorithm) — correct for every builtin op,
 // its fp order not the reference's (unpinned; integer, bitwise, logical and LOC results exact).
 enum MnRoute { MN_TWO_LEVEL_R = 0, MN_RING_R = 1, MN_FLAT_PROG = 2, MN_SCHED = 3, MN_FALLBACK = 4, MN_BASIC_R = 5 };
-// The most ranks a flat algorithm runs as per-element programs: kMaxRanks, or fewer with
-// MV2AMD_MN_PROG_MAX (tests: the message schedules on jobs small enough to share one GPU without
-// oversubscribing its hardware scheduler, DESIGN.md "Ranks per GPU")
-static int mn_prog_max() {
-    static const int m = [] {
-        const long v = env_long_coll("MV2AMD_MN_PROG_MAX", kMaxRanks);
-        return (int)(v < 1 ? 1 : v > kMaxRanks ? kMaxRanks : v);
-    }();
-    return m;
-}
 static int mn_flat_route(int gsize) {
     return gsize <= mn_prog_max() ? MN_FLAT_PROG : gsize <= kMeshMaxRanks ? MN_SCHED : MN_FALLBACK;
 }
@@ -2507,7 +2497,7 @@ namespace {
 int leader_prog(char *acc, size_t count, int dtype, int op, size_t bytes, int algo) {
     World &w = world();
     const int K = w.nnodes, me = w.node;
-    if (K > kMaxRanks) {
+    if (K > mn_prog_max()) {
         LeaderLinks x;
         return sched_allreduce(x, K, me, acc, g_mn.d1, count, bytes / count, dtype, op, algo == ALG_PT2PT_RD);
     }
@@ -2604,7 +2594,7 @@ static int mn_reduce_leaders(size_t count, const DtypeInfo *dt, int dtype, int o
     const int K = w.nnodes, me = w.node;
     const size_t ext = (size_t)dt->extent, bytes = count * ext;
     int rc = 0;
-    if (K > kMaxRanks) {
+    if (K > mn_prog_max()) {
         LeaderLinks x;
         if (algo == ALG_KNOMIAL) return sched_knomial_reduce(x, K, me, rnode, k, g_mn.d0, g_mn.d1, count, ext, dtype, op);
         if (algo == ALG_REDSCAT_GATHER)
@@ -2840,7 +2830,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
         const int chain[2] = {PV_RED_TWO_LEVEL_HELPER, fid};
         pvar_note_ids(chain, w.rank == 0 ? 2 : 1);
         if ((rc = plan_reduce_forced(L, 0, count, sel.intra, sel.k, &s->node))) return rc;
-        if (K > kMaxRanks) {
+        if (K > mn_prog_max()) {
             s->big = 1;
             s->forced = sel.algo;
             s->root = root / L;
@@ -2931,7 +2921,7 @@ int mv2::mn_host_schedule(int coll, size_t count, int tsize, int textent, bool i
     default: rc = plan_allreduce(L, 0, count, tsize, textent, in_place, 0, &s->node, opk); break;
     }
     if (rc) return rc;
-    if (K > kMaxRanks) {  // the leaders' pt2pt_rs / _rd: recursive doubling for a user op
+    if (K > mn_prog_max()) {  // the leaders' pt2pt_rs / _rd: recursive doubling for a user op
         s->big = 1;
         s->forced = ALG_PT2PT_RD;
         return 0;

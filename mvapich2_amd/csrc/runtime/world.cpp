@@ -258,6 +258,18 @@ static void host_windows_release() {
     g_own_win = HostWin{};
 }
 
+// The most ranks (and node leaders) a flat algorithm runs as per-element programs across nodes:
+// kMaxRanks, or fewer with MV2AMD_MN_PROG_MAX (tests: the message schedules of jobs above 8 ranks
+// on jobs small enough to share one GPU without oversubscribing its hardware scheduler, DESIGN.md
+// §5 "Ranks per GPU")
+int mn_prog_max() {
+    static const int m = [] {
+        const long v = env_long("MV2AMD_MN_PROG_MAX", kMaxRanks);
+        return (int)(v < 1 ? 1 : v > kMaxRanks ? kMaxRanks : v);
+    }();
+    return m;
+}
+
 void *get_scratch(int idx, size_t bytes) {
     World &w = g_world;
     if (w.scratch_bytes[idx] >= bytes && w.scratch[idx]) return w.scratch[idx];

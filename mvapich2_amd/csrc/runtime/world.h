@@ -231,6 +231,9 @@ void *pool_get(size_t bytes);
 void pool_put(void *p);  // back to the pool (the device work using it has completed)
 bool coll_context_poisoned();  // runtime/p2p.cpp: an abandoned collective request is still in flight
 unsigned long long p2p_unexpected_matched();  // runtime/p2p.cpp: unexpected messages later taken by a receive
+// runtime/coll.cpp: across nodes, the most ranks (and node leaders) a flat algorithm runs as
+// per-element programs; above it, its message schedule (MV2AMD_MN_PROG_MAX, default kMaxRanks)
+int mn_prog_max();
 int coll_selftest();  // coll.cpp: init-time check of the cross-GPU publish protocol
 void pipe_tiling_for(size_t seg_bytes, int *grid, size_t *tsub);  // coll.cpp: a segment's grid and bytes per round
 int pipe_autotune();  // coll.cpp: init-time choice of the pipelined kernels' tiling

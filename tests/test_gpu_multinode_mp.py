@@ -488,20 +488,24 @@ def user_reduce_across(xs, commute, count, ppn, root):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n,ppn", [(4, 2), (6, 3), (8, 4), (3, 1), (12, 1), (10, 2)])
-def test_user_ops_across_nodes(n, ppn, tmp_path):
+# (ranks, ranks per node, MV2AMD_MN_PROG_MAX): at most 8 processes share the one GPU (DESIGN.md §5
+# "Ranks per GPU"), so the schedules of jobs above 8 ranks / 8 nodes run at 8 and 6 ranks with the
+# programs' limit lowered to 4
+@pytest.mark.parametrize("n,ppn,pm", [(4, 2, 8), (6, 3, 8), (8, 4, 8), (3, 1, 8), (8, 1, 4), (6, 2, 4)])
+def test_user_ops_across_nodes(n, ppn, pm, tmp_path):
     """User MPI_Ops across nodes (host-evaluated, mpi/user_coll.cpp): the device path's schedule
     over the job's ranks — two-level (node step, leaders' step) or flat — with operands that travel
     packed over the leaders' links; MPI_Reduce: the two-level helper (node reduce to local rank 0,
     binomial over the leaders) for a commutative op, the flat binomial for a non-commutative one;
     MPI_Reduce_scatter: MPIR_Reduce_scatter_MV2's flat selection (non_comm forms included).  Above
-    8 ranks (12x1, 5x2) the host evaluates the message schedules themselves (user_coll.cpp
-    BigEval: recursive doubling, the ring's own chunk, the binomial; leaders' steps over more than
-    8 nodes; reduce-scatter's basic / recursive halving / ring for this rank's block, and the
-    non-commutative reduce-scatter's recursive doubling as an expression tree)."""
+    the programs' limit (8 ranks; 4 in the 8x1 and 6x2 cases) the host evaluates the message
+    schedules themselves (user_coll.cpp BigEval: recursive doubling, the ring's own chunk, the
+    binomial; leaders' steps over more nodes than the limit; reduce-scatter's basic / recursive
+    halving / ring for this rank's block, and the non-commutative reduce-scatter's recursive
+    doubling as an expression tree)."""
     cases, seed = [], 700
     for commute in (1, 0):
-        for count in (100, 2000, 33) + ((600001,) if commute and n > 8 else ()):
+        for count in (100, 2000, 33) + ((600001,) if commute and n > pm else ()):
             cases.append({"id": f"ua{seed}", "kind": "user_allreduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed})
             seed += 1
@@ -509,14 +513,14 @@ def test_user_ops_across_nodes(n, ppn, tmp_path):
             cases.append({"id": f"ur{seed}", "kind": "user_reduce", "commute": commute, "count": count,
                           "type": "MPI_INT", "seed": seed, "root": root})
             seed += 1
-        # above 8 ranks: basic (a 24-byte operand, half the blocks empty), halving, ring; the
+        # above the limit: basic (a 24-byte operand, half the blocks empty), halving, ring; the
         # non_comm recursive doubling from its expression tree (user_coll.cpp BigEval::expr)
-        for per in (3, 400) if n <= 8 else (0, 400, 12000) if commute else (5, 300):
+        for per in (3, 400) if n <= pm else (0, 400, 12000) if commute else (5, 300):
             counts = [per] * n if not commute else [per + (r % 2) for r in range(n)]
             cases.append({"id": f"us{seed}", "kind": "user_reduce_scatter", "commute": commute, "count": sum(counts),
                           "recvcounts": counts, "type": "MPI_INT", "seed": seed})
             seed += 1
-    res = run_workers(n, cases, tmp_path, ppn=ppn)
+    res = run_workers(n, cases, tmp_path, ppn=ppn, extra_env={"MV2AMD_MN_PROG_MAX": str(pm)})
     for case in cases:
         cid, k, count, commute = case["id"], case["kind"], case["count"], bool(case["commute"])
         if k == "user_allreduce":
@@ -622,15 +626,17 @@ def test_mpit_counts_across_nodes(tmp_path):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("n,ppn", [(12, 1), (12, 2), (10, 2), (12, 4)])
+@pytest.mark.parametrize("n,ppn", [(8, 1), (8, 2), (6, 2), (8, 4)])
 def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
-    """Jobs of more than 8 ranks (at most 12 processes on the one GPU): the flat pt2pt_rs /
-    pt2pt_rd the tables name over every rank, and the ring wrapper's pt2pt_rs remainder, run as
-    the reference's message schedule over the point-to-point channels (coll.cpp sched_allreduce,
-    RankChannels); the small-message shortcut's recursive doubling over more than 8 node leaders
-    (LeaderLinks); the tables' numproc 8 / 16 entries (10 and 12 ranks: comm_size_index of 8);
-    MPI_Reduce_scatter's schedules over every rank (sched_rs_halving / _pairwise / _ring); the
-    nonblocking Iallreduce / Ireduce schedules flat over every rank (mn_sched_naive)."""
+    """What jobs of more than 8 ranks run, on at most 8 processes (more must not share the one GPU,
+    DESIGN.md §5 "Ranks per GPU"): with the programs' limit lowered to 4 (MV2AMD_MN_PROG_MAX) the
+    flat pt2pt_rs / pt2pt_rd the tables name over every rank, and the ring wrapper's pt2pt_rs
+    remainder, run as the reference's message schedule over the point-to-point channels (coll.cpp
+    sched_allreduce, RankChannels); the small-message shortcut's recursive doubling over more node
+    leaders than the limit (8x1: LeaderLinks); MPI_Reduce_scatter's schedules over every rank
+    (sched_rs_halving / _pairwise / _ring); the nonblocking Iallreduce / Ireduce schedules flat over
+    every rank (mn_sched_naive).  (The tables' numproc 16 entries that 10 and 12 ranks select are
+    CPU-tested, tests/test_multinode_tables.py.)"""
     cases, seed = [], 1300
     for t, op, count, ties in (("MPI_FLOAT", "MPI_SUM", 10, False), ("MPI_FLOAT", "MPI_SUM", 300, False),
                                ("MPI_FLOAT", "MPI_SUM", 700, False), ("MPI_FLOAT", "MPI_SUM", 1500, False),
@@ -700,7 +706,7 @@ def test_more_than_eight_ranks_across_nodes(n, ppn, tmp_path):
             case["via"] = via
         cases.append(case)
         seed += 1
-    res = run_workers(n, cases, tmp_path, ppn=ppn)
+    res = run_workers(n, cases, tmp_path, ppn=ppn, extra_env={"MV2AMD_MN_PROG_MAX": "4"})
     nodes = n // ppn
     for case in cases:
         k, cid, t, count = case["kind"], case["id"], case["type"], case["count"]
