@@ -273,23 +273,28 @@ __device__ __forceinline__ void dseq_advance(DevSeq *d, uint64_t de, uint64_t dr
     }
 }
 
-template <class Rd, bool PROG>
+// SMALL: an operand with no whole 16-byte vectors (nvec == 0), element by element in workgroup 0;
+// the vector phases are compiled out, so the kernel's code is a fraction of the general body's
+// (the 8-byte allreduce: 45 KB of code against the one-shot allgather's 4.7 KB, profiles/r05ay)
+template <class Rd, bool PROG, bool SMALL = false>
 __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, uint64_t epoch, size_t poff) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
     const int blk = blockIdx.x, G = gridDim.x;
-    const size_t per = (a.nvec + G - 1) / G;
+    const size_t nvec = SMALL ? 0 : a.nvec;
+    const size_t per = (nvec + G - 1) / G;
     const size_t vb = (size_t)blk * per;
-    const size_t ve = vb + per < a.nvec ? vb + per : a.nvec;
+    const size_t ve = vb + per < nvec ? vb + per : nvec;
     const v4u *send = (const v4u *)a.send;
     // phase A: push my data to every peer's slot (me)
+    if constexpr (!SMALL)
     for (size_t i = vb + threadIdx.x; i < ve; i += kThreads) {
         const v4u x = send[i];
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j)
             if (j < a.n && j != a.me) ((v4u *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes))[i] = x;
     }
-    const size_t tail0 = a.nvec * N;
+    const size_t tail0 = nvec * N;
     if (blk == 0) {
         for (size_t e = tail0 + threadIdx.x; e < a.count; e += kThreads) {
             const T x = ((const T *)a.send)[e];
@@ -308,7 +313,8 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, uint64_t epoc
         for (int j = 0; j < kMaxRanks; ++j)
             v[j] = (j >= a.n) ? v4u{0, 0, 0, 0} : (j == a.me) ? send[i] : ld_nt((const v4u *)(arena_own + (size_t)j * a.slot_bytes) + i);
     };
-    if constexpr (PROG) {
+    if constexpr (SMALL) {
+    } else if constexpr (PROG) {
         // program order: the block of a range that lies in one block is fixed once
         int fb = -1;
         if (ve > vb) {
@@ -347,7 +353,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotArgs &a, uint64_t epoc
     }
 }
 
-template <class Rd, bool PROG>
+template <class Rd, bool PROG, bool SMALL = false>
 __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
     uint64_t epoch = a.epoch;
     size_t poff = 0;
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
         epoch = q.epoch + 1;
         poff = (q.os & 1) * a.half;
     }
-    oneshot_body<Rd, PROG>(a, epoch, poff);
+    oneshot_body<Rd, PROG, SMALL>(a, epoch, poff);
     if (a.dseq) dseq_advance(a.dseq, 1, 0, 1);
     block_done(a.done);
 }
@@ -436,6 +442,15 @@ struct LOneShot {
             static const int cap2 = resident_grid((const void *)k_oneshot_rs<Rd>, cfg);
             const int g = cfg.grid < cap2 ? cfg.grid : cap2;
             hipLaunchKernelGGL((k_oneshot_rs<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
+            return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+        }
+        if (a.nvec == 0 && cfg.grid == 1) {  // no whole vector: the compact element-wise kernel
+            if constexpr (Rd::kOrderFree) {
+                hipLaunchKernelGGL((k_oneshot<Rd, false, true>), dim3(1), dim3(kThreads), 0, cfg.stream, a);
+            } else {
+                if (prog) hipLaunchKernelGGL((k_oneshot<Rd, true, true>), dim3(1), dim3(kThreads), 0, cfg.stream, a);
+                else hipLaunchKernelGGL((k_oneshot<Rd, false, true>), dim3(1), dim3(kThreads), 0, cfg.stream, a);
+            }
             return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
         }
         static const int cap0 = resident_grid((const void *)k_oneshot<Rd, false>, cfg);

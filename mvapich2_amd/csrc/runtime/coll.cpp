@@ -1209,9 +1209,15 @@ static int allreduce_impl(const void *sendbuf, void *recvbuf, size_t count, cons
         a.send = s.send;
         a.recv = s.recv;
         a.count = count;
-        a.nvec = nvec;  // (an element-wise body for small operands measured no faster here, r05z)
+        // small operands element by element in one workgroup, on the compact kernel whose code
+        // holds no vector phases (kernels_impl.h LOneShot: 8 B launch -> completion 8.8 -> 7.8 us
+        // at 2 shared ranks, profiles/r05az; the general kernel's element-wise body measured no
+        // faster than its vector body, r05z)
+        static const long scalar_max = env_long_coll("MV2AMD_AR_SCALAR_MAX", 1024);
+        const size_t nv = bytes <= (size_t)scalar_max ? 0 : nvec;
+        a.nvec = nv;
         a.tp = tp;
-        const int g = oneshot_grid(nvec, gcap);
+        const int g = oneshot_grid(nv, gcap);
         LaunchCfg cfg = coll_cfg(g, st);
         tmark0(st);
         rc = launch_oneshot(oi, dt->kind, a, dt->extent, cfg);
