@@ -277,7 +277,7 @@ def bench_n1(args, L):
     extra["mpi_init_ms"] = {"total": round(m.info("init_us") / 1e3, 1), "hip_start": round(m.info("hip_init_us") / 1e3, 1),
                             "code_objects": round(m.info("code_load_us") / 1e3, 1),
                             "what": "MPI_Init wall time on this rank; code objects = loading libmpi.so's gfx950 "
-                                    "code (25 MB, one empty kernel per translation unit)"}
+                                    "code (26 MB, one empty kernel per translation unit)"}
     if args.cpu_seconds > 0:
         extra["cpu_host_allreduce_8rank"] = cpu_baseline_host_allreduce(args.cpu_seconds)
     return line

@@ -371,7 +371,8 @@ __global__ __launch_bounds__(kThreads) void k_oneshot(OneShotArgs a) {
 // j's block of my operand, flags, then reduces partition b of my own block from the n slots in
 // program order — the flag it waits for covers exactly the vectors it reads.  Block tails
 // (elements past the last whole vector) go through workgroup 0 on both sides.
-template <class Rd>
+// SMALL: nvec == 0 with the vector phases compiled out (the compact kernel, as k_oneshot's)
+template <class Rd, bool SMALL = false>
 __global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
     using T = typename Rd::T;
     constexpr int N = 16 / sizeof(T);
@@ -386,14 +387,16 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
     const v4u *send = (const v4u *)a.send;
     // nvec == 0: small blocks that do not start on 16-byte boundaries, element by element in
     // workgroup 0 (the vector range of every block is then empty)
-    const bool sc = a.nvec == 0;
+    const bool sc = SMALL || a.nvec == 0;
     for (int j = 0; j < a.n; ++j) {
         if (j == a.me) continue;
         const size_t v0 = a.wlo[j] / N, v1 = sc ? v0 : (a.wlo[j] + a.wcnt[j]) / N;
-        const size_t per = (v1 - v0 + G - 1) / G;
-        const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
         v4u *dst = (v4u *)(a.arena_peer.p[j] + poff + (size_t)a.me * a.slot_bytes);
-        for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) dst[i] = send[i];
+        if constexpr (!SMALL) {
+            const size_t per = (v1 - v0 + G - 1) / G;
+            const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
+            for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) dst[i] = send[i];
+        }
         if (blk == 0)
             for (size_t e = (sc ? a.wlo[j] : v1 * N) + threadIdx.x; e < a.wlo[j] + a.wcnt[j]; e += kThreads)
                 ((T *)dst)[e] = ((const T *)a.send)[e];
@@ -403,20 +406,22 @@ __global__ __launch_bounds__(kThreads) void k_oneshot_rs(OneShotArgs a) {
         const char *arena_own = a.arena_own + poff;
         const size_t lo = a.wlo[a.me], hi = lo + a.wcnt[a.me];
         const size_t v0 = lo / N, v1 = sc ? v0 : hi / N;
-        const size_t per = (v1 - v0 + G - 1) / G;
-        const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
-        int fb = -1;
-        if (b1 > b0) {
-            const int p0 = prog_block(a.tp.ps, b0 * N), p1 = prog_block(a.tp.ps, b1 * N - 1);
-            if (p0 == p1) fb = p0;
-        }
-        for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) {
-            v4u v[kMaxRanks];
+        if constexpr (!SMALL) {
+            const size_t per = (v1 - v0 + G - 1) / G;
+            const size_t b0 = v0 + (size_t)blk * per, b1 = b0 + per < v1 ? b0 + per : v1;
+            int fb = -1;
+            if (b1 > b0) {
+                const int p0 = prog_block(a.tp.ps, b0 * N), p1 = prog_block(a.tp.ps, b1 * N - 1);
+                if (p0 == p1) fb = p0;
+            }
+            for (size_t i = b0 + threadIdx.x; i < b1; i += kThreads) {
+                v4u v[kMaxRanks];
 #pragma unroll
-            for (int j = 0; j < kMaxRanks; ++j)
-                v[j] = (j >= a.n) ? v4u{0, 0, 0, 0}
-                                  : (j == a.me) ? send[i] : ld_nt((const v4u *)(arena_own + (size_t)j * a.slot_bytes) + i);
-            ((v4u *)a.recv)[i - v0] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
+                for (int j = 0; j < kMaxRanks; ++j)
+                    v[j] = (j >= a.n) ? v4u{0, 0, 0, 0}
+                                      : (j == a.me) ? send[i] : ld_nt((const v4u *)(arena_own + (size_t)j * a.slot_bytes) + i);
+                ((v4u *)a.recv)[i - v0] = vreduce_n<Rd, 4>(v, a.n, a.tp, i * N, fb);
+            }
         }
         if (blk == 0)
             for (size_t e = (sc ? lo : v1 * N) + threadIdx.x; e < hi; e += kThreads) {
@@ -439,6 +444,10 @@ struct LOneShot {
         const bool prog = a.tp.linear == 4;
         if (a.rs) {
             if (!prog) return E_ARG;  // a reduce-scatter block is always evaluated in program order
+            if (a.nvec == 0 && cfg.grid == 1) {
+                hipLaunchKernelGGL((k_oneshot_rs<Rd, true>), dim3(1), dim3(kThreads), 0, cfg.stream, a);
+                return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+            }
             static const int cap2 = resident_grid((const void *)k_oneshot_rs<Rd>, cfg);
             const int g = cfg.grid < cap2 ? cfg.grid : cap2;
             hipLaunchKernelGGL((k_oneshot_rs<Rd>), dim3(g), dim3(kThreads), 0, cfg.stream, a);
