@@ -1,7 +1,5 @@
 set -o pipefail
-# Round 5, pass ba: small allreduces on the compact element-wise one-shot kernel up to
-# MV2AMD_AR_SCALAR_MAX (0 / 1024 / 4096), OSU allreduce 4 B - 8 KiB at 2 and 4 shared ranks; then the
-# final tree: smoke, the whole -m gpu suite, the N = 1 line with rocprofv3 statistics, the 2-rank line
+# Round 5, pass bc: the final tree (compact one-shot allreduce and reduce-scatter kernels): smoke, the whole -m gpu suite, the N = 1 line with rocprofv3 statistics, the 2-rank line
 O=gpurun_out/r05bc
 mkdir -p $O
 export TMPDIR=/tmp
