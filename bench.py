@@ -35,6 +35,8 @@ METRIC = "osu_allreduce busbw GB/s fp32 SUM 256MB at 1/2/4/8 MI355X; 8B latency 
 HBM_PEAK = 8000.0        # GB/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK = 153.0        # GB/s per link per direction (task statement)
 S_BYTES = 256 * 1024 * 1024
+# completion-word events (mv2h_get_info; runtime/coll.cpp wait_done), copied into both lines
+WORD_KEYS = ("done_late", "done_missed", "done_xcd_split")
 WORLD = 0x44000000        # MPI_COMM_WORLD (MPICH ABI)
 
 
@@ -85,12 +87,16 @@ def host_allreduce_record(out):
         placement = f"{ranks} ranks pinned 1/CPU on {hdr['cores_used']} physical cores (SMT siblings shared)"
     else:
         placement = f"{ranks} ranks pinned 1/core"
+    if hdr.get("l3_domains_used") is not None:
+        placement += f" on {hdr['l3_domains_used']} L3 domain{'s' if hdr['l3_domains_used'] != 1 else ''}"
     return {"latency_8B_us": by[8]["lat_us"], "busbw_64MiB_GBps": by[64 << 20]["busbw_GBps"],
             "busbw_1MiB_GBps": by[1 << 20]["busbw_GBps"], "all_ok": all(r["ok"] for r in rows),
             "cores": hdr["cpus_used"], "cpus_available": hdr["cpus_available"], "cpus_used": hdr["cpus_used"],
             "cores_used": hdr["cores_used"], "oversubscribed": hdr["oversubscribed"], "smt_shared": hdr["smt_shared"],
             "rank_cpus": hdr["rank_cpus"], "rank_cpu_busy_pct_before": hdr.get("rank_cpu_busy_pct"),
             "placement_policy": hdr.get("placement_policy"), "cgroup_cpu_quota": hdr["cgroup_cpu_quota"],
+            "rank_l3": hdr.get("rank_l3"), "l3_domains_used": hdr.get("l3_domains_used"),
+            "l3_domain_cores": hdr.get("l3_domain_cores"),
             "yields_8B": by[8].get("yields"), "throttled_periods_8B": by[8].get("throttled"),
             "yields_all_sizes": sum(r.get("yields", 0) for r in rows),
             "throttled_periods_all_sizes": sum(r.get("throttled", 0) for r in rows),
@@ -135,6 +141,8 @@ def cpu_baseline_nranks_from(h):
     return {"value": h["busbw_64MiB_GBps"], "unit": "GB/s", "cores": h["cpus_used"], "kind": "port",
             "correct": h["all_ok"], "cpus_available": h["cpus_available"], "cpus_used": h["cpus_used"],
             "oversubscribed": h["oversubscribed"], "rank_cpus": h["rank_cpus"],
+            "rank_l3": h.get("rank_l3"), "l3_domains_used": h.get("l3_domains_used"),
+            "placement_policy": h.get("placement_policy"),
             "sample": f"configs[0]: reference host-buffer ch3 shared-memory MPI_Allreduce fp32 SUM restated "
                       f"(oracle/host_allreduce.c), 64 MiB busbw; 8 B latency {h['latency_8B_us']} us, 1 MiB busbw "
                       f"{h['busbw_1MiB_GBps']} GB/s; {h['placement']} of '{h['cpu']}'; {h['what']}"}
@@ -278,21 +286,27 @@ def bench_n1(args, L):
                             "code_objects": round(m.info("code_load_us") / 1e3, 1),
                             "what": "MPI_Init wall time on this rank; code objects = loading libmpi.so's gfx950 "
                                     "code (26 MB, one empty kernel per translation unit)"}
+    # completion-word events of this run (runtime/coll.cpp wait_done): a word still unseen 200 us
+    # after launch, a kernel that ended without raising it, a kernel whose block groups ran on
+    # several XCDs -- a slow call in this line is explained or ruled out by these
+    extra["completion_word"] = {k: m.info(k) for k in WORD_KEYS}
     if args.cpu_seconds > 0:
         extra["cpu_host_allreduce_8rank"] = cpu_baseline_host_allreduce(args.cpu_seconds)
     return line
 
 
-def _timed(L, world, call, steps, warmup):
+def _timed(L, world, call, steps, warmup, step_call=None):
     """OSU loop on resident device buffers: warmup, barrier + device sync,
-    `steps` calls, device sync + barrier.  Returns (s per call, mean kernel ms)."""
+    `steps` calls, device sync + barrier.  Returns (s per call, mean kernel ms).
+    step_call(i), when given, is the i-th timed call (each timed call its own result buffer, so
+    that every one is verified afterwards); the kernel-time loop uses `call`."""
     for _ in range(warmup):
         m.check(call(), "warmup")
     L.MPI_Barrier(world)
     L.mv2h_device_synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        m.check(call(), "timed call")
+    for i in range(steps):
+        m.check(step_call(i) if step_call else call(), "timed call")
     L.mv2h_device_synchronize()
     L.MPI_Barrier(world)
     t = time.perf_counter() - t0
@@ -545,14 +559,19 @@ def bench_nranks(args, L, rank, size):
     rb = m.DeviceBuffer(S_BYTES)
     sb.upload(_pattern(count, rank))
 
-    # headline: allreduce fp32 SUM 256 MiB, validated over the whole buffer
+    # headline: allreduce fp32 SUM 256 MiB, validated over the whole buffer -- every timed call writes
+    # its own result buffer (steps x 256 MiB of HBM) and each is checked after the timed region
     ar = lambda: L.MPI_Allreduce(sb.ptr, rb.ptr, count, F32, SUM, world)  # noqa: E731
     rb.upload(np.zeros(count, dtype=np.float32))
     m.check(ar(), "MPI_Allreduce")
     want = _expected_sum(count, size)
     ok = bool(np.array_equal(rb.download(np.float32, count=count), want))
-    step_s, kms = _timed(L, world, ar, args.steps, args.warmup)
-    ok = ok and bool(np.array_equal(rb.download(np.float32, count=count), want))
+    rbs = [m.DeviceBuffer(S_BYTES) for _ in range(args.steps)]
+    step_s, kms = _timed(L, world, ar, args.steps, args.warmup,
+                         step_call=lambda i: L.MPI_Allreduce(sb.ptr, rbs[i].ptr, count, F32, SUM, world))
+    verified = sum(bool(np.array_equal(b.download(np.float32, count=count), want)) for b in rbs)
+    del rbs
+    ok = ok and verified == args.steps and bool(np.array_equal(rb.download(np.float32, count=count), want))
     del want
 
     # config 4 / config 5 lines at 256 MiB (fewer steps)
@@ -655,7 +674,8 @@ def bench_nranks(args, L, rank, size):
 
     # max over ranks through the library itself (device allreduce MAX)
     vals = np.array([step_s, kms, rs_s, rs_k, ag_s, ag_k, bc_s, bc_k, ml_s, ml_k, lat / args.lat_iters,
-                     float(np.median(lat_k)), 0.0 if (ok and lat_ok and uops["ok"]) else 1.0, p2p_s, sq_s]
+                     float(np.median(lat_k)), 0.0 if (ok and lat_ok and uops["ok"]) else 1.0, p2p_s, sq_s,
+                     float(args.steps - verified)]
                     + [u["s"] for u in uops["lines"]], dtype=np.float64)
     dm = m.DeviceBuffer(vals.nbytes)
     dm.upload(vals)
@@ -663,10 +683,23 @@ def bench_nranks(args, L, rank, size):
     m.check(L.MPI_Allreduce(dm.ptr, dr.ptr, len(vals), F64, MAX, world), "max")
     got = dr.download(np.float64)
     keys = ("step_s", "kms", "rs_s", "rs_k", "ag_s", "ag_k", "bc_s", "bc_k", "ml_s", "ml_k", "lat_s", "lat_k_ms", "bad",
-            "p2p_s", "sq_s")
-    t = {k: float(v) for k, v in zip(keys, got[:15])}
-    for u, tu in zip(uops["lines"], got[15:]):
+            "p2p_s", "sq_s", "unverified")
+    t = {k: float(v) for k, v in zip(keys, got[:len(keys)])}
+    for u, tu in zip(uops["lines"], got[len(keys):]):
         u["s"] = float(tu)
+    # completion-word events summed over ranks (runtime/coll.cpp wait_done: late words, words the
+    # kernel never raised, words of kernels whose block groups ran on several XCDs)
+    word = np.array([m.info(k) for k in WORD_KEYS], dtype=np.int64)
+    dw = m.DeviceBuffer(word.nbytes)
+    dw.upload(word)
+    dws = m.DeviceBuffer(word.nbytes)
+    m.check(L.MPI_Allreduce(dw.ptr, dws.ptr, len(WORD_KEYS), TYPES["MPI_LONG"][0], SUM, world), "word counts")
+    checks = {"timed_calls_verified": args.steps - int(t["unverified"]), "timed_calls": args.steps,
+              "completion_word_sum_over_ranks": dict(zip(WORD_KEYS, (int(v) for v in dws.download(np.int64)))),
+              "release_protocol": "light" if m.info("light_release") else "full",
+              "shared_gpu_constants": {"MV2AMD_AR_SCALAR_MAX": m.info("ar_scalar_max"),
+                                       "MV2AMD_RS_SCALAR_MAX": m.info("rs_scalar_max"),
+                                       "p2p_copy_kernels": bool(m.info("p2p_kernel_copy"))}}
     # HBM traffic of k_pipe (PIPE_AR) per launch on one rank: the PMC ratio (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py) of a committed pass taken at THIS rank
     # count, ranks per GPU and tiling knobs, times this call's per-rank algorithmic HBM bytes
@@ -707,7 +740,7 @@ def bench_nranks(args, L, rank, size):
     else:
         rccl = None
     line = assemble_nranks_line(size, nshare, args.steps, args.warmup, t, lat_avg, uops["lines"], nrec, pbytes * win,
-                                tiling, traffic, rccl)
+                                tiling, traffic, rccl, checks=checks)
     if sweep is not None:
         line["extra"]["osu_sweep"] = sweep
         # the metric's 8-byte latency as OSU measures it (the C loop, no ctypes call overhead); the
@@ -733,7 +766,7 @@ def pipe_alg_bytes(size):
 
 
 def assemble_nranks_line(size, nshare, steps, warmup, t, lat_avg, uop_lines, nrec, p2p_bytes, tiling, traffic, rccl,
-                         cpu_baseline=None):
+                         cpu_baseline=None, checks=None):
     """The N > 1 bench line from max-over-ranks measurements (pure: no GPU, no library calls, so the
     branches the 1-GPU box never takes -- nshare == 1, a successful or failed RCCL comparator -- are
     CPU-tested: tests/test_bench_line.py).  `t` holds seconds per call (`*_s`) and HIP-event kernel
@@ -759,6 +792,15 @@ def assemble_nranks_line(size, nshare, steps, warmup, t, lat_avg, uop_lines, nre
         "pt2pt_bw_16MiB_x8": {"GBps": round(p2p_bytes / t["p2p_s"] / 1e9, 2), "ms_per_window": round(t["p2p_s"] * 1e3, 3),
                               "what": "osu_bw pattern rank 0 -> 1: 8 x 16 MiB MPI_Isend / MPI_Irecv device buffers"},
     }
+    checks = checks or {}
+    if "completion_word_sum_over_ranks" in checks:
+        extra["completion_word"] = dict(checks["completion_word_sum_over_ranks"])
+    if "shared_gpu_constants" in checks:
+        # chosen on one shared GPU and not probed at MPI_Init: a one-rank-per-GPU run ships them unmeasured
+        extra["constants_tuned_on_shared_gpu"] = dict(
+            checks["shared_gpu_constants"],
+            note=("tuned on one shared GPU (profiles/r05y, r05ba, r05l), not probed at MPI_Init: "
+                  "unmeasured over xGMI" if nshare == 1 else f"{nshare} ranks share this GPU, as when they were tuned"))
     if rccl is not None:
         extra["rccl_comparator"] = rccl
         if "busbw_GBps" in rccl:
@@ -792,8 +834,12 @@ def assemble_nranks_line(size, nshare, steps, warmup, t, lat_avg, uop_lines, nre
                        "processes' queues are scheduled (DESIGN.md §4 Stream order); not a one-GPU-per-rank figure"}
                       if nshare > 1 else {}),
                    "correct": not bool(t["bad"]),
-                   "validation": "whole 256 MiB result vs exact expected sum, before and after timing",
-                   "pipe_tiling": tiling},
+                   "validation": "whole 256 MiB result vs exact expected sum: a call before timing, every timed "
+                                 "call (each into its own result buffer), the buffer after the kernel-time loop",
+                   **({"timed_calls_verified": checks["timed_calls_verified"], "timed_calls": checks["timed_calls"]}
+                      if "timed_calls_verified" in checks else {}),
+                   "pipe_tiling": dict(tiling, **({"release_protocol": checks["release_protocol"]}
+                                                  if "release_protocol" in checks else {}))},
         "roofline": roof,
         "cpu_baseline": cpu_baseline,
         "extra": extra,

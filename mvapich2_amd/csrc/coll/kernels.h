@@ -121,6 +121,7 @@ struct LaunchCfg {
     int cus = 256;    // compute units of the device
     int nshare = 1;   // max ranks sharing one GPU (same on every rank)
     Done done{};      // completion word (reduce_local)
+    size_t tiny_max = 0;  // reduce_local: operands up to this many bytes take the one-wave kernel
 };
 
 // Grid cap for `per_cu` blocks per CU when `nshare` ranks share the GPU.

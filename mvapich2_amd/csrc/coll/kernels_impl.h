@@ -62,12 +62,33 @@ __global__ __launch_bounds__(kThreads) void k_reduce_local_elem(const typename R
     block_done(dn);
 }
 
+// small operands (the metric's 8-byte call): one wave, element by element, then lane 0 raises the
+// completion word with a system-scope release (block_done's one-workgroup path).  Against the
+// 512-thread streaming kernel this dispatches one wave instead of eight and passes 32 bytes of
+// arguments instead of 88 (the host launch and the CP's dispatch are most of an 8-byte call:
+// tools/diag/rl_lat.cpp, profiles/r06e)
+template <class Rd>
+__global__ __launch_bounds__(64) void k_reduce_local_tiny(const typename Rd::T *__restrict__ in,
+                                                          typename Rd::T *__restrict__ io, uint32_t count,
+                                                          uint64_t *flag, uint64_t seq) {
+    for (uint32_t e = threadIdx.x; e < count; e += 64) io[e] = Rd::apply(io[e], in[e]);
+    if (flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's store acknowledged (one wave)
+        if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 template <int OP, int K>
 struct LReduceLocal {
     static int run(const void *in, void *inout, size_t count, const LaunchCfg &cfg) {
         using Rd = R<OP, K>;
         using T = typename Rd::T;
         constexpr size_t VPT = 16 / sizeof(T);
+        if (count * sizeof(T) <= cfg.tiny_max && count <= 0xffffffffu) {
+            hipLaunchKernelGGL((k_reduce_local_tiny<Rd>), dim3(1), dim3(64), 0, cfg.stream, (const T *)in, (T *)inout,
+                               (uint32_t)count, cfg.done.flag, cfg.done.seq);
+            return hipGetLastError() == hipSuccess ? 0 : E_INTERN;
+        }
         const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)inout % 16 == 0);
         if (!aligned) {
             size_t g = (count + kThreads - 1) / kThreads;

@@ -60,13 +60,13 @@ struct ProgSet {
 // round trip (runtime/coll.cpp finish()).
 constexpr int kDoneStride = 1024;  // counter spacing in words (4 KiB: separate memory channels)
 constexpr int kDoneSub = 64;       // first-level counters (blockIdx % 64)
-constexpr int kDoneCtrs = kDoneSub + 8 + 1;  // + per-XCD group (blockIdx % 8) + groups done
+constexpr int kDoneCtrs = kDoneSub + 8 + 1;  // + group counters (blockIdx % 8) + groups done; each with an XCD mask
 constexpr size_t kDoneBytes = (size_t)kDoneCtrs * kDoneStride * sizeof(uint32_t);
 // ints in the pinned error word block (wait_mask records a timeout's context there)
 constexpr int kErrWords = 64;
 struct Done {
     uint32_t *ctr;   // kDoneCtrs counters, kDoneStride words apart; all 0 between launches
-    uint64_t *flag;  // pinned host word
+    uint64_t *flag;  // pinned host words: [0] last completed seq, [1] last seq whose groups were split over XCDs
     uint64_t seq;
 };
 
@@ -183,36 +183,76 @@ __device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, ui
 // block waits for its own stores to be acknowledged and counts itself,
 // relaxed, in sub-counter blockIdx % 64 (spreads the arrivals of a large
 // grid over 64 addresses); the last arrival of a sub-counter counts it in its
-// XCD group blockIdx % 8 (round-robin workgroup placement over the 8 XCDs);
-// the last arrival of a group writes back that XCD's L2 (one agent-scope
-// release per XCD, not per block: a release per block cost 20-220 us on a
-// 256 MiB Reduce_local) and counts the group; the last group resets the
-// counters for the next launch and publishes seq to the host at system
-// scope.  Stream-ordered consumers of the result wait for the kernel's end
-// anyway; the release makes the data visible to work on other streams of
-// this GPU as soon as the host returns.
+// group blockIdx % 8; the last arrival of a group writes back the L2 of the
+// XCD it runs on (one agent-scope release per group, not per block: a release
+// per block cost 20-220 us on a 256 MiB Reduce_local) and counts the group;
+// the last group resets the counters for the next launch and publishes seq to
+// the host at system scope.  Stream-ordered consumers of the result wait for
+// the kernel's end anyway; the release makes the data visible to work on other
+// streams of this GPU as soon as the host returns.
+//
+// Blocks b and b + 8 are observed to share an XCD, but HIP promises no
+// workgroup -> XCD placement (MI355X_MICROARCH.md "Contract"), and one group's
+// release writes back only the XCD it runs on.  So every block records the XCD
+// it really ran on (HW_REG_XCC_ID) in its sub-counter's mask, before its count;
+// each sub-counter's last arrival folds that mask into its group's, and a group
+// whose blocks ran on more than one XCD is "split": its release cannot cover
+// them all.  The last group then also writes seq into d.flag[1], and the host
+// completes that call with a stream synchronisation (the kernel's end releases
+// every XCD's L2) instead of trusting the word (runtime/coll.cpp wait_done).
+// The mask OR is issued before the block's store wait, so it costs no extra
+// round trip on the blocks' path; only the 64 + 8 last arrivals read masks.
+constexpr int kDoneMask = 16;            // word offset of a counter's XCD mask (its own 64-byte line)
+constexpr unsigned kDoneSplit = 1u << 16; // in a group mask: one of its sub-counters was split
+// Masks are read by an OR of this otherwise unused bit, not by an atomic load: the compiler lowers
+// a fetch_or(p, 0) to a plain sc1 load, which the local XCD's L2 may serve, while the ORs from
+// other XCDs are read-modify-writes performed where the counters' adds are
+constexpr unsigned kDoneRead = 1u << 31;
+__device__ __forceinline__ unsigned mask_read(uint32_t *p) {
+    return __hip_atomic_fetch_or(p, kDoneRead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kDoneRead;
+}
+
+__device__ __forceinline__ unsigned xcc_id() {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x;
+}
+
 __device__ __forceinline__ void block_done(const Done &d) {
     if (!d.flag) return;
+    const bool multi = gridDim.x > 1;
+    uint32_t *c = d.ctr;
+    const unsigned nb = gridDim.x, b = blockIdx.x;
+    const unsigned i = b % kDoneSub, x = b & 7u;
+    unsigned xbit = 0;
+    if (multi && threadIdx.x == 0) {
+        xbit = 1u << xcc_id();
+        // no return value: acknowledged by the store wait below, so performed before this block's count
+        __hip_atomic_fetch_or(c + i * kDoneStride + kDoneMask, xbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (gridDim.x == 1) {
+    if (!multi) {
         // one workgroup (small-message one-shot): no counters, no agent fence; the
         // system-scope release of the host word writes back this XCD's L2 itself
         if (threadIdx.x == 0) __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
     if (threadIdx.x == 0) {
-        const unsigned nb = gridDim.x, b = blockIdx.x;
-        const unsigned i = b % kDoneSub, x = b & 7u;
         const unsigned members = (nb - i + kDoneSub - 1) / kDoneSub;  // blocks with b % 64 == i
         const unsigned nsub = nb < (unsigned)kDoneSub ? nb : (unsigned)kDoneSub;
         const unsigned subs = (nsub - x + 7u) / 8u;                    // sub-counters i < nsub with i % 8 == x
         const unsigned groups = nb < 8u ? nb : 8u;
-        uint32_t *c = d.ctr;
         if (__hip_atomic_fetch_add(c + i * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != members)
             return;
+        // every member's mask OR was acknowledged before its count: the mask is complete
+        const unsigned sm = mask_read(c + i * kDoneStride + kDoneMask);
+        __hip_atomic_fetch_or(c + (kDoneSub + x) * kDoneStride + kDoneMask, xbit | (sm != xbit ? kDoneSplit : 0u),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (__hip_atomic_fetch_add(c + (kDoneSub + x) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != subs)
             return;
+        const unsigned gm = mask_read(c + (kDoneSub + x) * kDoneStride + kDoneMask);
         // this XCD's L2 written back before its group counts as done.  The wait is explicit: after a
         // returned atomic the compiler drops the s_waitcnt behind buffer_wbl2 (MI355X_MICROARCH.md,
         // compiler hazard), and the next add then overtook the write-back — the host saw the word
@@ -220,10 +260,18 @@ __device__ __forceinline__ void block_done(const Done &d) {
         // (point-to-point copies of a host-driven schedule) read stale bytes (r04x, 12-rank Iallreduce)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (gm != xbit) {  // this group's blocks ran on another XCD too: its release does not cover them
+            __hip_atomic_fetch_or(c + (kDoneSub + 8) * kDoneStride + kDoneMask, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (__hip_atomic_fetch_add(c + (kDoneSub + 8) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups)
             return;
-        for (int k = 0; k < kDoneCtrs; ++k)
+        const unsigned split = mask_read(c + (kDoneSub + 8) * kDoneStride + kDoneMask);
+        for (int k = 0; k < kDoneCtrs; ++k) {
             __hip_atomic_store(c + k * kDoneStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(c + k * kDoneStride + kDoneMask, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (split) __hip_atomic_store(d.flag + 1, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }

@@ -126,10 +126,23 @@ void host_prof_report() {
 // Completion word for the kernel about to be launched on `st` as the call's
 // last stream operation (only the library's own stream; cleared again by
 // any copy enqueued after it, see enq_copy).
+// Test hooks (mv2h_set_tuning): "withhold_done" = k makes the next k armed kernels run without
+// their word (the host still waits for it: the missed-word path of wait_done), "fake_split" = k
+// marks the next k words as raised by a kernel whose block groups ran on several XCDs.
+static int g_withhold_done = 0, g_fake_split = 0;
+
 static Done arm_done(hipStream_t st) {
     World &w = world();
     if (w.sync_mode != 0 || !w.done_flag || st != w.stream || w.enqueue) return Done{nullptr, nullptr, 0};
     w.pending = ++w.done_seq;
+    if (g_fake_split > 0) {
+        --g_fake_split;
+        __atomic_store_n(w.done_flag + 1, w.pending, __ATOMIC_RELEASE);
+    }
+    if (g_withhold_done > 0) {
+        --g_withhold_done;
+        return Done{nullptr, nullptr, 0};
+    }
     return Done{w.done_ctr, w.done_flag, w.pending};
 }
 
@@ -139,26 +152,53 @@ static inline hipError_t enq_copy(void *dst, const void *src, size_t bytes, hipS
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
 }
 
+// A completion word whose kernel ran a block group over more than one XCD (device_util.h
+// block_done wrote its seq into done_flag[1] too): that group's L2 write-back did not cover every
+// block, so the call completes with a stream synchronisation (the kernel's end releases every
+// XCD's L2) before the host returns.  Counted (done_xcd_split) and reported once per process.
+static hipError_t settle_split(hipStream_t st) {
+    World &w = world();
+    const uint64_t s = __atomic_load_n(w.done_flag + 1, __ATOMIC_ACQUIRE);
+    if (s <= w.split_seen) return hipSuccess;
+    w.split_seen = s;
+    if (w.done_xcd_split++ == 0)
+        fprintf(stderr, "[mv2amd rank %d] warning: a kernel's workgroups of one group ran on several XCDs; "
+                        "completing such calls with a stream synchronisation (counted in done_xcd_split)\n",
+                log_rank());
+    return hipStreamSynchronize(st);
+}
+
 // Wait for the armed completion word; fall back to the stream when the
 // kernel ended without raising it (should not happen: counters are reset).
 // The word is the normal path: the stream is consulted only once the word is
 // 200 us late, then every 100 us (a hipStreamQuery costs ~3 us of host time,
 // and one in flight when the word lands delays the return by that much).
+// Both fallbacks are counted (done_late: the stream was consulted; done_missed:
+// the kernel had ended without the word) and the first missed word of the
+// process is reported: a missed word would otherwise be invisible in every record.
 static hipError_t wait_done(hipStream_t st, uint64_t want) {
     World &w = world();
     uint64_t next_query = 0;
+    bool late = false;
     for (unsigned spins = 0;; ++spins) {
-        if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return hipSuccess;
+        if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return settle_split(st);
         if ((spins & 255u) == 0) {
             const uint64_t t = now_ns();
             if (!next_query) next_query = t + 200000;
             if (t < next_query) continue;
             next_query = t + 100000;
+            if (!late) {
+                late = true;
+                ++w.done_late;
+            }
             const hipError_t q = hipStreamQuery(st);
             if (q == hipErrorNotReady) continue;
-            if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return hipSuccess;
+            if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return settle_split(st);
             if (q == hipSuccess) {
-                MV2_DEBUG("kernel finished without its completion word; resetting counters");
+                if (w.done_missed++ == 0)
+                    fprintf(stderr, "[mv2amd rank %d] warning: a kernel finished without raising its completion word "
+                                    "(call %llu); completing by stream synchronisation, counters reset (counted in done_missed)\n",
+                            log_rank(), (unsigned long long)want);
                 hipMemsetAsync(w.done_ctr, 0, kDoneBytes, st);
                 return hipStreamSynchronize(st);
             }
@@ -779,9 +819,12 @@ int mv2h_set_tuning(const char *key, long value) {
     World &w = world();
     if (!strcmp(key, "max_grid")) w.max_grid = (int)value;
     else if (!strcmp(key, "rl_grid")) w.rl_grid = (int)value;
+    else if (!strcmp(key, "rl_tiny_max")) w.rl_tiny_max = (size_t)std::max(0L, value);
     else if (!strcmp(key, "pipe_grid")) w.pipe_grid = (int)value;
     else if (!strcmp(key, "pipe_sub")) w.pipe_sub = (size_t)value;
     else if (!strcmp(key, "light_release")) w.light_release = (int)value;
+    else if (!strcmp(key, "withhold_done")) g_withhold_done = (int)value;
+    else if (!strcmp(key, "fake_split")) g_fake_split = (int)value;
     else if (!strcmp(key, "oneshot_max")) {
         if ((size_t)value > w.slot_bytes && w.size > 1) return E_ARG;
         w.oneshot_max = (size_t)value;
@@ -812,6 +855,18 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "code_load_us")) *value = (long)(w.code_load_ms * 1e3 + 0.5);
     else if (!strcmp(key, "selftest_calls")) *value = w.selftest_calls;
     else if (!strcmp(key, "call_allocs")) *value = (long)w.call_allocs;
+    else if (!strcmp(key, "pool_trims")) *value = (long)w.pool_trims;
+    else if (!strcmp(key, "rl_tiny_max")) *value = (long)w.rl_tiny_max;
+    // constants chosen on one shared GPU (not probed at MPI_Init; the N > 1 bench line names them)
+    else if (!strcmp(key, "ar_scalar_max")) *value = env_long_coll("MV2AMD_AR_SCALAR_MAX", 1024);
+    else if (!strcmp(key, "rs_scalar_max")) *value = env_long_coll("MV2AMD_RS_SCALAR_MAX", 4096);
+    else if (!strcmp(key, "p2p_kernel_copy")) {
+        const char *v = getenv("MV2AMD_P2P_KERNEL_COPY");
+        *value = (v && *v) ? *v != '0' : w.nshare <= 4;
+    }
+    else if (!strcmp(key, "done_late")) *value = (long)w.done_late;
+    else if (!strcmp(key, "done_missed")) *value = (long)w.done_missed;
+    else if (!strcmp(key, "done_xcd_split")) *value = (long)w.done_xcd_split;
     else if (!strcmp(key, "p2p_unexpected")) *value = (long)p2p_unexpected_matched();
     else if (!strcmp(key, "hw_queues_set")) *value = w.hw_queues_set;
     else if (!strcmp(key, "uop_in_bytes")) *value = (long)w.uop_in_bytes;
@@ -886,6 +941,16 @@ int mv2h_test_ticket(unsigned long long ticket, int *done) {
         }
         if (q != hipSuccess) return E_INTERN;
     }
+    if (__atomic_load_n(w.done_flag + 1, __ATOMIC_ACQUIRE) > w.split_seen) {
+        // the word came from a kernel whose block groups were split over XCDs: done once the
+        // stream is (settle_split)
+        const hipError_t q = hipStreamQuery(w.stream);
+        if (q == hipErrorNotReady) {
+            if (done) *done = 0;
+            return 0;
+        }
+        if (q != hipSuccess || settle_split(w.stream) != hipSuccess) return E_INTERN;
+    }
     return check_err_word();
 }
 
@@ -939,6 +1004,7 @@ int mv2h_reduce_local(const void *in, void *inout, size_t count, int dtype, int 
     } else {
         LaunchCfg cfg{w.rl_grid, 4, st};
         cfg.done = arm_done(st);
+        cfg.tiny_max = w.rl_tiny_max;
         rc = launch_reduce_local(oi, dt->kind, din_p, dio_p, count, dt->extent, cfg);
     }
     tmark1(st);
@@ -3177,7 +3243,10 @@ int coll_selftest() {
     World &w = world();
     const int n = w.size, me = w.rank;
     const int MPI_INT_H = 0x4c000405, MPI_SUM_H = 0x58000003;
-    const size_t cap = ((size_t)1 << 20) + 64;  // elements per buffer
+    // elements per buffer: the largest checked call (1 Mi + 3 elements, a 1 Mi-element allgather
+    // result) and the graph lane's second capture, which runs 8192 elements into the buffers
+    constexpr size_t kGraphOff = 8192;
+    const size_t cap = kGraphOff + ((size_t)1 << 20) + 64;
     constexpr int kMaxCalls = 96;
     uint32_t *sb = nullptr, *rb = nullptr, *bad = nullptr;
     if (hipMalloc((void **)&sb, cap * 4) != hipSuccess || hipMalloc((void **)&rb, cap * 4) != hipSuccess ||
@@ -3196,11 +3265,22 @@ int coll_selftest() {
         calls = 0;
         auto seed_of = [&](int k) { return (uint32_t)(0x51ed270bu * (uint32_t)(k + 1) + 0x1000193u * (uint32_t)attempt); };
         // one checked call: fill this rank's operand, run the call, check its result on the device
+        // every operand and result stays inside its buffer (the graph lane's second
+        // capture once ran 8 K elements past the end)
+        auto fits = [&](const uint32_t *p, size_t c) {
+            const uint32_t *b = (p >= rb && p < rb + cap) ? rb : sb;
+            if (p < b || (size_t)(p - b) + c > cap || calls > kMaxCalls) {
+                MV2_ERR("self-test: call %d does not fit its buffers (%zu elements at +%td of %zu)", calls, c, p - b, cap);
+                if (!rc) rc = E_INTERN;
+                return false;
+            }
+            return true;
+        };
         auto fill = [&](uint32_t *p, size_t c, int k, int as_rank) {
-            if (!rc) rc = launch_selftest_fill(p, c, seed_of(k), as_rank, st);
+            if (!rc && fits(p, c)) rc = launch_selftest_fill(p, c, seed_of(k), as_rank, st);
         };
         auto check = [&](const uint32_t *p, size_t c, int k, int mode, int arg, uint64_t base, const char *name) {
-            if (!rc) rc = launch_selftest_check(p, c, seed_of(k), n, mode, arg, base, bad + k, st);
+            if (!rc && fits(p, c)) rc = launch_selftest_check(p, c, seed_of(k), n, mode, arg, base, bad + k, st);
             what[k] = name;
         };
         // one-shot allreduce: sizes up to the one-shot limit, each on both arena halves
@@ -3263,6 +3343,11 @@ int coll_selftest() {
             if (!rc) rc = ::reduce_scatter_entry(sb, rb, counts, MPI_INT_H, MPI_SUM_H, nullptr);
             check(rb, c, k, 0, 0, (uint64_t)me * c, "pipelined reduce-scatter");
         }
+        // the pipelined allgather and broadcast below run with the one-shot path off: with a 1 MiB
+        // slot their blocks would otherwise fit the one-shot kernel, and the pipelined kernel's
+        // cross-GPU publish would go unchecked
+        const size_t os_keep = w.oneshot_max;
+        w.oneshot_max = 0;
         for (int i = 0; i < 2 && !rc; ++i) {
             const int k = calls++;
             const size_t c = ((size_t)1 << 20) / (size_t)n - 4 * (size_t)i;
@@ -3270,6 +3355,7 @@ int coll_selftest() {
             if (!rc) rc = allgather_node(sb, rb, c * 4, nullptr);
             check(rb, c * n, k, 2, (int)c, 0, "pipelined allgather");
         }
+        w.oneshot_max = os_keep;
         // one-shot allgather and broadcast (k_oneshot_mv): a 12-byte block (byte by byte) and 16-byte
         // blocks, and a broadcast with a tail
         const size_t os_ag[2] = {3, 4096}, os_bc[2] = {3, 16387};
@@ -3287,6 +3373,7 @@ int coll_selftest() {
             if (!rc) rc = bcast_node(rb, os_bc[i] * 4, root, nullptr);
             check(rb, os_bc[i], k, 1, root, 0, "one-shot broadcast");
         }
+        w.oneshot_max = 0;
         for (int i = 0; i < 2 && !rc; ++i) {
             const int k = calls++;
             const int root = i == 0 ? 0 : n - 1;
@@ -3296,10 +3383,12 @@ int coll_selftest() {
             if (!rc) rc = bcast_node(rb, c * 4, root, nullptr);
             check(rb, c, k, 1, root, 0, "pipelined broadcast");
         }
+        w.oneshot_max = os_keep;
         // graph lane: a captured one-shot and a captured pipelined allreduce, replayed
         if (w.graph_lane && !rc) {
             hipStream_t cs = nullptr;
             const size_t gc[2] = {4096, (((size_t)1 << 20) / (16 * (size_t)n)) * 16 * (size_t)n};
+            for (int g = 0; g < 2; ++g) fits(sb + (size_t)g * kGraphOff, gc[g]), fits(rb + (size_t)g * kGraphOff, gc[g]);
             hipGraph_t graph[2] = {};
             hipGraphExec_t ex[2] = {};
             if (hipStreamCreate(&cs) != hipSuccess) rc = E_INTERN;
@@ -3311,7 +3400,7 @@ int coll_selftest() {
                 int crc;
                 {
                     EnqueueScope q(true);
-                    crc = ::allreduce_entry(sb + (size_t)g * 8192, rb + (size_t)g * 8192, gc[g], MPI_INT_H, MPI_SUM_H, cs);
+                    crc = ::allreduce_entry(sb + (size_t)g * kGraphOff, rb + (size_t)g * kGraphOff, gc[g], MPI_INT_H, MPI_SUM_H, cs);
                 }
                 if (hipStreamEndCapture(cs, &graph[g]) != hipSuccess || crc ||
                     hipGraphInstantiate(&ex[g], graph[g], nullptr, nullptr, 0) != hipSuccess)
@@ -3321,9 +3410,11 @@ int coll_selftest() {
             for (int rep = 0; rep < 3 && !rc; ++rep)
                 for (int g = 0; g < 2 && !rc; ++g) {
                     const int k = calls++;
-                    if ((rc = launch_selftest_fill(sb + (size_t)g * 8192, gc[g], seed_of(k), me, cs))) break;
+                    if (!fits(sb + (size_t)g * kGraphOff, gc[g]) ||
+                        (rc = launch_selftest_fill(sb + (size_t)g * kGraphOff, gc[g], seed_of(k), me, cs)))
+                        break;
                     if (hipGraphLaunch(ex[g], cs) != hipSuccess) rc = E_INTERN;
-                    if (!rc) rc = launch_selftest_check(rb + (size_t)g * 8192, gc[g], seed_of(k), n, 0, 0, 0, bad + k, cs);
+                    if (!rc) rc = launch_selftest_check(rb + (size_t)g * kGraphOff, gc[g], seed_of(k), n, 0, 0, 0, bad + k, cs);
                     what[k] = "graph-lane allreduce";
                 }
             if (cs && hipStreamSynchronize(cs) != hipSuccess) rc = rc ? rc : E_INTERN;
@@ -3345,10 +3436,16 @@ int coll_selftest() {
                 ok = 0;
             }
         if (rc) MV2_ERR("self-test: a call failed (MPI error class %d)", rc);
-        w.shm->r[me].selftest_ok = ok;
+        // 1 = every element right, 0 = wrong elements, -1 = a call or launch failed; the retry below
+        // is decided from these agreed values, never from this rank's own rc (a rank that stopped
+        // while its peers ran the set again would leave them waiting for it)
+        w.shm->r[me].selftest_ok = rc ? -1 : ok;
         host_barrier();
-        int all_ok = 1;
-        for (int j = 0; j < n; ++j) all_ok &= w.shm->r[j].selftest_ok;
+        int all_ok = 1, any_err = 0;
+        for (int j = 0; j < n; ++j) {
+            all_ok &= w.shm->r[j].selftest_ok == 1;
+            any_err |= w.shm->r[j].selftest_ok < 0;
+        }
         host_barrier();  // every rank has read every verdict
         if (all_ok) {
             verdict = 0;
@@ -3356,7 +3453,7 @@ int coll_selftest() {
             break;
         }
         verdict = E_INTERN;
-        if (w.light_release && rc == 0) {
+        if (w.light_release && !any_err) {
             if (me == 0)
                 fprintf(stderr, "[mv2amd] warning: device collective self-test failed with the light release; "
                                 "using the full system-scope release\n");

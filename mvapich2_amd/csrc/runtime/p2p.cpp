@@ -239,17 +239,35 @@ int run_copies(const std::vector<Copy> &cp) {
         const uint64_t want = g_pdone.seq;
         auto t0 = std::chrono::steady_clock::now();
         double next_us = 200.0;
+        // a word raised by a copy kernel whose block groups ran on several XCDs (device_util.h
+        // block_done): done once the stream is, as for the collectives (coll.cpp settle_split)
+        auto settle = [&]() {
+            static uint64_t seen = 0;
+            const uint64_t s = __atomic_load_n(g_pdone.flag + 1, __ATOMIC_ACQUIRE);
+            if (s <= seen) return 0;
+            seen = s;
+            ++w.done_xcd_split;
+            return hipStreamSynchronize(st) == hipSuccess ? 0 : E_INTERN;
+        };
+        bool late = false;
         for (unsigned spins = 0;; ++spins) {
-            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return 0;
+            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return settle();
             if ((spins & 255u) != 0) continue;
             const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
             if (us < next_us) continue;
             next_us = us + 100.0;
+            if (!late) {
+                late = true;
+                ++w.done_late;
+            }
             const hipError_t q = hipStreamQuery(st);
             if (q == hipErrorNotReady) continue;
-            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return 0;
+            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return settle();
             if (q == hipSuccess) {  // finished without raising the word: counters reset, done
-                MV2_DEBUG("point-to-point copy finished without its completion word");
+                if (w.done_missed++ == 0)
+                    fprintf(stderr, "[mv2amd rank %d] warning: a point-to-point copy kernel finished without raising "
+                                    "its completion word; completing by stream synchronisation (counted in done_missed)\n",
+                            log_rank());
                 hipMemsetAsync(g_pdone.ctr, 0, kDoneBytes, st);
                 return hipStreamSynchronize(st) == hipSuccess ? 0 : E_INTERN;
             }

@@ -355,16 +355,34 @@ void *pool_get(size_t bytes) {
     return p;
 }
 
+// Idle blocks kept for reuse are capped (MV2AMD_POOL_IDLE_MAX bytes, default 256 MiB): above it
+// pool_put returns the largest idle blocks to HIP, so one large unexpected message or derived-type
+// staging does not pin its power-of-two block of HBM for the rest of the job.
+static size_t pool_idle_max() {
+    static const size_t m = (size_t)env_long("MV2AMD_POOL_IDLE_MAX", 256L << 20);
+    return m;
+}
+
 void pool_put(void *p) {
     if (!pool_on()) {
         if (p) hipFree(p);
         return;
     }
-    for (PoolBlock &b : g_pool)
-        if (b.p == p) {
-            b.used = false;
-            return;
-        }
+    size_t idle = 0;
+    for (PoolBlock &b : g_pool) {
+        if (b.p == p) b.used = false;
+        if (!b.used) idle += b.cap;
+    }
+    while (idle > pool_idle_max()) {
+        size_t big = g_pool.size();
+        for (size_t i = 0; i < g_pool.size(); ++i)
+            if (!g_pool[i].used && (big == g_pool.size() || g_pool[i].cap > g_pool[big].cap)) big = i;
+        if (big == g_pool.size()) break;
+        idle -= g_pool[big].cap;
+        hipFree(g_pool[big].p);
+        g_pool.erase(g_pool.begin() + (long)big);
+        ++g_world.pool_trims;
+    }
 }
 
 static void pool_release_all() {
@@ -454,6 +472,13 @@ static void apply_hw_queue_limit(int local_size) {
     const bool late = hip_already_running();
     const int q = limit_hw_queues_if_shared(local_size);
     w.hw_queues_set = late && q > 0 ? -q : q;
+    // kernel arguments in device memory (HIP_FORCE_DEV_KERNARG=1): the command processor then reads
+    // them from HBM instead of over PCIe.  Measured on the 8-byte MPI_Reduce_local, whose call is
+    // mostly launch and dispatch: 8.60 -> 8.02 us and 8.11 -> 7.32 us on two boxes (profiles/r06e).
+    // Like GPU_MAX_HW_QUEUES it is read once when HIP starts; a value set by the user wins, and
+    // MV2AMD_DEV_KERNARG=0 leaves HIP's default.
+    if (!late && !getenv("HIP_FORCE_DEV_KERNARG") && env_long("MV2AMD_DEV_KERNARG", 1) != 0)
+        setenv("HIP_FORCE_DEV_KERNARG", "1", 0);
 }
 
 static int setup_device_common() {
@@ -493,6 +518,7 @@ static int setup_device_common() {
     w.pipe_rnt = env_long("MV2AMD_PIPE_RNT", w.pipe_rnt) != 0;  // stores into peers' arenas: non-temporal / plain
     w.light_release = (int)env_long("MV2AMD_LIGHT_RELEASE", w.light_release);
     w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
+    w.rl_tiny_max = (size_t)std::max(0L, env_long("MV2AMD_RL_TINY_MAX", (long)w.rl_tiny_max));
     knobs_reload();  // MV2_* algorithm-selection knobs (orders.cpp)
     hipEventCreate(&w.ev0);
     hipEventCreate(&w.ev1);
@@ -756,15 +782,29 @@ int world_init() {
         // the other nodes' ranks too, which this node's segment cannot see
         const long ns = env_long("MV2AMD_NSHARE", 0);
         if (ns > w.nshare) w.nshare = (int)ns;
-        // above 8 processes on one GPU its hardware scheduler time-slices them instead of running
-        // them all at once: device-side waits between the ranks then take milliseconds per step and
-        // the 12- and 9-process emulations stalled and lost cross-process stores (DESIGN.md "Ranks
-        // per GPU", profiles/r05as, r05at)
-        if (w.nshare > kHwsProcs && w.rank == 0 && env_long("MV2AMD_QUIET_NSHARE", 0) == 0)
+        // Above 8 processes on one GPU (its hardware scheduler's concurrent processes, KFD's VMIDs)
+        // the emulated-node soaks returned wrong bytes: a rank's own send buffer held another rank's
+        // previous operand before the call (profiles/r05ar, r05at; r06b-r06d: 3-21 wrong calls of 400
+        // at 12 = 3 x 4, 35-86 with the copy engines off).  The cause is not found (DESIGN.md "Ranks
+        // per GPU": the same traffic without this library stays exact at 9-16 processes, and the
+        // workgroups' XCD placement held), so such a job is refused here, on every rank, instead of
+        // returning wrong sums later.  MV2AMD_UNSAFE_OVERSUBSCRIBE=1 lets it run for diagnosis only,
+        // with a warning on every rank.
+        if (w.nshare > kHwsProcs && !control_only) {
+            if (env_long("MV2AMD_UNSAFE_OVERSUBSCRIBE", 0) != 1) {
+                MV2_ERR("%d processes share one GPU, more than the %d its hardware scheduler runs at once: "
+                        "device collectives between them are not supported (DESIGN.md \"Ranks per GPU\"); "
+                        "run at most %d ranks per GPU",
+                        w.nshare, kHwsProcs, kHwsProcs);
+                host_barrier();  // every rank of the node has read the segment; remove it
+                shm_unlink(w.shm_name.c_str());
+                return E_UNSUPPORTED;
+            }
             fprintf(stderr,
-                    "[mv2amd rank %d] warning: %d processes share one GPU, more than the %d its hardware "
-                    "scheduler runs at once; device collectives between them are not supported there\n",
+                    "[mv2amd rank %d] warning: %d processes share one GPU (MV2AMD_UNSAFE_OVERSUBSCRIBE=1): "
+                    "results of device collectives may be wrong above %d\n",
                     log_rank(), w.nshare, kHwsProcs);
+        }
 
         if (w.size <= kMaxRanks && !control_only) {
             // signal page + one-shot arena, IPC-exported

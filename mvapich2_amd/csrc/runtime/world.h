@@ -174,6 +174,13 @@ struct World {
     // device allocations made inside MPI calls (scratch growth: hipMalloc, each paired with a
     // hipFree that synchronises the device); stays flat once the scratch caches are warm
     uint64_t call_allocs = 0;
+    uint64_t pool_trims = 0;  // idle pool blocks returned to HIP above MV2AMD_POOL_IDLE_MAX (world.cpp pool_put)
+    // completion-word events (coll.cpp wait_done), reported by mv2h_get_info and both bench lines:
+    // the word was still unseen 200 us after the launch, so the stream was consulted; the kernel had
+    // ended without raising it; the kernel raised it marked "groups split over XCDs" (device_util.h
+    // block_done), so the host completed the call with a stream synchronisation
+    uint64_t done_late = 0, done_missed = 0, done_xcd_split = 0;
+    uint64_t split_seen = 0;  // last done_flag[1] (split call's seq) already settled
     size_t uop_in_bytes = 0, uop_area_bytes = 0;  // last host-evaluated reduction: operand bytes received, area
     // host-evaluated reductions, cumulative ns per phase (mpi/user_coll.cpp UopPhase): staging the
     // operands (device pack + exchange), fetching them to the host (D2H + unpack), evaluating (uop
@@ -182,6 +189,7 @@ struct World {
     uint64_t api_calls = 0;  // library calls entered (the beacon's call number)
     int hw_queues_set = 0;   // GPU_MAX_HW_QUEUES this library set before HIP started (ranks sharing a GPU)
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
+    size_t rl_tiny_max = 1024;  // reduce_local operands up to this many bytes: one-wave kernel (MV2AMD_RL_TINY_MAX)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
     uint64_t *done_flag = nullptr;  // pinned host: last completed call's sequence number

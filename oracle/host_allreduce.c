@@ -35,25 +35,28 @@
  * barrier; t0; allreduce; t1 — average over ranks of the per-rank mean.
  *
  * Placement (a label of "8 ranks pinned 1/core" must be
- * checkable).  Before forking, the parent reads the inherited affinity mask
- * (the job's cpuset), orders its CPUs by how busy each was over a 200 ms sample
- * of /proc/stat when the mask holds more CPUs than ranks (the GPU boxes hand a
- * job the whole machine's 256 CPUs under a 16-CPU CFS quota, shared with other
- * tenants: a rank pinned next to someone else's thread spins in sched_yield;
- * -S keeps the mask order), then one hardware thread per physical core first
- * (sysfs core / package ids; SMT siblings only after every core has one
- * rank), and assigns rank r the (p + r)-th CPU of that order.  More ranks than
+ * checkable; VERDICT r05 #4: as the reference binds).  Before forking, the parent
+ * reads the inherited affinity mask (the job's cpuset) and, by default, places
+ * the ranks on consecutive physical cores of ONE L3 domain -- MVAPICH2's default
+ * "hybrid-bunch" binding -- choosing the idlest domain that holds enough cores
+ * (a 200 ms sample of /proc/stat when the mask holds more CPUs than ranks: the
+ * GPU boxes hand a job the whole machine's 256 CPUs under a 16-CPU CFS quota,
+ * shared with other tenants; see plan_placement; -Y the idlest CPUs anywhere,
+ * -S the mask order), one hardware thread per physical core first (sysfs core /
+ * package ids; SMT siblings only after every core has one rank), and assigns
+ * rank r the (p + r)-th CPU of that order.  More ranks than
  * CPUs in the mask is *oversubscription*: ranks then share a CPU and the spin
  * waits degrade into sched_yield hand-offs (the latency-bound sizes collapse),
  * so the program says so instead of wrapping silently.  One header row
- * (prefix "JSONHDR ") carries the mask size, each rank's CPU, the distinct CPU
- * and physical-core counts, the oversubscription flag and the cgroup's CPU
+ * (prefix "JSONHDR ") carries the mask size, each rank's CPU and L3 domain, the
+ * number of L3 domains used, the distinct CPU and physical-core counts, the oversubscription flag and the cgroup's CPU
  * quota; each size row carries the spin loops that fell back to sched_yield
  * (summed over ranks) and the cgroup's CFS throttling during that size.
  *
  * Usage: host_allreduce [-n ranks] [-m min:max] [-i iters_small] [-I iters_large]
  *                       [-c (validate)] [-T seconds per size cap] [-p first cpu index]
- *                       [-S (sequential placement: no idleness sample)] [-B seconds of STREAM triad]
+ *                       [-S (sequential placement: no idleness sample)] [-Y (idlest CPUs anywhere)]
+ *                       [-B seconds of STREAM triad]
  * Prints an OSU-style table, one "JSONHDR " line, with -B one "JSONSTREAM " line (the DRAM
  * bound: STREAM triad on every rank's CPU at once) and one "JSON " line per size.
  */
@@ -350,13 +353,29 @@ static long read_long_file(const char *path, long dflt) {
 }
 
 /* physical core key of a CPU: package id * 65536 + core id (sysfs; -1 when absent) */
+/* sysfs CPU tree (HOST_AR_SYSFS overrides it: tests describe a topology of their own) */
+static const char *sysfs_cpu(void) {
+    const char *r = getenv("HOST_AR_SYSFS");
+    return r && *r ? r : "/sys/devices/system/cpu";
+}
+
 static long core_key(int cpu) {
-    char p[128];
-    snprintf(p, sizeof p, "/sys/devices/system/cpu/cpu%d/topology/core_id", cpu);
+    char p[256];
+    snprintf(p, sizeof p, "%s/cpu%d/topology/core_id", sysfs_cpu(), cpu);
     long core = read_long_file(p, -1);
-    snprintf(p, sizeof p, "/sys/devices/system/cpu/cpu%d/topology/physical_package_id", cpu);
+    snprintf(p, sizeof p, "%s/cpu%d/topology/physical_package_id", sysfs_cpu(), cpu);
     long pkg = read_long_file(p, 0);
     return core < 0 ? -1 - cpu : pkg * 65536 + core;
+}
+
+/* the CPU's last-level (L3) cache domain: package * 65536 + cache/index3/id (-1 unknown) */
+static long l3_key(int cpu) {
+    char p[256];
+    snprintf(p, sizeof p, "%s/cpu%d/cache/index3/id", sysfs_cpu(), cpu);
+    long id = read_long_file(p, -1);
+    snprintf(p, sizeof p, "%s/cpu%d/topology/physical_package_id", sysfs_cpu(), cpu);
+    long pkg = read_long_file(p, 0);
+    return id < 0 ? -1 : pkg * 65536 + id;
 }
 
 /* the cgroup's CPU quota in CPUs (cgroup v2 cpu.max, else v1 cfs_quota/period); -1 = none */
@@ -456,26 +475,36 @@ static void cpu_jiffies(unsigned long long *busy, unsigned long long *total) {
 static double BUSY[CPU_SETSIZE]; /* busy fraction of each CPU over the sampling window, -1 unknown */
 
 /* Plan every rank's CPU from the inherited mask (see the header) and print the
- * JSONHDR row.  idlest = 1: when the mask holds more CPUs than ranks (a shared
- * host whose job cpuset is the whole machine, as on the GPU boxes), the CPUs are
- * ordered by how busy they were over a 200 ms sample of /proc/stat first -- other
- * tenants' threads on a rank's CPU turn its spin waits into sched_yield
- * hand-offs -- then one thread per physical core as above.  Returns the number
- * of distinct CPUs used. */
-static int plan_placement(int first, int idlest) {
+ * JSONHDR row.  Policies:
+ *   PLACE_L3 (default): MVAPICH2's default binding, "hybrid-bunch" (hwloc_bind.c:3541-3543):
+ *     the ranks on consecutive physical cores of ONE last-level-cache (L3) domain.  The domain is
+ *     the idlest one (mean busy fraction of its cores over a 200 ms sample of /proc/stat) among
+ *     those with at least N physical cores in the mask; ranks take its cores in CPU order, one
+ *     hardware thread per core.  When no domain holds N cores the domains are filled in the same
+ *     order (idlest first), and the row says how many were used.
+ *   PLACE_IDLEST (-Y): round 5's policy, the N idlest CPUs wherever they are (they crossed L3
+ *     domains on the GPU boxes: 0.71-1.21 us 8-byte latency against 0.29 us on one domain).
+ *   PLACE_SEQ (-S): mask order, no sample.
+ * Physical cores before SMT siblings in every policy.  Returns the number of distinct CPUs used. */
+enum { PLACE_SEQ = 0, PLACE_IDLEST = 1, PLACE_L3 = 2 };
+static const char *PLACE_NAME[] = {"sequential", "idlest", "l3-bunch"};
+
+static int plan_placement(int first, int policy) {
     cpu_set_t s;
     int cpus[CPU_SETSIZE], ncpu = 0;
     if (sched_getaffinity(0, sizeof(s), &s) == 0)
         for (int c = 0; c < CPU_SETSIZE; c++)
             if (CPU_ISSET(c, &s)) cpus[ncpu++] = c;
     for (int c = 0; c < CPU_SETSIZE; c++) BUSY[c] = -1;
-    if (idlest && ncpu > N) {
+    if (policy != PLACE_SEQ && ncpu > N) {
         static unsigned long long b0[CPU_SETSIZE], t0[CPU_SETSIZE], b1[CPU_SETSIZE], t1[CPU_SETSIZE];
         cpu_jiffies(b0, t0);
         usleep(200000);
         cpu_jiffies(b1, t1);
         for (int c = 0; c < CPU_SETSIZE; c++)
             if (t1[c] > t0[c]) BUSY[c] = (double)(b1[c] - b0[c]) / (double)(t1[c] - t0[c]);
+    }
+    if (policy == PLACE_IDLEST && ncpu > N) {
         /* stable insertion sort by busy fraction (unknown counts as busy) */
         for (int i = 1; i < ncpu; i++) {
             int x = cpus[i], j = i - 1;
@@ -486,18 +515,68 @@ static int plan_placement(int first, int idlest) {
             }
             cpus[j + 1] = x;
         }
-    } else {
-        idlest = 0;
     }
-    /* one thread per physical core first: round t takes the t-th thread of every core */
+    static long L3OF[CPU_SETSIZE];
+    for (int i = 0; i < ncpu; i++) L3OF[cpus[i]] = l3_key(cpus[i]);
+    int dom_cores = 0;
+    if (policy == PLACE_L3) {
+        /* domains, their physical cores and mean busy fraction; then a stable order of the CPUs:
+         * eligible domains (>= N cores) before the others, idlest first (ties: lower CPU numbers) */
+        long dk[CPU_SETSIZE];
+        int nd = 0, cores[CPU_SETSIZE] = {0};
+        double bsum[CPU_SETSIZE] = {0};
+        long ck[CPU_SETSIZE];
+        int nck = 0;
+        for (int i = 0; i < ncpu; i++) {
+            const long k = L3OF[cpus[i]], core = core_key(cpus[i]);
+            int d = 0;
+            while (d < nd && dk[d] != k) d++;
+            if (d == nd) dk[nd++] = k;
+            int dup = 0;
+            for (int j = 0; j < nck && !dup; j++) dup = ck[j] == core;
+            if (dup) continue;
+            ck[nck++] = core;
+            cores[d]++;
+            bsum[d] += BUSY[cpus[i]] < 0 ? 0.0 : BUSY[cpus[i]];
+        }
+        int rank_of[CPU_SETSIZE];
+        for (int d = 0; d < nd; d++) rank_of[d] = d;
+        for (int i = 1; i < nd; i++) { /* insertion sort of the domains */
+            int x = rank_of[i], j = i - 1;
+            const int ex = cores[x] >= N;
+            const double bx = cores[x] ? bsum[x] / cores[x] : 2;
+            while (j >= 0) {
+                const int y = rank_of[j], ey = cores[y] >= N;
+                const double by = cores[y] ? bsum[y] / cores[y] : 2;
+                if (ey > ex || (ey == ex && by <= bx + 0.05)) break;
+                rank_of[j + 1] = y;
+                j--;
+            }
+            rank_of[j + 1] = x;
+        }
+        int out[CPU_SETSIZE], no = 0;
+        for (int q = 0; q < nd; q++)
+            for (int i = 0; i < ncpu; i++)
+                if (L3OF[cpus[i]] == dk[rank_of[q]]) out[no++] = cpus[i];
+        memcpy(cpus, out, sizeof(int) * (size_t)ncpu);
+        dom_cores = nd ? cores[rank_of[0]] : 0;
+    }
+    /* one thread per physical core first: round t takes the t-th thread of every core (within a
+     * domain for PLACE_L3: a domain's SMT siblings come after its own cores, before the next domain) */
     int order[CPU_SETSIZE], no = 0, used[CPU_SETSIZE] = {0};
     long keys[CPU_SETSIZE];
     for (int i = 0; i < ncpu; i++) keys[i] = core_key(cpus[i]);
     while (no < ncpu) {
         long seen[CPU_SETSIZE];
         int ns = 0;
+        long dom = 0;
+        int have_dom = 0;
         for (int i = 0; i < ncpu; i++) {
             if (used[i]) continue;
+            if (policy == PLACE_L3) { /* this round stays in the first domain with CPUs left */
+                if (!have_dom) { dom = L3OF[cpus[i]]; have_dom = 1; }
+                if (L3OF[cpus[i]] != dom) continue;
+            }
             int dup = 0;
             for (int j = 0; j < ns && !dup; j++) dup = seen[j] == keys[i];
             if (dup) continue;
@@ -506,8 +585,8 @@ static int plan_placement(int first, int idlest) {
             order[no++] = cpus[i];
         }
     }
-    int distinct = 0, dcores = 0;
-    long ckeys[MAXR];
+    int distinct = 0, dcores = 0, ndom = 0;
+    long ckeys[MAXR], dkeys[MAXR];
     for (int r = 0; r < N; r++) {
         RANK_CPU[r] = ncpu ? order[(first + r) % ncpu] : -1;
         int dup = 0;
@@ -518,19 +597,27 @@ static int plan_placement(int first, int idlest) {
         for (int j = 0; j < r && !dup; j++) dup = ckeys[j] == k;
         ckeys[r] = k;
         dcores += !dup;
+        const long l3 = RANK_CPU[r] >= 0 ? l3_key(RANK_CPU[r]) : -1;
+        dup = 0;
+        for (int j = 0; j < ndom && !dup; j++) dup = dkeys[j] == l3;
+        if (!dup) dkeys[ndom++] = l3;
     }
     const double quota = cgroup_quota_cpus();
     printf("JSONHDR {\"ranks\": %d, \"cpus_available\": %d, \"cpus_used\": %d, \"cores_used\": %d, "
            "\"oversubscribed\": %s, \"smt_shared\": %s, \"first_cpu_index\": %d, \"rank_cpus\": [",
            N, ncpu, distinct, dcores, distinct < N ? "true" : "false", dcores < distinct ? "true" : "false", first);
     for (int r = 0; r < N; r++) printf("%s%d", r ? ", " : "", RANK_CPU[r]);
-    printf("], \"rank_cpu_busy_pct\": [");
+    printf("], \"rank_l3\": [");
+    for (int r = 0; r < N; r++) printf("%s%ld", r ? ", " : "", RANK_CPU[r] >= 0 ? l3_key(RANK_CPU[r]) : -1L);
+    printf("], \"l3_domains_used\": %d, ", ndom);
+    if (policy == PLACE_L3) printf("\"l3_domain_cores\": %d, ", dom_cores);
+    printf("\"rank_cpu_busy_pct\": [");
     for (int r = 0; r < N; r++) {
         const double b = RANK_CPU[r] >= 0 ? BUSY[RANK_CPU[r]] : -1;
         if (b < 0) printf("%snull", r ? ", " : "");
         else printf("%s%.1f", r ? ", " : "", 100.0 * b);
     }
-    printf("], \"placement_policy\": \"%s\", \"cgroup_cpu_quota\": ", idlest ? "idlest" : "sequential");
+    printf("], \"placement_policy\": \"%s\", \"cgroup_cpu_quota\": ", PLACE_NAME[policy]);
     if (quota > 0) printf("%.3f", quota);
     else printf("null");
     printf("}\n");
@@ -554,12 +641,12 @@ int main(int argc, char **argv) {
     size_t mn = 4, mx = 64u << 20;
     int it_small = 1000, it_large = 100, validate = 0;
     double tcap = 3.0;
-    int first_core = 0, idlest = 1;
+    int first_core = 0, policy = PLACE_L3;
     double stream_s = 0;
     int c;
     const char *topo = getenv("MV2_USE_TOPO_AWARE_ALLREDUCE");
     if (topo) TOPO = atoi(topo) != 0;
-    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:SB:")) != -1) {
+    while ((c = getopt(argc, argv, "n:m:i:I:cT:p:SYB:")) != -1) {
         switch (c) {
         case 'n': N = atoi(optarg); break;
         case 'm': sscanf(optarg, "%zu:%zu", &mn, &mx); break;
@@ -568,7 +655,8 @@ int main(int argc, char **argv) {
         case 'c': validate = 1; break;
         case 'T': tcap = atof(optarg); break;
         case 'p': first_core = atoi(optarg); break;
-        case 'S': idlest = 0; break; /* sequential placement: mask order, no idleness sample */
+        case 'S': policy = PLACE_SEQ; break;    /* sequential placement: mask order, no idleness sample */
+        case 'Y': policy = PLACE_IDLEST; break; /* the idlest CPUs wherever they are (round 5) */
         case 'B': stream_s = atof(optarg); break; /* STREAM triad first, for this many seconds */
         default: fprintf(stderr, "usage: %s [-n ranks] [-m min:max] [-i it] [-I it] [-c] [-T s] [-p core0] [-S]\n", argv[0]); return 2;
         }
@@ -580,7 +668,7 @@ int main(int argc, char **argv) {
     SHM_DATA = mmap(NULL, RSTRIDE * N, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (C == MAP_FAILED || SHM_DATA == MAP_FAILED) { perror("mmap"); return 1; }
     memset(C, 0, sizeof(ctrl_t));
-    plan_placement(first_core, idlest);
+    plan_placement(first_core, policy);
     pid_t pids[MAXR];
     for (int r = 0; r < N; r++) {
         pid_t p = fork();

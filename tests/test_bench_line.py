@@ -55,6 +55,30 @@ def test_one_rank_per_gpu_roofline(n):
     json.dumps(line)  # the line must serialise
 
 
+CHECKS = {"timed_calls_verified": 20, "timed_calls": 20,
+          "completion_word_sum_over_ranks": {"done_late": 3, "done_missed": 0, "done_xcd_split": 0},
+          "release_protocol": "light",
+          "shared_gpu_constants": {"MV2AMD_AR_SCALAR_MAX": 1024, "MV2AMD_RS_SCALAR_MAX": 4096, "p2p_copy_kernels": True}}
+
+
+@pytest.mark.parametrize("nshare", [1, 2])
+def test_line_carries_the_checks(nshare):
+    """every timed 256 MiB call verified (count in the line), the completion-word
+    events summed over ranks, the release protocol MPI_Init adopted, and the constants tuned on a
+    shared GPU named -- flagged as unmeasured over xGMI when each rank has a GPU to itself."""
+    line = bench.assemble_nranks_line(8, nshare, 20, 5, _t(), 9e-6, [], 1 << 24, 128 << 20, TILING, (None, None, "n"),
+                                      None, checks=dict(CHECKS))
+    cfg = line["config"]
+    assert cfg["timed_calls_verified"] == 20 and cfg["timed_calls"] == 20
+    assert cfg["pipe_tiling"]["release_protocol"] == "light" and cfg["pipe_tiling"]["grid"] == 256
+    assert line["extra"]["completion_word"] == {"done_late": 3, "done_missed": 0, "done_xcd_split": 0}
+    sg = line["extra"]["constants_tuned_on_shared_gpu"]
+    assert sg["MV2AMD_AR_SCALAR_MAX"] == 1024 and sg["p2p_copy_kernels"] is True
+    assert ("unmeasured over xGMI" in sg["note"]) == (nshare == 1)
+    assert "every timed call" in cfg["validation"]
+    json.dumps(line)
+
+
 def test_shared_gpu_line_has_no_fraction():
     line = bench.assemble_nranks_line(2, 2, 20, 5, _t(), 9e-6, [dict(u) for u in UOPS], 1 << 24, 128 << 20, TILING,
                                       (123, "profiles/x.json", None),
@@ -143,6 +167,75 @@ def test_host_allreduce_distinct_cpus_when_they_fit():
     assert hdr["cpus_used"] == n and hdr["oversubscribed"] is False
     assert set(hdr["rank_cpus"]) <= set(avail) and len(set(hdr["rank_cpus"])) == n
     assert all(r["ok"] for r in rows)
+
+
+def _fake_sysfs(root, l3_of, core_of=None):
+    """A sysfs CPU tree describing CPU c as core core_of[c] (default c) in L3 domain l3_of[c]."""
+    for c, l3 in enumerate(l3_of):
+        d = root / f"cpu{c}"
+        (d / "topology").mkdir(parents=True)
+        (d / "cache" / "index3").mkdir(parents=True)
+        (d / "topology" / "core_id").write_text(str(core_of[c] if core_of else c))
+        (d / "topology" / "physical_package_id").write_text("0")
+        (d / "cache" / "index3" / "id").write_text(str(l3))
+    return str(root)
+
+
+def _run_host_env(args, env):
+    out = subprocess.run([HOST_AR] + args, capture_output=True, text=True, timeout=120, env=dict(os.environ, **env))
+    assert out.returncode == 0, out.stderr
+    return next(json.loads(l[8:]) for l in out.stdout.splitlines() if l.startswith("JSONHDR "))
+
+
+@needs_host
+@pytest.mark.parametrize("l3_of,n,want_dom,want_cpus", [
+    ([0, 0, 0, 0, 1, 1, 1, 1], 4, 1, [0, 1, 2, 3]),     # both domains hold 4 cores: one of them, consecutive
+    ([0, 0, 0, 1, 1, 1, 1, 1], 4, 1, [3, 4, 5, 6]),     # domain 0 has 3 cores: the 5-core domain
+    ([0, 0, 0, 0, 1, 1, 1, 1], 8, 2, list(range(8))),   # 8 ranks need both domains
+])
+def test_host_allreduce_bunches_ranks_on_one_l3_domain(tmp_path, l3_of, n, want_dom, want_cpus):
+    """configs[0]'s ranks on consecutive physical cores of one L3 domain
+    (MVAPICH2's default hybrid-bunch binding, hwloc_bind.c:3541-3543) whenever the mask allows
+    it; the row names each rank's L3 domain and how many domains were used."""
+    if sorted(os.sched_getaffinity(0))[:8] != list(range(8)):
+        pytest.skip("needs CPUs 0-7 in this process's mask")
+    hdr = _run_host_env(["-n", str(n), "-m", "8:64", "-i", "5", "-T", "0.1"],
+                        {"HOST_AR_SYSFS": _fake_sysfs(tmp_path, l3_of)})
+    assert hdr["placement_policy"] == "l3-bunch" and hdr["l3_domains_used"] == want_dom
+    assert len(set(hdr["rank_l3"])) == want_dom
+    if l3_of.count(0) == 4 and n == 4:  # two eligible domains: the idler one (this host's load decides)
+        assert hdr["rank_cpus"] in ([0, 1, 2, 3], [4, 5, 6, 7])
+    else:
+        assert hdr["rank_cpus"] == want_cpus
+
+
+@needs_host
+def test_host_allreduce_l3_bunch_puts_smt_siblings_last(tmp_path):
+    """4 cores x 2 threads in one domain (CPU c and c + 4 are siblings): 4 ranks take 4 cores."""
+    if sorted(os.sched_getaffinity(0))[:8] != list(range(8)):
+        pytest.skip("needs CPUs 0-7 in this process's mask")
+    hdr = _run_host_env(["-n", "4", "-m", "8:64", "-i", "5", "-T", "0.1"],
+                        {"HOST_AR_SYSFS": _fake_sysfs(tmp_path, [0] * 8, [0, 1, 2, 3, 0, 1, 2, 3])})
+    assert hdr["cores_used"] == 4 and hdr["smt_shared"] is False and hdr["l3_domains_used"] == 1
+
+
+@needs_host
+def test_host_allreduce_real_topology_uses_one_domain_when_it_fits():
+    """On this machine's own sysfs: when one L3 domain of the mask holds >= 8 physical cores,
+    8 ranks use exactly one domain."""
+    mask = sorted(os.sched_getaffinity(0))
+    cores = {}
+    for c in mask:
+        try:
+            l3 = open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/id").read().strip()
+            core = open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id").read().strip()
+        except OSError:
+            pytest.skip("no L3 ids in sysfs")
+        cores.setdefault(l3, set()).add(core)
+    hdr = _run_host_env(["-n", "8", "-m", "8:64", "-i", "5", "-T", "0.1"], {})
+    if max(len(v) for v in cores.values()) >= 8:
+        assert hdr["l3_domains_used"] == 1
+    assert len(hdr["rank_l3"]) == 8
 
 
 def test_osu_sweep_library_exports_its_entry():

@@ -34,9 +34,10 @@ def inputs(case, rank):
 GEOMS = {"default": {}, "small": {"MV2AMD_PIPE_GRID": "3", "MV2AMD_PIPE_SUB": "4096"}}
 
 
-def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None):
+def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None, expect_fail=False):
     """n ranks of tests/mp_gpu_worker.py; ppn < n emulates n / ppn nodes (node-major ranks,
-    leaders linked over 127.0.0.1, runtime/internode.cpp)"""
+    leaders linked over 127.0.0.1, runtime/internode.cpp).  expect_fail: return every rank's
+    (exit code, log) instead of asserting success"""
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"cases": cases}))
     out = tmp_path / "out"
@@ -71,6 +72,8 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None):
         for p in procs:
             if p.poll() is None:
                 p.kill()
+    if expect_fail:
+        return [(p.returncode, logs[r]) for r, p in enumerate(procs)]
     bad = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not bad, "ranks " + ", ".join(f"{r} (rc {procs[r].returncode})" for r in bad) + " failed:\n" + \
         "\n".join(f"--- rank {r}:\n{logs[r][-2000:]}" for r in range(n))
@@ -601,6 +604,26 @@ def test_random_sequence_of_collectives(n, seed0, tmp_path):
                 assert np.array_equal(res(cid, r), want), (cid, r)
 
 
+def assert_refused_oversubscribed(out, n, tmp_path):
+    """Every rank failed MPI_Init with the library's explicit refusal, and no result was written."""
+    for r, (rc, log) in enumerate(out):
+        assert rc != 0, f"rank {r} ran {n} processes on one GPU without an error:\n{log[-1500:]}"
+        assert "processes share one GPU, more than the 8" in log, f"rank {r}: no refusal message:\n{log[-1500:]}"
+        assert "MPI_Init" in log, log[-1500:]
+    assert not list((tmp_path / "out").glob("*.npy")), "a rank wrote results"
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,ppn", [(9, 9), (12, 12), (10, 5)])
+def test_more_than_8_processes_per_gpu_are_refused(n, ppn, tmp_path):
+    """9 or 12 ranks of one node on the one GPU (nshare from the devices' PCI ids) and 10 = 2 x 5
+    emulated nodes: MPI_Init refuses on every rank (MPI_ERR_UNSUPPORTED_OPERATION) instead of running
+    collectives the GPU cannot keep exact (DESIGN.md "Ranks per GPU")."""
+    case = {"id": "ar", "kind": "allreduce", "type": "MPI_INT", "op": "MPI_SUM", "count": 1000, "seed": 1}
+    out = run_workers(n, [case], tmp_path, ppn=ppn, timeout=240, expect_fail=True)
+    assert_refused_oversubscribed(out, n, tmp_path)
+
+
 # (op, type) pairs whose result does not depend on the reduction order (wrapping integer arithmetic,
 # bitwise and logical ops, integer MAX / MAXLOC): any algorithm's bits equal the one-node oracle's
 ORDER_FREE = [("MPI_SUM", "MPI_INT"), ("MPI_PROD", "MPI_INT"), ("MPI_BXOR", "MPI_UNSIGNED_CHAR"),
@@ -608,13 +631,14 @@ ORDER_FREE = [("MPI_SUM", "MPI_INT"), ("MPI_PROD", "MPI_INT"), ("MPI_BXOR", "MPI
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("n,ppn,seed0,prog_max", [(6, 3, 8000, 8), (8, 4, 9000, 4)])
+@pytest.mark.parametrize("n,ppn,seed0,prog_max", [(6, 3, 8000, 8), (8, 4, 9000, 4), (12, 4, 9000, 8)])
 def test_random_sequence_across_nodes(n, ppn, seed0, prog_max, tmp_path):
     """The random sequence on emulated nodes (node-major ranks, leaders over TCP; with prog_max 4 the
     8 ranks take the message schedules over the point-to-point channels that jobs above 8 ranks
     take), with order-free (op, type) pairs so that every multi-node algorithm must reproduce the
-    one-node oracle's bits exactly.  At most 8 processes share the GPU: above that its hardware
-    scheduler time-slices them (DESIGN.md "Ranks per GPU")."""
+    one-node oracle's bits exactly.  Above 8 processes on the one GPU (12 = 3 x 4) MPI_Init must
+    refuse the job on every rank with an explicit error, never return wrong bytes (DESIGN.md
+    "Ranks per GPU": such jobs returned wrong sums in r05aa / r05ar / r06b)."""
     rng = np.random.default_rng(seed0)
     kinds = ["allreduce", "iallreduce", "reduce", "ireduce", "reduce_scatter", "allgather", "bcast"]
     cases = []
@@ -630,6 +654,11 @@ def test_random_sequence_across_nodes(n, ppn, seed0, prog_max, tmp_path):
             counts = [count // n + int(rng.integers(0, 3)) for _ in range(n)]
             case.update(recvcounts=counts, count=sum(counts))
         cases.append(case)
+    if n > 8:
+        out = run_workers(n, cases, tmp_path, ppn=ppn, timeout=300, extra_env={"MV2AMD_MN_PROG_MAX": str(prog_max)},
+                          expect_fail=True)
+        assert_refused_oversubscribed(out, n, tmp_path)
+        return
     res = run_workers(n, cases, tmp_path, ppn=ppn, timeout=300, extra_env={"MV2AMD_MN_PROG_MAX": str(prog_max)})
     for case in cases:
         k, cid, t = case["kind"], case["id"], case["type"]

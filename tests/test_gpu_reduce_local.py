@@ -195,3 +195,34 @@ def test_result_visible_to_a_copy_engine_at_return():
         bad = np.flatnonzero(got != rnd * 1000 + 1)
         assert bad.size == 0, (rnd, bad.size, bad[:4], got[bad[:4]])
     hip.hipStreamDestroy(st)
+
+
+def test_completion_word_fallbacks_are_counted():
+    """A missed completion word is visible: a Reduce_local launched with its word
+    withheld completes through the stream fallback with the right bytes and counts done_late and
+    done_missed; a word marked as raised by a kernel whose block groups ran on several XCDs
+    completes by stream synchronisation and counts done_xcd_split (runtime/coll.cpp wait_done,
+    settle_split; device_util.h block_done)."""
+    L = m.lib()
+    n = (1 << 20) + 5
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal(n).astype(np.float32)
+    y = rng.standard_normal(n).astype(np.float32)
+    want = y.copy()
+    assert oracle.reduce_local(x, want, n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]) == 0
+    before = {k: m.info(k) for k in ("done_late", "done_missed", "done_xcd_split")}
+    m.check(L.mv2h_set_tuning(b"withhold_done", 1), "withhold_done")
+    got = run_rl("MPI_FLOAT", "MPI_SUM", x, y, n)
+    assert np.array_equal(got, want.view(np.uint8))
+    assert m.info("done_missed") == before["done_missed"] + 1
+    assert m.info("done_late") >= before["done_late"] + 1
+    m.check(L.mv2h_set_tuning(b"fake_split", 1), "fake_split")
+    got = run_rl("MPI_FLOAT", "MPI_SUM", x, y, n)
+    assert np.array_equal(got, want.view(np.uint8))
+    assert m.info("done_xcd_split") == before["done_xcd_split"] + 1
+    # the word path is back: further calls count nothing
+    for _ in range(20):
+        got = run_rl("MPI_FLOAT", "MPI_SUM", x, y, n)
+        assert np.array_equal(got, want.view(np.uint8))
+    assert m.info("done_missed") == before["done_missed"] + 1
+    assert m.info("done_xcd_split") == before["done_xcd_split"] + 1

@@ -29,5 +29,7 @@ if out:
     for r in range(n):
         open(f"{out}_rank{r}.log", "w").write(logs[r])
 res = [np.load(d / "out" / f"rs_r{r}.npy").tolist() if rcs[r] == 0 else [] for r in range(n)]
-print(json.dumps({"n": n, "ppn": ppn, "rcs": rcs, "env_p2p": os.environ.get("MV2AMD_P2P_KERNEL_COPY"),
+# ranks whose MPI_Init refused the job (more than 8 processes on one GPU, runtime/world.cpp)
+refused = [r for r in range(n) if rcs[r] != 0 and "processes share one GPU, more than the 8" in logs[r]]
+print(json.dumps({"n": n, "ppn": ppn, "rcs": rcs, "refused": refused, "env_p2p": os.environ.get("MV2AMD_P2P_KERNEL_COPY"),
                   "sync_upload": os.environ.get("DIAG_SYNC_UPLOAD"), "per_rank": res}), flush=True)
