@@ -250,14 +250,19 @@ def bench_n1(args, L):
     U32, SUM = TYPES["MPI_UNSIGNED"][0], OPS["MPI_SUM"]
     for _ in range(100):
         L.MPI_Reduce_local(s8.ptr, r8.ptr, 2, U32, SUM)
+    aql0 = m.info("aql_calls")
     t0 = time.perf_counter()
     for _ in range(args.lat_iters):
         m.check(L.MPI_Reduce_local(s8.ptr, r8.ptr, 2, U32, SUM), "MPI_Reduce_local 8 B")
     lat = (time.perf_counter() - t0) / args.lat_iters
+    via_queue = m.info("aql_calls") - aql0
     ok8 = bool(np.all(r8.download(np.uint32, count=2) == 100 + args.lat_iters))
     extra["reduce_local_8B_latency_us"] = {"us": round(lat * 1e6, 2), "correct": ok8,
+                                           "calls_via_hsa_queue": via_queue, "calls": args.lat_iters,
                                            "what": "MPI_Reduce_local SUM on 2 MPI_UNSIGNED (8 B), device buffers, "
-                                                   "blocking call incl. launch and completion word"}
+                                                   "blocking call incl. dispatch and completion word (one-wave "
+                                                   "kernel in the library's own HSA queue, runtime/aql.cpp), "
+                                                   "Python ctypes loop"}
     del s8, r8
     # HBM traffic of this kernel from the newest committed PMC pass (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py); the file is named in the line

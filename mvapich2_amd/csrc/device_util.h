@@ -62,10 +62,11 @@ constexpr int kDoneStride = 1024;  // counter spacing in words (4 KiB: separate 
 constexpr int kDoneSub = 64;       // first-level counters (blockIdx % 64)
 constexpr int kDoneCtrs = kDoneSub + 8 + 1;  // + group counters (blockIdx % 8) + groups done; each with an XCD mask
 constexpr size_t kDoneBytes = (size_t)kDoneCtrs * kDoneStride * sizeof(uint32_t);
+constexpr int kDoneMaxGrid = 1 << 22;  // largest grid whose arrivals block_done's counter fields hold exactly
 // ints in the pinned error word block (wait_mask records a timeout's context there)
 constexpr int kErrWords = 64;
 struct Done {
-    uint32_t *ctr;   // kDoneCtrs counters, kDoneStride words apart; all 0 between launches
+    uint32_t *ctr;   // kDoneCtrs 64-bit counters, kDoneStride words apart; all 0 between launches
     uint64_t *flag;  // pinned host words: [0] last completed seq, [1] last seq whose groups were split over XCDs
     uint64_t seq;
 };
@@ -193,66 +194,64 @@ __device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, ui
 //
 // Blocks b and b + 8 are observed to share an XCD, but HIP promises no
 // workgroup -> XCD placement (MI355X_MICROARCH.md "Contract"), and one group's
-// release writes back only the XCD it runs on.  So every block records the XCD
-// it really ran on (HW_REG_XCC_ID) in its sub-counter's mask, before its count;
-// each sub-counter's last arrival folds that mask into its group's, and a group
-// whose blocks ran on more than one XCD is "split": its release cannot cover
-// them all.  The last group then also writes seq into d.flag[1], and the host
-// completes that call with a stream synchronisation (the kernel's end releases
-// every XCD's L2) instead of trusting the word (runtime/coll.cpp wait_done).
-// The mask OR is issued before the block's store wait, so it costs no extra
-// round trip on the blocks' path; only the 64 + 8 last arrivals read masks.
-constexpr int kDoneMask = 16;            // word offset of a counter's XCD mask (its own 64-byte line)
-constexpr unsigned kDoneSplit = 1u << 16; // in a group mask: one of its sub-counters was split
-// Masks are read by an OR of this otherwise unused bit, not by an atomic load: the compiler lowers
-// a fetch_or(p, 0) to a plain sc1 load, which the local XCD's L2 may serve, while the ORs from
-// other XCDs are read-modify-writes performed where the counters' adds are
-constexpr unsigned kDoneRead = 1u << 31;
-__device__ __forceinline__ unsigned mask_read(uint32_t *p) {
-    return __hip_atomic_fetch_or(p, kDoneRead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kDoneRead;
-}
+// release writes back only the XCD it runs on.  So every arrival carries the XCD
+// it really ran on (HW_REG_XCC_ID) in the same 64-bit atomic add that counts it:
+// the count, the sum of the XCD ids and the sum of their squares.  For m
+// arrivals sum^2 <= m * sumsq, with equality exactly when all m ran on one XCD
+// (Cauchy-Schwarz), so a counter's last arrival knows whether its blocks shared
+// its XCD without one more atomic.  A split sub-counter or group is "split" (it
+// adds to the split field of the level above); the last group then also writes
+// seq into d.flag[1], and the host completes that call with a stream
+// synchronisation (the kernel's end releases every XCD's L2) instead of trusting
+// the word (runtime/coll.cpp wait_done).  Fields of a counter word: count bits
+// 0-16, sum 17-35, sum of squares 36-57, split subs / groups 58-63 (exact for
+// up to 65536 arrivals per sub-counter, i.e. grids up to 4 Mi blocks: the
+// launchers' grids stay below kDoneMaxGrid, runtime/world.cpp clamps rl_grid).
+constexpr int kDoneSumShift = 17, kDoneSqShift = 36, kDoneSplitShift = 58;
+constexpr uint64_t kDoneCntMask = (1ull << kDoneSumShift) - 1;
 
 __device__ __forceinline__ unsigned xcc_id() {
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
     return x;
 }
+// one arrival from XCD x (plus `split` split arrivals of the level below)
+__device__ __forceinline__ uint64_t done_arrival(unsigned x, bool split) {
+    return 1ull + ((uint64_t)x << kDoneSumShift) + ((uint64_t)(x * x) << kDoneSqShift) +
+           (split ? 1ull << kDoneSplitShift : 0ull);
+}
+// the counter's arrivals did not all run on one XCD, or one of them was split
+__device__ __forceinline__ bool done_split(uint64_t v) {
+    const uint64_t m = v & kDoneCntMask, sum = (v >> kDoneSumShift) & ((1ull << (kDoneSqShift - kDoneSumShift)) - 1),
+                   sq = (v >> kDoneSqShift) & ((1ull << (kDoneSplitShift - kDoneSqShift)) - 1);
+    return (v >> kDoneSplitShift) != 0 || sum * sum != m * sq;
+}
 
 __device__ __forceinline__ void block_done(const Done &d) {
     if (!d.flag) return;
-    const bool multi = gridDim.x > 1;
-    uint32_t *c = d.ctr;
-    const unsigned nb = gridDim.x, b = blockIdx.x;
-    const unsigned i = b % kDoneSub, x = b & 7u;
-    unsigned xbit = 0;
-    if (multi && threadIdx.x == 0) {
-        xbit = 1u << xcc_id();
-        // no return value: acknowledged by the store wait below, so performed before this block's count
-        __hip_atomic_fetch_or(c + i * kDoneStride + kDoneMask, xbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!multi) {
+    if (gridDim.x == 1) {
         // one workgroup (small-message one-shot): no counters, no agent fence; the
         // system-scope release of the host word writes back this XCD's L2 itself
         if (threadIdx.x == 0) __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
     if (threadIdx.x == 0) {
+        const unsigned nb = gridDim.x, b = blockIdx.x;
+        const unsigned i = b % kDoneSub, x = b & 7u, me = xcc_id();
         const unsigned members = (nb - i + kDoneSub - 1) / kDoneSub;  // blocks with b % 64 == i
         const unsigned nsub = nb < (unsigned)kDoneSub ? nb : (unsigned)kDoneSub;
         const unsigned subs = (nsub - x + 7u) / 8u;                    // sub-counters i < nsub with i % 8 == x
         const unsigned groups = nb < 8u ? nb : 8u;
-        if (__hip_atomic_fetch_add(c + i * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != members)
-            return;
-        // every member's mask OR was acknowledged before its count: the mask is complete
-        const unsigned sm = mask_read(c + i * kDoneStride + kDoneMask);
-        __hip_atomic_fetch_or(c + (kDoneSub + x) * kDoneStride + kDoneMask, xbit | (sm != xbit ? kDoneSplit : 0u),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (__hip_atomic_fetch_add(c + (kDoneSub + x) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != subs)
-            return;
-        const unsigned gm = mask_read(c + (kDoneSub + x) * kDoneStride + kDoneMask);
+        uint64_t *sub = (uint64_t *)(d.ctr + i * kDoneStride), *grp = (uint64_t *)(d.ctr + (kDoneSub + x) * kDoneStride),
+                 *all = (uint64_t *)(d.ctr + (kDoneSub + 8) * kDoneStride);
+        const uint64_t a = done_arrival(me, false);
+        const uint64_t vs = __hip_atomic_fetch_add(sub, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a;
+        if ((vs & kDoneCntMask) != members) return;
+        const uint64_t ag = done_arrival(me, done_split(vs));
+        const uint64_t vg = __hip_atomic_fetch_add(grp, ag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ag;
+        if ((vg & kDoneCntMask) != subs) return;
         // this XCD's L2 written back before its group counts as done.  The wait is explicit: after a
         // returned atomic the compiler drops the s_waitcnt behind buffer_wbl2 (MI355X_MICROARCH.md,
         // compiler hazard), and the next add then overtook the write-back — the host saw the word
@@ -260,18 +259,12 @@ __device__ __forceinline__ void block_done(const Done &d) {
         // (point-to-point copies of a host-driven schedule) read stale bytes (r04x, 12-rank Iallreduce)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (gm != xbit) {  // this group's blocks ran on another XCD too: its release does not cover them
-            __hip_atomic_fetch_or(c + (kDoneSub + 8) * kDoneStride + kDoneMask, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (__hip_atomic_fetch_add(c + (kDoneSub + 8) * kDoneStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups)
-            return;
-        const unsigned split = mask_read(c + (kDoneSub + 8) * kDoneStride + kDoneMask);
-        for (int k = 0; k < kDoneCtrs; ++k) {
-            __hip_atomic_store(c + k * kDoneStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(c + k * kDoneStride + kDoneMask, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (split) __hip_atomic_store(d.flag + 1, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t aa = done_arrival(0, done_split(vg));
+        const uint64_t va = __hip_atomic_fetch_add(all, aa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + aa;
+        if ((va & kDoneCntMask) != groups) return;
+        for (int k = 0; k < kDoneCtrs; ++k)
+            __hip_atomic_store((uint64_t *)(d.ctr + k * kDoneStride), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (va >> kDoneSplitShift) __hip_atomic_store(d.flag + 1, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }

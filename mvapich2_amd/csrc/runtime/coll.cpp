@@ -818,7 +818,7 @@ double mv2h_last_kernel_ms(void) { return world().last_ms; }
 int mv2h_set_tuning(const char *key, long value) {
     World &w = world();
     if (!strcmp(key, "max_grid")) w.max_grid = (int)value;
-    else if (!strcmp(key, "rl_grid")) w.rl_grid = (int)value;
+    else if (!strcmp(key, "rl_grid")) w.rl_grid = (int)std::min<long>(std::max(1L, value), kDoneMaxGrid);
     else if (!strcmp(key, "rl_tiny_max")) w.rl_tiny_max = (size_t)std::max(0L, value);
     else if (!strcmp(key, "pipe_grid")) w.pipe_grid = (int)value;
     else if (!strcmp(key, "pipe_sub")) w.pipe_sub = (size_t)value;
@@ -857,6 +857,10 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "call_allocs")) *value = (long)w.call_allocs;
     else if (!strcmp(key, "pool_trims")) *value = (long)w.pool_trims;
     else if (!strcmp(key, "rl_tiny_max")) *value = (long)w.rl_tiny_max;
+    else if (!strcmp(key, "aql_calls")) *value = (long)w.aql_calls;
+    else if (!strcmp(key, "aql_kernels")) *value = aql_kernels();
+    else if (!strcmp(key, "aql_skip_lib")) *value = aql_skips(0);
+    else if (!strcmp(key, "aql_skip_null")) *value = aql_skips(1);
     // constants chosen on one shared GPU (not probed at MPI_Init; the N > 1 bench line names them)
     else if (!strcmp(key, "ar_scalar_max")) *value = env_long_coll("MV2AMD_AR_SCALAR_MAX", 1024);
     else if (!strcmp(key, "rs_scalar_max")) *value = env_long_coll("MV2AMD_RS_SCALAR_MAX", 4096);
@@ -977,11 +981,21 @@ int mv2h_reduce_local(const void *in, void *inout, size_t count, int dtype, int 
     if ((rc = kind_supported(dt))) return rc;
     if ((rc = ensure_init_for_device())) return rc;
     World &w = world();
-    hipStream_t st = pick_stream(stream);
     const int oi = op_index(op);
     const size_t bytes = count * (size_t)dt->extent;
     // host buffers: staged through device scratch, reduced on the GPU
     const bool din = is_device(in), dio = is_device(inout);
+    // small device operands on the library's stream: the one-wave kernel dispatched straight into
+    // the library's HSA queue when nothing of HIP's ordering is pending (runtime/aql.cpp)
+    if (din && dio && !stream && oi < OP_REPLACE && bytes <= w.rl_tiny_max && (!w.last_st || w.last_st == w.stream)) {
+        const int r = aql_reduce_local(oi, dt->kind, in, inout, count, dt->extent);
+        if (r < 0) return -r;
+        if (r == 1) {
+            ++w.aql_calls;
+            return check_err_word();
+        }
+    }
+    hipStream_t st = pick_stream(stream);
     const void *din_p = in;
     void *dio_p = inout;
     if (!din) {

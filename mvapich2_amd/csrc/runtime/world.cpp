@@ -517,7 +517,7 @@ static int setup_device_common() {
     w.pipe_sub = (size_t)env_long("MV2AMD_PIPE_SUB", (long)w.pipe_sub);
     w.pipe_rnt = env_long("MV2AMD_PIPE_RNT", w.pipe_rnt) != 0;  // stores into peers' arenas: non-temporal / plain
     w.light_release = (int)env_long("MV2AMD_LIGHT_RELEASE", w.light_release);
-    w.rl_grid = (int)env_long("MV2AMD_RL_GRID", w.rl_grid);
+    w.rl_grid = (int)std::min<long>(env_long("MV2AMD_RL_GRID", w.rl_grid), kDoneMaxGrid);
     w.rl_tiny_max = (size_t)std::max(0L, env_long("MV2AMD_RL_TINY_MAX", (long)w.rl_tiny_max));
     knobs_reload();  // MV2_* algorithm-selection knobs (orders.cpp)
     hipEventCreate(&w.ev0);
@@ -1015,6 +1015,7 @@ int world_finalize() {
     if (!w.inited || w.finalized) return 0;
     if (w.stream) hipStreamSynchronize(w.stream);
     host_prof_report();
+    aql_finalize();
     if (w.nnodes > 1) {
         global_barrier();
         net_finalize();  // the rank mesh on every rank, the leaders' links on the leaders

@@ -190,6 +190,7 @@ struct World {
     int hw_queues_set = 0;   // GPU_MAX_HW_QUEUES this library set before HIP started (ranks sharing a GPU)
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     size_t rl_tiny_max = 1024;  // reduce_local operands up to this many bytes: one-wave kernel (MV2AMD_RL_TINY_MAX)
+    uint64_t aql_calls = 0;     // reduce_local calls dispatched straight into the HSA queue (runtime/aql.cpp)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
     uint64_t *done_flag = nullptr;  // pinned host: last completed call's sequence number
@@ -214,6 +215,12 @@ struct World {
 World &world();
 int world_init();
 int world_finalize();
+// runtime/aql.cpp: small MPI_Reduce_local dispatched straight into an HSA queue (1 done, 0 not
+// taken, < 0 an MPI error class); the kernels it found; its queue torn down at MPI_Finalize
+int aql_reduce_local(int op, int kind, const void *in, void *io, size_t count, size_t esize);
+int aql_kernels();
+long aql_skips(int which);  // 0: library words pending, 1: null stream busy
+void aql_finalize();
 void host_barrier();
 // Host shared-memory windows between the ranks of a node, for host-evaluated reductions that
 // exchange partial results the way the reference's point-to-point algorithms do: this rank's

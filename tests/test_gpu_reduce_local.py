@@ -226,3 +226,65 @@ def test_completion_word_fallbacks_are_counted():
         assert np.array_equal(got, want.view(np.uint8))
     assert m.info("done_missed") == before["done_missed"] + 1
     assert m.info("done_xcd_split") == before["done_xcd_split"] + 1
+
+
+def test_small_reduce_local_takes_the_hsa_queue():
+    """Small device operands go through the library's own HSA queue (runtime/aql.cpp): the kernel
+    objects were found, the calls were dispatched there, and every result is bit-exact with the
+    oracle -- interleaved with large calls (HIP launches on the library's stream) on the same
+    buffers, so that the two paths' ordering is exercised."""
+    L = m.lib()
+    assert m.info("nshare") == 1
+    rng = np.random.default_rng(5)
+    before = m.info("aql_calls")
+    big = (1 << 20) + 3
+    for i, (op, t) in enumerate(PAIRS[::3]):
+        count = [1, 2, 7, 64, 100][i % 5]
+        small = op == "MPI_PROD"
+        x = rand_typed(t, big, rng, small=small)
+        y = rand_typed(t, big, rng, small=small)
+        ext = TYPES[t][3]
+        a, b = m.DeviceBuffer(big * ext), m.DeviceBuffer(big * ext)
+        a.upload(x)
+        b.upload(y)
+        want = y.copy()
+        assert oracle.reduce_local(x, want, big, TYPES[t][0], OPS[op]) == 0  # large call: HIP launch
+        assert L.MPI_Reduce_local(a.ptr, b.ptr, big, TYPES[t][0], OPS[op]) == 0
+        assert oracle.reduce_local(x, want, count, TYPES[t][0], OPS[op]) == 0  # then a small one: the queue
+        assert L.MPI_Reduce_local(a.ptr, b.ptr, count, TYPES[t][0], OPS[op]) == 0
+        assert_bytes_equal(b.download(np.uint8, count=big * ext), as_bytes(want), t, big, f"{op} {t} count {count}")
+    assert m.info("aql_kernels") > 50
+    assert m.info("aql_calls") > before
+
+
+def test_small_reduce_local_orders_after_null_stream_work():
+    """The HSA-queue path keeps the HIP path's ordering: operands written by asynchronous work on
+    the legacy null stream just before the call (hipMemsetD32Async, stream 0, not waited for), and
+    operands rewritten by a host -> device copy after a call of the queue read them (L2 lines of the
+    old values must not be served), are both seen by the reduction (runtime/aql.cpp)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemsetD32Async.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+    L = m.lib()
+    U32, SUM = TYPES["MPI_UNSIGNED"][0], OPS["MPI_SUM"]
+    a, b = m.DeviceBuffer(1 << 20), m.DeviceBuffer(64)
+    b.upload(np.zeros(16, dtype=np.uint32))
+    want = 0
+    for i in range(300):
+        # a large async memset first, so that the null stream is still busy at the call
+        assert hip.hipMemsetD32Async(a.ptr, i + 1, (1 << 20) // 4, None) == 0
+        assert L.MPI_Reduce_local(a.ptr, b.ptr, 2, U32, SUM) == 0
+        want += i + 1
+    assert np.array_equal(b.download(np.uint32, count=2), np.array([want, want], dtype=np.uint32))
+    # rewrite the operand by copies between calls of the queue
+    before = m.info("aql_calls")
+    b.upload(np.zeros(16, dtype=np.uint32))
+    want = 0
+    for i in range(300):
+        a.upload(np.full(4, 1000 + i, dtype=np.uint32))
+        assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, U32, SUM) == 0
+        want += 1000 + i
+        if i % 50 == 0:
+            assert np.array_equal(b.download(np.uint32, count=4), np.full(4, want, dtype=np.uint32)), i
+    assert np.array_equal(b.download(np.uint32, count=4), np.full(4, want, dtype=np.uint32))
+    assert m.info("aql_calls") > before

@@ -15,6 +15,10 @@
 #include <algorithm>
 #include <vector>
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <hsa/hsa_ven_amd_loader.h>
+
 #include "mpi.h"
 
 static double now_us() {
@@ -53,9 +57,198 @@ __global__ void k_word(unsigned *p, unsigned long long *flag, unsigned long long
     }
 }
 
+// ---- raw AQL dispatch of k_word from this program's own code object (mode "aql") ----
+static hsa_agent_t g_agent;
+static uint64_t g_kobj, g_tiny;
+static hsa_status_t pick_gpu(hsa_agent_t a, void *) {
+    hsa_device_type_t t;
+    hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+    if (t == HSA_DEVICE_TYPE_GPU) {
+        g_agent = a;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t sym(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t s, void *) {
+    hsa_symbol_kind_t k;
+    hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &k);
+    if (k != HSA_SYMBOL_KIND_KERNEL) return HSA_STATUS_SUCCESS;
+    uint32_t len = 0;
+    hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_NAME_LENGTH, &len);
+    char name[512] = {0};
+    if (len < 500) hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_NAME, name);
+    if (strstr(name, "k_wordPj")) hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &g_kobj);
+    if (strstr(name, "k_reduce_local_tinyINS_1RILi2ELi5E"))  // the library's one-wave SUM on MPI_UNSIGNED
+        hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &g_tiny);
+    return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t exe(hsa_executable_t e, void *) {
+    hsa_executable_iterate_agent_symbols(e, g_agent, sym, nullptr);
+    return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t karg_region(hsa_region_t r, void *d) {
+    uint32_t f = 0;
+    hsa_region_get_info(r, HSA_REGION_INFO_GLOBAL_FLAGS, &f);
+    if (f & HSA_REGION_GLOBAL_FLAG_KERNARG) {
+        *(hsa_region_t *)d = r;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+static int aql_mode(int iters) {
+    if (MPI_Init(nullptr, nullptr)) return 2;  // loads the library's code objects (its tiny kernel below)
+    std::vector<double> v(iters);
+    unsigned *p = nullptr;
+    unsigned long long *flag = nullptr;
+    hipStream_t st;
+    if (hipMalloc(&p, 64) || hipMemset(p, 0, 64) || hipHostMalloc((void **)&flag, 64, hipHostMallocDefault) ||
+        hipStreamCreate(&st))
+        return 3;
+    *flag = 0;
+    hipLaunchKernelGGL(k_word, dim3(1), dim3(64), 0, st, p, flag, 1ull, 0);  // loads the code object
+    hipStreamSynchronize(st);
+    // host cost of the ordering checks the library's fast path makes
+    for (int i = 0; i < iters; ++i) {
+        const double t0 = now_us();
+        hipStreamQuery(st);
+        v[i] = now_us() - t0;
+    }
+    report("hipStreamQuery(idle blocking stream)", v);
+    for (int i = 0; i < iters; ++i) {
+        const double t0 = now_us();
+        hipStreamQuery(nullptr);
+        v[i] = now_us() - t0;
+    }
+    report("hipStreamQuery(null stream, idle)", v);
+    hsa_init();
+    hsa_iterate_agents(pick_gpu, nullptr);
+    hsa_ven_amd_loader_1_03_pfn_t ldr{};
+    if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(ldr), &ldr) != HSA_STATUS_SUCCESS) return 4;
+    ldr.hsa_ven_amd_loader_iterate_executables(exe, nullptr);
+    if (!g_kobj) {
+        printf("{\"error\": \"k_word kernel object not found\"}\n");
+        return 5;
+    }
+    hsa_region_t kr{};
+    hsa_agent_iterate_regions(g_agent, karg_region, &kr);
+    char *karg = nullptr;
+    hsa_queue_t *q = nullptr;
+    if (hsa_memory_allocate(kr, 64 * 64, (void **)&karg) || hsa_queue_create(g_agent, 1024, HSA_QUEUE_TYPE_SINGLE, nullptr,
+                                                                              nullptr, UINT32_MAX, UINT32_MAX, &q))
+        return 6;
+    struct Args {
+        unsigned *p;
+        unsigned long long *flag;
+        unsigned long long seq;
+        int light, pad;
+    };
+    unsigned long long seq = 1000;
+    const int scopes[4][2] = {{HSA_FENCE_SCOPE_SYSTEM, HSA_FENCE_SCOPE_SYSTEM},
+                              {HSA_FENCE_SCOPE_AGENT, HSA_FENCE_SCOPE_AGENT},
+                              {HSA_FENCE_SCOPE_AGENT, HSA_FENCE_SCOPE_NONE},
+                              {HSA_FENCE_SCOPE_SYSTEM, HSA_FENCE_SCOPE_NONE}};
+    const char *names[4] = {"AQL dispatch (acquire system, release system) + host word",
+                            "AQL dispatch (acquire agent, release agent) + host word",
+                            "AQL dispatch (acquire agent, release none) + host word",
+                            "AQL dispatch (acquire system, release none) + host word"};
+    for (int sc = 0; sc < 4; ++sc) {
+        for (int i = -200; i < iters; ++i) {
+            const double t0 = now_us();
+            const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
+            Args *a = (Args *)(karg + (idx % 64) * 64);
+            a->p = p;
+            a->flag = flag;
+            a->seq = ++seq;
+            a->light = 0;
+            hsa_kernel_dispatch_packet_t *k = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+            k->workgroup_size_x = 64;
+            k->workgroup_size_y = k->workgroup_size_z = 1;
+            k->reserved0 = 0;
+            k->grid_size_x = 64;
+            k->grid_size_y = k->grid_size_z = 1;
+            k->private_segment_size = 0;
+            k->group_segment_size = 0;
+            k->kernel_object = g_kobj;
+            k->kernarg_address = a;
+            k->reserved2 = 0;
+            k->completion_signal.handle = 0;
+            const uint16_t h = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                          (1 << HSA_PACKET_HEADER_BARRIER) |
+                                          (scopes[sc][0] << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                          (scopes[sc][1] << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+            __atomic_store_n((uint32_t *)k, (uint32_t)h | (1u << 16), __ATOMIC_RELEASE);
+            hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
+            const double t1 = now_us();
+            uint64_t spins = 0;
+            while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq)
+                if (++spins > 4000000000ull) {
+                    printf("{\"error\": \"AQL word never arrived\"}\n");
+                    return 7;
+                }
+            if (i >= 0) v[i] = now_us() - t0;
+            (void)t1;
+        }
+        report(names[sc], v);
+    }
+    // the library's k_reduce_local_tiny (SUM, 2 x uint32) dispatched the same way, system acquire,
+    // no release: the kernel object's own cost beside k_word's
+    if (g_tiny) {
+        unsigned *b = nullptr;
+        if (hipMalloc(&b, 64) || hipMemset(b, 0, 64)) return 8;
+        struct TArgs {
+            const void *in;
+            void *io;
+            unsigned count, pad;
+            unsigned long long *flag;
+            unsigned long long seq;
+        };
+        for (int sc = 0; sc < 2; ++sc) {
+            for (int i = -200; i < iters; ++i) {
+                const double t0 = now_us();
+                const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
+                TArgs *a = (TArgs *)(karg + (idx % 64) * 64);
+                a->in = p;
+                a->io = b;
+                a->count = 2;
+                a->pad = 0;
+                a->flag = flag;
+                a->seq = ++seq;
+                hsa_kernel_dispatch_packet_t *k = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+                k->workgroup_size_x = 64;
+                k->workgroup_size_y = k->workgroup_size_z = 1;
+                k->reserved0 = 0;
+                k->grid_size_x = 64;
+                k->grid_size_y = k->grid_size_z = 1;
+                k->private_segment_size = 0;
+                k->group_segment_size = 0;
+                k->kernel_object = g_tiny;
+                k->kernarg_address = a;
+                k->reserved2 = 0;
+                k->completion_signal.handle = 0;
+                const int acq = sc ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM;
+                const uint16_t h = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                              (1 << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE));
+                __atomic_store_n((uint32_t *)k, (uint32_t)h | (1u << 16), __ATOMIC_RELEASE);
+                hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
+                uint64_t spins = 0;
+                while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq)
+                    if (++spins > 4000000000ull) return 9;
+                if (i >= 0) v[i] = now_us() - t0;
+            }
+            report(sc ? "AQL dispatch of libmpi k_reduce_local_tiny (agent acquire)"
+                      : "AQL dispatch of libmpi k_reduce_local_tiny (system acquire)", v);
+        }
+    }
+    hsa_queue_destroy(q);
+    MPI_Finalize();
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const char *mode = argc > 1 ? argv[1] : "lib";
     const int iters = argc > 2 ? atoi(argv[2]) : 5000;
+    if (!strcmp(mode, "aql")) return aql_mode(iters);
     std::vector<double> v(iters);
     if (!strcmp(mode, "lib")) {
         if (MPI_Init(nullptr, nullptr)) return 2;
