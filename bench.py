@@ -264,6 +264,11 @@ def bench_n1(args, L):
                                                    "kernel in the library's own HSA queue, runtime/aql.cpp), "
                                                    "Python ctypes loop"}
     del s8, r8
+    # the same 8-byte call from the OSU loop in C (tools/osu/libosu_coll.so -c reduce_local, MPI_FLOAT
+    # SUM on 2 elements, validated), without the ctypes call in every iteration
+    osu8 = osu_reduce_local_8b()
+    if osu8 is not None:
+        extra["reduce_local_8B_latency_us"]["osu_c_loop_us"] = osu8
     # HBM traffic of this kernel from the newest committed PMC pass (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py); the file is named in the line
     traffic, tsrc = None, None
@@ -431,6 +436,30 @@ def rccl_comparator(L, world, rank, size, steps, timeout=150):
 
 SWEEP_MAX = 1 << 30        # configs[2]: osu_allreduce 8 B .. 1 GiB
 SWEEP_CAP = 256 << 20      # configs[3]: reduce_scatter / allgather / bcast up to 256 MiB
+
+
+def osu_reduce_local_8b():
+    """N = 1: the 8-byte MPI_Reduce_local latency from tools/osu's C OSU loop (osu_coll -c reduce_local,
+    2000 iterations after 200 untimed, result validated); None when the harness is not built."""
+    so = os.path.join(ROOT, "tools", "osu", "libosu_coll.so")
+    if not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    lib.osu_coll_main.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
+    lib.osu_coll_main.restype = ctypes.c_int
+    path = os.path.join("/tmp", f"mv2amd_rl8_{os.getpid()}.jsonl")
+    args = ["osu_coll", "-c", "reduce_local", "-m", "8:8", "-i", "2000", "-x", "200", "-v", "-j", "-o", path]
+    argv = (ctypes.c_char_p * len(args))(*[a.encode() for a in args])
+    rc = lib.osu_coll_main(len(args), argv)
+    try:
+        rows = [json.loads(l[5:]) for l in open(path) if l.startswith("JSON ")]
+        os.unlink(path)
+    except OSError:
+        return None
+    row = next((r for r in rows if r.get("coll") == "reduce_local" and r.get("bytes") == 8), None)
+    if rc != 0 or row is None or row.get("valid") is not True:
+        return None
+    return row["lat_us"]
 
 
 def osu_sweep(L, world, rank, size):
