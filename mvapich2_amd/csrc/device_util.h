@@ -381,7 +381,8 @@ __device__ __forceinline__ typename Rd::T prog_eval(const typename Rd::T (&v)[kM
     using T = typename Rd::T;
     if constexpr (Rd::kOrderFree) {
         // every order gives these bits (ops/functors.h): fold the program's leaves (each register
-        // it names is one rank's operand, used once) in index order
+        // it names is one rank's operand, used once, all in res's tree -- runtime/orders.cpp
+        // Sym::compile checks that for every program it builds) in index order
         unsigned leaves = p.nsteps ? 0u : 1u << p.res;
 #pragma unroll
         for (int s = 0; s < kMaxRanks - 1; ++s)

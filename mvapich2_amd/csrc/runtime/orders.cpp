@@ -178,12 +178,20 @@ struct Sym {
         ++p.nsteps;
         return ra;
     }
+    // Every program is compiled here, from one expression tree walked from its root: each step
+    // belongs to res's tree and each register is one rank's operand, used once (emit refuses a
+    // leaf twice).  device_util.h prog_eval's order-free shortcut folds exactly the registers a
+    // program names, which equals the program's result only under that property, so it is checked
+    // once more on the result: a tree with k leaves has k - 1 steps.
     bool compile(int e, Prog &p) const {
         memset(&p, 0, sizeof(p));
         unsigned used = 0;
         const int r = emit(e, p, used);
         if (r < 0) return false;
         p.res = (uint8_t)r;
+        unsigned named = p.nsteps ? 0u : 1u << p.res;
+        for (int k = 0; k < p.nsteps; ++k) named |= (1u << p.dst[k]) | (1u << p.src[k]);
+        if (named != used || __builtin_popcount(used) != p.nsteps + 1) return false;
         return true;
     }
 };
