@@ -36,7 +36,7 @@ HBM_PEAK = 8000.0        # GB/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK = 153.0        # GB/s per link per direction (task statement)
 S_BYTES = 256 * 1024 * 1024
 # completion-word events (mv2h_get_info; runtime/coll.cpp wait_done), copied into both lines
-WORD_KEYS = ("done_late", "done_missed", "done_xcd_split")
+WORD_KEYS = ("done_queried", "done_late", "done_missed", "done_xcd_split")
 WORLD = 0x44000000        # MPI_COMM_WORLD (MPICH ABI)
 
 

@@ -173,13 +173,15 @@ static hipError_t settle_split(hipStream_t st) {
 // The word is the normal path: the stream is consulted only once the word is
 // 200 us late, then every 100 us (a hipStreamQuery costs ~3 us of host time,
 // and one in flight when the word lands delays the return by that much).
-// Both fallbacks are counted (done_late: the stream was consulted; done_missed:
-// the kernel had ended without the word) and the first missed word of the
-// process is reported: a missed word would otherwise be invisible in every record.
+// Every fallback is counted and the first missed word of the process is reported (a missed word
+// would otherwise be invisible in every record): done_queried -- the stream was consulted at least
+// once (any call whose kernel runs longer than 200 us, e.g. a 256 MiB allreduce on a shared GPU);
+// done_late -- the stream already reported the kernel finished when the word was seen (the word
+// trailed the kernel's end); done_missed -- the kernel had ended without raising the word.
 static hipError_t wait_done(hipStream_t st, uint64_t want) {
     World &w = world();
     uint64_t next_query = 0;
-    bool late = false;
+    bool queried = false;
     for (unsigned spins = 0;; ++spins) {
         if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return settle_split(st);
         if ((spins & 255u) == 0) {
@@ -187,13 +189,16 @@ static hipError_t wait_done(hipStream_t st, uint64_t want) {
             if (!next_query) next_query = t + 200000;
             if (t < next_query) continue;
             next_query = t + 100000;
-            if (!late) {
-                late = true;
-                ++w.done_late;
+            if (!queried) {
+                queried = true;
+                ++w.done_queried;
             }
             const hipError_t q = hipStreamQuery(st);
             if (q == hipErrorNotReady) continue;
-            if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) return settle_split(st);
+            if (__atomic_load_n(w.done_flag, __ATOMIC_ACQUIRE) >= want) {
+                if (q == hipSuccess) ++w.done_late;
+                return settle_split(st);
+            }
             if (q == hipSuccess) {
                 if (w.done_missed++ == 0)
                     fprintf(stderr, "[mv2amd rank %d] warning: a kernel finished without raising its completion word "
@@ -869,6 +874,7 @@ int mv2h_get_info(const char *key, long *value) {
         *value = (v && *v) ? *v != '0' : w.nshare <= 4;
     }
     else if (!strcmp(key, "done_late")) *value = (long)w.done_late;
+    else if (!strcmp(key, "done_queried")) *value = (long)w.done_queried;
     else if (!strcmp(key, "done_missed")) *value = (long)w.done_missed;
     else if (!strcmp(key, "done_xcd_split")) *value = (long)w.done_xcd_split;
     else if (!strcmp(key, "p2p_unexpected")) *value = (long)p2p_unexpected_matched();

@@ -249,20 +249,23 @@ int run_copies(const std::vector<Copy> &cp) {
             ++w.done_xcd_split;
             return hipStreamSynchronize(st) == hipSuccess ? 0 : E_INTERN;
         };
-        bool late = false;
+        bool queried = false;
         for (unsigned spins = 0;; ++spins) {
             if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return settle();
             if ((spins & 255u) != 0) continue;
             const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
             if (us < next_us) continue;
             next_us = us + 100.0;
-            if (!late) {
-                late = true;
-                ++w.done_late;
+            if (!queried) {
+                queried = true;
+                ++w.done_queried;
             }
             const hipError_t q = hipStreamQuery(st);
             if (q == hipErrorNotReady) continue;
-            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) return settle();
+            if (__atomic_load_n(g_pdone.flag, __ATOMIC_ACQUIRE) >= want) {
+                if (q == hipSuccess) ++w.done_late;
+                return settle();
+            }
             if (q == hipSuccess) {  // finished without raising the word: counters reset, done
                 if (w.done_missed++ == 0)
                     fprintf(stderr, "[mv2amd rank %d] warning: a point-to-point copy kernel finished without raising "

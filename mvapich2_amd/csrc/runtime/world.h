@@ -176,10 +176,11 @@ struct World {
     uint64_t call_allocs = 0;
     uint64_t pool_trims = 0;  // idle pool blocks returned to HIP above MV2AMD_POOL_IDLE_MAX (world.cpp pool_put)
     // completion-word events (coll.cpp wait_done), reported by mv2h_get_info and both bench lines:
-    // the word was still unseen 200 us after the launch, so the stream was consulted; the kernel had
-    // ended without raising it; the kernel raised it marked "groups split over XCDs" (device_util.h
-    // block_done), so the host completed the call with a stream synchronisation
-    uint64_t done_late = 0, done_missed = 0, done_xcd_split = 0;
+    // the stream was consulted (the word unseen 200 us after the launch); the word was seen only
+    // after the stream reported the kernel finished; the kernel had ended without raising it; the
+    // kernel raised it marked "groups split over XCDs" (device_util.h block_done), so the host
+    // completed the call with a stream synchronisation
+    uint64_t done_queried = 0, done_late = 0, done_missed = 0, done_xcd_split = 0;
     uint64_t split_seen = 0;  // last done_flag[1] (split call's seq) already settled
     size_t uop_in_bytes = 0, uop_area_bytes = 0;  // last host-evaluated reduction: operand bytes received, area
     // host-evaluated reductions, cumulative ns per phase (mpi/user_coll.cpp UopPhase): staging the

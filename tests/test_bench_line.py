@@ -56,7 +56,7 @@ def test_one_rank_per_gpu_roofline(n):
 
 
 CHECKS = {"timed_calls_verified": 20, "timed_calls": 20,
-          "completion_word_sum_over_ranks": {"done_late": 3, "done_missed": 0, "done_xcd_split": 0},
+          "completion_word_sum_over_ranks": {"done_queried": 3, "done_late": 0, "done_missed": 0, "done_xcd_split": 0},
           "release_protocol": "light",
           "shared_gpu_constants": {"MV2AMD_AR_SCALAR_MAX": 1024, "MV2AMD_RS_SCALAR_MAX": 4096, "p2p_copy_kernels": True}}
 
@@ -71,7 +71,7 @@ def test_line_carries_the_checks(nshare):
     cfg = line["config"]
     assert cfg["timed_calls_verified"] == 20 and cfg["timed_calls"] == 20
     assert cfg["pipe_tiling"]["release_protocol"] == "light" and cfg["pipe_tiling"]["grid"] == 256
-    assert line["extra"]["completion_word"] == {"done_late": 3, "done_missed": 0, "done_xcd_split": 0}
+    assert line["extra"]["completion_word"] == {"done_queried": 3, "done_late": 0, "done_missed": 0, "done_xcd_split": 0}
     sg = line["extra"]["constants_tuned_on_shared_gpu"]
     assert sg["MV2AMD_AR_SCALAR_MAX"] == 1024 and sg["p2p_copy_kernels"] is True
     assert ("unmeasured over xGMI" in sg["note"]) == (nshare == 1)

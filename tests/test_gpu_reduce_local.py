@@ -199,7 +199,7 @@ def test_result_visible_to_a_copy_engine_at_return():
 
 def test_completion_word_fallbacks_are_counted():
     """A missed completion word is visible: a Reduce_local launched with its word
-    withheld completes through the stream fallback with the right bytes and counts done_late and
+    withheld completes through the stream fallback with the right bytes and counts done_queried and
     done_missed; a word marked as raised by a kernel whose block groups ran on several XCDs
     completes by stream synchronisation and counts done_xcd_split (runtime/coll.cpp wait_done,
     settle_split; device_util.h block_done)."""
@@ -210,12 +210,12 @@ def test_completion_word_fallbacks_are_counted():
     y = rng.standard_normal(n).astype(np.float32)
     want = y.copy()
     assert oracle.reduce_local(x, want, n, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"]) == 0
-    before = {k: m.info(k) for k in ("done_late", "done_missed", "done_xcd_split")}
+    before = {k: m.info(k) for k in ("done_queried", "done_late", "done_missed", "done_xcd_split")}
     m.check(L.mv2h_set_tuning(b"withhold_done", 1), "withhold_done")
     got = run_rl("MPI_FLOAT", "MPI_SUM", x, y, n)
     assert np.array_equal(got, want.view(np.uint8))
     assert m.info("done_missed") == before["done_missed"] + 1
-    assert m.info("done_late") >= before["done_late"] + 1
+    assert m.info("done_queried") >= before["done_queried"] + 1
     m.check(L.mv2h_set_tuning(b"fake_split", 1), "fake_split")
     got = run_rl("MPI_FLOAT", "MPI_SUM", x, y, n)
     assert np.array_equal(got, want.view(np.uint8))
