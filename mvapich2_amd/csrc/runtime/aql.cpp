@@ -11,8 +11,8 @@
 // objects, which MPI_Init loads (world.cpp, code-object preload), found through the AMD loader
 // extension (every executable of the process, its kernel symbols for this GPU) and keyed by the
 // (op, kind) in the mangled name.  The queue is created once on the HSA agent of this rank's HIP
-// device.  A packet carries a system-scope acquire (the kernel reads operands other agents wrote)
-// and release; the kernel raises the call's completion word (device_util.h contract) and the host
+// device.  A packet carries an agent-scope acquire and no release (see Aql::acquire); the kernel
+// releases its result and raises the call's completion word (device_util.h contract) and the host
 // spins on it, as for a HIP launch.
 //
 // Ordering: the HIP path runs on the library's blocking stream, ordered after the legacy null
@@ -54,11 +54,19 @@ struct Aql {
     int kernels = 0;
     uint64_t skip_lib = 0, skip_null = 0;  // calls that took the HIP launch: library words pending / null stream busy
     bool hsa_ref = false;  // aql_init's hsa_init reference, released by aql_finalize
-    // the packet's fences: a system-scope acquire (operands written by copy engines or other
-    // agents may be stale in this GPU's L2s); no release -- the kernel releases its result at
-    // system scope itself before raising the word (MV2AMD_AQL_ACQUIRE / _RELEASE: 0 none, 1 agent,
-    // 2 system, for measurement)
-    int acquire = HSA_FENCE_SCOPE_SYSTEM, release = HSA_FENCE_SCOPE_NONE;
+    // the packet's fences: an agent-scope acquire (this CU's caches invalidated before the kernel
+    // reads its operands) and no release -- the kernel releases its result at system scope itself
+    // before raising the word.  The operands' producers completed before the call through HIP
+    // (stream or device synchronisation, or the library's own words), whose completion releases
+    // them from every XCD's L2; tools/diag/stale_probe.hip rewrote an operand 3,000 times by a copy
+    // engine and 3,000 times by a kernel on a HIP stream between two kernels of such a queue that
+    // read it on every XCD, and saw no stale word even with no acquire at all (profiles/r06/r06p).
+    // A system-scope acquire costs ~0.9-1.5 us more per call (DESIGN.md §6 *8-byte latency*).
+    // That probe cannot cover a writer on another GPU (over xGMI into this GPU's memory, which does
+    // not pass this GPU's L2s), so a job with other ranks keeps the system scope (aql_init).
+    // MV2AMD_AQL_ACQUIRE / _RELEASE: 0 none, 1 agent, 2 system.
+    int acquire = HSA_FENCE_SCOPE_AGENT, release = HSA_FENCE_SCOPE_NONE;
+    int acquire_set = -1;  // MV2AMD_AQL_ACQUIRE, else agent for a one-rank job and system otherwise
     int stream_checks = 1;  // MV2AMD_AQL_STREAM_CHECKS=0: measurement only (drops the null-stream ordering)
     std::atomic<int> queue_error{0};
 };
@@ -217,7 +225,7 @@ int aql_init() {
         g_aql.kernarg = nullptr;
         return -1;
     }
-    if (const char *e = getenv("MV2AMD_AQL_ACQUIRE")) g_aql.acquire = atoi(e) & 3;
+    if (const char *e = getenv("MV2AMD_AQL_ACQUIRE")) g_aql.acquire_set = atoi(e) & 3;
     if (const char *e = getenv("MV2AMD_AQL_RELEASE")) g_aql.release = atoi(e) & 3;
     if (const char *e = getenv("MV2AMD_AQL_STREAM_CHECKS")) g_aql.stream_checks = atoi(e) != 0;
     g_aql.state = 1;
@@ -252,9 +260,12 @@ int aql_reduce_local(int op, int kind, const void *in, void *io, size_t count, s
     // still counts a kernel of the library's stream as running waits for it (7-10 us, profiles/r06j),
     // so a call that follows a HIP launch first lets HIP retire it -- one stream synchronisation per
     // switch from the HIP launch to this queue, none between calls of this queue
-    if (g_aql.stream_checks && hipStreamQuery(w.stream) != hipSuccess) {
-        (void)hipGetLastError();
-        if (hipStreamSynchronize(w.stream) != hipSuccess) return 0;
+    if (g_aql.stream_checks && w.stream_hip_busy) {
+        if (hipStreamQuery(w.stream) != hipSuccess) {
+            (void)hipGetLastError();
+            if (hipStreamSynchronize(w.stream) != hipSuccess) return 0;
+        }
+        w.stream_hip_busy = false;  // until the next launch on it (coll.cpp pick_stream)
     }
     if (g_aql.stream_checks && hipStreamQuery(nullptr) != hipSuccess) {
         (void)hipGetLastError();
@@ -287,9 +298,12 @@ int aql_reduce_local(int op, int kind, const void *in, void *io, size_t count, s
     p->kernarg_address = a;
     p->reserved2 = 0;
     p->completion_signal.handle = 0;
+    const int acquire = g_aql.acquire_set >= 0 ? g_aql.acquire_set
+                        : w.gsize > 1               ? (int)HSA_FENCE_SCOPE_SYSTEM
+                                                    : g_aql.acquire;
     const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                        (1 << HSA_PACKET_HEADER_BARRIER) |
-                                       (g_aql.acquire << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                       (acquire << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                        (g_aql.release << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     const uint16_t setup = (uint16_t)(1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS);
     __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);

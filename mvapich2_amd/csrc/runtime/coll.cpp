@@ -53,6 +53,7 @@ bool log_debug_on() {
 static hipStream_t pick_stream(void *s) {
     World &w = world();
     hipStream_t st = s ? (hipStream_t)s : w.stream;
+    if (st == w.stream) w.stream_hip_busy = true;  // runtime/aql.cpp consults HIP before its next dispatch
     if (w.graph) return st;  // graph lane: disjoint arenas and epochs, ordered by the graph itself
     if (w.last_st && st != w.last_st) {
         if (!w.sw_ev) hipEventCreateWithFlags(&w.sw_ev, hipEventDisableTiming);

@@ -192,6 +192,7 @@ struct World {
     int rl_grid = 1 << 20;    // reduce_local grid cap (default: one tile per workgroup, tools/rl_variants.hip)
     size_t rl_tiny_max = 1024;  // reduce_local operands up to this many bytes: one-wave kernel (MV2AMD_RL_TINY_MAX)
     uint64_t aql_calls = 0;     // reduce_local calls dispatched straight into the HSA queue (runtime/aql.cpp)
+    bool stream_hip_busy = true;  // HIP may still count work on `stream` as running (set by every launch there)
     int sync_mode = 0;        // completion wait: 0 kernel-written completion word, 1 hipStreamSynchronize only
     uint32_t *done_ctr = nullptr;   // device: 9 arrival counters of the completion word (Done)
     uint64_t *done_flag = nullptr;  // pinned host: last completed call's sequence number
