@@ -396,7 +396,7 @@ def derived_no_alloc(L, case, rank, n):
         tot += time.perf_counter() - t0
         L.MPI_Barrier(WORLD)
     assert L.MPI_Type_free(ctypes.byref(vt)) == 0
-    return np.array([bad, allocs, tot / iters * 1e6], dtype=np.float64)
+    return np.array([bad, allocs, tot / iters * 1e6, m.info("pool_trims")], dtype=np.float64)
 
 
 def arg_checks(L, rank, n):

@@ -877,15 +877,21 @@ def test_derived_type_calls_make_no_device_allocations(n, tmp_path):
     allocates on every round; the OSU-style latency of the 64 KiB derived MPI_Bcast is recorded
     for both (MV2AMD_TEST_RECORD: a JSON file the numbers are appended to)."""
     lat = {}
-    for pool in ("1", "0"):
+    # "1c": the pool with its idle cap at 1 byte (MV2AMD_POOL_IDLE_MAX): every block goes back to HIP
+    # when it is returned, so warm calls allocate again and the trims are counted (ADVICE r05)
+    for pool in ("1", "0", "1c"):
         case = {"id": f"dna{pool}", "kind": "derived_no_alloc", "nblocks": 4096, "rounds": 10, "lat_iters": 200}
         (tmp_path / f"p{pool}").mkdir()
-        res = run_workers(n, [case], tmp_path / f"p{pool}", extra_env={"MV2AMD_POOL": pool})
+        env = {"MV2AMD_POOL": pool[0], **({"MV2AMD_POOL_IDLE_MAX": "1"} if pool == "1c" else {})}
+        res = run_workers(n, [case], tmp_path / f"p{pool}", extra_env=env)
         got = [res(case["id"], r) for r in range(n)]
         for r in range(n):
             assert got[r][0] == 0, f"rank {r}: wrong results with MV2AMD_POOL={pool}"
             if pool == "1":
                 assert got[r][1] == 0, f"rank {r}: {got[r][1]} device allocations inside warm calls"
+                assert got[r][3] == 0, f"rank {r}: idle blocks trimmed under the default cap"
+            elif pool == "1c":
+                assert got[r][1] > 0 and got[r][3] > 0, f"rank {r}: allocations {got[r][1]}, trims {got[r][3]}"
             else:
                 assert got[r][1] > 0
         lat[f"pool={pool}"] = round(float(np.mean([g[2] for g in got])), 2)
