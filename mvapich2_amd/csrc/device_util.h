@@ -62,7 +62,9 @@ constexpr int kDoneStride = 1024;  // counter spacing in words (4 KiB: separate 
 constexpr int kDoneSub = 64;       // first-level counters (blockIdx % 64)
 constexpr int kDoneCtrs = kDoneSub + 8 + 1;  // + group counters (blockIdx % 8) + groups done; each with an XCD mask
 constexpr size_t kDoneBytes = (size_t)kDoneCtrs * kDoneStride * sizeof(uint32_t);
-constexpr int kDoneMaxGrid = 1 << 22;  // largest grid whose arrivals block_done's counter fields hold exactly
+// largest grid whose arrivals block_done's counter fields hold exactly: <= 16384 per sub-counter,
+// so the sums stay in their fields for any 4-bit HW_REG_XCC_ID (sum of squares <= 225 x 16384)
+constexpr int kDoneMaxGrid = 1 << 20;
 // ints in the pinned error word block (wait_mask records a timeout's context there)
 constexpr int kErrWords = 64;
 struct Done {
@@ -205,8 +207,8 @@ __device__ __forceinline__ bool wait_peers(uint64_t *own_sig, int n, int blk, ui
 // synchronisation (the kernel's end releases every XCD's L2) instead of trusting
 // the word (runtime/coll.cpp wait_done).  Fields of a counter word: count bits
 // 0-16, sum 17-35, sum of squares 36-57, split subs / groups 58-63 (exact for
-// up to 65536 arrivals per sub-counter, i.e. grids up to 4 Mi blocks: the
-// launchers' grids stay below kDoneMaxGrid, runtime/world.cpp clamps rl_grid).
+// up to 16384 arrivals per sub-counter, i.e. grids up to 1 Mi blocks: the
+// launchers' grids stay within kDoneMaxGrid, runtime/world.cpp clamps rl_grid).
 constexpr int kDoneSumShift = 17, kDoneSqShift = 36, kDoneSplitShift = 58;
 constexpr uint64_t kDoneCntMask = (1ull << kDoneSumShift) - 1;
 

@@ -823,7 +823,7 @@ double mv2h_last_kernel_ms(void) { return world().last_ms; }
 
 int mv2h_set_tuning(const char *key, long value) {
     World &w = world();
-    if (!strcmp(key, "max_grid")) w.max_grid = (int)value;
+    if (!strcmp(key, "max_grid")) w.max_grid = (int)std::min<long>(std::max(1L, value), kDoneMaxGrid);
     else if (!strcmp(key, "rl_grid")) w.rl_grid = (int)std::min<long>(std::max(1L, value), kDoneMaxGrid);
     else if (!strcmp(key, "rl_tiny_max")) w.rl_tiny_max = (size_t)std::max(0L, value);
     else if (!strcmp(key, "pipe_grid")) w.pipe_grid = (int)value;

@@ -512,7 +512,7 @@ static int setup_device_common() {
         w.wall_clock_khz = khz;
     w.timeout_ticks = (uint64_t)(env_long("MV2AMD_TIMEOUT_S", 120) * w.wall_clock_khz * 1000.0);
     w.oneshot_max = (size_t)env_long("MV2AMD_ONESHOT_MAX", (long)w.oneshot_max);
-    w.max_grid = (int)env_long("MV2AMD_MAX_GRID", w.max_grid);
+    w.max_grid = (int)std::min<long>(env_long("MV2AMD_MAX_GRID", w.max_grid), kDoneMaxGrid);
     w.pipe_grid = (int)env_long("MV2AMD_PIPE_GRID", w.pipe_grid);
     w.pipe_sub = (size_t)env_long("MV2AMD_PIPE_SUB", (long)w.pipe_sub);
     w.pipe_rnt = env_long("MV2AMD_PIPE_RNT", w.pipe_rnt) != 0;  // stores into peers' arenas: non-temporal / plain
