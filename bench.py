@@ -266,9 +266,14 @@ def bench_n1(args, L):
     del s8, r8
     # the same 8-byte call from the OSU loop in C (tools/osu/libosu_coll.so -c reduce_local, MPI_FLOAT
     # SUM on 2 elements, validated), without the ctypes call in every iteration
+    # it is the line's figure, as the N > 1 line's 8-byte latency is its C sweep's (OSU is a C
+    # benchmark); the Python loop's figure stays beside it
     osu8 = osu_reduce_local_8b()
     if osu8 is not None:
-        extra["reduce_local_8B_latency_us"]["osu_c_loop_us"] = osu8
+        rl8 = extra["reduce_local_8B_latency_us"]
+        rl8["python_loop_us"] = rl8["us"]
+        rl8["us"] = osu8
+        rl8["source"] = "tools/osu/osu_coll -c reduce_local (C OSU loop, MPI_FLOAT SUM on 2 elements, 2000 iterations)"
     # HBM traffic of this kernel from the newest committed PMC pass (rocprofv3 FETCH_SIZE x2 +
     # WRITE_SIZE in separate passes, tools/pmc_summary.py); the file is named in the line
     traffic, tsrc = None, None

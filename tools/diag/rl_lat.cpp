@@ -203,17 +203,63 @@ static int aql_mode(int iters) {
             unsigned long long *flag;
             unsigned long long seq;
         };
-        for (int sc = 0; sc < 2; ++sc) {
+        // variant 2: kernel arguments in device memory the host writes through the BAR (what
+        // HIP_FORCE_DEV_KERNARG does for HIP launches), system acquire
+        char *dkarg = nullptr;
+        {
+            struct PoolFind {
+                hsa_amd_memory_pool_t pool;
+                bool found;
+            } pf{{0}, false};
+            hsa_amd_agent_iterate_memory_pools(
+                g_agent,
+                [](hsa_amd_memory_pool_t pl, void *d) -> hsa_status_t {
+                    hsa_amd_segment_t seg;
+                    hsa_amd_memory_pool_get_info(pl, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+                    uint32_t fl = 0;
+                    hsa_amd_memory_pool_get_info(pl, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &fl);
+                    if (seg == HSA_AMD_SEGMENT_GLOBAL && (fl & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED)) {
+                        ((PoolFind *)d)->pool = pl;
+                        ((PoolFind *)d)->found = true;
+                        return HSA_STATUS_INFO_BREAK;
+                    }
+                    return HSA_STATUS_SUCCESS;
+                },
+                &pf);
+            hsa_agent_t cpu{};
+            hsa_iterate_agents(
+                [](hsa_agent_t a, void *d) -> hsa_status_t {
+                    hsa_device_type_t t;
+                    hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+                    if (t == HSA_DEVICE_TYPE_CPU) {
+                        *(hsa_agent_t *)d = a;
+                        return HSA_STATUS_INFO_BREAK;
+                    }
+                    return HSA_STATUS_SUCCESS;
+                },
+                &cpu);
+            if (pf.found && hsa_amd_memory_pool_allocate(pf.pool, 64 * 64, 0, (void **)&dkarg) == HSA_STATUS_SUCCESS) {
+                if (hsa_amd_agents_allow_access(1, &cpu, nullptr, dkarg) != HSA_STATUS_SUCCESS) dkarg = nullptr;
+            } else {
+                dkarg = nullptr;
+            }
+            if (!dkarg) printf("{\"note\": \"no host-visible device kernarg memory\"}\n");
+        }
+        for (int sc = 0; sc < (dkarg ? 3 : 2); ++sc) {
             for (int i = -200; i < iters; ++i) {
                 const double t0 = now_us();
                 const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-                TArgs *a = (TArgs *)(karg + (idx % 64) * 64);
+                TArgs *a = (TArgs *)((sc == 2 ? dkarg : karg) + (idx % 64) * 64);
                 a->in = p;
                 a->io = b;
                 a->count = 2;
                 a->pad = 0;
                 a->flag = flag;
                 a->seq = ++seq;
+                if (sc == 2) {  // the BAR writes land before the doorbell: fence and read one back
+                    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+                    (void)*(volatile unsigned long long *)&a->seq;
+                }
                 hsa_kernel_dispatch_packet_t *k = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
                 k->workgroup_size_x = 64;
                 k->workgroup_size_y = k->workgroup_size_z = 1;
@@ -226,7 +272,7 @@ static int aql_mode(int iters) {
                 k->kernarg_address = a;
                 k->reserved2 = 0;
                 k->completion_signal.handle = 0;
-                const int acq = sc ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM;
+                const int acq = sc == 1 ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM;
                 const uint16_t h = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                               (1 << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE));
                 __atomic_store_n((uint32_t *)k, (uint32_t)h | (1u << 16), __ATOMIC_RELEASE);
@@ -236,8 +282,9 @@ static int aql_mode(int iters) {
                     if (++spins > 4000000000ull) return 9;
                 if (i >= 0) v[i] = now_us() - t0;
             }
-            report(sc ? "AQL dispatch of libmpi k_reduce_local_tiny (agent acquire)"
-                      : "AQL dispatch of libmpi k_reduce_local_tiny (system acquire)", v);
+            report(sc == 2 ? "AQL dispatch of libmpi k_reduce_local_tiny (system acquire, kernargs in device memory)"
+                   : sc ? "AQL dispatch of libmpi k_reduce_local_tiny (agent acquire)"
+                        : "AQL dispatch of libmpi k_reduce_local_tiny (system acquire)", v);
         }
     }
     hsa_queue_destroy(q);
