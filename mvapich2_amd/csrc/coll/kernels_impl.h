@@ -71,11 +71,16 @@ template <class Rd>
 __global__ __launch_bounds__(64) void k_reduce_local_tiny(const typename Rd::T *__restrict__ in,
                                                           typename Rd::T *__restrict__ io, uint32_t count,
                                                           uint64_t *flag, uint64_t seq) {
+    // every argument in SGPRs before the first branch: the kernel-argument fetches issue together
+    // and are waited for once (left to the compiler, the count, the operand pointers and the word's
+    // pointer and value are three dependent fetches from host memory, ~0.1 us each)
+    asm volatile("" ::"s"(in), "s"(io), "s"(count), "s"(flag), "s"(seq));
     for (uint32_t e = threadIdx.x; e < count; e += 64) io[e] = Rd::apply(io[e], in[e]);
-    if (flag) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's store acknowledged (one wave)
-        if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    // One wave: the release's own `buffer_wbl2; s_waitcnt vmcnt(0)` (issued after the store
+    // instruction that wrote every lane's element) covers all 64 lanes' stores, so no separate wait
+    // for them first -- that wait made the stores' acknowledgement and the write-back two round
+    // trips (0.2-0.3 us of the 8-byte call, profiles/r06/r06w-r06y)
+    if (flag && threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int OP, int K>

@@ -213,6 +213,51 @@ static hipError_t wait_done(hipStream_t st, uint64_t want) {
     }
 }
 
+static void log_epochs(uint64_t lo, uint64_t hi, hipStream_t st) {
+    World &w = world();
+    w.epoch_log[w.epoch_pos++ % 8] = World::EpochRec{w.api_calls, lo, hi, st != w.stream};
+}
+
+// The waited slot of every rank in `mask` as it is in memory now (read by a copy on a stream of
+// its own, after the kernel gave up): a value above the one the kernel last saw means its loads
+// were served stale; the same value means the peer's flag store never landed.
+static void report_slot_now(int blk, unsigned mask) {
+    World &w = world();
+    if (!w.sig || blk < 0 || blk >= kMaxBlocks) return;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    uint64_t *h = nullptr;
+    if (hipHostMalloc((void **)&h, kMaxRanks * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        hipStreamDestroy(s);
+        return;
+    }
+    bool ok = true;
+    for (int j = 0; j < kMaxRanks && ok; ++j)
+        if ((mask >> j) & 1u)
+            ok = hipMemcpyAsync(h + j, w.sig + (size_t)j * kMaxBlocks + blk, sizeof(uint64_t), hipMemcpyDeviceToHost, s) ==
+                 hipSuccess;
+    const uint64_t t0 = now_ns();
+    hipError_t q = hipErrorNotReady;
+    while (ok && (q = hipStreamQuery(s)) == hipErrorNotReady && now_ns() - t0 < 2000000000ull) usleep(100);
+    if (ok && q == hipSuccess) {
+        char line[256];
+        int o = 0;
+        for (int j = 0; j < kMaxRanks && o < (int)sizeof(line) - 40; ++j)
+            if ((mask >> j) & 1u) o += snprintf(line + o, sizeof(line) - o, " r%d=%llu", j, (unsigned long long)h[j]);
+        line[o] = 0;
+        MV2_ERR("  the waited slot now (host copy):%s", line);
+    }
+    (void)hipGetLastError();
+    if (q != hipErrorNotReady) {  // a copy still in flight keeps its buffers
+        hipHostFree(h);
+        hipStreamDestroy(s);
+    }
+}
+
 // A kernel gave up waiting for a peer (device_util.h wait_mask): report what it waited for —
 // the epoch, the ranks and the flag values it last saw from each, next to this rank's host
 // counters — so a failure tells a late peer (flag = an earlier epoch of the same call
@@ -234,6 +279,19 @@ static int check_err_word() {
             "%llu from ranks 0x%x; flags seen:%s; host epoch %llu, round %llu, one-shot calls %llu, call %llu",
             e[1], (unsigned long long)ep, (unsigned)e[4], seen, (unsigned long long)w.epoch, (unsigned long long)w.round,
             (unsigned long long)w.os_calls, (unsigned long long)w.done_seq);
+    {
+        char line[512];
+        int o = 0;
+        for (unsigned k = w.epoch_pos > 8 ? w.epoch_pos - 8 : 0; k < w.epoch_pos && o < (int)sizeof(line) - 80; ++k) {
+            const World::EpochRec &r = w.epoch_log[k % 8];
+            o += snprintf(line + o, sizeof(line) - o, " %llu:%llu-%llu%s%s", (unsigned long long)r.call,
+                          (unsigned long long)r.lo, (unsigned long long)r.hi, r.user_stream ? "(caller's stream)" : "",
+                          r.lo <= ep && ep <= r.hi ? "<-" : "");
+        }
+        line[o] = 0;
+        MV2_ERR("  this rank's last launches with flag epochs (call:epochs, <- the waiting one):%s", line);
+    }
+    report_slot_now(e[1], (unsigned)e[4]);
     // where each late peer's host is now (its beacon in the control segment), next to this rank's
     if (w.shm) {
         const uint64_t t = now_ns();
@@ -538,6 +596,7 @@ static int run_pipe(PipeArgs &a, int oi, const DtypeInfo *dt, hipStream_t st) {
         w.round += (uint64_t)g.nrounds;
         a.epoch0 = w.epoch + 1;
         w.epoch += 2 * (uint64_t)g.nrounds;
+        log_epochs(a.epoch0, w.epoch, st);
     }
     a.err = w.h_err;
     a.timeout = w.timeout_ticks;
@@ -571,6 +630,7 @@ static void oneshot_common(OneShotArgs &a, hipStream_t st) {
         a.sig_peer = w.peer_sig;
         a.sig_own = w.sig;
         a.epoch = ++w.epoch;
+        log_epochs(a.epoch, a.epoch, st);
     }
     a.slot_bytes = w.slot_bytes;
     a.n = n;

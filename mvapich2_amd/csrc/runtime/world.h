@@ -127,6 +127,13 @@ struct World {
     uint64_t epoch = 0;       // last flag epoch used (identical on every rank)
     uint64_t round = 0;       // pipeline rounds issued (slot parity)
     uint64_t os_calls = 0;    // one-shot calls issued (arena parity)
+    // the last launches that took flag epochs (a timeout report names the one that waited)
+    struct EpochRec {
+        uint64_t call, lo, hi;
+        int user_stream;
+    };
+    EpochRec epoch_log[8] = {};
+    unsigned epoch_pos = 0;
 
     // graph lane (HIP graph capture of stream-ordered allreduce, coll.cpp): its own signal page,
     // one-shot arena and pipeline arenas, with the sequence numbers kept on the device (DevSeq)

@@ -57,9 +57,21 @@ __global__ void k_word(unsigned *p, unsigned long long *flag, unsigned long long
     }
 }
 
+// the payload written through to memory (system-scope relaxed stores: the line leaves this XCD's L2
+// with the store), then the word after the wave's stores are acknowledged: no L2 write-back
+__global__ void k_word_wt(unsigned *p, unsigned long long *flag, unsigned long long seq, int) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(p + 1, p[1] + p[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+void load_word_pl(unsigned *p, unsigned long long *flag, hipStream_t st);  // rl_lat_pl.hip
+
 // ---- raw AQL dispatch of k_word from this program's own code object (mode "aql") ----
 static hsa_agent_t g_agent;
-static uint64_t g_kobj, g_tiny;
+static uint64_t g_kobj, g_tiny, g_wt, g_pl;
 static hsa_status_t pick_gpu(hsa_agent_t a, void *) {
     hsa_device_type_t t;
     hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
@@ -78,6 +90,8 @@ static hsa_status_t sym(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t s
     char name[512] = {0};
     if (len < 500) hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_NAME, name);
     if (strstr(name, "k_wordPj")) hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &g_kobj);
+    if (strstr(name, "k_word_wtPj")) hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &g_wt);
+    if (strstr(name, "k_word_plPj")) hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &g_pl);
     if (strstr(name, "k_reduce_local_tinyINS_1RILi2ELi5E"))  // the library's one-wave SUM on MPI_UNSIGNED
         hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &g_tiny);
     return HSA_STATUS_SUCCESS;
@@ -107,6 +121,7 @@ static int aql_mode(int iters) {
         return 3;
     *flag = 0;
     hipLaunchKernelGGL(k_word, dim3(1), dim3(64), 0, st, p, flag, 1ull, 0);  // loads the code object
+    load_word_pl(p, flag, st);  // and rl_lat_pl.hip's
     hipStreamSynchronize(st);
     // host cost of the ordering checks the library's fast path makes
     for (int i = 0; i < iters; ++i) {
@@ -190,6 +205,63 @@ static int aql_mode(int iters) {
             (void)t1;
         }
         report(names[sc], v);
+    }
+    // the word kernel's variants, acquire agent / release none: (a) system-release word (as above),
+    // (b) plain payload + relaxed word after vmcnt (not a valid hand-off: the floor without any L2
+    // write-back), (c) write-through payload + relaxed word after vmcnt (valid), (d) (a) with
+    // kernel-argument preloading
+    {
+        const uint64_t objs[4] = {g_kobj, g_kobj, g_wt, g_pl};
+        const int light[4] = {0, 1, 0, 0};
+        const char *vn[4] = {"AQL agent/none: k_word system-release word", "AQL agent/none: k_word plain payload, relaxed word (floor)",
+                             "AQL agent/none: k_word_wt write-through payload, relaxed word",
+                             "AQL agent/none: k_word_pl (kernarg preload) system-release word"};
+        for (int rep = 0; rep < 2; ++rep)
+            for (int vi = 0; vi < 4; ++vi) {
+                if (!objs[vi]) {
+                    printf("{\"note\": \"%s: kernel object not found\"}\n", vn[vi]);
+                    continue;
+                }
+                for (int i = -200; i < iters; ++i) {
+                    const double t0 = now_us();
+                    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
+                    Args *a = (Args *)(karg + (idx % 64) * 64);
+                    a->p = p;
+                    a->flag = flag;
+                    a->seq = ++seq;
+                    a->light = light[vi];
+                    hsa_kernel_dispatch_packet_t *k = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+                    k->workgroup_size_x = 64;
+                    k->workgroup_size_y = k->workgroup_size_z = 1;
+                    k->reserved0 = 0;
+                    k->grid_size_x = 64;
+                    k->grid_size_y = k->grid_size_z = 1;
+                    k->private_segment_size = 0;
+                    k->group_segment_size = 0;
+                    k->kernel_object = objs[vi];
+                    k->kernarg_address = a;
+                    k->reserved2 = 0;
+                    k->completion_signal.handle = 0;
+                    const uint16_t h = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                                  (1 << HSA_PACKET_HEADER_BARRIER) |
+                                                  (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                                  (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+                    __atomic_store_n((uint32_t *)k, (uint32_t)h | (1u << 16), __ATOMIC_RELEASE);
+                    hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
+                    uint64_t spins = 0;
+                    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq)
+                        if (++spins > 4000000000ull) {
+                            printf("{\"error\": \"%s: word never arrived\"}\n", vn[vi]);
+                            return 7;
+                        }
+                    if (i >= 0) v[i] = now_us() - t0;
+                }
+                report(vn[vi], v);
+            }
+        // the payload of the last calls: every variant computes p[1] += p[0] on zeros
+        unsigned hp[4] = {9, 9, 9, 9};
+        hipMemcpy(hp, p, 16, hipMemcpyDeviceToHost);
+        printf("{\"payload_after\": [%u, %u]}\n", hp[0], hp[1]);
     }
     // the library's k_reduce_local_tiny (SUM, 2 x uint32) dispatched the same way, system acquire,
     // no release: the kernel object's own cost beside k_word's
@@ -308,6 +380,21 @@ int main(int argc, char **argv) {
             v[i] = now_us() - t0;
         }
         report("MPI_Reduce_local 8 B (C loop)", v);
+        // host costs inside the call: the pointer classification (twice per call) and the API
+        // layer up to the count test
+        for (int i = 0; i < iters; ++i) {
+            hipPointerAttribute_t at;
+            const double t0 = now_us();
+            (void)hipPointerGetAttributes(&at, a);
+            v[i] = now_us() - t0;
+        }
+        report("hipPointerGetAttributes(device pointer)", v);
+        for (int i = 0; i < iters; ++i) {
+            const double t0 = now_us();
+            MPI_Reduce_local(a, b, 0, MPI_UNSIGNED, MPI_SUM);
+            v[i] = now_us() - t0;
+        }
+        report("MPI_Reduce_local count 0 (API layer)", v);
         MPI_Finalize();
         return 0;
     }
