@@ -298,9 +298,7 @@ int aql_reduce_local(int op, int kind, const void *in, void *io, size_t count, s
     p->kernarg_address = a;
     p->reserved2 = 0;
     p->completion_signal.handle = 0;
-    const int acquire = g_aql.acquire_set >= 0 ? g_aql.acquire_set
-                        : w.gsize > 1               ? (int)HSA_FENCE_SCOPE_SYSTEM
-                                                    : g_aql.acquire;
+    const int acquire = aql_acquire_scope();
     const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                        (1 << HSA_PACKET_HEADER_BARRIER) |
                                        (acquire << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
@@ -336,6 +334,11 @@ int aql_reduce_local(int op, int kind, const void *in, void *io, size_t count, s
 }
 
 int aql_kernels() { return g_aql.state == 1 ? g_aql.kernels : 0; }
+// the acquire scope the queue's dispatches take (HSA_FENCE_SCOPE_*: 1 agent, 2 system); -1 path off
+int aql_acquire_scope() {
+    if (g_aql.state != 1) return -1;
+    return g_aql.acquire_set >= 0 ? g_aql.acquire_set : world().gsize > 1 ? (int)HSA_FENCE_SCOPE_SYSTEM : g_aql.acquire;
+}
 long aql_skips(int which) { return (long)(which ? g_aql.skip_null : g_aql.skip_lib); }
 
 void aql_finalize() {

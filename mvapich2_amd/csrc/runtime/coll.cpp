@@ -925,6 +925,7 @@ int mv2h_get_info(const char *key, long *value) {
     else if (!strcmp(key, "rl_tiny_max")) *value = (long)w.rl_tiny_max;
     else if (!strcmp(key, "aql_calls")) *value = (long)w.aql_calls;
     else if (!strcmp(key, "aql_kernels")) *value = aql_kernels();
+    else if (!strcmp(key, "aql_acquire")) *value = aql_acquire_scope();
     else if (!strcmp(key, "aql_skip_lib")) *value = aql_skips(0);
     else if (!strcmp(key, "aql_skip_null")) *value = aql_skips(1);
     // constants chosen on one shared GPU (not probed at MPI_Init; the N > 1 bench line names them)

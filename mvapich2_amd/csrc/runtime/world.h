@@ -228,6 +228,7 @@ int world_finalize();
 // taken, < 0 an MPI error class); the kernels it found; its queue torn down at MPI_Finalize
 int aql_reduce_local(int op, int kind, const void *in, void *io, size_t count, size_t esize);
 int aql_kernels();
+int aql_acquire_scope();  // the HSA-queue Reduce_local's acquire scope: 1 agent, 2 system, -1 path off
 long aql_skips(int which);  // 0: library words pending, 1: null stream busy
 void aql_finalize();
 void host_barrier();

@@ -237,6 +237,9 @@ def test_small_reduce_local_takes_the_hsa_queue():
     assert m.info("nshare") == 1
     rng = np.random.default_rng(5)
     before = m.info("aql_calls")
+    p, q = m.DeviceBuffer(8), m.DeviceBuffer(8)
+    assert L.MPI_Reduce_local(p.ptr, q.ptr, 2, TYPES["MPI_INT"][0], OPS["MPI_SUM"]) == 0
+    assert m.info("aql_acquire") == 1  # a one-rank job: the agent scope
     big = (1 << 20) + 3
     for i, (op, t) in enumerate(PAIRS[::3]):
         count = [1, 2, 7, 64, 100][i % 5]
@@ -288,3 +291,71 @@ def test_small_reduce_local_orders_after_null_stream_work():
             assert np.array_equal(b.download(np.uint32, count=4), np.full(4, want, dtype=np.uint32)), i
     assert np.array_equal(b.download(np.uint32, count=4), np.full(4, want, dtype=np.uint32))
     assert m.info("aql_calls") > before
+
+
+SYSTEM_ACQUIRE_CHILD = r"""
+import ctypes, json, sys
+import numpy as np
+import mvapich2_amd as m
+from mvapich2_amd.consts import OPS, TYPES
+from oracle import oracle
+from tests.helpers import as_bytes, data_mask, rand_typed
+hip = ctypes.CDLL("libamdhip64.so")
+hip.hipMemsetD32Async.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+L = m.lib()
+U32, SUM = TYPES["MPI_UNSIGNED"][0], OPS["MPI_SUM"]
+bad = []
+a, b = m.DeviceBuffer(1 << 20), m.DeviceBuffer(64)
+b.upload(np.zeros(16, dtype=np.uint32))
+want = 0
+for i in range(300):  # operands written by null-stream work not waited for
+    assert hip.hipMemsetD32Async(a.ptr, i + 1, (1 << 20) // 4, None) == 0
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 2, U32, SUM) == 0
+    want += i + 1
+bad += [] if np.array_equal(b.download(np.uint32, count=2), np.array([want, want], dtype=np.uint32)) else ["memset"]
+scope = m.info("aql_acquire")
+b.upload(np.zeros(16, dtype=np.uint32))
+want = 0
+for i in range(300):  # operands rewritten by host -> device copies between calls
+    a.upload(np.full(4, 1000 + i, dtype=np.uint32))
+    assert L.MPI_Reduce_local(a.ptr, b.ptr, 4, U32, SUM) == 0
+    want += 1000 + i
+bad += [] if np.array_equal(b.download(np.uint32, count=4), np.full(4, want, dtype=np.uint32)) else ["upload"]
+rng = np.random.default_rng(11)
+for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_BXOR", "MPI_INT"),
+              ("MPI_MAXLOC", "MPI_DOUBLE_INT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX")):
+    for count in (1, 7, 60):
+        ext = TYPES[t][3]
+        x, y = rand_typed(t, count, rng, small=op == "MPI_PROD"), rand_typed(t, count, rng, small=op == "MPI_PROD")
+        want_b = y.copy()
+        assert oracle.reduce_local(x, want_b, count, TYPES[t][0], OPS[op]) == 0
+        xa, yb = m.DeviceBuffer(count * ext), m.DeviceBuffer(count * ext)
+        xa.upload(x)
+        yb.upload(y)
+        assert L.MPI_Reduce_local(xa.ptr, yb.ptr, count, TYPES[t][0], OPS[op]) == 0
+        mask = data_mask(t, count)  # pair types: the padding bytes carry no value
+        if not np.array_equal(yb.download(np.uint8, count=count * ext)[mask], as_bytes(want_b)[mask]):
+            bad.append(f"{op} {t} {count}")
+print(json.dumps({"scope": scope, "aql_calls": m.info("aql_calls"), "bad": bad}))
+"""
+
+
+def test_small_reduce_local_system_acquire():
+    """A job with other ranks dispatches the HSA-queue Reduce_local with the system-scope acquire (a
+    peer GPU's stores over xGMI pass none of this GPU's L2s, runtime/aql.cpp).  One GPU cannot hold
+    such a job with a rank per GPU, so a fresh process sets that scope with MV2AMD_AQL_ACQUIRE=2 and
+    runs the ordering checks of the test above (null-stream writes not waited for, host copies
+    between calls) and a bit-exact sweep through it."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MV2AMD_AQL_ACQUIRE="2", PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-c", SYSTEM_ACQUIRE_CHILD], env=env, cwd=root, capture_output=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-3000:]
+    got = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert got["scope"] == 2, got
+    assert got["aql_calls"] >= 300, got  # every call of the copy loop (the memset loop's wait for the null stream)
+    assert got["bad"] == [], got
