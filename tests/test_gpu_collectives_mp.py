@@ -31,7 +31,11 @@ def inputs(case, rank):
                       ties=case.get("ties", False))
 
 
-GEOMS = {"default": {}, "small": {"MV2AMD_PIPE_GRID": "3", "MV2AMD_PIPE_SUB": "4096"}}
+GEOMS = {"default": {}, "small": {"MV2AMD_PIPE_GRID": "3", "MV2AMD_PIPE_SUB": "4096"},
+         # what a rank with a GPU to itself adopts, through the documented knobs:
+         # full grids (the cap is max_grid / ranks per GPU), MPI_Init's tiling and one-shot crossover
+         # probes with their 1 MiB one-shot slots, point-to-point copy kernels
+         "full": {"MV2AMD_MAX_GRID": "8192", "MV2AMD_PIPE_AUTOTUNE": "1", "MV2AMD_P2P_KERNEL_COPY": "1"}}
 
 
 def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None, expect_fail=False):
@@ -107,7 +111,7 @@ COUNTS = [1, 3, 100, 4099, 70001, 300007]  # one-shot (<=256 KiB) and pipelined 
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "default"), (4, "default"), (3, "small"), (4, "small"),
-                                    (7, "small"), (8, "default")])
+                                    (7, "small"), (8, "default"), (2, "full"), (3, "full")])
 def test_collectives_multiprocess(n, geom, tmp_path, golden):
     cases = []
     seed = 1
