@@ -845,6 +845,16 @@ def main():
             res = arg_checks(L, rank, n)
         elif k == "soak":
             res = soak(L, case, rank, n)
+        elif k == "peer_absent":  # a collective one rank never enters: the others' device wait runs out
+            if rank == case["absent"]:
+                # into MPI_Finalize's host barrier (bounded by the same timeout) only after the peer's
+                # device wait has run out and been reported
+                time.sleep(case["sleep"])
+                res = np.array([0], dtype=np.int64)
+            else:
+                sb, rb = m.DeviceBuffer.from_array(np.ones(2, dtype=np.float32)), m.DeviceBuffer(8)
+                rc = L.MPI_Allreduce(sb.ptr, rb.ptr, 2, TYPES["MPI_FLOAT"][0], OPS["MPI_SUM"], WORLD)
+                res = np.array([rc], dtype=np.int64)
         elif k == "vector_bcast":
             # MPI_Type_vector(N, 4, 8, MPI_FLOAT) operand broadcast (device pack/unpack path)
             vt = ctypes.c_int()

@@ -63,7 +63,8 @@ def run_workers(n, cases, tmp_path, timeout=100, extra_env=None, ppn=None, expec
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r % ppn), LOCAL_WORLD_SIZE=str(ppn),
-                   MV2AMD_JOBID=jobid, **{"MV2AMD_TIMEOUT_S": "30", **boot}, **(extra_env or {}))
+                   MV2AMD_JOBID=jobid)
+        env.update({"MV2AMD_TIMEOUT_S": "30", **boot, **(extra_env or {})})
         env.pop("MV2AMD_DEVICE", None)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), str(spec),
                                        str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -967,3 +968,32 @@ def test_hw_queue_limit_reported_when_too_late(tmp_path):
         got[first] = [int(res("ti", r).view(np.int64)[8]) for r in range(2)]
     assert got["0"] == [2, 2], got
     assert got["1"] == [-2, -2], got
+
+
+def test_absent_peer_is_reported_not_hung(tmp_path):
+    """A collective that one rank never enters: the other rank's device wait runs out after
+    MV2AMD_TIMEOUT_S, its MPI_Allreduce returns MPI_ERR_OTHER (MPI_ERRORS_RETURN) instead of hanging,
+    and the report names what was awaited -- the epoch, the flags seen, the launch that waited
+    (call number and epochs), the waited slot as a copy re-reads it from memory (the absent rank's
+    older than the epoch), and where the absent rank's host is (coll.cpp check_err_word).  Both
+    ranks then finalize normally."""
+    # the host barriers share the timeout: the absent rank reaches MPI_Finalize's after 4.5 s, once the
+    # other rank's 3 s device wait has been reported, and well within that rank's 3 s barrier wait
+    case = {"id": "absent", "kind": "peer_absent", "absent": 1, "sleep": 4.5}
+    got = run_workers(2, [case], tmp_path, extra_env={"MV2AMD_TIMEOUT_S": "3"}, expect_fail=True)
+    assert [rc for rc, _ in got] == [0, 0], got
+    assert int(np.load(tmp_path / "out" / "absent_r0.npy")[0]) == 15  # MPI_ERR_OTHER
+    log = got[0][1]
+    assert "device collective timed out waiting for a peer" in log, log[-3000:]
+    import re
+    m0 = re.search(r"waited for epoch (\d+) from ranks 0x3; flags seen: r0=(\d+) r1=(\d+)", log)
+    assert m0, log[-3000:]
+    ep, f0, f1 = (int(v) for v in m0.groups())
+    assert f0 >= ep > f1
+    launches = re.search(r"last launches with flag epochs \(call:epochs, <- the waiting one\):(.*)", log)
+    waiting = [(int(a), int(b)) for a, b in re.findall(r"(\d+)-(\d+)(?:\(caller's stream\))?<-", launches.group(1))] \
+        if launches else []
+    assert len(waiting) == 1 and waiting[0][0] <= ep <= waiting[0][1], log[-3000:]
+    now = re.search(r"the waited slot now \(host copy\): r0=(\d+) r1=(\d+)", log)
+    assert now and int(now.group(1)) >= ep > int(now.group(2)), log[-3000:]
+    assert "late peer: local rank 1" in log, log[-3000:]
