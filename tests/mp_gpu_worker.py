@@ -587,6 +587,37 @@ def collops_comm(L, rank, n):
     return _COMM
 
 
+def upload_churn(L, case, rank, n):
+    """Diagnosis of the r06u / r06al / r06am stall: small blocking allreduces, with `churn_bytes` of
+    freshly allocated pageable host memory uploaded (hipMemcpy) and freed between calls on the ranks
+    in case["churn_ranks"] ("fresh"), or the same bytes from one array kept for the whole run
+    ("kept").  Returns [first failing call or -1, calls made, wrong results]."""
+    I, SUM = TYPES["MPI_INT"][0], OPS["MPI_SUM"]
+    nb = case["churn_bytes"]
+    scratch = m.DeviceBuffer(nb)
+    kept = np.ones(nb // 4, dtype=np.int32)
+    sb, rb = m.DeviceBuffer(64), m.DeviceBuffer(64)
+    fail, wrong = -1, 0
+    i = 0
+    for i in range(case["calls"]):
+        if rank in case["churn_ranks"]:
+            if case["mode"] == "fresh":
+                junk = np.full(nb // 4, i, dtype=np.int32)
+                scratch.upload(junk)
+                del junk
+            else:
+                kept[0] = i
+                scratch.upload(kept)
+        sb.upload(np.full(16, rank + i, dtype=np.int32))
+        rc = L.MPI_Allreduce(P(sb.ptr), P(rb.ptr), 16, I, SUM, WORLD)
+        if rc:
+            fail = i
+            break
+        want = sum(r + i for r in range(n))
+        wrong += int(not np.array_equal(rb.download(np.int32, count=16), np.full(16, want, dtype=np.int32)))
+    return np.array([fail, i + 1, wrong], dtype=np.int64)
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     out = sys.argv[2]
@@ -845,6 +876,8 @@ def main():
             res = arg_checks(L, rank, n)
         elif k == "soak":
             res = soak(L, case, rank, n)
+        elif k == "upload_churn":  # diagnosis (tools/runs/run_r06an.sh): pageable uploads between calls
+            res = upload_churn(L, case, rank, n)
         elif k == "peer_absent":  # a collective one rank never enters: the others' device wait runs out
             if rank == case["absent"]:
                 # into MPI_Finalize's host barrier (bounded by the same timeout) only after the peer's
