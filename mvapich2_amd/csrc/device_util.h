@@ -5,7 +5,8 @@
 //   producer: stores -> every wave s_waitcnt vmcnt(0) -> __syncthreads ->
 //             lane 0 system-scope release fence (buffer_wbl2) -> asm vmcnt(0)
 //             -> relaxed system-scope flag stores (one lane per peer)
-//   consumer: one wave polls its own (uncached, local) flag words relaxed,
+//   consumer: one wave polls its own (uncached, local) flag words with
+//             never-writing atomics (flag_load: read where the memory is),
 //             with s_sleep, bounded by a wall-clock timeout -> lane 0
 //             system-scope acquire fence (buffer_inv sc0 sc1: drops stale
 //             L1/L2 lines of peer memory) -> __syncthreads -> plain loads.
@@ -101,8 +102,14 @@ __device__ __forceinline__ T ld_nt_elem(const T *p) {
 __device__ __forceinline__ void flag_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// A flag poll is an atomic that never writes -- a compare-and-swap against a value no epoch reaches
+// -- so it is performed where the memory is, and returns the slot as memory holds it.  A plain
+// system-scope load was once served a stale copy of the slot for 30 s while memory held the newer
+// epoch, and a system-scope invalidate every 200 us did not clear it (profiles/r06/r06al, r06am).
 __device__ __forceinline__ uint64_t flag_load(uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint64_t v = ~0ull;
+    __hip_atomic_compare_exchange_strong(p, &v, ~0ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return v;
 }
 
 // Release this workgroup's prior global stores at system scope and raise
